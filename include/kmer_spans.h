@@ -1,0 +1,183 @@
+/*
+ * kmer_spans.h -- C ABI of the MI355X-native k-mer span scanner
+ * (libkmerspans.so, built from kmer_spans_amd/csrc/).
+ *
+ * This is the drop-in boundary for the span-scan path of lmjakt/kmer_spans
+ * (reference snapshot /root/reference, 2025-03-21).  Every entry point is plain
+ * C: pointers, sizes and status codes; no torch or HIP types in signatures
+ * (HIP streams travel as void*).  The R `.Call` shim
+ * (kmer_spans_amd/rcall/kmer_spans_call.c) maps the reference's six
+ * registered routines (kmer_spans.c:795-808) onto these functions; see
+ * INTEGRATION.md for that binding and for the ctypes binding Python uses.
+ *
+ * Conventions
+ *  - Sequences are byte strings given as (pointer, length); like R CHARSXPs
+ *    they contain no NUL.  Bytes N/n split runs; every other byte is encoded
+ *    as (c >> 1) & 3 (A/a=0, C/c=1, T/t=2, G/g=3), kmer_spans.c:34-35.
+ *  - k-mer codes: first base in the most significant bits, 4^k entries in
+ *    the internal A,C,T,G order (kmer_spans.c:41, kmer_seq :161-171).
+ *  - 1 <= k <= 15.  The reference admits k = 16 in kmer_counts (UB shift,
+ *    Q2), has no lower bound in kmer_regions_r (k = 0 loops forever on an N)
+ *    and no check in kmer_low_comp_regions (Q7); those are errors here.
+ *  - Every function validates all arguments before touching the device and
+ *    returns KS_OK or an error code; ks_last_error() returns the message
+ *    (the reference's error() strings where one exists).
+ *  - Output regions are allocated by the library; free with ks_regions_free.
+ *  - Results are bit-exact with the reference: region triples and their
+ *    order, scores (FP64, 0 ulp), counts and visit histograms.
+ */
+#ifndef KMER_SPANS_H
+#define KMER_SPANS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t ks_status;
+#define KS_OK 0
+#define KS_ERR_ARG 1         /* invalid argument (reference: error()) */
+#define KS_ERR_DEVICE 2      /* HIP runtime failure */
+#define KS_ERR_NOMEM 3       /* host or device allocation failed */
+#define KS_ERR_INTERNAL 4    /* internal consistency check failed */
+
+#define KS_MAX_K 15
+
+/* Thread-local message of the last failing call. */
+const char *ks_last_error(void);
+/* Library version string, e.g. "kmer_spans_amd 0.1 gfx950". */
+const char *ks_version(void);
+
+/* Region list in the reference's record layout (seq_regions, kmer_spans.c:
+ * 46-58): per region (seq_id, beg, end) int32 and score double; the second
+ * double the reference stores ("entropy") is always 0.0 and is not kept.
+ * Regions are ordered by (seq_id, beg), the reference's emission order. */
+typedef struct ks_regions {
+  int64_t n;
+  int32_t *seq_id; /* 0-based index into the input sequences (:536, :610) */
+  int32_t *beg;    /* scan index of the first positive k-mer (:272)       */
+  int32_t *end;    /* scan index of the first maximum (:289)              */
+  double *score;   /* maximum score (:280, :302)                          */
+} ks_regions;
+void ks_regions_free(ks_regions *r);
+
+/* Execution context: one GPU, one HIP stream, a grow-only device workspace.
+ * Created lazily per process (fork-safe: never touches HIP until first use,
+ * test.R:550-567 forks with mclapply).  Not thread-safe; one call at a time,
+ * like the reference on R's main thread. */
+typedef struct ks_ctx ks_ctx;
+ks_status ks_ctx_create(int32_t device, ks_ctx **out);
+void ks_ctx_destroy(ks_ctx *ctx);
+/* Use an external HIP stream (hipStream_t as void*); NULL = the ctx's own. */
+ks_status ks_ctx_set_stream(ks_ctx *ctx, void *hip_stream);
+/* Process-wide default context on device 0 (what the .Call shim uses). */
+ks_ctx *ks_default_ctx(void);
+
+/* ---------------------------------------------------------------------
+ * Host-buffer entry points: one per reference .Call routine on the path.
+ * Sequences are host pointers; the library stages them to the device.
+ * --------------------------------------------------------------------- */
+
+/* kmer_counts(seq_r, k_r) -- replaces kmer_spans.c:453-487.
+ * counts: int32[4^k] (overwritten), *n_words: words counted over sequences
+ * with length >= k (sequence_kmer_count :135-155, incl. quirk Q1). */
+ks_status ks_kmer_counts(ks_ctx *ctx, const char *const *seqs, const int64_t *lens,
+                         int32_t nseq, int32_t k, int32_t *counts, double *n_words);
+
+/* kmer_regions_r(seq_r, k_r, kmer_w_r, min_width_r, min_score_r) -- replaces
+ * kmer_spans.c:490-546.  w: double[4^k] in internal order; threshold 0.
+ * visits: int32[4^k] visit histogram incl. restart re-visits (Q6), may be NULL
+ * to skip it; *n_bases: total length of sequences with length >= k. */
+ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const int64_t *lens,
+                          int32_t nseq, int32_t k, const double *w, int64_t w_len,
+                          int32_t min_width, double min_score, int32_t *visits,
+                          double *n_bases, ks_regions *out);
+
+/* kmer_low_comp_regions(seq_r, k_r, min_width_r, min_score_r, threshold_r) --
+ * replaces kmer_spans.c:548-621: count -> weighted rank (rank_kmers_w
+ * :189-202, stable (count, index) order) -> scan with threshold thr in (0,1).
+ * counts int32[4^k], ranks double[4^k], n[2] = {#words, 0} (Q8). */
+ks_status ks_low_comp_regions(ks_ctx *ctx, const char *const *seqs, const int64_t *lens,
+                              int32_t nseq, int32_t k, int32_t min_width, double min_score,
+                              double thr, int32_t *counts, double *ranks, double *n,
+                              ks_regions *out);
+
+/* kmer_seq_r(k_r) -- replaces kmer_spans.c:623-639.  out: 4^k * (k+1) bytes,
+ * NUL-terminated k-char strings in internal code order. Host only. */
+ks_status ks_kmer_seq(int32_t k, char *out, size_t out_len);
+
+/* ---------------------------------------------------------------------
+ * Score-table builders (host, exact).  The reference computes the weighted
+ * rank in C (rank_kmers_w :189-202) and leaves log2(f/f_med) and +-1 to user
+ * R code (README.md:27-42, kmer.counts()$f kmer_spans.R:25).
+ * --------------------------------------------------------------------- */
+ks_status ks_rank_table(const int32_t *counts, int32_t k, double total, double *ranks);
+ks_status ks_log2_table(const int32_t *counts, int32_t k, double *w);
+ks_status ks_pm1_table(const int32_t *counts, int32_t k, double *w);
+
+/* ---------------------------------------------------------------------
+ * Device-resident entry points (inputs already in HBM).  Used by bench.py,
+ * the multi-GPU driver and callers that keep a genome resident.
+ * --------------------------------------------------------------------- */
+
+/* A batch of sequences concatenated in one device buffer.
+ * seq: device bytes; offsets_host/offsets_dev: nseq+1 int64 offsets (host
+ * and device copies of the same array); sequence q is
+ * seq[offsets[q] .. offsets[q+1]). */
+typedef struct ks_dev_seqs {
+  const uint8_t *seq;
+  const int64_t *offsets_host;
+  const int64_t *offsets_dev;
+  int32_t nseq;
+} ks_dev_seqs;
+
+/* A score table resident on the device, s = w[code] - thr precomputed
+ * bitwise as the reference computes it (kmer_spans.c:268).  When the table
+ * has at most 65536 distinct values it is stored as a uint16 code table plus
+ * an FP64 value LUT (exact: the LUT holds the very same doubles). */
+typedef struct ks_table ks_table;
+ks_status ks_table_create(ks_ctx *ctx, const double *w_host, int32_t k, double thr,
+                          int32_t allow_compress, ks_table **out);
+void ks_table_destroy(ks_table *t);
+/* 1 if the table is stored compressed (uint16 codes + LUT), else 0. */
+int32_t ks_table_is_compressed(const ks_table *t);
+int64_t ks_table_distinct(const ks_table *t);
+
+/* Scan statistics of the last ks_scan_dev call (device time of each phase,
+ * measured with hipEvents on the ctx stream). */
+typedef struct ks_scan_stats {
+  double ms_total;      /* whole scan (runs + kernels + compaction) */
+  double ms_runs;       /* run segmentation */
+  double ms_scan;       /* dominant scan kernel(s) */
+  double ms_rescan;     /* rescan rounds */
+  double ms_finish;     /* region ordering + D2H */
+  int64_t n_bases;      /* bytes of sequences with length >= k */
+  int64_t n_scored;     /* top-level scored positions */
+  int64_t n_runs;       /* N-free runs with scored positions */
+  int64_t n_regions;
+  int64_t n_rescan;     /* rescan ranges processed */
+  int32_t scan_algo;    /* 0 = lane per run, 1 = chunked carry scan */
+} ks_scan_stats;
+
+/* Span scan of device-resident sequences (the hot path).  visits_dev: device
+ * int32[4^k] accumulated (caller zeroes), or NULL.  Regions are returned in
+ * host memory.  stats may be NULL. */
+ks_status ks_scan_dev(ks_ctx *ctx, const ks_dev_seqs *seqs, int32_t k, const ks_table *table,
+                      int32_t min_width, double min_score, int32_t *visits_dev,
+                      ks_regions *out, ks_scan_stats *stats);
+
+/* k-mer counting of device-resident sequences into counts_dev (int32[4^k],
+ * accumulated: the caller zeroes it).  *n_words as in ks_kmer_counts. */
+ks_status ks_count_dev(ks_ctx *ctx, const ks_dev_seqs *seqs, int32_t k, int32_t *counts_dev,
+                       double *n_words);
+
+/* Scan algorithm selection (testing/benchmarking): -1 auto, 0 lane-per-run,
+ * 1 chunked carry scan. */
+ks_status ks_ctx_set_scan_algo(ks_ctx *ctx, int32_t algo);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMER_SPANS_H */

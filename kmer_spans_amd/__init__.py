@@ -1,0 +1,14 @@
+"""kmer_spans_amd -- MI355X-native k-mer span scanner (drop-in for the
+span-scan path of lmjakt/kmer_spans).
+
+Public API mirrors kmer_spans.R: kmer_counts, kmer_regions,
+kmer_low_comp_regions, kmer_seq; score tables log2_table, pm1_table,
+rank_table.  Device-resident entry points live in kmer_spans_amd.device.
+All results come from libkmerspans.so (HIP, gfx950); there is no CPU path.
+"""
+from ._lib import KmerSpansError, LIB_PATH, context  # noqa: F401
+from .api import (kmer_counts, kmer_low_comp_regions, kmer_regions, kmer_seq,  # noqa: F401
+                  log2_table, pm1_table, rank_table)
+
+__all__ = ["kmer_counts", "kmer_regions", "kmer_low_comp_regions", "kmer_seq", "log2_table",
+           "pm1_table", "rank_table", "KmerSpansError", "context"]

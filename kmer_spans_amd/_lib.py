@@ -1,0 +1,156 @@
+"""ctypes binding of libkmerspans.so (the C ABI in include/kmer_spans.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()``
+(kmer_spans_amd/csrc/Makefile).  There is no fallback: importing this module
+without the library raises, so a missing build can never silently turn into
+a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkmerspans.so")
+
+KS_OK = 0
+KS_MAX_K = 15
+
+
+class KmerSpansError(RuntimeError):
+    """An error reported by libkmerspans (the reference's error() strings)."""
+
+
+class Regions(C.Structure):
+    _fields_ = [("n", C.c_int64), ("seq_id", C.POINTER(C.c_int32)), ("beg", C.POINTER(C.c_int32)),
+                ("end", C.POINTER(C.c_int32)), ("score", C.POINTER(C.c_double))]
+
+
+class DevSeqs(C.Structure):
+    _fields_ = [("seq", C.c_void_p), ("offsets_host", C.c_void_p), ("offsets_dev", C.c_void_p),
+                ("nseq", C.c_int32)]
+
+
+class ScanStats(C.Structure):
+    _fields_ = [("ms_total", C.c_double), ("ms_runs", C.c_double), ("ms_scan", C.c_double),
+                ("ms_rescan", C.c_double), ("ms_finish", C.c_double), ("n_bases", C.c_int64),
+                ("n_scored", C.c_int64), ("n_runs", C.c_int64), ("n_regions", C.c_int64),
+                ("n_rescan", C.c_int64), ("scan_algo", C.c_int32)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+# Every symbol include/kmer_spans.h declares (tests check they are exported).
+EXPORTS = [
+    "ks_last_error", "ks_version", "ks_regions_free", "ks_ctx_create", "ks_ctx_destroy",
+    "ks_ctx_set_stream", "ks_default_ctx", "ks_kmer_counts", "ks_kmer_regions",
+    "ks_low_comp_regions", "ks_kmer_seq", "ks_rank_table", "ks_log2_table", "ks_pm1_table",
+    "ks_table_create", "ks_table_destroy", "ks_table_is_compressed", "ks_table_distinct",
+    "ks_scan_dev", "ks_count_dev", "ks_ctx_set_scan_algo",
+]
+
+_lib = None
+
+
+def load():
+    """Load and type the library (raises if it is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+    L = C.CDLL(LIB_PATH)
+    P, I32, I64, D = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+    sigs = {
+        "ks_last_error": ([], C.c_char_p),
+        "ks_version": ([], C.c_char_p),
+        "ks_regions_free": ([P], None),
+        "ks_ctx_create": ([I32, P], I32),
+        "ks_ctx_destroy": ([P], None),
+        "ks_ctx_set_stream": ([P, P], I32),
+        "ks_default_ctx": ([], P),
+        "ks_ctx_set_scan_algo": ([P, I32], I32),
+        "ks_kmer_counts": ([P, P, P, I32, I32, P, P], I32),
+        "ks_kmer_regions": ([P, P, P, I32, I32, P, I64, I32, D, P, P, P], I32),
+        "ks_low_comp_regions": ([P, P, P, I32, I32, I32, D, D, P, P, P, P], I32),
+        "ks_kmer_seq": ([I32, P, C.c_size_t], I32),
+        "ks_rank_table": ([P, I32, D, P], I32),
+        "ks_log2_table": ([P, I32, P], I32),
+        "ks_pm1_table": ([P, I32, P], I32),
+        "ks_table_create": ([P, P, I32, D, I32, P], I32),
+        "ks_table_destroy": ([P], None),
+        "ks_table_is_compressed": ([P], I32),
+        "ks_table_distinct": ([P], I64),
+        "ks_scan_dev": ([P, P, I32, P, I32, D, P, P, P], I32),
+        "ks_count_dev": ([P, P, I32, P, P], I32),
+    }
+    for name, (args, res) in sigs.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != KS_OK:
+        msg = load().ks_last_error().decode(errors="replace")
+        raise KmerSpansError(msg or f"libkmerspans error {rc}")
+
+
+def regions_to_numpy(r: Regions):
+    """Copy a ks_regions into (pos int32[3, n], score float64[2, n]) and free it."""
+    n = int(r.n)
+    pos = np.zeros((3, n), dtype=np.int32)
+    score = np.zeros((2, n), dtype=np.float64)
+    if n:
+        pos[0] = np.ctypeslib.as_array(r.seq_id, shape=(n,))
+        pos[1] = np.ctypeslib.as_array(r.beg, shape=(n,))
+        pos[2] = np.ctypeslib.as_array(r.end, shape=(n,))
+        score[0] = np.ctypeslib.as_array(r.score, shape=(n,))
+    load().ks_regions_free(C.byref(r))
+    return pos, score
+
+
+class Context:
+    """One GPU + HIP stream + device workspace (ks_ctx).  Created lazily, so a
+    process that only forks workers never touches HIP in the parent."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self._h = C.c_void_p()
+        check(load().ks_ctx_create(device, C.byref(self._h)))
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, stream_ptr: int | None):
+        check(load().ks_ctx_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def set_scan_algo(self, algo: int):
+        check(load().ks_ctx_set_scan_algo(self._h, int(algo)))
+
+    def close(self):
+        if self._h:
+            load().ks_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_contexts: dict[int, Context] = {}
+
+
+def context(device: int = 0) -> Context:
+    ctx = _contexts.get(device)
+    if ctx is None:
+        ctx = _contexts[device] = Context(device)
+    return ctx

@@ -1,0 +1,162 @@
+"""The reference's user API (kmer_spans.R) on top of the C ABI.
+
+Same function names (dots become underscores), argument meaning, return
+layout and error behaviour as /root/reference/kmer_spans.R:
+
+  kmer_counts(seq, k, with_f=True)               kmer_spans.R:18-27
+  kmer_regions(seq, k, kmer_scores, min_width, min_score)   :41-52
+  kmer_low_comp_regions(seq, k, min_w, min_score, thr=0.75) :72-79
+  kmer_seq(k)                                     :84-86
+
+Sequences are a str/bytes or a list of them (R character vectors).  Results
+come from libkmerspans.so on the GPU; nothing here computes a result on the
+CPU.  Table builders for the README score functions are exposed as
+``log2_table`` / ``pm1_table`` / ``rank_table``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import KmerSpansError, Regions, check, load, regions_to_numpy
+
+
+class _HostSeqs:
+    """(char* const*, int64 lens) view of a list of byte strings."""
+
+    def __init__(self, seq):
+        if isinstance(seq, (str, bytes, bytearray, memoryview, np.ndarray)):
+            seq = [seq]
+        self.bufs = []
+        for s in seq:
+            if isinstance(s, np.ndarray):
+                b = np.ascontiguousarray(s, dtype=np.uint8)
+            elif isinstance(s, str):
+                b = np.frombuffer(s.encode("latin-1"), dtype=np.uint8)
+            else:
+                b = np.frombuffer(bytes(s), dtype=np.uint8)
+            self.bufs.append(b)
+        self.n = len(self.bufs)
+        self._empty = np.zeros(1, dtype=np.uint8)
+        self.ptrs = (C.c_void_p * max(self.n, 1))()
+        for i, b in enumerate(self.bufs):
+            self.ptrs[i] = b.ctypes.data if b.size else self._empty.ctypes.data
+        self.lens = np.array([b.size for b in self.bufs] or [0], dtype=np.int64)
+
+
+def _ctx(device):
+    """Device 0 uses the library's lazily created default context, so that
+    argument errors surface before any HIP call (kmer_spans.c validates before
+    allocating); other devices get an explicit context."""
+    return None if int(device) == 0 else _lib.context(device).handle
+
+
+def kmer_seq(k: int) -> list[str]:
+    """k-mer strings in the internal A,C,T,G code order (kmer_seq_r)."""
+    k = int(k)
+    if k < 1 or k > _lib.KS_MAX_K:
+        check(load().ks_kmer_seq(k, None, 0))
+    n = 4 ** k
+    buf = C.create_string_buffer(n * (k + 1))
+    check(load().ks_kmer_seq(k, buf, n * (k + 1)))
+    raw = buf.raw
+    return [raw[i * (k + 1):i * (k + 1) + k].decode() for i in range(n)]
+
+
+def kmer_counts(seq, k: int, with_f: bool = True, device: int = 0) -> dict:
+    """kmer.counts: {'n': {'k': k, 'n': words}, 'counts': int32[4^k], 'f': ...}."""
+    k = int(k)
+    hs = _HostSeqs(seq)
+    counts = np.zeros(4 ** k if 1 <= k <= _lib.KS_MAX_K else 1, dtype=np.int32)
+    n = C.c_double(0)
+    check(load().ks_kmer_counts(_ctx(device), hs.ptrs, hs.lens.ctypes.data, hs.n, k,
+                                counts.ctypes.data, C.byref(n)))
+    out = {"n": {"k": k, "n": n.value}, "counts": counts}
+    if with_f:
+        with np.errstate(invalid="ignore", divide="ignore"):
+            out["f"] = counts / float(counts.astype(np.int64).sum())
+    return out
+
+
+def _ordered_scores(k: int, kmer_scores):
+    """kmer.regions reorders a named score vector by kmer.seq(k)
+    (kmer_spans.R:42-47); an unnamed array is taken as internal order."""
+    if isinstance(kmer_scores, dict):
+        if len(kmer_scores) != 4 ** k:
+            raise KmerSpansError("There should be a total of 4^k scores")
+        names = kmer_seq(k)
+        if any(nm not in kmer_scores for nm in names):
+            raise KmerSpansError("all kmers not defined")
+        return np.array([kmer_scores[nm] for nm in names], dtype=np.float64)
+    if hasattr(kmer_scores, "index") and hasattr(kmer_scores, "values"):  # pandas Series
+        return _ordered_scores(k, dict(zip(kmer_scores.index, kmer_scores.values)))
+    w = np.ascontiguousarray(kmer_scores, dtype=np.float64).ravel()
+    if w.size != 4 ** k:
+        raise KmerSpansError("There should be a total of 4^k scores")
+    return w
+
+
+def kmer_regions(seq, k: int, kmer_scores, min_width: int, min_score: float, visits: bool = True,
+                 device: int = 0) -> dict:
+    """kmer.regions: {'n', 'counts' (visit histogram), 'pos' int32[3, R]
+    (seq_id, beg, end), 'score' float64[2, R] (score, 0)} -- not transposed,
+    exactly as kmer_spans.R:48-51 returns it."""
+    k = int(k)
+    w = _ordered_scores(k, kmer_scores)
+    hs = _HostSeqs(seq)
+    vis = np.zeros(4 ** k, dtype=np.int32) if visits else None
+    n = C.c_double(0)
+    r = Regions()
+    check(load().ks_kmer_regions(_ctx(device), hs.ptrs, hs.lens.ctypes.data, hs.n, k, w.ctypes.data,
+                                 w.size, int(min_width), float(min_score),
+                                 vis.ctypes.data if vis is not None else None, C.byref(n), C.byref(r)))
+    pos, score = regions_to_numpy(r)
+    return {"n": n.value, "counts": vis, "pos": pos, "score": score}
+
+
+def kmer_low_comp_regions(seq, k: int, min_w: int, min_score: float, thr: float = 0.75,
+                          device: int = 0) -> dict:
+    """kmer.low.comp.regions: {'n' [#words, 0], 'counts', 'w_rank',
+    'pos' int32[R, 3], 'score' float64[R, 2]} (pos/score transposed as
+    kmer_spans.R:76-77 does)."""
+    k = int(k)
+    hs = _HostSeqs(seq)
+    nk = 4 ** k if 1 <= k <= _lib.KS_MAX_K else 1
+    counts = np.zeros(nk, dtype=np.int32)
+    ranks = np.zeros(nk, dtype=np.float64)
+    n = np.zeros(2, dtype=np.float64)
+    r = Regions()
+    check(load().ks_low_comp_regions(_ctx(device), hs.ptrs, hs.lens.ctypes.data, hs.n, k, int(min_w),
+                                     float(min_score), float(thr), counts.ctypes.data,
+                                     ranks.ctypes.data, n.ctypes.data, C.byref(r)))
+    pos, score = regions_to_numpy(r)
+    return {"n": n, "counts": counts, "w_rank": ranks, "pos": pos.T.copy(), "score": score.T.copy()}
+
+
+# ------------------------------------------------------------ table builders
+
+def _table(fn, counts, k):
+    counts = np.ascontiguousarray(counts, dtype=np.int32)
+    out = np.zeros(4 ** int(k), dtype=np.float64)
+    check(fn(counts.ctypes.data, int(k), out.ctypes.data))
+    return out
+
+
+def log2_table(counts, k: int) -> np.ndarray:
+    """log2(f / f_med) with f = counts / sum(counts) (README.md:27-29)."""
+    return _table(load().ks_log2_table, counts, k)
+
+
+def pm1_table(counts, k: int) -> np.ndarray:
+    """ifelse(f >= f_med, 1, -1) (README.md:37-42)."""
+    return _table(load().ks_pm1_table, counts, k)
+
+
+def rank_table(counts, k: int, total: float) -> np.ndarray:
+    """Weighted rank (rank_kmers_w, kmer_spans.c:189-202)."""
+    counts = np.ascontiguousarray(counts, dtype=np.int32)
+    out = np.zeros(4 ** int(k), dtype=np.float64)
+    check(load().ks_rank_table(counts.ctypes.data, int(k), float(total), out.ctypes.data))
+    return out

@@ -1,0 +1,374 @@
+// ks_abi.cpp -- the C ABI (include/kmer_spans.h): contexts, workspace,
+// argument validation and the host-buffer entry points that stand in for the
+// reference's .Call routines (kmer_spans.c:452-639).
+//
+// Validation happens before any device work, with the reference's error
+// strings, because R's error() longjmps out of the caller.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
+#include "ks_internal.h"
+
+namespace ks {
+
+static thread_local char g_err[512];
+
+void set_error(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+ks_status fail(ks_status st, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return st;
+}
+
+ks_status activate(ks_ctx *ctx) {
+  KS_HIP(hipSetDevice(ctx->device));
+  return KS_OK;
+}
+
+ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out) {
+  DevBuf &b = ctx->slots[s];
+  if (b.bytes < bytes) {
+    if (b.ptr) {
+      KS_HIP(hipStreamSynchronize(ctx->stream));
+      KS_HIP(hipFree(b.ptr));
+      b.ptr = nullptr;
+      b.bytes = 0;
+    }
+    size_t want = std::max<size_t>(bytes, 256);
+    want = (want + 4095) & ~(size_t)4095;
+    hipError_t e = hipMalloc(&b.ptr, want);
+    if (e != hipSuccess) {
+      b.ptr = nullptr;
+      return fail(KS_ERR_NOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+    }
+    b.bytes = want;
+  }
+  *out = b.ptr;
+  return KS_OK;
+}
+
+ks_status ensure_pinned(ks_ctx *ctx, size_t bytes, void **out) {
+  if (ctx->pinned_bytes < bytes) {
+    if (ctx->pinned) {
+      KS_HIP(hipStreamSynchronize(ctx->stream));
+      KS_HIP(hipHostFree(ctx->pinned));
+      ctx->pinned = nullptr;
+      ctx->pinned_bytes = 0;
+    }
+    size_t want = (std::max<size_t>(bytes, 4096) + 4095) & ~(size_t)4095;
+    hipError_t e = hipHostMalloc(&ctx->pinned, want, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      ctx->pinned = nullptr;
+      return fail(KS_ERR_NOMEM, "hipHostMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+    }
+    ctx->pinned_bytes = want;
+  }
+  *out = ctx->pinned;
+  return KS_OK;
+}
+
+namespace {
+
+// Stage host sequences into the ctx's device buffer (16-byte aligned base).
+struct Staged {
+  ks_dev_seqs dev{};
+  std::vector<int64_t> offs;
+  int64_t total = 0;
+};
+
+ks_status stage(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq, Staged *st) {
+  st->offs.assign((size_t)nseq + 1, 0);
+  for (int32_t q = 0; q < nseq; ++q) st->offs[q + 1] = st->offs[q] + std::max<int64_t>(lens[q], 0);
+  st->total = st->offs[nseq];
+  void *d_seq = nullptr, *d_offs = nullptr, *h = nullptr;
+  KS_TRY(ensure(ctx, SLOT_SEQ, (size_t)st->total + 32, &d_seq));
+  KS_TRY(ensure(ctx, SLOT_OFFS, ((size_t)nseq + 1) * 8, &d_offs));
+  KS_TRY(ensure_pinned(ctx, (size_t)st->total + 32, &h));
+  char *hp = static_cast<char *>(h);
+  for (int32_t q = 0; q < nseq; ++q)
+    if (lens[q] > 0) memcpy(hp + st->offs[q], seqs[q], (size_t)lens[q]);
+  if (st->total) KS_HIP(hipMemcpyAsync(d_seq, h, (size_t)st->total, hipMemcpyHostToDevice, ctx->stream));
+  KS_HIP(hipMemcpyAsync(d_offs, st->offs.data(), ((size_t)nseq + 1) * 8, hipMemcpyHostToDevice,
+                        ctx->stream));
+  KS_HIP(hipStreamSynchronize(ctx->stream));
+  st->dev.seq = static_cast<const uint8_t *>(d_seq);
+  st->dev.offsets_dev = static_cast<const int64_t *>(d_offs);
+  st->dev.offsets_host = st->offs.data();
+  st->dev.nseq = nseq;
+  return KS_OK;
+}
+
+ks_status check_seqs(const char *const *seqs, const int64_t *lens, int32_t nseq) {
+  if (nseq < 1 || !seqs || !lens)
+    return fail(KS_ERR_ARG, "seq_r must be a character vector of length at least one");
+  for (int32_t q = 0; q < nseq; ++q) {
+    if (lens[q] < 0 || lens[q] > INT32_MAX) return fail(KS_ERR_ARG, "sequence %d has an invalid length", q);
+    if (lens[q] > 0 && !seqs[q]) return fail(KS_ERR_ARG, "sequence %d is NULL", q);
+  }
+  return KS_OK;
+}
+
+ks_status check_dev_seqs(const ks_dev_seqs *s) {
+  if (!s || s->nseq < 1 || !s->offsets_host || !s->offsets_dev)
+    return fail(KS_ERR_ARG, "seq_r must be a character vector of length at least one");
+  if (s->offsets_host[s->nseq] > 0 && !s->seq) return fail(KS_ERR_ARG, "null device sequence buffer");
+  if (((uintptr_t)s->seq & 15u) != 0) return fail(KS_ERR_ARG, "device sequence buffer must be 16-byte aligned");
+  for (int32_t q = 0; q < s->nseq; ++q)
+    if (s->offsets_host[q + 1] < s->offsets_host[q]) return fail(KS_ERR_ARG, "offsets must be non-decreasing");
+  return KS_OK;
+}
+
+std::mutex g_default_mu;
+ks_ctx *g_default = nullptr;
+
+}  // namespace
+}  // namespace ks
+
+using namespace ks;
+
+extern "C" const char *ks_last_error(void) { return g_err; }
+extern "C" const char *ks_version(void) { return "kmer_spans_amd 0.1 gfx950"; }
+
+extern "C" void ks_regions_free(ks_regions *r) {
+  if (!r) return;
+  free(r->seq_id);
+  free(r->beg);
+  free(r->end);
+  free(r->score);
+  memset(r, 0, sizeof(*r));
+}
+
+extern "C" ks_status ks_ctx_create(int32_t device, ks_ctx **out) {
+  if (!out) return fail(KS_ERR_ARG, "null output");
+  int ndev = 0;
+  KS_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(KS_ERR_ARG, "device %d out of range (%d devices)", device, ndev);
+  ks_ctx *c = new ks_ctx();
+  c->device = device;
+  KS_HIP(hipSetDevice(device));
+  KS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  c->own_stream = true;
+  hipDeviceProp_t prop;
+  KS_HIP(hipGetDeviceProperties(&prop, device));
+  c->num_cus = prop.multiProcessorCount;
+  for (auto &e : c->ev) KS_HIP(hipEventCreate(&e));
+  *out = c;
+  return KS_OK;
+}
+
+extern "C" void ks_ctx_destroy(ks_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto &b : c->slots)
+    if (b.ptr) (void)hipFree(b.ptr);
+  if (c->pinned) (void)hipHostFree(c->pinned);
+  for (auto &e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+extern "C" ks_status ks_ctx_set_stream(ks_ctx *c, void *stream) {
+  if (!c) return fail(KS_ERR_ARG, "null ctx");
+  if (c->own_stream && c->stream) {
+    KS_HIP(hipStreamSynchronize(c->stream));
+    KS_HIP(hipStreamDestroy(c->stream));
+    c->own_stream = false;
+    c->stream = nullptr;
+  }
+  if (stream) {
+    c->stream = static_cast<hipStream_t>(stream);
+  } else {
+    KS_HIP(hipSetDevice(c->device));
+    KS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->own_stream = true;
+  }
+  return KS_OK;
+}
+
+extern "C" ks_status ks_ctx_set_scan_algo(ks_ctx *c, int32_t algo) {
+  if (!c || algo < -1 || algo > 1) return fail(KS_ERR_ARG, "invalid scan algorithm");
+  c->scan_algo = algo;
+  return KS_OK;
+}
+
+extern "C" ks_ctx *ks_default_ctx(void) {
+  std::lock_guard<std::mutex> g(g_default_mu);
+  if (!g_default) {
+    if (ks_ctx_create(0, &g_default) != KS_OK) g_default = nullptr;
+  }
+  return g_default;
+}
+
+// ------------------------------------------------------------ host entries
+
+extern "C" ks_status ks_kmer_seq(int32_t k, char *out, size_t out_len) {
+  if (k < 1 || k > KS_MAX_K)  // kmer_spans.c:627-628
+    return fail(KS_ERR_ARG, "k_r (%d) should be smaller than MAX_K (%d) and larger than 0", k, KS_MAX_K + 1);
+  const size_t n = (size_t)1 << (2 * k);
+  if (!out || out_len < n * (size_t)(k + 1)) return fail(KS_ERR_ARG, "output buffer too small");
+  static const char nuc[4] = {'A', 'C', 'T', 'G'};
+  for (size_t i = 0; i < n; ++i) {
+    char *o = out + i * (size_t)(k + 1);
+    for (int p = 0; p < k; ++p) o[p] = nuc[(i >> (2 * (k - 1 - p))) & 3u];
+    o[k] = 0;
+  }
+  return KS_OK;
+}
+
+extern "C" ks_status ks_rank_table(const int32_t *counts, int32_t k, double total, double *ranks) {
+  if (k < 1 || k > KS_MAX_K) return fail(KS_ERR_ARG, "k must be between 1 and %d", KS_MAX_K);
+  if (!counts || !ranks) return fail(KS_ERR_ARG, "null argument");
+  return rank_table_host(counts, k, total, ranks);
+}
+
+extern "C" ks_status ks_log2_table(const int32_t *counts, int32_t k, double *w) {
+  if (k < 1 || k > KS_MAX_K) return fail(KS_ERR_ARG, "k must be between 1 and %d", KS_MAX_K);
+  if (!counts || !w) return fail(KS_ERR_ARG, "null argument");
+  return log2_table_host(counts, k, w);
+}
+
+extern "C" ks_status ks_pm1_table(const int32_t *counts, int32_t k, double *w) {
+  if (k < 1 || k > KS_MAX_K) return fail(KS_ERR_ARG, "k must be between 1 and %d", KS_MAX_K);
+  if (!counts || !w) return fail(KS_ERR_ARG, "null argument");
+  return pm1_table_host(counts, k, w);
+}
+
+extern "C" ks_status ks_count_dev(ks_ctx *ctx, const ks_dev_seqs *s, int32_t k, int32_t *counts_dev,
+                                  double *n_words) {
+  if (!ctx) return fail(KS_ERR_ARG, "null ctx");
+  KS_TRY(check_dev_seqs(s));
+  if (k < 1 || k > KS_MAX_K) return fail(KS_ERR_ARG, "k must be a positive integer less than 1+MAX_K");
+  if (!counts_dev || !n_words) return fail(KS_ERR_ARG, "null argument");
+  KS_TRY(activate(ctx));
+  Runs none;
+  return launch_count(ctx, s, s->offsets_host[s->nseq], none, k, counts_dev, n_words);
+}
+
+extern "C" ks_status ks_scan_dev(ks_ctx *ctx, const ks_dev_seqs *s, int32_t k, const ks_table *t,
+                                 int32_t min_width, double min_score, int32_t *visits_dev,
+                                 ks_regions *out, ks_scan_stats *stats) {
+  if (!ctx || !t || !out) return fail(KS_ERR_ARG, "null argument");
+  KS_TRY(check_dev_seqs(s));
+  if (k < 1 || k > KS_MAX_K)
+    return fail(KS_ERR_ARG, "kmer sizes larger than or equal to %d not currently supported", KS_MAX_K + 1);
+  if (t->k != k) return fail(KS_ERR_ARG, "table built for k=%d used with k=%d", t->k, k);
+  memset(out, 0, sizeof(*out));
+  KS_TRY(activate(ctx));
+  return scan_impl(ctx, s, s->offsets_host[s->nseq], k, t, min_width, min_score, visits_dev, out, stats);
+}
+
+extern "C" ks_status ks_kmer_counts(ks_ctx *ctx, const char *const *seqs, const int64_t *lens,
+                                    int32_t nseq, int32_t k, int32_t *counts, double *n_words) {
+  KS_TRY(check_seqs(seqs, lens, nseq));                       // kmer_spans.c:454-455
+  if (k < 1 || k > KS_MAX_K)                                  // :461-462 (and Q2)
+    return fail(KS_ERR_ARG, "k must be a positive integer less than 1+MAX_K");
+  if (!counts || !n_words) return fail(KS_ERR_ARG, "null output");
+  if (!ctx) ctx = ks_default_ctx();
+  if (!ctx) return fail(KS_ERR_DEVICE, "no HIP device available");
+  KS_TRY(activate(ctx));
+  Staged st;
+  KS_TRY(stage(ctx, seqs, lens, nseq, &st));
+  const size_t nb = (size_t)4 << (2 * k);
+  void *d_counts = nullptr;
+  KS_TRY(ensure(ctx, SLOT_COUNTS, nb, &d_counts));
+  KS_HIP(hipMemsetAsync(d_counts, 0, nb, ctx->stream));
+  Runs none;
+  KS_TRY(launch_count(ctx, &st.dev, st.total, none, k, (int32_t *)d_counts, n_words));
+  KS_HIP(hipMemcpyAsync(counts, d_counts, nb, hipMemcpyDeviceToHost, ctx->stream));
+  KS_HIP(hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const int64_t *lens,
+                                     int32_t nseq, int32_t k, const double *w, int64_t w_len,
+                                     int32_t min_width, double min_score, int32_t *visits,
+                                     double *n_bases, ks_regions *out) {
+  KS_TRY(check_seqs(seqs, lens, nseq));                       // :491-492
+  if (!w) return fail(KS_ERR_ARG, "kmer_w_r must be a double vector of length k^4");  // :495-496
+  if (k >= KS_MAX_K + 1)                                      // :504-505
+    return fail(KS_ERR_ARG, "kmer sizes larger than or equal to %d not currently supported", KS_MAX_K + 1);
+  if (k < 1) return fail(KS_ERR_ARG, "k must be a positive integer");
+  const int64_t want = (int64_t)1 << (2 * k);
+  if (w_len != want)                                          // :508-509
+    return fail(KS_ERR_ARG, "kmer_w contains %lld elements but should have %lld", (long long)w_len,
+                (long long)want);
+  if (!out || !n_bases) return fail(KS_ERR_ARG, "null output");
+  memset(out, 0, sizeof(*out));
+  if (!ctx) ctx = ks_default_ctx();
+  if (!ctx) return fail(KS_ERR_DEVICE, "no HIP device available");
+  KS_TRY(activate(ctx));
+  double n = 0;
+  for (int32_t q = 0; q < nseq; ++q)
+    if (lens[q] >= k) n += (double)lens[q];                   // :535
+  *n_bases = n;
+  Staged st;
+  KS_TRY(stage(ctx, seqs, lens, nseq, &st));
+  ks_table *t = nullptr;
+  KS_TRY(ks_table_create(ctx, w, k, 0.0, k >= 9 ? 1 : 0, &t));
+  const size_t nb = (size_t)4 << (2 * k);
+  void *d_vis = nullptr;
+  ks_status rc = KS_OK;
+  if (visits) {
+    rc = ensure(ctx, SLOT_COUNTS, nb, &d_vis);
+    if (rc == KS_OK && hipMemsetAsync(d_vis, 0, nb, ctx->stream) != hipSuccess)
+      rc = fail(KS_ERR_DEVICE, "hipMemsetAsync failed");
+  }
+  if (rc == KS_OK)
+    rc = scan_impl(ctx, &st.dev, st.total, k, t, min_width, min_score, (int32_t *)d_vis, out, nullptr);
+  if (rc == KS_OK && visits) {
+    if (hipMemcpyAsync(visits, d_vis, nb, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+      rc = fail(KS_ERR_DEVICE, "visit histogram copy failed");
+  }
+  ks_table_destroy(t);
+  if (rc != KS_OK) ks_regions_free(out);
+  return rc;
+}
+
+extern "C" ks_status ks_low_comp_regions(ks_ctx *ctx, const char *const *seqs, const int64_t *lens,
+                                         int32_t nseq, int32_t k, int32_t min_width, double min_score,
+                                         double thr, int32_t *counts, double *ranks, double *n,
+                                         ks_regions *out) {
+  KS_TRY(check_seqs(seqs, lens, nseq));                       // :549-550
+  if (thr <= 0 || thr >= 1)                                   // :567-568
+    return fail(KS_ERR_ARG, "the threshold must be between 0 and 1");
+  if (k < 1 || k > KS_MAX_K)                                  // Q7: unchecked in the reference
+    return fail(KS_ERR_ARG, "k must be a positive integer less than 1+MAX_K");
+  if (!counts || !ranks || !n || !out) return fail(KS_ERR_ARG, "null output");
+  memset(out, 0, sizeof(*out));
+  if (!ctx) ctx = ks_default_ctx();
+  if (!ctx) return fail(KS_ERR_DEVICE, "no HIP device available");
+  KS_TRY(activate(ctx));
+  Staged st;
+  KS_TRY(stage(ctx, seqs, lens, nseq, &st));
+  const size_t nb = (size_t)4 << (2 * k);
+  void *d_counts = nullptr;
+  KS_TRY(ensure(ctx, SLOT_COUNTS, nb, &d_counts));
+  KS_HIP(hipMemsetAsync(d_counts, 0, nb, ctx->stream));
+  double words = 0;
+  Runs none;
+  KS_TRY(launch_count(ctx, &st.dev, st.total, none, k, (int32_t *)d_counts, &words));  // :592-601
+  KS_HIP(hipMemcpyAsync(counts, d_counts, nb, hipMemcpyDeviceToHost, ctx->stream));
+  KS_HIP(hipStreamSynchronize(ctx->stream));
+  n[0] = words;
+  KS_TRY(rank_table_host(counts, k, words, ranks));           // :602
+  ks_table *t = nullptr;
+  KS_TRY(ks_table_create(ctx, ranks, k, thr, 0, &t));         // ranks are ~unique: no LUT
+  ks_status rc = scan_impl(ctx, &st.dev, st.total, k, t, min_width, min_score, nullptr, out, nullptr);
+  ks_table_destroy(t);
+  n[1] = 0;                                                   // Q8 (:613)
+  if (rc != KS_OK) ks_regions_free(out);
+  return rc;
+}

@@ -1,0 +1,131 @@
+// ks_internal.h -- shared definitions of libkmerspans (HIP, gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/kmer_spans.h"
+
+namespace ks {
+
+// ---------------------------------------------------------------- errors
+void set_error(const char *fmt, ...);
+ks_status fail(ks_status st, const char *fmt, ...);
+
+#define KS_HIP(call)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (call);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return ::ks::fail(KS_ERR_DEVICE, "%s failed: %s (%s:%d)", #call,                \
+                        hipGetErrorString(e_), __FILE__, __LINE__);                   \
+  } while (0)
+
+#define KS_TRY(expr)                 \
+  do {                               \
+    ks_status s_ = (expr);           \
+    if (s_ != KS_OK) return s_;      \
+  } while (0)
+
+// ------------------------------------------------------ device workspace
+// Grow-only device buffers, one per slot.  Never freed inside a call, so a
+// call sequence can be captured or replayed without allocation.
+enum Slot : int {
+  SLOT_SEQ = 0,     // staged sequence bytes (host entry points)
+  SLOT_OFFS,        // staged offsets
+  SLOT_EVENTS,      // run boundary events
+  SLOT_EVENTS_TMP,
+  SLOT_RUNS,        // run table
+  SLOT_REGIONS,     // region records
+  SLOT_REG_TMP,
+  SLOT_SCALARS,     // small counters
+  SLOT_SORT_TMP,    // hipcub temp storage
+  SLOT_COUNTS,      // count / visit histograms
+  SLOT_CHUNK_A,     // chunk summaries
+  SLOT_CHUNK_B,
+  SLOT_CHUNK_C,
+  SLOT_CHUNK_D,
+  SLOT_WORK_A,      // rescan work lists
+  SLOT_WORK_B,
+  SLOT_TABLE_TMP,
+  SLOT_COUNT
+};
+
+struct DevBuf {
+  void *ptr = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace ks
+
+struct ks_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int scan_algo = -1;
+  int num_cus = 256;
+  ks::DevBuf slots[ks::SLOT_COUNT];
+  // pinned host staging
+  void *pinned = nullptr;
+  size_t pinned_bytes = 0;
+  hipEvent_t ev[8] = {};
+};
+
+struct ks_table {
+  ks_ctx *ctx = nullptr;
+  int k = 0;
+  double thr = 0;
+  bool compressed = false;
+  int64_t distinct = 0;
+  double *d_vals = nullptr;     // full table s = w - thr (uncompressed), 4^k doubles
+  uint16_t *d_codes = nullptr;  // compressed: 4^k u16 codes
+  double *d_lut = nullptr;      // compressed: distinct s values
+};
+
+namespace ks {
+
+ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out);
+ks_status ensure_pinned(ks_ctx *ctx, size_t bytes, void **out);
+ks_status activate(ks_ctx *ctx);  // hipSetDevice
+
+// -------------------------------------------------------------- encoding
+__host__ __device__ __forceinline__ bool is_n(uint8_t c) { return (c | 0x20) == 'n'; }
+__host__ __device__ __forceinline__ uint32_t enc(uint8_t c) { return (c >> 1) & 3u; }
+
+// Run table produced by run segmentation: maximal N-free runs [a, b) inside
+// one sequence (SoA).
+struct Runs {
+  int64_t *a = nullptr;
+  int64_t *b = nullptr;
+  int32_t *seq = nullptr;
+  int64_t n = 0;
+};
+
+// Region record buffer written by scan kernels.
+struct RegionBuf {
+  int32_t *seq;
+  int64_t *beg;
+  int64_t *end;
+  double *score;
+  unsigned long long *count;  // device counter
+  int64_t cap;
+};
+
+// Launch wrappers (defined in the .hip files).
+ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs, float *ms);
+ks_status launch_count(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const Runs &runs, int k,
+                       int32_t *counts_dev, double *n_words);
+ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, const ks_table *t,
+                    int32_t min_width, double min_score, int32_t *visits_dev, ks_regions *out,
+                    ks_scan_stats *stats);
+
+// Host table builders (ks_tables.cpp).
+ks_status rank_table_host(const int32_t *counts, int k, double total, double *ranks);
+ks_status log2_table_host(const int32_t *counts, int k, double *w);
+ks_status pm1_table_host(const int32_t *counts, int k, double *w);
+
+}  // namespace ks

@@ -1,0 +1,132 @@
+"""Device-resident sequences and tables (the hot path with inputs in HBM).
+
+PyTorch is used only as the device allocator and stream provider: a genome is
+one ``torch.uint8`` CUDA tensor holding the concatenated sequences plus an
+int64 offsets array (host and device copies).  All compute goes through
+libkmerspans.so (ks_scan_dev / ks_count_dev / ks_table_create).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import DevSeqs, Regions, ScanStats, check, load, regions_to_numpy
+
+
+@dataclass
+class DeviceSeqs:
+    seq: torch.Tensor          # uint8 [total + pad] on cuda
+    offsets: np.ndarray        # int64 [nseq + 1] host
+    offsets_dev: torch.Tensor  # int64 [nseq + 1] on cuda
+
+    @property
+    def nseq(self) -> int:
+        return int(self.offsets.size - 1)
+
+    @property
+    def total(self) -> int:
+        return int(self.offsets[-1])
+
+    def struct(self) -> DevSeqs:
+        s = DevSeqs()
+        s.seq = self.seq.data_ptr()
+        s.offsets_host = self.offsets.ctypes.data
+        s.offsets_dev = self.offsets_dev.data_ptr()
+        s.nseq = self.nseq
+        return s
+
+    def host_seq(self, q: int) -> bytes:
+        a, b = int(self.offsets[q]), int(self.offsets[q + 1])
+        return self.seq[a:b].cpu().numpy().tobytes()
+
+    def subset(self, ids) -> "DeviceSeqs":
+        """A new DeviceSeqs holding the given sequences (device copy)."""
+        parts = [self.seq[int(self.offsets[q]):int(self.offsets[q + 1])] for q in ids]
+        lens = [int(self.offsets[q + 1] - self.offsets[q]) for q in ids]
+        return from_parts(parts, lens, self.seq.device)
+
+
+def _pad16(n: int) -> int:
+    return (n + 16 + 15) // 16 * 16
+
+
+def from_parts(parts, lens, device) -> DeviceSeqs:
+    offs = np.zeros(len(lens) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(np.asarray(lens, dtype=np.int64))
+    buf = torch.empty(_pad16(int(offs[-1])), dtype=torch.uint8, device=device)
+    buf[int(offs[-1]):] = ord("N")
+    for p, a, b in zip(parts, offs[:-1], offs[1:]):
+        if b > a:
+            buf[int(a):int(b)].copy_(p)
+    return DeviceSeqs(buf, offs, torch.from_numpy(offs).to(device))
+
+
+def from_host(seqs, device="cuda") -> DeviceSeqs:
+    """Upload a list of str/bytes sequences."""
+    bs = [s.encode("latin-1") if isinstance(s, str) else bytes(s) for s in seqs]
+    lens = [len(b) for b in bs]
+    parts = [torch.frombuffer(bytearray(b), dtype=torch.uint8) if b else torch.empty(0, dtype=torch.uint8)
+             for b in bs]
+    return from_parts(parts, lens, device)
+
+
+class DeviceTable:
+    """A score table s = w - thr on the device (ks_table)."""
+
+    def __init__(self, ctx: _lib.Context, w, k: int, thr: float = 0.0, compress: bool = True):
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        if w.size != 4 ** k:
+            raise _lib.KmerSpansError(f"kmer_w contains {w.size} elements but should have {4 ** k}")
+        self.k = k
+        self._h = C.c_void_p()
+        check(load().ks_table_create(ctx.handle, w.ctypes.data, k, float(thr), int(bool(compress)),
+                                     C.byref(self._h)))
+
+    @property
+    def compressed(self) -> bool:
+        return bool(load().ks_table_is_compressed(self._h))
+
+    @property
+    def distinct(self) -> int:
+        return int(load().ks_table_distinct(self._h))
+
+    def close(self):
+        if self._h:
+            load().ks_table_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def bind_torch_stream(ctx: _lib.Context) -> None:
+    """Run library work on torch's current stream (ordering with torch ops)."""
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+
+
+def scan(ctx: _lib.Context, ds: DeviceSeqs, k: int, table: DeviceTable, min_width: int, min_score: float,
+         visits: torch.Tensor | None = None):
+    """ks_scan_dev: returns (pos int32[3, R], score float64[2, R], stats dict)."""
+    st = ScanStats()
+    r = Regions()
+    s = ds.struct()
+    check(load().ks_scan_dev(ctx.handle, C.byref(s), int(k), table._h, int(min_width), float(min_score),
+                             C.c_void_p(visits.data_ptr()) if visits is not None else None, C.byref(r),
+                             C.byref(st)))
+    pos, score = regions_to_numpy(r)
+    return pos, score, st.as_dict()
+
+
+def count(ctx: _lib.Context, ds: DeviceSeqs, k: int, counts: torch.Tensor) -> float:
+    """ks_count_dev: accumulates into counts (int32[4^k] cuda); returns #words."""
+    n = C.c_double(0)
+    s = ds.struct()
+    check(load().ks_count_dev(ctx.handle, C.byref(s), int(k), C.c_void_p(counts.data_ptr()), C.byref(n)))
+    return n.value

@@ -1,0 +1,213 @@
+"""GPU parity: the HIP path (libkmerspans.so through the C ABI) against the
+CPU oracle and the reference's recorded outputs.  Bit-exact everywhere:
+region triples and order, FP64 scores (0 ulp), counts, visit histograms.
+Runs on an MI355X (pytest -m gpu); skipped where no HIP device exists."""
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _regions_from(pos, score):
+    return [(int(pos[0][i]), int(pos[1][i]), int(pos[2][i]), float(score[0][i])) for i in range(pos.shape[1])]
+
+
+def _assert_same_regions(a_pos, a_score, b_pos, b_score, what=""):
+    assert a_pos.shape == b_pos.shape, (what, a_pos.shape, b_pos.shape)
+    assert np.array_equal(a_pos, b_pos), what
+    # bitwise FP64 equality of the scores
+    assert np.array_equal(a_score.view(np.uint64), b_score.view(np.uint64)), what
+
+
+@pytest.fixture(scope="module")
+def K():
+    import kmer_spans_amd as K
+    return K
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from kmer_spans_amd import _lib
+    return _lib.context(0)
+
+
+# ------------------------------------------------------------- known answers
+
+def test_golden_through_gpu(K, golden):
+    for case in golden["kmer_counts"]:
+        r = K.kmer_counts(case["seq"], case["k"])
+        assert r["n"]["n"] == case["n"], case
+        if "counts" in case:
+            assert r["counts"].tolist() == case["counts"]
+    for case in golden["kmer_regions_r"]:
+        r = K.kmer_regions(case["seq"], case["k"], case["w"], case["min_width"], case["min_score"])
+        got = [[a, b, c, d] for a, b, c, d in _regions_from(r["pos"], r["score"])]
+        assert got == case["regions"], case
+        assert int(r["counts"].sum()) == case["visits_total"]
+    for case in golden["kmer_low_comp_regions"]:
+        r = K.kmer_low_comp_regions(case["seq"], case["k"], case["min_width"], case["min_score"], case["thr"])
+        assert r["w_rank"].tolist() == case["w_rank"] and r["n"].tolist() == case["n"]
+        assert r["pos"].shape[0] == len(case["regions"])
+
+
+def test_n_gap_property_gpu(K):
+    rng = random.Random(7)
+    seqs = ["".join(rng.choice("ACGT") for _ in range(100)) for _ in range(2)]
+    seqs.append("AG" * 50 + seqs[0] + seqs[1] + seqs[0])
+    c2 = K.kmer_counts(seqs, 2)["counts"]
+    c3 = K.kmer_counts([s + "N" * 36 + s for s in seqs], 2)["counts"]
+    assert np.array_equal(2 * c2, c3)
+
+
+# ----------------------------------------------------------- random corpus
+
+def _random_inputs(rng, kmax=5, lmax=200):
+    k = rng.randint(1, kmax)
+    seqs = []
+    for _ in range(rng.randint(1, 4)):
+        L = rng.randint(0, lmax)
+        alpha = rng.choice(["ACGT", "ACGTN", "ACGTNacgtn", "AC", "ACGTNNNN", "ACGTRY", "A"])
+        seqs.append("".join(rng.choice(alpha) for _ in range(L)))
+    kind = rng.random()
+    if kind < 0.4:
+        w = np.array([rng.randint(-3, 3) for _ in range(4 ** k)], dtype=float)
+    elif kind < 0.8:
+        w = np.array([rng.uniform(-2, 1.5) for _ in range(4 ** k)])
+    else:  # specials flow through the clamp (NaN -> 0, +-Inf)
+        w = np.array([rng.choice([1.0, -1.0, np.inf, -np.inf, np.nan, 0.0, 2.5]) for _ in range(4 ** k)])
+    return k, seqs, w, rng.randint(-1, 6), rng.choice([0.0, 1.0, 2.5, 5.0, -1.0])
+
+
+ALGOS = [0]  # scan algorithms exercised (0 lane-per-run, 1 chunked carry scan)
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_random_regions_vs_oracle(K, oracle, ctx, algo):
+    from kmer_spans_amd import _lib
+    dctx = _lib.load().ks_default_ctx()
+    _lib.check(_lib.load().ks_ctx_set_scan_algo(dctx, algo))
+    try:
+        rng = random.Random(11 + algo)
+        for _ in range(300):
+            k, seqs, w, mw, ms = _random_inputs(rng)
+            g = K.kmer_regions(seqs, k, w, mw, ms)
+            o = oracle.kmer_regions(seqs, k, w, mw, ms)
+            _assert_same_regions(g["pos"], g["score"], o["pos"], o["score"], (seqs, k, mw, ms))
+            assert np.array_equal(g["counts"], o["counts"])
+            assert g["n"] == o["n"]
+    finally:
+        _lib.check(_lib.load().ks_ctx_set_scan_algo(dctx, -1))
+
+
+def test_random_counts_vs_oracle(K, oracle):
+    rng = random.Random(5)
+    for _ in range(200):
+        k = rng.randint(1, 9)
+        seqs = ["".join(rng.choice(rng.choice(["ACGT", "ACGTNacgtn", "NNNNA"])) for _ in range(rng.randint(0, 300)))
+                for _ in range(rng.randint(1, 4))]
+        g = K.kmer_counts(seqs, k)
+        n, c = oracle.kmer_counts(seqs, k)
+        assert g["n"]["n"] == n and np.array_equal(g["counts"], c), (seqs, k)
+
+
+def test_random_low_comp_vs_oracle(K, oracle):
+    rng = random.Random(9)
+    for _ in range(120):
+        k = rng.randint(1, 6)
+        seqs = ["".join(rng.choice("ACGTN" if rng.random() < 0.3 else "ACGT") for _ in range(rng.randint(0, 400)))
+                for _ in range(rng.randint(1, 3))]
+        thr = rng.choice([0.5, 0.75, 0.9])
+        mw, ms = rng.randint(0, 20), rng.choice([0.0, 2.0, 5.0])
+        g = K.kmer_low_comp_regions(seqs, k, mw, ms, thr)
+        o = oracle.low_comp_regions(seqs, k, mw, ms, thr)
+        assert np.array_equal(g["counts"], o["counts"])
+        assert np.array_equal(g["w_rank"].view(np.uint64), o["w_rank"].view(np.uint64))
+        assert np.array_equal(g["n"], o["n"])
+        _assert_same_regions(g["pos"].T, g["score"].T, o["pos"], o["score"], (seqs, k, thr))
+
+
+# ---------------------------------------------------- configuration shapes
+
+def test_config1_uniform_pm1_k7(K, oracle):
+    """Config 1: 1 Mbp uniform xorshift64 (seed 1), k=7, +-1 from its own
+    counts, min_width 100, min_score 20."""
+    from kmer_spans_amd import genome
+    s = genome.uniform_xorshift(1_000_000, 1)
+    c = K.kmer_counts(s, 7)
+    n, oc = oracle.kmer_counts(s, 7)
+    assert np.array_equal(c["counts"], oc) and c["n"]["n"] == n
+    w = K.pm1_table(c["counts"], 7)
+    assert np.array_equal(w, oracle.pm1_table(oc, 7))
+    g = K.kmer_regions(s, 7, w, 100, 20)
+    o = oracle.kmer_regions(s, 7, w, 100, 20)
+    _assert_same_regions(g["pos"], g["score"], o["pos"], o["score"], "config1")
+    assert np.array_equal(g["counts"], o["counts"])
+
+
+@pytest.mark.parametrize("k,score", [(9, "log2"), (11, "log2"), (9, "pm1"), (8, "rank")])
+def test_human_like_device_path(K, oracle, ctx, k, score):
+    """Scaled config-3 genome (~6 Mbp, repeats + N gaps), device-resident
+    entry points, both scan algorithms, against the oracle."""
+    import torch
+    from kmer_spans_amd import device as D, genome
+    parts, lens = genome.human_like(scale=0.002, seed=3, device="cuda")
+    ds = D.from_parts(parts, lens, "cuda")
+    D.bind_torch_stream(ctx)
+    counts = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+    words = D.count(ctx, ds, k, counts)
+    host = [ds.host_seq(q) for q in range(ds.nseq)]
+    n, oc = oracle.kmer_counts(host, k)
+    assert words == n and np.array_equal(counts.cpu().numpy(), oc)
+    thr = 0.0
+    if score == "log2":
+        w = K.log2_table(oc, k)
+    elif score == "pm1":
+        w = K.pm1_table(oc, k)
+    else:
+        w, thr = K.rank_table(oc, k, n), 0.75
+    tab = D.DeviceTable(ctx, w, k, thr, compress=True)
+    o = oracle.scan(host, k, w, thr, 100, 20.0, visits=True)
+    for algo in ALGOS:
+        ctx.set_scan_algo(algo)
+        vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+        pos, sc, st = D.scan(ctx, ds, k, tab, 100, 20.0, vis)
+        _assert_same_regions(pos, sc, o["pos"], o["score"], (k, score, algo))
+        assert np.array_equal(vis.cpu().numpy(), o["counts"]), (k, score, algo)
+    ctx.set_scan_algo(-1)
+    D.bind_torch_stream(ctx)
+
+
+def test_edge_inputs(K, oracle):
+    w = np.array([1.0, -1.0, -3.0, 2.0])
+    cases = [[""], ["N" * 50], ["A"], ["ACGT" * 3, "", "NNN", "G"], ["n" * 3 + "acgt" + "N"],
+             ["A" * 5000], ["AC" * 3000 + "N" + "GT" * 3000]]
+    for seqs in cases:
+        for k in (1, 2, 3):
+            ww = np.resize(w, 4 ** k)
+            g = K.kmer_regions(seqs, k, ww, 0, 0.0)
+            o = oracle.kmer_regions(seqs, k, ww, 0, 0.0)
+            _assert_same_regions(g["pos"], g["score"], o["pos"], o["score"], (seqs, k))
+            assert np.array_equal(g["counts"], o["counts"])
+            gc = K.kmer_counts(seqs, k)
+            n, c = oracle.kmer_counts(seqs, k)
+            assert gc["n"]["n"] == n and np.array_equal(gc["counts"], c)
+
+
+def test_compressed_table_matches_full(K, ctx):
+    import torch
+    from kmer_spans_amd import device as D
+    rng = np.random.default_rng(4)
+    k = 10
+    vals = rng.normal(size=300)
+    w = vals[rng.integers(0, 300, 4 ** k)]
+    seq = "".join(rng.choice(list("ACGT"), 200000))
+    ds = D.from_host([seq, seq[:5000]], "cuda")
+    D.bind_torch_stream(ctx)
+    t1 = D.DeviceTable(ctx, w, k, 0.1, compress=True)
+    t2 = D.DeviceTable(ctx, w, k, 0.1, compress=False)
+    assert t1.compressed and not t2.compressed and t1.distinct == len(np.unique(w))
+    p1, s1, _ = D.scan(ctx, ds, k, t1, 5, 1.0)
+    p2, s2, _ = D.scan(ctx, ds, k, t2, 5, 1.0)
+    _assert_same_regions(p1, s1, p2, s2, "compressed vs full")

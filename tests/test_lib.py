@@ -23,11 +23,14 @@ def test_exports_match_header():
     assert b"gfx950" in L.ks_version()
 
 
-def test_library_is_gfx950():
+def test_library_is_gfx950(tmp_path):
+    import shutil
     import subprocess
     from kmer_spans_amd import _lib
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _lib.LIB_PATH],
-                         capture_output=True, text=True)
+    lib = tmp_path / "lib.so"  # objdump --offloading extracts bundles next to its input
+    shutil.copy(_lib.LIB_PATH, lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
+                         capture_output=True, text=True, cwd=tmp_path)
     if out.returncode != 0:
         pytest.skip("llvm-objdump --offloading unavailable")
     assert "gfx950" in out.stdout + out.stderr

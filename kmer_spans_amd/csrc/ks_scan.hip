@@ -23,6 +23,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
 
 namespace {
 
+// Values of a batch of kBatch consecutive scan indices are gathered before
+// the sequential state machine consumes them, so a lane keeps kBatch random
+// table reads in flight instead of one (the gathers do not depend on S).
+constexpr int kBatch = 16;
+
 __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ seq,
                                                   const int64_t *__restrict__ ra,
                                                   const int64_t *__restrict__ rbnd,
@@ -37,28 +42,46 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
   const uint32_t mask = (1u << (2 * k)) - 1u;
   int64_t i = a;  // priming point
   for (;;) {
-    uint32_t code = prime_code(seq, i, k);
+    uint32_t code = prime_code(seq, i, k);  // k-mer scored at index i + k
     double S = 0.0, prev = 0.0, best = 0.0;
     int64_t beg = 0, arg = 0;
     bool restart = false;
-    for (int64_t p = i + k; p < b; ++p) {
-      if (visits) atomicAdd(&visits[code], 1u);
-      const double t = prev + tv_get(tv, code);
-      S = t > 0 ? t : 0.0;
-      if (prev == 0 && S > 0) { beg = p; arg = p; best = S; }
-      if (S == 0 && prev > 0) {
-        if ((uint64_t)(arg - beg) >= mw && best >= min_score) {
-          push_region(out, sid, beg, arg, best);
-          i = arg + 1 - k;
-          restart = true;
-          break;
-        }
-        best = 0.0;
-        arg = p;
+    for (int64_t p0 = i + k; p0 < b && !restart; p0 += kBatch) {
+      const int n = (int)((b - p0) < kBatch ? (b - p0) : kBatch);
+      double v[kBatch];
+      uint32_t c[kBatch];
+      uint32_t cc = code;
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        c[j] = cc;
+        if (j < n) v[j] = tv_get(tv, cc);
+        if (j < n) cc = ((cc << 2) | enc(seq[p0 + j])) & mask;
       }
-      if (S > best) { best = S; arg = p; }
-      prev = S;
-      code = ((code << 2) | enc(seq[p])) & mask;
+      code = cc;
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {  // fully unrolled: v[]/c[] stay in registers
+        if (j < n && !restart) {
+          const int64_t p = p0 + j;
+          if (visits) atomicAdd(&visits[c[j]], 1u);
+          const double t = prev + v[j];
+          S = t > 0 ? t : 0.0;
+          if (prev == 0 && S > 0) { beg = p; arg = p; best = S; }
+          if (S == 0 && prev > 0) {
+            if ((uint64_t)(arg - beg) >= mw && best >= min_score) {
+              push_region(out, sid, beg, arg, best);
+              i = arg + 1 - k;
+              restart = true;
+            } else {
+              best = 0.0;
+              arg = p;
+            }
+          }
+          if (!restart) {
+            if (S > best) { best = S; arg = p; }
+            prev = S;
+          }
+        }
+      }
     }
     if (restart) continue;
     if (S > 0 && (uint64_t)(arg - beg) >= mw && best >= min_score) {
@@ -106,7 +129,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
   TableView tv{t->d_vals, t->d_codes, t->d_lut, t->compressed ? 1 : 0};
   const uint64_t mw = (uint64_t)(int64_t)min_width;
   int algo = ctx->scan_algo;
-  if (algo < 0) algo = (longest > (1 << 16)) ? 1 : 0;
+  if (algo < 0) algo = 0;  // chunked scan: opt-in until it lands
   S->scan_algo = algo;
 
   int64_t cap = std::max<int64_t>(4096, (int64_t)(ctx->slots[SLOT_REGIONS].bytes / 28));

@@ -1,0 +1,99 @@
+"""Multi-GPU: one process per GPU, contigs sharded, span records gathered.
+
+N-free runs (hence contigs) are independent (restarts never leave a run,
+kmer_spans.c:281,303), so the scan shards with no exchange on the data path.
+The only collectives are after the scan:
+  * span-record gather to rank 0 (all_gather of per-rank counts, then
+    all_gather of the padded records; payload = 32 B/region) -- RCCL over
+    xGMI with the "nccl" backend, gloo in the CPU tests;
+  * an int32 sum of per-rank histograms when one genome's counts or visits
+    are split across ranks (exact, order-independent).
+Contigs are assigned by LPT (longest processing time first) on length.
+"""
+from __future__ import annotations
+
+import heapq
+
+import numpy as np
+import torch
+import torch.distributed as tdist
+
+
+def lpt_shards(lengths, n: int):
+    """Greedy LPT: contig ids per shard, each shard's ids in ascending order."""
+    heap = [(0, s) for s in range(n)]
+    heapq.heapify(heap)
+    shards = [[] for _ in range(n)]
+    for q in sorted(range(len(lengths)), key=lambda i: (-int(lengths[i]), i)):
+        load, s = heapq.heappop(heap)
+        shards[s].append(q)
+        heapq.heappush(heap, (load + int(lengths[q]), s))
+    return [sorted(x) for x in shards]
+
+
+def _pack(pos: np.ndarray, score: np.ndarray) -> np.ndarray:
+    rec = np.zeros((pos.shape[1], 4), dtype=np.int64)
+    if pos.shape[1]:
+        rec[:, 0:3] = pos.T
+        rec[:, 3] = np.ascontiguousarray(score[0]).view(np.int64)
+    return rec
+
+
+def _unpack(rec: np.ndarray):
+    pos = np.ascontiguousarray(rec[:, 0:3].T.astype(np.int32))
+    score = np.zeros((2, rec.shape[0]), dtype=np.float64)
+    score[0] = np.ascontiguousarray(rec[:, 3]).view(np.float64)
+    return pos, score
+
+
+def gather_regions(pos: np.ndarray, score: np.ndarray, device=None):
+    """Gather every rank's (pos[3,n], score[2,n]) to rank 0.
+
+    Returns (list of pos, list of score) indexed by rank on rank 0 and
+    ([], []) elsewhere.  Uses the process group's backend: CUDA tensors for
+    nccl (RCCL), CPU tensors for gloo."""
+    world, rank = tdist.get_world_size(), tdist.get_rank()
+    dev = device if tdist.get_backend() == "nccl" else torch.device("cpu")
+    n = torch.tensor([pos.shape[1]], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    tdist.all_gather(ns, n)
+    ns = [int(x.item()) for x in ns]
+    m = max(max(ns), 1)
+    rec = np.zeros((m, 4), dtype=np.int64)
+    rec[:pos.shape[1]] = _pack(pos, score)
+    t = torch.from_numpy(rec).to(dev)
+    outs = [torch.zeros_like(t) for _ in range(world)]
+    tdist.all_gather(outs, t)
+    if rank != 0:
+        return [], []
+    P, S = [], []
+    for r in range(world):
+        p, s = _unpack(outs[r][:ns[r]].cpu().numpy())
+        P.append(p)
+        S.append(s)
+    return P, S
+
+
+def merge_shards(shard_ids, pos_list, score_list):
+    """Map shard-local seq ids back to global contig ids and order the union
+    by (seq_id, beg) -- the reference's emission order."""
+    if not pos_list:
+        return np.zeros((3, 0), np.int32), np.zeros((2, 0), np.float64)
+    ps, ss = [], []
+    for ids, p, s in zip(shard_ids, pos_list, score_list):
+        p = p.copy()
+        if p.shape[1]:
+            p[0] = np.asarray(ids, dtype=np.int32)[p[0]]
+        ps.append(p)
+        ss.append(s)
+    pos = np.concatenate(ps, axis=1)
+    score = np.concatenate(ss, axis=1)
+    order = np.lexsort((pos[1], pos[0]))
+    return pos[:, order], score[:, order]
+
+
+def allreduce_histogram(h: torch.Tensor) -> torch.Tensor:
+    """Exact int32 sum of per-rank count/visit histograms (wraps mod 2^32
+    like the reference's int counters)."""
+    tdist.all_reduce(h, op=tdist.ReduceOp.SUM)
+    return h

@@ -93,7 +93,22 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
   }
 }
 
+__global__ void k_add_hist(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] += src[i];
+}
+
 }  // namespace
+
+ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, const int64_t *ra, const int64_t *rb,
+                           const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
+                           double min_score, uint32_t *visits, const RegionBuf &out) {
+  if (n <= 0) return KS_OK;
+  hipLaunchKernelGGL(k_scan_lane, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, ra, rb, rs, n, k,
+                     tv, mw, min_score, visits, out);
+  KS_HIP(hipGetLastError());
+  return KS_OK;
+}
 
 ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, const ks_table *t,
                     int32_t min_width, double min_score, int32_t *visits_dev, ks_regions *out,
@@ -129,7 +144,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
   TableView tv{t->d_vals, t->d_codes, t->d_lut, t->compressed ? 1 : 0};
   const uint64_t mw = (uint64_t)(int64_t)min_width;
   int algo = ctx->scan_algo;
-  if (algo < 0) algo = 0;  // chunked scan: opt-in until it lands
+  if (algo < 0) algo = (longest > (1 << 15)) ? 1 : 0;
   S->scan_algo = algo;
 
   int64_t cap = std::max<int64_t>(4096, (int64_t)(ctx->slots[SLOT_REGIONS].bytes / 28));
@@ -150,14 +165,36 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     rb.cap = cap;
     KS_HIP(hipMemsetAsync(d_rcount, 0, 8, st));
     KS_HIP(hipEventRecord(ctx->ev[3], st));
-    if (algo == 0) {
-      if (runs.n) {
-        hipLaunchKernelGGL(k_scan_lane, dim3((unsigned)((runs.n + 63) / 64)), dim3(64), 0, st, s->seq,
-                           runs.a, runs.b, runs.seq, runs.n, k, tv, mw, min_score, vis, rb);
-        KS_HIP(hipGetLastError());
+    if (algo == 1) {
+      // visits of the chunked path go to a scratch histogram first, so that a
+      // fallback to the lane kernel cannot count them twice
+      uint32_t *vscr = nullptr;
+      const size_t nb = (size_t)4 << (2 * k);
+      if (vis) {
+        void *vp = nullptr;
+        KS_TRY(ensure(ctx, SLOT_TABLE_TMP, nb, &vp));
+        vscr = static_cast<uint32_t *>(vp);
+        KS_HIP(hipMemsetAsync(vscr, 0, nb, st));
       }
-    } else {
-      KS_TRY(scan_chunked(ctx, s, runs, k, tv, mw, min_score, vis, rb, S));
+      ks_status rc = scan_chunked(ctx, s, runs, k, tv, mw, min_score, vscr, rb, S);
+      if (rc == KS_OK) {
+        if (vis) {
+          const int64_t n = (int64_t)1 << (2 * k);
+          hipLaunchKernelGGL(k_add_hist, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, st,
+                             vis, vscr, n);
+          KS_HIP(hipGetLastError());
+        }
+      } else if (rc == KS_ERR_INTERNAL) {
+        fprintf(stderr, "kmer_spans_amd: chunked scan fell back to the lane kernel: %s\n", ks_last_error());
+        algo = 0;
+        S->scan_algo = 0;
+        KS_HIP(hipMemsetAsync(d_rcount, 0, 8, st));
+      } else {
+        return rc;
+      }
+    }
+    if (algo == 0) {
+      if (runs.n) KS_TRY(launch_scan_lane(ctx, s->seq, runs.a, runs.b, runs.seq, runs.n, k, tv, mw, min_score, vis, rb));
     }
     KS_HIP(hipEventRecord(ctx->ev[4], st));
     KS_HIP(hipMemcpyAsync(&n_reg, d_rcount, 8, hipMemcpyDeviceToHost, st));

@@ -1,10 +1,818 @@
-// ks_scan_chunked.hip -- chunked carry scan (algo 1).  Placeholder until the
-// chunked implementation lands; dispatch never selects it automatically yet.
+// ks_scan_chunked.hip -- chunked carry scan (algo 1): the span scan with
+// parallelism inside runs, bit-exact with the sequential reference.
+//
+// The sequential state machine of kmer_regions (kmer_spans.c:243-307) is
+// decomposed (SURVEY 8(a) a5', verified by oracle/pyoracle.py):
+//   T_i = max(fl(T_{i-1} + s_i), 0) over each run's scan indices [a+k, b-1];
+//   excursions = maximal stretches with T > 0 (beg, first argmax, max, end);
+//   an emitted excursion adds a region and a fresh rescan of (argmax, end].
+// Every run is cut into chunks of CH = 256 scan indices, one lane each.
+//
+//  P1 (gather pass, the only random-access pass): codes -> table values;
+//     clean-entry trajectory C_j (entry 0) of every chunk: exit value, the
+//     open trailing excursion, closed emittable excursions ("candidates");
+//     approximate aggregates (sum, min/max prefix); compressed tables also
+//     store each index's uint16 table code so later passes stream 2 B/index.
+//  P2 approximate max-plus scan of (sum, clean exit) per run -> predicted
+//     entry x~_j; where x~_j puts the whole chunk inside one binade
+//     [2^e, 2^(e+1)) far from 0, the chunk's binade-integer summary is built:
+//     with S = m * 2^(e-52), fl(S + s) = S + RN(s / 2^(e-52)) exactly, ties to
+//     even decided by the parity of m, so a chunk is an integer map
+//     m -> m + D[parity(m)] with max/argmax/min per entry parity.
+//  P3 exact carry per run (sequential over chunks, O(1) per chunk):
+//     entry 0 -> exit C_j exactly;  summary valid for the exact entry ->
+//     integer arithmetic;  x + minprefix < -margin -> the true trajectory
+//     clamps in the chunk and then coincides with C_j (monotone rounding),
+//     so the exit is C_j exactly;  otherwise exact replay of the chunk.
+//  P4 heads: per chunk with positive exact entry, the part of the carried
+//     excursion before its first clamp (replay, or the summary).
+//  P5 stitch per run: excursions from heads, tails and candidates; emit
+//     regions + rescan ranges; rescans run on the lane kernel.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <vector>
+
 #include "ks_scan_common.h"
 
 namespace ks {
-ks_status scan_chunked(ks_ctx *, const ks_dev_seqs *, const Runs &, int, const TableView &, uint64_t,
-                       double, uint32_t *, const RegionBuf &, ks_scan_stats *) {
-  return fail(KS_ERR_INTERNAL, "chunked scan not available in this build");
+
+ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, const int64_t *ra, const int64_t *rb,
+                           const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
+                           double min_score, uint32_t *visits, const RegionBuf &out);
+
+namespace {
+
+constexpr int CH = 256;  // scan indices per chunk (one lane)
+constexpr int NB = 16;   // indices per gather batch
+constexpr int kModeClean = 0, kModeL = 1, kModeR = 2, kModeU = 3;
+
+struct Chunks {
+  int64_t *start;  // first scan index (global position)
+  int32_t *n;      // indices in the chunk
+  int32_t *run;    // run id
+  int64_t nch;
+};
+
+struct P1 {  // per-chunk results of the gather pass
+  double *cexit, *asum, *pmin, *pmax, *sabs, *tmax;
+  int32_t *tbeg, *targ;  // trailing open excursion (relative), tbeg = -1: none
+  uint8_t *special;      // a non-finite value occurred
+};
+
+struct Summ {  // binade-integer summaries (P2)
+  int32_t *e;  // binade exponent, INT32_MIN: no summary
+  long long *D, *M, *N;  // [2 * nch] (entry parity 0/1)
+  int32_t *A;            // [2 * nch]
+};
+
+struct Carry {  // P3/P4
+  double *x;      // exact entry value
+  uint8_t *mode;
+  int32_t *hq;    // first clamp in the chunk (relative), -1 none
+  double *hmax;   // max of the carried head (valid if the head is non-empty)
+  int32_t *harg;
+};
+
+struct Cand {  // closed emittable excursions of the clean trajectories
+  long long *beg, *arg, *rst;
+  double *best;
+  unsigned long long *count;
+  int64_t cap;
+};
+
+struct Rescan {
+  int64_t *a, *b;  // virtual runs [a, b) for the lane kernel
+  int32_t *seq;
+  unsigned long long *count;
+  int64_t cap;
+};
+
+__device__ __forceinline__ uint32_t roll(uint32_t c, uint8_t b, uint32_t mask) {
+  return ((c << 2) | enc(b)) & mask;
 }
+
+// 16 bytes at an arbitrary position (two aligned 16-byte loads).
+__device__ __forceinline__ void load16(const uint8_t *__restrict__ seq, int64_t p, int64_t total,
+                                       uint8_t out[16]) {
+  const int64_t a0 = p & ~(int64_t)15;
+  const int sh = (int)(p - a0);
+  uint32_t w[8];
+  const uint4 v0 = *reinterpret_cast<const uint4 *>(seq + a0);
+  uint4 v1 = make_uint4(0x4e4e4e4eu, 0x4e4e4e4eu, 0x4e4e4e4eu, 0x4e4e4e4eu);
+  if (a0 + 16 < total) v1 = *reinterpret_cast<const uint4 *>(seq + a0 + 16);
+  w[0] = v0.x; w[1] = v0.y; w[2] = v0.z; w[3] = v0.w; w[4] = v1.x; w[5] = v1.y; w[6] = v1.z; w[7] = v1.w;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int q = sh + j;
+    out[j] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+  }
+}
+
+__device__ __forceinline__ size_t code_slot(int64_t c, int i) {
+  // [tile = c/64][i/8][lane = c%64][i%8]: a wave's lanes store 16 B each, contiguous
+  return ((((size_t)(c >> 6) * (CH / 8) + (size_t)(i >> 3)) * 64 + (size_t)(c & 63)) << 3) + (size_t)(i & 7);
+}
+
+// Value of scan index i of chunk c, computed from scratch (rare paths).
+__device__ __forceinline__ double value_at(const Chunks &g, const uint8_t *__restrict__ seq, int k,
+                                           const TableView &tv, const uint16_t *__restrict__ codes,
+                                           int64_t c, int i) {
+  if (codes) return tv.lut[codes[code_slot(c, i)]];
+  const int64_t p = g.start[c] + i;
+  return tv_get(tv, prime_code(seq, p - k, k));
+}
+
+// ------------------------------------------------------------------- P0
+
+__global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__restrict__ rb,
+                              const int64_t *__restrict__ cbase, int64_t nruns, int k, Chunks g) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nruns) return;
+  const int64_t lo = ra[r] + k, hi = rb[r] - 1;
+  if (hi < lo) return;
+  int64_t c = cbase[r];
+  for (int64_t p = lo; p <= hi; p += CH, ++c) {
+    g.start[c] = p;
+    g.n[c] = (int32_t)min((int64_t)CH, hi - p + 1);
+    g.run[c] = (int32_t)r;
+  }
+}
+
+// ------------------------------------------------------------------- P1
+
+template <bool kCompressed>
+__global__ void __launch_bounds__(256) k_pass1(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
+                                               int k, TableView tv, uint16_t *__restrict__ codes,
+                                               uint64_t mw, double min_score, uint32_t *__restrict__ visits,
+                                               P1 o, Cand cand) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= g.nch) return;
+  const uint32_t mask = (1u << (2 * k)) - 1u;
+  const int64_t start = g.start[c];
+  const int n = g.n[c];
+  uint32_t code = prime_code(seq, start - k, k);
+  double prev = 0.0, best = 0.0;
+  int beg = -1, arg = 0;
+  double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
+  bool special = false;
+  for (int b0 = 0; b0 < CH; b0 += NB) {
+    if (b0 >= n) break;
+    uint8_t by[16];
+    load16(seq, start + b0, total, by);
+    uint32_t cc[NB];
+    double v[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      cc[j] = code;
+      code = roll(code, by[j], mask);
+    }
+    if (kCompressed) {
+      uint16_t q[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) q[j] = (b0 + j < n) ? tv.codes[cc[j]] : (uint16_t)0;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v[j] = tv.lut[q[j]];
+      uint4 w0, w1;
+      w0.x = q[0] | ((uint32_t)q[1] << 16); w0.y = q[2] | ((uint32_t)q[3] << 16);
+      w0.z = q[4] | ((uint32_t)q[5] << 16); w0.w = q[6] | ((uint32_t)q[7] << 16);
+      w1.x = q[8] | ((uint32_t)q[9] << 16); w1.y = q[10] | ((uint32_t)q[11] << 16);
+      w1.z = q[12] | ((uint32_t)q[13] << 16); w1.w = q[14] | ((uint32_t)q[15] << 16);
+      *reinterpret_cast<uint4 *>(codes + code_slot(c, b0)) = w0;
+      *reinterpret_cast<uint4 *>(codes + code_slot(c, b0 + 8)) = w1;
+    } else {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v[j] = (b0 + j < n) ? tv.vals[cc[j]] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int i = b0 + j;
+      if (i < n) {
+        if (visits) atomicAdd(&visits[cc[j]], 1u);
+        const double s = v[j];
+        asum += s;
+        pmin = fmin(pmin, asum);
+        pmax = fmax(pmax, asum);
+        sabs += fabs(s);
+        special |= !isfinite(s);
+        const double t = prev + s;
+        const double S = t > 0 ? t : 0.0;
+        if (prev == 0 && S > 0) {
+          beg = i; arg = i; best = S;
+        } else if (prev > 0 && S == 0) {
+          if ((uint64_t)(arg - beg) >= mw && best >= min_score) {
+            const unsigned long long slot = atomicAdd(cand.count, 1ull);
+            if ((int64_t)slot < cand.cap) {
+              cand.beg[slot] = start + beg;
+              cand.arg[slot] = start + arg;
+              cand.rst[slot] = start + i;
+              cand.best[slot] = best;
+            }
+          }
+          beg = -1;
+        } else if (S > best) {
+          best = S; arg = i;
+        }
+        prev = S;
+      }
+    }
+  }
+  o.cexit[c] = prev;
+  o.asum[c] = asum;
+  o.pmin[c] = pmin;
+  o.pmax[c] = pmax;
+  o.sabs[c] = sabs;
+  o.special[c] = special ? 1 : 0;
+  if (prev > 0) {
+    o.tbeg[c] = beg; o.tmax[c] = best; o.targ[c] = arg;
+  } else {
+    o.tbeg[c] = -1; o.tmax[c] = 0.0; o.targ[c] = 0;
+  }
+}
+
+// ------------------------------------------------------------------- P2
+
+// Approximate max-plus scan, one wave per run: chunk j maps x -> max(x + a, b)
+// (a = sum, b = clean exit); x~_j = composite of chunks < j applied to 0.
+__global__ void __launch_bounds__(64) k_approx_scan(const int64_t *__restrict__ cbase, int64_t nruns,
+                                                    P1 o, double *__restrict__ xt) {
+  const int64_t r = blockIdx.x;
+  if (r >= nruns) return;
+  const int lane = threadIdx.x;
+  const int64_t c0 = cbase[r], c1 = cbase[r + 1];
+  double carry = 0.0;
+  for (int64_t cb = c0; cb < c1; cb += 64) {
+    const int64_t c = cb + lane;
+    double a = 0.0, b = -INFINITY;  // identity
+    if (c < c1) {
+      a = o.special[c] ? -INFINITY : o.asum[c];
+      b = o.cexit[c];
+    }
+    // inclusive scan: (a1,b1) then (a2,b2) = (a1 + a2, max(b1 + a2, b2))
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const double pa = __shfl_up(a, d, 64), pb = __shfl_up(b, d, 64);
+      if (lane >= d) {
+        b = fmax(pb + a, b);
+        a = pa + a;
+      }
+    }
+    double ea = __shfl_up(a, 1, 64), eb = __shfl_up(b, 1, 64);
+    if (lane == 0) { ea = 0.0; eb = -INFINITY; }
+    if (c < c1) xt[c] = fmax(carry + ea, eb);
+    const double la = __shfl(a, 63, 64), lb = __shfl(b, 63, 64);
+    carry = fmax(carry + la, lb);
+    if (!(carry == carry)) carry = 0.0;  // NaN guard: only a prediction
+  }
+}
+
+// Binade-integer summary of the chunk for the binade its predicted
+// trajectory lies in (lane per chunk).
+template <bool kCompressed>
+__global__ void __launch_bounds__(256) k_summaries(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
+                                                   int k, TableView tv, const uint16_t *__restrict__ codes,
+                                                   P1 o, const double *__restrict__ xt, Summ sm) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= g.nch) return;
+  sm.e[c] = INT32_MIN;
+  if (o.special[c]) return;
+  const double x = xt[c];
+  if (!(x >= 4096.0) || !(x < 1e18)) return;
+  int E;
+  frexp(x, &E);
+  const int e = E - 1;  // x in [2^e, 2^(e+1))
+  const double lo = fmin(x, x + o.pmin[c]), hi = fmax(x, x + o.pmax[c]);
+  const double slack = ldexp(1.0, e - 30) + o.sabs[c] * 1e-9;
+  if (!(lo - slack >= ldexp(1.0, e)) || !(hi + slack < ldexp(1.0, e + 1))) return;
+  const int n = g.n[c];
+  const int64_t start = g.start[c];
+  const uint32_t mask = (1u << (2 * k)) - 1u;
+  uint32_t code = kCompressed ? 0u : prime_code(seq, start - k, k);
+  long long cur[2] = {0, 0}, M[2] = {LLONG_MIN, LLONG_MIN}, N[2] = {LLONG_MAX, LLONG_MAX};
+  int A[2] = {0, 0};
+  for (int b0 = 0; b0 < n; b0 += NB) {
+    double v[NB];
+    if (kCompressed) {
+      const uint4 w0 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0));
+      const uint4 w1 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0 + 8));
+      const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v[j] = tv.lut[(w[j >> 1] >> (16 * (j & 1))) & 0xffffu];
+    } else {
+      uint8_t by[16];
+      load16(seq, start + b0, total, by);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        v[j] = (b0 + j < n) ? tv.vals[code] : 0.0;
+        code = roll(code, by[j], mask);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int i = b0 + j;
+      if (i < n) {
+        const double y = ldexp(v[j], 52 - e);  // exact (power-of-two scaling)
+        const double fq = floor(y);
+        const double f = y - fq;               // exact fractional part
+        const long long q = (long long)fq;
+        const bool up = f > 0.5;
+        const bool tie = f == 0.5;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const long long par = (t + cur[t]) & 1;            // parity of the current m
+          const long long d = q + ((up || (tie && ((par + q) & 1))) ? 1 : 0);
+          cur[t] += d;
+          if (cur[t] > M[t]) { M[t] = cur[t]; A[t] = i; }
+          N[t] = min(N[t], cur[t]);
+        }
+      }
+    }
+  }
+  sm.e[c] = e;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    sm.D[2 * c + t] = cur[t];
+    sm.M[2 * c + t] = M[t];
+    sm.N[2 * c + t] = N[t];
+    sm.A[2 * c + t] = A[t];
+  }
+}
+
+// ------------------------------------------------------------------- P3
+
+__device__ __forceinline__ bool summary_step(const Summ &sm, int64_t c, double x, long long *m0_out,
+                                             int *par_out) {
+  const int e = sm.e[c];
+  if (e == INT32_MIN) return false;
+  int E;
+  frexp(x, &E);
+  if (E - 1 != e) return false;
+  const long long m0 = (long long)ldexp(x, 52 - e);  // exact integer in [2^52, 2^53)
+  const int par = (int)(m0 & 1);
+  const long long lo = m0 + sm.N[2 * c + par], hi = m0 + sm.M[2 * c + par];
+  if (lo < (1LL << 52) + 1 || hi > (1LL << 53) - 2) return false;
+  *m0_out = m0;
+  *par_out = par;
+  return true;
+}
+
+// Exact carry, one wave per run.  The per-chunk inputs of 64 chunks are
+// staged in LDS by the whole wave (coalesced), then every lane walks the
+// chain redundantly (wave-uniform values; the lanes are needed together only
+// for the cooperative loads of a replayed chunk).
+template <bool kCompressed>
+__global__ void __launch_bounds__(64) k_carry(Chunks g, const int64_t *__restrict__ cbase, int64_t nruns,
+                                              const uint8_t *__restrict__ seq, int k, TableView tv,
+                                              const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
+                                              unsigned long long *__restrict__ nreplay) {
+  __shared__ double vals[CH];
+  __shared__ double b_cexit[64], b_pmin[64], b_sabs[64];
+  __shared__ long long b_D[2][64], b_N[2][64], b_M[2][64];
+  __shared__ int b_e[64], b_spec[64];
+  __shared__ double b_x[64];
+  __shared__ uint8_t b_mode[64];
+  const int64_t r = blockIdx.x;
+  if (r >= nruns) return;
+  const int lane = threadIdx.x;
+  const int64_t c0 = cbase[r], c1 = cbase[r + 1];
+  double x = 0.0;
+  unsigned long long replays = 0;
+  for (int64_t cb = c0; cb < c1; cb += 64) {
+    {
+      const int64_t c = cb + lane;
+      if (c < c1) {
+        b_cexit[lane] = o.cexit[c];
+        b_pmin[lane] = o.pmin[c];
+        b_sabs[lane] = o.sabs[c];
+        b_spec[lane] = o.special[c];
+        const int e = sm.e[c];
+        b_e[lane] = e;
+        if (e != INT32_MIN) {
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            b_D[t][lane] = sm.D[2 * c + t];
+            b_N[t][lane] = sm.N[2 * c + t];
+            b_M[t][lane] = sm.M[2 * c + t];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const int nb = (int)min((int64_t)64, c1 - cb);
+    for (int j = 0; j < nb; ++j) {
+      b_x[j] = x;
+      int mode;
+      bool done = false;
+      if (x == 0.0) {
+        mode = kModeClean;
+        x = b_cexit[j];
+        done = true;
+      }
+      if (!done && b_e[j] != INT32_MIN) {  // binade-integer summary
+        const int e = b_e[j];
+        int E;
+        frexp(x, &E);
+        if (E - 1 == e) {
+          const long long m0 = (long long)ldexp(x, 52 - e);
+          const int par = (int)(m0 & 1);
+          const long long lo = m0 + b_N[par][j], hi = m0 + b_M[par][j];
+          if (lo >= (1LL << 52) + 1 && hi <= (1LL << 53) - 2) {
+            mode = kModeL;
+            x = ldexp((double)(m0 + b_D[par][j]), e - 52);
+            done = true;
+          }
+        }
+      }
+      if (!done && !b_spec[j] && x + b_pmin[j] < -ldexp(fabs(x) + b_sabs[j], -40)) {
+        mode = kModeR;  // certain clamp -> coincides with the clean trajectory
+        x = b_cexit[j];
+        done = true;
+      }
+      if (!done) {  // exact replay of the chunk from x
+        mode = kModeU;
+        ++replays;
+        const int64_t c = cb + j;
+        const int n = g.n[c];
+        __syncthreads();
+        for (int i = lane; i < n; i += 64) vals[i] = value_at(g, seq, k, tv, kCompressed ? codes : nullptr, c, i);
+        __syncthreads();
+        double T = x;
+        bool clamped = false;
+        for (int i = 0; i < n; ++i) {
+          const double t = T + vals[i];
+          T = t > 0 ? t : 0.0;
+          if (T == 0.0) { clamped = true; break; }
+        }
+        x = clamped ? b_cexit[j] : T;
+      }
+      b_mode[j] = (uint8_t)mode;
+    }
+    __syncthreads();
+    {
+      const int64_t c = cb + lane;
+      if (c < c1) {
+        cr.x[c] = b_x[lane];
+        cr.mode[c] = b_mode[lane];
+      }
+    }
+    __syncthreads();
+  }
+  if (lane == 0 && replays) atomicAdd(nreplay, replays);
+}
+
+// ------------------------------------------------------------------- P4
+
+template <bool kCompressed>
+__global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
+                                               int k, TableView tv, const uint16_t *__restrict__ codes,
+                                               Summ sm, Carry cr, unsigned int *__restrict__ err) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= g.nch) return;
+  const int mode = cr.mode[c];
+  cr.hq[c] = -1;
+  cr.hmax[c] = -1.0;
+  cr.harg[c] = 0;
+  if (mode == kModeClean) return;
+  const double x = cr.x[c];
+  if (mode == kModeL) {
+    long long m0;
+    int par;
+    if (!summary_step(sm, c, x, &m0, &par)) { atomicOr(err, 1u); return; }
+    cr.hmax[c] = ldexp((double)(m0 + sm.M[2 * c + par]), sm.e[c] - 52);
+    cr.harg[c] = sm.A[2 * c + par];
+    return;
+  }
+  const int n = g.n[c];
+  const int64_t start = g.start[c];
+  const uint32_t mask = (1u << (2 * k)) - 1u;
+  uint32_t code = kCompressed ? 0u : prime_code(seq, start - k, k);
+  double T = x, hmax = -1.0;
+  int harg = 0, hq = -1;
+  for (int b0 = 0; b0 < n && hq < 0; b0 += NB) {
+    double v[NB];
+    if (kCompressed) {
+      const uint4 w0 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0));
+      const uint4 w1 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0 + 8));
+      const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v[j] = tv.lut[(w[j >> 1] >> (16 * (j & 1))) & 0xffffu];
+    } else {
+      uint8_t by[16];
+      load16(seq, start + b0, total, by);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        v[j] = (b0 + j < n) ? tv.vals[code] : 0.0;
+        code = roll(code, by[j], mask);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int i = b0 + j;
+      if (i < n && hq < 0) {
+        const double t = T + v[j];
+        T = t > 0 ? t : 0.0;
+        if (T == 0.0) hq = i;
+        else if (T > hmax) { hmax = T; harg = i; }
+      }
+    }
+  }
+  if (mode == kModeR && hq < 0) atomicOr(err, 2u);  // predicted clamp did not happen
+  cr.hq[c] = hq;
+  cr.hmax[c] = hmax;
+  cr.harg[c] = harg;
+}
+
+// ------------------------------------------------------------------- P5
+
+__device__ __forceinline__ void emit(const RegionBuf &rb, const Rescan &rs, int32_t sid, int k, int64_t beg,
+                                     int64_t arg, double best, int64_t end) {
+  push_region(rb, sid, beg, arg, best);
+  if (arg + 1 <= end) {
+    const unsigned long long slot = atomicAdd(rs.count, 1ull);
+    if ((int64_t)slot < rs.cap) {
+      rs.a[slot] = arg + 1 - k;  // virtual run: scan indices arg+1 .. end
+      rs.b[slot] = end + 1;
+      rs.seq[slot] = sid;
+    }
+  }
+}
+
+// Stitch, one wave per run: the wave stages 64 chunks' fragments in LDS,
+// lane 0 walks them in order (candidates in begin order), emitting regions
+// and rescan ranges.
+__global__ void __launch_bounds__(64) k_stitch(Chunks g, const int64_t *__restrict__ cbase, int64_t nruns,
+                                               const int64_t *__restrict__ rb_end, const int32_t *__restrict__ rseq,
+                                               int k, P1 o, Carry cr, Cand cand, int64_t ncand,
+                                               const int32_t *__restrict__ corder, uint64_t mw,
+                                               double min_score, RegionBuf out, Rescan rs,
+                                               unsigned int *__restrict__ err) {
+  __shared__ int64_t b_st[64];
+  __shared__ int32_t b_n[64], b_hq[64], b_harg[64], b_tbeg[64], b_targ[64];
+  __shared__ double b_hmax[64], b_tmax[64];
+  __shared__ uint8_t b_mode[64];
+  const int64_t r = blockIdx.x;
+  if (r >= nruns) return;
+  const int lane = threadIdx.x;
+  const int64_t c0 = cbase[r], c1 = cbase[r + 1];
+  if (c0 == c1) return;
+  const int32_t sid = rseq[r];
+  const int64_t last = rb_end[r] - 1;
+  int64_t cp = 0;
+  if (lane == 0) {  // first candidate of this run (candidates sorted by begin)
+    const int64_t first_pos = g.start[c0];
+    int64_t lo = 0, hi = ncand;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (cand.beg[corder[mid]] < first_pos) lo = mid + 1; else hi = mid;
+    }
+    cp = lo;
+  }
+  bool open = false, bad = false;
+  int64_t xb = 0, xa = 0;
+  double xm = 0.0;
+  for (int64_t cb = c0; cb < c1; cb += 64) {
+    const int64_t c = cb + lane;
+    if (c < c1) {
+      b_st[lane] = g.start[c];
+      b_n[lane] = g.n[c];
+      b_mode[lane] = cr.mode[c];
+      b_hq[lane] = cr.hq[c];
+      b_hmax[lane] = cr.hmax[c];
+      b_harg[lane] = cr.harg[c];
+      b_tbeg[lane] = o.tbeg[c];
+      b_tmax[lane] = o.tmax[c];
+      b_targ[lane] = o.targ[c];
+    }
+    __syncthreads();
+    if (lane == 0 && !bad) {
+      const int nb = (int)min((int64_t)64, c1 - cb);
+      for (int j = 0; j < nb && !bad; ++j) {
+        const int64_t st = b_st[j];
+        const int64_t en = st + b_n[j];
+        int64_t valid_from = st;  // candidates / tail must begin at or after this
+        bool tail_ok = true;
+        if (b_mode[j] != kModeClean) {
+          if (!open) { bad = true; atomicOr(err, 4u); break; }
+          const int hq = b_hq[j];
+          if (hq != 0 && b_hmax[j] > xm) { xm = b_hmax[j]; xa = st + b_harg[j]; }
+          if (hq >= 0) {
+            const int64_t rpos = st + hq;
+            if ((uint64_t)(xa - xb) >= mw && xm >= min_score) emit(out, rs, sid, k, xb, xa, xm, rpos);
+            open = false;
+            valid_from = rpos + 1;
+          } else {
+            valid_from = en;  // the carried excursion covers the whole chunk
+            tail_ok = false;
+          }
+        }
+        while (cp < ncand) {
+          const int32_t q = corder[cp];
+          const int64_t b = cand.beg[q];
+          if (b >= en) break;
+          if (b >= valid_from) emit(out, rs, sid, k, b, cand.arg[q], cand.best[q], cand.rst[q]);
+          ++cp;
+        }
+        if (tail_ok && b_tbeg[j] >= 0 && st + b_tbeg[j] >= valid_from) {
+          if (open) { bad = true; atomicOr(err, 8u); break; }
+          open = true;
+          xb = st + b_tbeg[j];
+          xa = st + b_targ[j];
+          xm = b_tmax[j];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (lane == 0 && !bad && open && (uint64_t)(xa - xb) >= mw && xm >= min_score)
+    emit(out, rs, sid, k, xb, xa, xm, last);
+}
+
+}  // namespace
+
+ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int k, const TableView &tv,
+                       uint64_t mw, double min_score, uint32_t *visits, const RegionBuf &rb,
+                       ks_scan_stats *stats) {
+  hipStream_t st = ctx->stream;
+  const int64_t total = s->offsets_host[s->nseq];
+  const int64_t nruns = runs.n;
+  if (nruns == 0) return KS_OK;
+  // chunk bases (host prefix over runs)
+  std::vector<int64_t> ha(nruns), hb(nruns), cb(nruns + 1, 0);
+  KS_HIP(hipMemcpyAsync(ha.data(), runs.a, nruns * 8, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipMemcpyAsync(hb.data(), runs.b, nruns * 8, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipStreamSynchronize(st));
+  for (int64_t r = 0; r < nruns; ++r) {
+    const int64_t P = hb[r] - ha[r] - k;
+    cb[r + 1] = cb[r] + (P > 0 ? (P + CH - 1) / CH : 0);
+  }
+  const int64_t nch = cb[nruns];
+  if (nch == 0) return KS_OK;
+  const bool comp = tv.compressed != 0;
+
+  // ---- workspace
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  size_t off = 0;
+  const size_t o_cbase = off; off += al((nruns + 1) * 8);
+  const size_t o_start = off; off += al(nch * 8);
+  const size_t o_n = off; off += al(nch * 4);
+  const size_t o_run = off; off += al(nch * 4);
+  const size_t o_p1d = off; off += al(nch * 8 * 6);
+  const size_t o_p1i = off; off += al(nch * 4 * 2);
+  const size_t o_spec = off; off += al(nch);
+  const size_t o_xt = off; off += al(nch * 8);
+  const size_t o_se = off; off += al(nch * 4);
+  const size_t o_sD = off; off += al(nch * 8 * 6);
+  const size_t o_sA = off; off += al(nch * 4 * 2);
+  const size_t o_x = off; off += al(nch * 8);
+  const size_t o_mode = off; off += al(nch);
+  const size_t o_hq = off; off += al(nch * 4 * 2);
+  const size_t o_hmax = off; off += al(nch * 8);
+  const size_t o_cnt = off; off += al(64);
+  void *wsp = nullptr;
+  KS_TRY(ensure(ctx, SLOT_CHUNK_A, off, &wsp));
+  char *W = static_cast<char *>(wsp);
+  int64_t *d_cbase = reinterpret_cast<int64_t *>(W + o_cbase);
+  Chunks g{reinterpret_cast<int64_t *>(W + o_start), reinterpret_cast<int32_t *>(W + o_n),
+           reinterpret_cast<int32_t *>(W + o_run), nch};
+  double *p1d = reinterpret_cast<double *>(W + o_p1d);
+  int32_t *p1i = reinterpret_cast<int32_t *>(W + o_p1i);
+  P1 p1{p1d, p1d + nch, p1d + 2 * nch, p1d + 3 * nch, p1d + 4 * nch, p1d + 5 * nch, p1i, p1i + nch,
+        reinterpret_cast<uint8_t *>(W + o_spec)};
+  double *xt = reinterpret_cast<double *>(W + o_xt);
+  long long *sD = reinterpret_cast<long long *>(W + o_sD);
+  Summ sm{reinterpret_cast<int32_t *>(W + o_se), sD, sD + 2 * nch, sD + 4 * nch,
+          reinterpret_cast<int32_t *>(W + o_sA)};
+  int32_t *hqp = reinterpret_cast<int32_t *>(W + o_hq);
+  Carry cr{reinterpret_cast<double *>(W + o_x), reinterpret_cast<uint8_t *>(W + o_mode), hqp,
+           reinterpret_cast<double *>(W + o_hmax), hqp + nch};
+  unsigned long long *cnts = reinterpret_cast<unsigned long long *>(W + o_cnt);
+  // cnts: [0] candidates, [1] rescans, [2] replays, [3] error bits (u32)
+  KS_HIP(hipMemsetAsync(cnts, 0, 64, st));
+  KS_HIP(hipMemcpyAsync(d_cbase, cb.data(), (nruns + 1) * 8, hipMemcpyHostToDevice, st));
+
+  uint16_t *codes = nullptr;
+  if (comp) {
+    void *cp = nullptr;
+    const int64_t ntiles = (nch + 63) / 64;
+    KS_TRY(ensure(ctx, SLOT_CHUNK_B, (size_t)ntiles * 64 * CH * 2, &cp));
+    codes = static_cast<uint16_t *>(cp);
+  }
+  int64_t ccap = std::max<int64_t>(1 << 16, nch / 4);
+  if (ctx->slots[SLOT_CHUNK_C].bytes / 40 > (size_t)ccap) ccap = ctx->slots[SLOT_CHUNK_C].bytes / 40;
+  void *cbuf = nullptr;
+  KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)ccap * 40 + 1024, &cbuf));
+  Cand cand{reinterpret_cast<long long *>(cbuf), reinterpret_cast<long long *>(cbuf) + ccap,
+            reinterpret_cast<long long *>(cbuf) + 2 * ccap, reinterpret_cast<double *>(cbuf) + 3 * ccap,
+            cnts, ccap};
+
+  KS_HIP(hipEventRecord(ctx->ev[7], st));
+  hipLaunchKernelGGL(k_make_chunks, dim3((unsigned)((nruns + 255) / 256)), dim3(256), 0, st, runs.a, runs.b,
+                     d_cbase, nruns, k, g);
+  KS_HIP(hipGetLastError());
+  const unsigned gch = (unsigned)((nch + 255) / 256);
+  hipEvent_t e_p1a, e_p1b;
+  KS_HIP(hipEventCreate(&e_p1a));
+  KS_HIP(hipEventCreate(&e_p1b));
+  KS_HIP(hipEventRecord(e_p1a, st));
+  if (comp)
+    hipLaunchKernelGGL(k_pass1<true>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, mw, min_score,
+                       visits, p1, cand);
+  else
+    hipLaunchKernelGGL(k_pass1<false>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, mw,
+                       min_score, visits, p1, cand);
+  KS_HIP(hipGetLastError());
+  KS_HIP(hipEventRecord(e_p1b, st));
+  hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)nruns), dim3(64), 0, st, d_cbase, nruns, p1, xt);
+  KS_HIP(hipGetLastError());
+  if (comp)
+    hipLaunchKernelGGL(k_summaries<true>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, p1, xt, sm);
+  else
+    hipLaunchKernelGGL(k_summaries<false>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, p1, xt,
+                       sm);
+  KS_HIP(hipGetLastError());
+  if (comp)
+    hipLaunchKernelGGL(k_carry<true>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, k, tv,
+                       codes, p1, sm, cr, cnts + 2);
+  else
+    hipLaunchKernelGGL(k_carry<false>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, k, tv,
+                       codes, p1, sm, cr, cnts + 2);
+  KS_HIP(hipGetLastError());
+  unsigned int *d_err = reinterpret_cast<unsigned int *>(cnts + 3);
+  if (comp)
+    hipLaunchKernelGGL(k_heads<true>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, sm, cr, d_err);
+  else
+    hipLaunchKernelGGL(k_heads<false>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, sm, cr,
+                       d_err);
+  KS_HIP(hipGetLastError());
+  // candidates: order by begin position
+  unsigned long long hc[4] = {0, 0, 0, 0};
+  KS_HIP(hipMemcpyAsync(hc, cnts, 32, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipStreamSynchronize(st));
+  if ((int64_t)hc[0] > ccap) {
+    KS_HIP(hipEventDestroy(e_p1a));
+    KS_HIP(hipEventDestroy(e_p1b));
+    return fail(KS_ERR_INTERNAL, "candidate buffer overflow (%llu > %lld)", hc[0], (long long)ccap);
+  }
+  const int64_t ncand = (int64_t)hc[0];
+  void *sbuf = nullptr;
+  KS_TRY(ensure(ctx, SLOT_CHUNK_D, (size_t)std::max<int64_t>(ncand, 1) * 32 + 1024, &sbuf));
+  unsigned long long *kin = reinterpret_cast<unsigned long long *>(sbuf);
+  unsigned long long *kout = kin + std::max<int64_t>(ncand, 1);
+  int32_t *vin = reinterpret_cast<int32_t *>(kout + std::max<int64_t>(ncand, 1));
+  int32_t *vout = vin + std::max<int64_t>(ncand, 1);
+  if (ncand > 0) {
+    std::vector<int32_t> iota(ncand);
+    for (int64_t i = 0; i < ncand; ++i) iota[i] = (int32_t)i;
+    KS_HIP(hipMemcpyAsync(kin, cand.beg, ncand * 8, hipMemcpyDeviceToDevice, st));
+    KS_HIP(hipMemcpyAsync(vin, iota.data(), ncand * 4, hipMemcpyHostToDevice, st));
+    size_t tb = 0;
+    KS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin, vout, (int)ncand, 0, 64, st));
+    void *tmp = nullptr;
+    KS_TRY(ensure(ctx, SLOT_SORT_TMP, tb, &tmp));
+    KS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout, (int)ncand, 0, 64, st));
+  }
+  // rescan buffer
+  int64_t rcap = std::max<int64_t>(rb.cap, 4096);
+  void *rsb = nullptr;
+  KS_TRY(ensure(ctx, SLOT_WORK_A, (size_t)rcap * 20 + 1024, &rsb));
+  Rescan rs{reinterpret_cast<int64_t *>(rsb), reinterpret_cast<int64_t *>(rsb) + rcap,
+            reinterpret_cast<int32_t *>(reinterpret_cast<int64_t *>(rsb) + 2 * rcap), cnts + 1, rcap};
+  hipLaunchKernelGGL(k_stitch, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, runs.b,
+                     runs.seq, k, p1, cr, cand, ncand, vout, mw, min_score, rb, rs, d_err);
+  KS_HIP(hipGetLastError());
+  KS_HIP(hipMemcpyAsync(hc, cnts, 32, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipStreamSynchronize(st));
+  const unsigned int errbits = (unsigned int)(hc[3] & 0xffffffffu);
+  float ms_p1 = 0;
+  KS_HIP(hipEventElapsedTime(&ms_p1, e_p1a, e_p1b));
+  KS_HIP(hipEventDestroy(e_p1a));
+  KS_HIP(hipEventDestroy(e_p1b));
+  if (errbits) return fail(KS_ERR_INTERNAL, "chunked scan consistency check failed (bits %u)", errbits);
+  if ((int64_t)hc[1] > rcap) return fail(KS_ERR_INTERNAL, "rescan buffer overflow");
+  float ms_all = 0;
+  KS_HIP(hipEventRecord(ctx->ev[6], st));
+  KS_HIP(hipEventSynchronize(ctx->ev[6]));
+  KS_HIP(hipEventElapsedTime(&ms_all, ctx->ev[7], ctx->ev[6]));
+  // rescans: the lane kernel on virtual runs
+  const int64_t nres = (int64_t)hc[1];
+  hipEvent_t e_ra, e_rb;
+  KS_HIP(hipEventCreate(&e_ra));
+  KS_HIP(hipEventCreate(&e_rb));
+  KS_HIP(hipEventRecord(e_ra, st));
+  if (nres > 0) KS_TRY(launch_scan_lane(ctx, s->seq, rs.a, rs.b, rs.seq, nres, k, tv, mw, min_score, visits, rb));
+  KS_HIP(hipEventRecord(e_rb, st));
+  KS_HIP(hipEventSynchronize(e_rb));
+  float ms_res = 0;
+  KS_HIP(hipEventElapsedTime(&ms_res, e_ra, e_rb));
+  KS_HIP(hipEventDestroy(e_ra));
+  KS_HIP(hipEventDestroy(e_rb));
+  if (stats) {
+    stats->ms_scan = ms_p1;
+    stats->ms_rescan = ms_res;
+    stats->ms_finish += ms_all - ms_p1;
+    stats->n_rescan = nres;
+  }
+  return KS_OK;
+}
+
 }  // namespace ks

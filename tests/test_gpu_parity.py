@@ -80,7 +80,7 @@ def _random_inputs(rng, kmax=5, lmax=200):
     return k, seqs, w, rng.randint(-1, 6), rng.choice([0.0, 1.0, 2.5, 5.0, -1.0])
 
 
-ALGOS = [0]  # scan algorithms exercised (0 lane-per-run, 1 chunked carry scan)
+ALGOS = [0, 1]  # scan algorithms exercised (0 lane-per-run, 1 chunked carry scan)
 
 
 @pytest.mark.parametrize("algo", ALGOS)
@@ -211,3 +211,57 @@ def test_compressed_table_matches_full(K, ctx):
     p1, s1, _ = D.scan(ctx, ds, k, t1, 5, 1.0)
     p2, s2, _ = D.scan(ctx, ds, k, t2, 5, 1.0)
     _assert_same_regions(p1, s1, p2, s2, "compressed vs full")
+
+
+@pytest.mark.parametrize("big", [1.5 * 2.0 ** 50, 3.0 * 2.0 ** 20])
+def test_binade_summary_ties(K, oracle, ctx, big):
+    """Long runs where S sits deep inside one binade and steps are dyadic, so
+    fl(S + s) rounds with exact ties (decided by the accumulator's parity):
+    the chunked scan's binade-integer summaries must reproduce the sequential
+    FP64 chain bit for bit."""
+    import torch
+    from kmer_spans_amd import device as D
+    rng = np.random.default_rng(8)
+    k = 4
+    steps = np.array([0.125, -0.125, 0.375, -0.375, 0.625, -0.875, 1.125, 0.0])
+    w = rng.choice(steps, 4 ** k)
+    w[rng.integers(0, 4 ** k, 3)] = big
+    w[rng.integers(0, 4 ** k, 2)] = -2.0 * big
+    seqs = ["".join(rng.choice(list("ACGT"), 400_000)), "".join(rng.choice(list("ACGT"), 70_000))]
+    ds = D.from_host(seqs, "cuda")
+    D.bind_torch_stream(ctx)
+    tab = D.DeviceTable(ctx, w, k, 0.0)
+    o = oracle.scan(seqs, k, w, 0.0, 0, 0.0, visits=True)
+    for algo in ALGOS:
+        ctx.set_scan_algo(algo)
+        vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+        pos, sc, st = D.scan(ctx, ds, k, tab, 0, 0.0, vis)
+        _assert_same_regions(pos, sc, o["pos"], o["score"], ("ties", algo))
+        assert np.array_equal(vis.cpu().numpy(), o["counts"])
+    ctx.set_scan_algo(-1)
+
+
+@pytest.mark.parametrize("k", [6, 12])
+def test_long_drift_run(K, oracle, ctx, k):
+    """One 3 Mbp run with positive drift (a giant excursion, the log-ratio
+    shape): exercised through the chunked carry (summaries + replays)."""
+    import torch
+    from kmer_spans_amd import device as D, genome
+    s = genome.contig(3_000_000, 21, device="cuda", repeats=True)
+    s[s == ord("N")] = ord("A")
+    ds = D.from_parts([s], [s.numel()], "cuda")
+    host = [ds.host_seq(0)]
+    n, oc = oracle.kmer_counts(host, k)
+    w = K.log2_table(oc, k)
+    w[~np.isfinite(w)] = -5.0
+    D.bind_torch_stream(ctx)
+    tab = D.DeviceTable(ctx, w, k, 0.0)
+    o = oracle.scan(host, k, w, 0.0, 100, 20.0, visits=True)
+    for algo in ALGOS:
+        ctx.set_scan_algo(algo)
+        vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+        pos, sc, st = D.scan(ctx, ds, k, tab, 100, 20.0, vis)
+        _assert_same_regions(pos, sc, o["pos"], o["score"], ("drift", k, algo))
+        assert np.array_equal(vis.cpu().numpy(), o["counts"])
+        assert st["scan_algo"] == algo
+    ctx.set_scan_algo(-1)

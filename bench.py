@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-sample", type=float, default=2.0e8, help="bases in the CPU-baseline sample")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-expand", action="store_true", help="do not build the expanded (k+J-1)-mer table")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
     return p.parse_args()
 
@@ -96,7 +97,7 @@ def main():
     else:
         w, thr = api.rank_table(hc, k, words), 0.75
     t0 = time.time()
-    table = D.DeviceTable(ctx, w, k, thr, compress=True)
+    table = D.DeviceTable(ctx, w, k, thr, compress=True, expand=not args.no_expand)
     torch.cuda.synchronize()
     t_table = time.time() - t0
 
@@ -181,7 +182,7 @@ def main():
                                f"min_score {args.min_score}, device-resident",
                    "k": k, "score": args.score, "genome_bp": n_bases, "parallelism": f"contig-shard x{world}",
                    "scan_algo": int(stats[-1]["scan_algo"]), "table_compressed": table.compressed,
-                   "table_distinct": table.distinct},
+                   "table_distinct": table.distinct, "positions_per_read": table.positions_per_read},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "parity_sample": parity,

@@ -134,16 +134,27 @@ typedef struct ks_dev_seqs {
 } ks_dev_seqs;
 
 /* A score table resident on the device, s = w[code] - thr precomputed
- * bitwise as the reference computes it (kmer_spans.c:268).  When the table
- * has at most 65536 distinct values it is stored as a uint16 code table plus
- * an FP64 value LUT (exact: the LUT holds the very same doubles). */
+ * bitwise as the reference computes it (kmer_spans.c:268).  Flags:
+ *  KS_TABLE_COMPRESS  if the table has at most 65536 distinct values, store
+ *                     it as a uint16 code table plus an FP64 value LUT
+ *                     (exact: the LUT holds the very same doubles);
+ *  KS_TABLE_EXPAND    also build the expanded table: one entry per
+ *                     (k+J-1)-mer holding the J codes/values of its J
+ *                     consecutive k-mers (J <= 4, <= 32 GiB), so the scan
+ *                     issues one random read per J scan indices.  Skipped
+ *                     when it does not fit. */
+#define KS_TABLE_COMPRESS 1
+#define KS_TABLE_EXPAND 2
 typedef struct ks_table ks_table;
 ks_status ks_table_create(ks_ctx *ctx, const double *w_host, int32_t k, double thr,
-                          int32_t allow_compress, ks_table **out);
+                          int32_t flags, ks_table **out);
 void ks_table_destroy(ks_table *t);
 /* 1 if the table is stored compressed (uint16 codes + LUT), else 0. */
 int32_t ks_table_is_compressed(const ks_table *t);
 int64_t ks_table_distinct(const ks_table *t);
+/* Scan indices served per random table read (J of the expanded table, 1 if
+ * it was not built). */
+int32_t ks_table_positions_per_read(const ks_table *t);
 
 /* Scan statistics of the last ks_scan_dev call (device time of each phase,
  * measured with hipEvents on the ctx stream). */

@@ -84,6 +84,13 @@ struct ks_table {
   double *d_vals = nullptr;     // full table s = w - thr (uncompressed), 4^k doubles
   uint16_t *d_codes = nullptr;  // compressed: 4^k u16 codes
   double *d_lut = nullptr;      // compressed: distinct s values
+  // Expanded table: one entry per (k+J-1)-mer holding the values (or uint16
+  // codes) of its J consecutive k-mers, so one random request serves J scan
+  // indices.  J = 1: not built.
+  int ext_J = 1;
+  void *d_ext = nullptr;        // uint64 (J <= 4 codes) or double[4] (J <= 3 values)
+  size_t ext_bytes = 0;
+  double ms_ext = 0;            // build time
 };
 
 namespace ks {
@@ -122,6 +129,9 @@ ks_status launch_count(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const R
 ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, const ks_table *t,
                     int32_t min_width, double min_score, int32_t *visits_dev, ks_regions *out,
                     ks_scan_stats *stats);
+
+// Build the expanded table of t (no-op if it exists or does not fit).
+ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes);
 
 // Host table builders (ks_tables.cpp).
 ks_status rank_table_host(const int32_t *counts, int k, double total, double *ranks);

@@ -98,8 +98,8 @@ __device__ __forceinline__ void load16(const uint8_t *__restrict__ seq, int64_t 
   const int64_t a0 = p & ~(int64_t)15;
   const int sh = (int)(p - a0);
   uint32_t w[8];
-  const uint4 v0 = *reinterpret_cast<const uint4 *>(seq + a0);
-  uint4 v1 = make_uint4(0x4e4e4e4eu, 0x4e4e4e4eu, 0x4e4e4e4eu, 0x4e4e4e4eu);
+  uint4 v0 = make_uint4(0x4e4e4e4eu, 0x4e4e4e4eu, 0x4e4e4e4eu, 0x4e4e4e4eu), v1 = v0;
+  if (a0 < total) v0 = *reinterpret_cast<const uint4 *>(seq + a0);
   if (a0 + 16 < total) v1 = *reinterpret_cast<const uint4 *>(seq + a0 + 16);
   w[0] = v0.x; w[1] = v0.y; w[2] = v0.z; w[3] = v0.w; w[4] = v1.x; w[5] = v1.y; w[6] = v1.z; w[7] = v1.w;
 #pragma unroll
@@ -141,54 +141,89 @@ __global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__r
 
 // ------------------------------------------------------------------- P1
 
-template <bool kCompressed>
+// J = scan indices served by one table read: 1 reads the base table
+// (uint16 code or FP64 value per index); J >= 2 reads the expanded table
+// entry of the (k+J-1)-mer that spans J consecutive indices.
+template <int J, bool kCompressed>
 __global__ void __launch_bounds__(256) k_pass1(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
                                                int k, TableView tv, uint16_t *__restrict__ codes,
                                                uint64_t mw, double min_score, uint32_t *__restrict__ visits,
                                                P1 o, Cand cand) {
+  constexpr int G = (J == 1) ? 16 : 8;  // table reads in flight per lane and batch
+  constexpr int PB = G * J;             // scan indices per batch (16, 16, 24, 32)
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
-  const uint32_t mask = (1u << (2 * k)) - 1u;
+  const int kx = k + J - 1;
+  const uint32_t xmask = (kx >= 16) ? 0xffffffffu : ((1u << (2 * kx)) - 1u);
+  const uint32_t kmask = (1u << (2 * k)) - 1u;
   const int64_t start = g.start[c];
   const int n = g.n[c];
-  uint32_t code = prime_code(seq, start - k, k);
+  uint32_t gcode = prime_code_guarded(seq, start - k, kx, total);  // (k+J-1)-mer of group 0
   double prev = 0.0, best = 0.0;
   int beg = -1, arg = 0;
   double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
   bool special = false;
-  for (int b0 = 0; b0 < CH; b0 += NB) {
-    if (b0 >= n) break;
-    uint8_t by[16];
-    load16(seq, start + b0, total, by);
-    uint32_t cc[NB];
-    double v[NB];
+  for (int b0 = 0; b0 < n; b0 += PB) {
+    uint8_t by[32];  // bytes rolled in by groups 1..G: start + b0 + J - 1 + [0, PB)
+    load16(seq, start + b0 + J - 1, total, by);
+    if (PB > 16) load16(seq, start + b0 + J - 1 + 16, total, by + 16);
+    uint32_t gc[G];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      cc[j] = code;
-      code = roll(code, by[j], mask);
+    for (int gi = 0; gi < G; ++gi) {
+      gc[gi] = gcode;
+#pragma unroll
+      for (int t = 0; t < J; ++t) gcode = ((gcode << 2) | enc(by[gi * J + t])) & xmask;
+    }
+    double v[PB];
+    uint16_t q[PB];
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+      const bool live = b0 + gi * J < n;
+      if (J == 1) {
+        if (kCompressed) q[gi] = live ? tv.codes[gc[gi]] : (uint16_t)0;
+        else v[gi] = live ? tv.vals[gc[gi]] : 0.0;
+      } else if (kCompressed) {
+        uint64_t e = 0;
+        if (live) e = (J <= 2) ? (uint64_t)reinterpret_cast<const uint32_t *>(tv.ext)[gc[gi]]
+                               : reinterpret_cast<const uint64_t *>(tv.ext)[gc[gi]];
+#pragma unroll
+        for (int t = 0; t < J; ++t) q[gi * J + t] = (uint16_t)(e >> (16 * t));
+      } else {
+        double2 e0 = make_double2(0.0, 0.0), e1 = e0;
+        if (live) {
+          const double2 *E = reinterpret_cast<const double2 *>(tv.ext);
+          if (J <= 2) {
+            e0 = E[gc[gi]];
+          } else {
+            e0 = E[2 * (size_t)gc[gi]];
+            e1 = E[2 * (size_t)gc[gi] + 1];
+          }
+        }
+        const double ev[4] = {e0.x, e0.y, e1.x, e1.y};
+#pragma unroll
+        for (int t = 0; t < J; ++t) v[gi * J + t] = ev[t];
+      }
     }
     if (kCompressed) {
-      uint16_t q[NB];
 #pragma unroll
-      for (int j = 0; j < NB; ++j) q[j] = (b0 + j < n) ? tv.codes[cc[j]] : (uint16_t)0;
+      for (int j = 0; j < PB; ++j) v[j] = tv.lut[q[j]];
 #pragma unroll
-      for (int j = 0; j < NB; ++j) v[j] = tv.lut[q[j]];
-      uint4 w0, w1;
-      w0.x = q[0] | ((uint32_t)q[1] << 16); w0.y = q[2] | ((uint32_t)q[3] << 16);
-      w0.z = q[4] | ((uint32_t)q[5] << 16); w0.w = q[6] | ((uint32_t)q[7] << 16);
-      w1.x = q[8] | ((uint32_t)q[9] << 16); w1.y = q[10] | ((uint32_t)q[11] << 16);
-      w1.z = q[12] | ((uint32_t)q[13] << 16); w1.w = q[14] | ((uint32_t)q[15] << 16);
-      *reinterpret_cast<uint4 *>(codes + code_slot(c, b0)) = w0;
-      *reinterpret_cast<uint4 *>(codes + code_slot(c, b0 + 8)) = w1;
-    } else {
-#pragma unroll
-      for (int j = 0; j < NB; ++j) v[j] = (b0 + j < n) ? tv.vals[cc[j]] : 0.0;
+      for (int r8 = 0; r8 < PB / 8; ++r8) {
+        if (b0 + 8 * r8 < CH) {
+          uint4 w;
+          w.x = q[8 * r8 + 0] | ((uint32_t)q[8 * r8 + 1] << 16);
+          w.y = q[8 * r8 + 2] | ((uint32_t)q[8 * r8 + 3] << 16);
+          w.z = q[8 * r8 + 4] | ((uint32_t)q[8 * r8 + 5] << 16);
+          w.w = q[8 * r8 + 6] | ((uint32_t)q[8 * r8 + 7] << 16);
+          *reinterpret_cast<uint4 *>(codes + code_slot(c, b0 + 8 * r8)) = w;
+        }
+      }
     }
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
+    for (int j = 0; j < PB; ++j) {
       const int i = b0 + j;
       if (i < n) {
-        if (visits) atomicAdd(&visits[cc[j]], 1u);
+        if (visits) atomicAdd(&visits[(gc[j / J] >> (2 * (J - 1 - j % J))) & kmask], 1u);
         const double s = v[j];
         asum += s;
         pmin = fmin(pmin, asum);
@@ -714,12 +749,16 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
   KS_HIP(hipEventCreate(&e_p1a));
   KS_HIP(hipEventCreate(&e_p1b));
   KS_HIP(hipEventRecord(e_p1a, st));
-  if (comp)
-    hipLaunchKernelGGL(k_pass1<true>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, mw, min_score,
-                       visits, p1, cand);
-  else
-    hipLaunchKernelGGL(k_pass1<false>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, mw,
-                       min_score, visits, p1, cand);
+#define KS_P1(J, C)                                                                                   \
+  hipLaunchKernelGGL((k_pass1<J, C>), dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, mw, min_score, \
+                     visits, p1, cand)
+  const int J = (tv.ext != nullptr) ? tv.ext_J : 1;
+  if (comp) {
+    if (J == 4) KS_P1(4, true); else if (J == 3) KS_P1(3, true); else if (J == 2) KS_P1(2, true); else KS_P1(1, true);
+  } else {
+    if (J == 4) KS_P1(4, false); else if (J == 3) KS_P1(3, false); else if (J == 2) KS_P1(2, false); else KS_P1(1, false);
+  }
+#undef KS_P1
   KS_HIP(hipGetLastError());
   KS_HIP(hipEventRecord(e_p1b, st));
   hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)nruns), dim3(64), 0, st, d_cbase, nruns, p1, xt);

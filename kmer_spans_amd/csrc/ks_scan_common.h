@@ -12,6 +12,8 @@ struct TableView {
   const uint16_t *codes;
   const double *lut;
   int compressed;
+  const void *ext;  // expanded table (see ks_table), nullptr if absent
+  int ext_J;
 };
 
 __device__ __forceinline__ double tv_get(const TableView &t, uint32_t code) {
@@ -29,6 +31,15 @@ __device__ __forceinline__ void push_region(const RegionBuf &rb, int32_t seq, in
     rb.end[slot] = end;
     rb.score[slot] = score;
   }
+}
+
+// Encode the n bases [p, p + n), reading 'N' beyond total (only the bases
+// inside the run matter; the rest feed k-mers of indices past the run end).
+__device__ __forceinline__ uint32_t prime_code_guarded(const uint8_t *__restrict__ seq, int64_t p, int n,
+                                                       int64_t total) {
+  uint32_t c = 0;
+  for (int j = 0; j < n; ++j) c = (c << 2) | enc(p + j < total ? seq[p + j] : (uint8_t)'N');
+  return c;
 }
 
 // Encode the k bases [p, p + k) (all non-N, inside one run).

@@ -38,13 +38,103 @@ __global__ void k_assign_codes(const double *__restrict__ s, const unsigned long
   }
 }
 
+// Expanded table, uint16 codes: entry for the (k+J-1)-mer x packs the codes of
+// its J k-mers (first k-mer in the low 16 bits).  Consecutive entries share
+// their k-mers, so the base-table reads are cached and the build is a stream.
+template <int J, typename E>
+__global__ void k_build_ext_u16(const uint16_t *__restrict__ codes, int k, uint64_t nent, E *__restrict__ ext) {
+  const uint64_t mk = ((uint64_t)1 << (2 * k)) - 1;
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nent;
+       e += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int t = 0; t < J; ++t) v |= (uint64_t)codes[(e >> (2 * (J - 1 - t))) & mk] << (16 * t);
+    ext[e] = (E)v;
+  }
+}
+
+// Expanded table, FP64 values: J values per entry (double2 / double4).
+template <int J>
+__global__ void k_build_ext_f64(const double *__restrict__ vals, int k, uint64_t nent, double *__restrict__ ext) {
+  constexpr int W = (J <= 2) ? 2 : 4;
+  const uint64_t mk = ((uint64_t)1 << (2 * k)) - 1;
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nent;
+       e += (uint64_t)gridDim.x * blockDim.x) {
+    double v[W];
+#pragma unroll
+    for (int t = 0; t < W; ++t) v[t] = (t < J) ? vals[(e >> (2 * (J - 1 - t))) & mk] : 0.0;
+    if (W == 2) {
+      reinterpret_cast<double2 *>(ext)[e] = make_double2(v[0], v[1]);
+    } else {
+      reinterpret_cast<double2 *>(ext)[2 * e] = make_double2(v[0], v[1]);
+      reinterpret_cast<double2 *>(ext)[2 * e + 1] = make_double2(v[2], v[3]);
+    }
+  }
+}
+
 }  // namespace
+
+// Entry bytes of an expanded table with J values per entry.
+static size_t ext_entry_bytes(bool u16, int J) {
+  if (u16) return J <= 2 ? 4 : 8;
+  return J <= 2 ? 16 : 32;
+}
+
+ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes) {
+  if (t->d_ext || t->ext_J > 1) return KS_OK;
+  const bool u16 = t->compressed;
+  int J = 0;
+  for (int cand = 4; cand >= 2; --cand) {
+    const int kx = t->k + cand - 1;
+    if (kx > 16) continue;  // (k+J-1)-mer codes are 32-bit
+    const size_t bytes = ((size_t)1 << (2 * kx)) * ext_entry_bytes(u16, cand);
+    if (bytes <= max_bytes) { J = cand; break; }
+  }
+  if (J == 0) return KS_OK;
+  const int kx = t->k + J - 1;
+  const uint64_t nent = (uint64_t)1 << (2 * kx);
+  const size_t bytes = nent * ext_entry_bytes(u16, J);
+  size_t free_b = 0, total_b = 0;
+  KS_HIP(hipMemGetInfo(&free_b, &total_b));
+  if (bytes > free_b / 10 * 4) return KS_OK;  // leave room for the scan workspace
+  hipStream_t st = ctx->stream;
+  void *ext = nullptr;
+  if (hipMalloc(&ext, bytes) != hipSuccess) { (void)hipGetLastError(); return KS_OK; }
+  hipEvent_t a, b;
+  KS_HIP(hipEventCreate(&a));
+  KS_HIP(hipEventCreate(&b));
+  KS_HIP(hipEventRecord(a, st));
+  const unsigned grid = (unsigned)std::min<uint64_t>((nent + 255) / 256, (uint64_t)ctx->num_cus * 32);
+  if (u16) {
+    if (J == 4) hipLaunchKernelGGL((k_build_ext_u16<4, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
+    else if (J == 3) hipLaunchKernelGGL((k_build_ext_u16<3, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
+    else hipLaunchKernelGGL((k_build_ext_u16<2, uint32_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint32_t *)ext);
+  } else {
+    if (J == 4) hipLaunchKernelGGL(k_build_ext_f64<4>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
+    else if (J == 3) hipLaunchKernelGGL(k_build_ext_f64<3>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
+    else hipLaunchKernelGGL(k_build_ext_f64<2>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
+  }
+  KS_HIP(hipGetLastError());
+  KS_HIP(hipEventRecord(b, st));
+  KS_HIP(hipEventSynchronize(b));
+  float ms = 0;
+  KS_HIP(hipEventElapsedTime(&ms, a, b));
+  KS_HIP(hipEventDestroy(a));
+  KS_HIP(hipEventDestroy(b));
+  t->d_ext = ext;
+  t->ext_J = J;
+  t->ext_bytes = bytes;
+  t->ms_ext = ms;
+  return KS_OK;
+}
+
 }  // namespace ks
 
 using namespace ks;
 
 extern "C" ks_status ks_table_create(ks_ctx *ctx, const double *w_host, int32_t k, double thr,
-                                     int32_t allow_compress, ks_table **out) {
+                                     int32_t flags, ks_table **out) {
+  const int32_t allow_compress = flags & KS_TABLE_COMPRESS;
   if (!ctx || !w_host || !out) return fail(KS_ERR_ARG, "ks_table_create: null argument");
   if (k < 1 || k > KS_MAX_K) return fail(KS_ERR_ARG, "k must be between 1 and %d", KS_MAX_K);
   KS_TRY(activate(ctx));
@@ -111,6 +201,10 @@ extern "C" ks_status ks_table_create(ks_ctx *ctx, const double *w_host, int32_t 
   KS_TBL_HIP(hipStreamSynchronize(st));
 #undef KS_TBL_HIP
   cleanup();
+  if (flags & KS_TABLE_EXPAND) {
+    const ks_status rc = table_expand(ctx, t, (size_t)32 << 30);
+    if (rc != KS_OK) { ks_table_destroy(t); return rc; }
+  }
   *out = t;
   return KS_OK;
 }
@@ -120,8 +214,10 @@ extern "C" void ks_table_destroy(ks_table *t) {
   if (t->d_vals) (void)hipFree(t->d_vals);
   if (t->d_codes) (void)hipFree(t->d_codes);
   if (t->d_lut) (void)hipFree(t->d_lut);
+  if (t->d_ext) (void)hipFree(t->d_ext);
   delete t;
 }
 
 extern "C" int32_t ks_table_is_compressed(const ks_table *t) { return t && t->compressed ? 1 : 0; }
 extern "C" int64_t ks_table_distinct(const ks_table *t) { return t ? t->distinct : -1; }
+extern "C" int32_t ks_table_positions_per_read(const ks_table *t) { return t ? t->ext_J : 0; }

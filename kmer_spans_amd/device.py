@@ -77,18 +77,23 @@ def from_host(seqs, device="cuda") -> DeviceSeqs:
 class DeviceTable:
     """A score table s = w - thr on the device (ks_table)."""
 
-    def __init__(self, ctx: _lib.Context, w, k: int, thr: float = 0.0, compress: bool = True):
+    def __init__(self, ctx: _lib.Context, w, k: int, thr: float = 0.0, compress: bool = True,
+                 expand: bool = False):
         w = np.ascontiguousarray(w, dtype=np.float64)
         if w.size != 4 ** k:
             raise _lib.KmerSpansError(f"kmer_w contains {w.size} elements but should have {4 ** k}")
         self.k = k
         self._h = C.c_void_p()
-        check(load().ks_table_create(ctx.handle, w.ctypes.data, k, float(thr), int(bool(compress)),
-                                     C.byref(self._h)))
+        flags = (1 if compress else 0) | (2 if expand else 0)
+        check(load().ks_table_create(ctx.handle, w.ctypes.data, k, float(thr), flags, C.byref(self._h)))
 
     @property
     def compressed(self) -> bool:
         return bool(load().ks_table_is_compressed(self._h))
+
+    @property
+    def positions_per_read(self) -> int:
+        return int(load().ks_table_positions_per_read(self._h))
 
     @property
     def distinct(self) -> int:

@@ -167,14 +167,17 @@ def test_human_like_device_path(K, oracle, ctx, k, score):
         w = K.pm1_table(oc, k)
     else:
         w, thr = K.rank_table(oc, k, n), 0.75
-    tab = D.DeviceTable(ctx, w, k, thr, compress=True)
     o = oracle.scan(host, k, w, thr, 100, 20.0, visits=True)
-    for algo in ALGOS:
-        ctx.set_scan_algo(algo)
-        vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
-        pos, sc, st = D.scan(ctx, ds, k, tab, 100, 20.0, vis)
-        _assert_same_regions(pos, sc, o["pos"], o["score"], (k, score, algo))
-        assert np.array_equal(vis.cpu().numpy(), o["counts"]), (k, score, algo)
+    for expand in (False, True):
+        tab = D.DeviceTable(ctx, w, k, thr, compress=True, expand=expand)
+        assert (tab.positions_per_read > 1) == expand
+        for algo in ALGOS:
+            ctx.set_scan_algo(algo)
+            vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+            pos, sc, st = D.scan(ctx, ds, k, tab, 100, 20.0, vis)
+            _assert_same_regions(pos, sc, o["pos"], o["score"], (k, score, algo, expand))
+            assert np.array_equal(vis.cpu().numpy(), o["counts"]), (k, score, algo, expand)
+        tab.close()
     ctx.set_scan_algo(-1)
     D.bind_torch_stream(ctx)
 
@@ -213,8 +216,9 @@ def test_compressed_table_matches_full(K, ctx):
     _assert_same_regions(p1, s1, p2, s2, "compressed vs full")
 
 
+@pytest.mark.parametrize("expand", [False, True])
 @pytest.mark.parametrize("big", [1.5 * 2.0 ** 50, 3.0 * 2.0 ** 20])
-def test_binade_summary_ties(K, oracle, ctx, big):
+def test_binade_summary_ties(K, oracle, ctx, big, expand):
     """Long runs where S sits deep inside one binade and steps are dyadic, so
     fl(S + s) rounds with exact ties (decided by the accumulator's parity):
     the chunked scan's binade-integer summaries must reproduce the sequential
@@ -230,7 +234,7 @@ def test_binade_summary_ties(K, oracle, ctx, big):
     seqs = ["".join(rng.choice(list("ACGT"), 400_000)), "".join(rng.choice(list("ACGT"), 70_000))]
     ds = D.from_host(seqs, "cuda")
     D.bind_torch_stream(ctx)
-    tab = D.DeviceTable(ctx, w, k, 0.0)
+    tab = D.DeviceTable(ctx, w, k, 0.0, expand=expand)
     o = oracle.scan(seqs, k, w, 0.0, 0, 0.0, visits=True)
     for algo in ALGOS:
         ctx.set_scan_algo(algo)
@@ -255,7 +259,7 @@ def test_long_drift_run(K, oracle, ctx, k):
     w = K.log2_table(oc, k)
     w[~np.isfinite(w)] = -5.0
     D.bind_torch_stream(ctx)
-    tab = D.DeviceTable(ctx, w, k, 0.0)
+    tab = D.DeviceTable(ctx, w, k, 0.0, expand=True)
     o = oracle.scan(host, k, w, 0.0, 100, 20.0, visits=True)
     for algo in ALGOS:
         ctx.set_scan_algo(algo)
@@ -264,4 +268,32 @@ def test_long_drift_run(K, oracle, ctx, k):
         _assert_same_regions(pos, sc, o["pos"], o["score"], ("drift", k, algo))
         assert np.array_equal(vis.cpu().numpy(), o["counts"])
         assert st["scan_algo"] == algo
+    ctx.set_scan_algo(-1)
+
+
+@pytest.mark.parametrize("k,compress", [(3, False), (7, False), (5, True), (10, True)])
+def test_expanded_table_edges(K, oracle, ctx, k, compress):
+    """Expanded tables (FP64 and uint16 entries) on ragged inputs: runs
+    shorter than J, N runs, sequence ends inside a read group."""
+    import torch
+    from kmer_spans_amd import device as D
+    rng = np.random.default_rng(k)
+    w = rng.normal(size=4 ** k) - 0.1
+    if compress:
+        w = np.round(w * 8) / 8
+    seqs = []
+    for L in (0, k, k + 1, k + 2, k + 3, 17, 255, 256, 257, 1000, 5003):
+        seqs.append("".join(rng.choice(list("ACGTN"), L, p=[0.24, 0.24, 0.24, 0.24, 0.04])))
+    seqs.append("".join(rng.choice(list("ACGT"), 200000)))
+    ds = D.from_host(seqs, "cuda")
+    D.bind_torch_stream(ctx)
+    tab = D.DeviceTable(ctx, w, k, 0.05, compress=compress, expand=True)
+    assert tab.positions_per_read >= 2
+    o = oracle.scan(seqs, k, w, 0.05, 0, 0.5, visits=True)
+    for algo in ALGOS:
+        ctx.set_scan_algo(algo)
+        vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+        pos, sc, st = D.scan(ctx, ds, k, tab, 0, 0.5, vis)
+        _assert_same_regions(pos, sc, o["pos"], o["score"], ("ext", k, algo))
+        assert np.array_equal(vis.cpu().numpy(), o["counts"])
     ctx.set_scan_algo(-1)

@@ -187,6 +187,7 @@ def main():
         "cpu_baseline": cpu,
         "parity_sample": parity,
         "regions": n_regions_all,
+        "replayed_chunks": int(stats[-1]["n_replay"]),
         "phase_ms": {key: round(float(np.mean([s[key] for s in stats])), 3)
                      for key in ("ms_runs", "ms_scan", "ms_rescan", "ms_finish", "ms_total")},
         "setup_s": {"genome": round(t_gen, 2), "count": round(t_count, 3), "table": round(t_table, 3)},

@@ -170,6 +170,7 @@ typedef struct ks_scan_stats {
   int64_t n_regions;
   int64_t n_rescan;     /* rescan ranges processed */
   int32_t scan_algo;    /* 0 = lane per run, 1 = chunked carry scan */
+  int64_t n_replay;     /* chunks whose carry needed an exact replay */
 } ks_scan_stats;
 
 /* Span scan of device-resident sequences (the hot path).  visits_dev: device

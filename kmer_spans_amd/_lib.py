@@ -37,7 +37,8 @@ class ScanStats(C.Structure):
     _fields_ = [("ms_total", C.c_double), ("ms_runs", C.c_double), ("ms_scan", C.c_double),
                 ("ms_rescan", C.c_double), ("ms_finish", C.c_double), ("n_bases", C.c_int64),
                 ("n_scored", C.c_int64), ("n_runs", C.c_int64), ("n_regions", C.c_int64),
-                ("n_rescan", C.c_int64), ("scan_algo", C.c_int32)]
+                ("n_rescan", C.c_int64), ("scan_algo", C.c_int32),
+                ("n_replay", C.c_int64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

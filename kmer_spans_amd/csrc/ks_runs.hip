@@ -4,75 +4,35 @@
 // kmer_spans.c:111-132).  Here runs are materialised once per call so that
 // counting and scanning can parallelise over them: a run is a maximal
 // [a, b) of non-N bytes inside one sequence.  Boundaries are sparse (N gaps,
-// sequence ends), so the kernel emits (position, START/END) events with a
-// wave-aggregated atomic append and a radix sort restores position order;
+// sequence ends), so one streaming pass (16 bytes per lane-step, SWAR N test)
+// emits (position, START/END) events with a wave-aggregated atomic append,
+// a second tiny kernel splits runs at sequence boundaries, and a radix sort
+// restores position order;
 // END sorts before START at the same position (sequence boundary between two
 // non-N bytes), so the sorted events alternate START, END, START, ...
 #include <hipcub/hipcub.hpp>
+
+#include <algorithm>
 
 #include "ks_internal.h"
 
 namespace ks {
 namespace {
 
-constexpr int kTile = 4096;        // positions per block
-constexpr int kPerThread = 16;     // 256 threads x 16 bytes
+// Byte mask (bit i <-> byte i) of the N/n bytes of a 32-bit word: exact
+// per-byte zero test of (w | 0x20) ^ 'n'.
+__device__ __forceinline__ uint32_t n_mask4(uint32_t w) {
+  const uint32_t x = (w | 0x20202020u) ^ 0x6e6e6e6eu;
+  const uint32_t z = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;  // 0x80 in zero bytes
+  return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
 
-__device__ __forceinline__ bool bit_at(const uint32_t *m, int r) { return (m[r >> 5] >> (r & 31)) & 1u; }
-
-// Emits key = (p << 1) | is_start for every run START (first byte) and END
-// (one past the last byte) in positions [t0, t0 + kTile) intersect [0, total].
-__global__ void __launch_bounds__(256) k_run_events(const uint8_t *__restrict__ seq, int64_t total,
-                                                    const int64_t *__restrict__ offs, int32_t nseq,
-                                                    unsigned long long *__restrict__ ev,
-                                                    unsigned long long *__restrict__ ev_count,
-                                                    int64_t cap) {
-  __shared__ uint32_t bmask[kTile / 32 + 1];
-  const int64_t t0 = (int64_t)blockIdx.x * kTile;
-  for (int i = threadIdx.x; i < kTile / 32 + 1; i += blockDim.x) bmask[i] = 0;
-  __syncthreads();
-  if (threadIdx.x == 0) {  // sequence boundaries (offsets) falling in this tile
-    int lo = 0, hi = nseq + 1;
-    while (lo < hi) {
-      int mid = (lo + hi) >> 1;
-      if (offs[mid] < t0) lo = mid + 1; else hi = mid;
-    }
-    for (int q = lo; q <= nseq && offs[q] < t0 + kTile; ++q) {
-      const int r = (int)(offs[q] - t0);
-      bmask[r >> 5] |= 1u << (r & 31);
-    }
-  }
-  __syncthreads();
-
-  const int64_t p0 = t0 + (int64_t)threadIdx.x * kPerThread;
-  uint8_t b[kPerThread + 1];
-  b[0] = (p0 >= 1 && p0 - 1 < total) ? seq[p0 - 1] : (uint8_t)'N';
-  if (p0 + kPerThread <= total) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(seq + p0);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) b[j + 1] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
-  } else {
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) b[j + 1] = (p0 + j < total) ? seq[p0 + j] : (uint8_t)'N';
-  }
-  uint32_t starts = 0, ends = 0;  // bit j: event at p0 + j
-  int cnt = 0;
-  if (p0 <= total) {
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) {
-      const int64_t p = p0 + j;
-      if (p > total) break;
-      const bool v = (p < total) && !is_n(b[j + 1]);
-      const bool vp = (p >= 1) && !is_n(b[j]);
-      const bool bd = bit_at(bmask, (int)(p - t0));
-      if (v && (bd || !vp)) { starts |= 1u << j; ++cnt; }
-      if (vp && (bd || !v)) { ends |= 1u << j; ++cnt; }
-    }
-  }
-  // wave-aggregated append
-  const unsigned long long any = __ballot(cnt > 0);
-  if (any == 0) return;
+// Appends the events of `cnt` set bits of starts/ends (bit i <-> p0 + i).
+__device__ __forceinline__ void append_events(uint32_t starts, uint32_t ends, int64_t p0,
+                                              unsigned long long *__restrict__ ev,
+                                              unsigned long long *__restrict__ ev_count, int64_t cap) {
+  const int cnt = __popc(starts) + __popc(ends);
+  if (__ballot(cnt > 0) == 0) return;
   const int lane = threadIdx.x & 63;
   int incl = cnt;
 #pragma unroll
@@ -84,10 +44,69 @@ __global__ void __launch_bounds__(256) k_run_events(const uint8_t *__restrict__ 
   if (lane == 63) base = atomicAdd(ev_count, (unsigned long long)incl);
   base = __shfl(base, 63, 64);
   unsigned long long slot = base + (unsigned long long)(incl - cnt);
-  for (int j = 0; j < kPerThread; ++j) {
-    const unsigned long long p = (unsigned long long)(p0 + j);
-    if ((ends >> j) & 1u) { if ((int64_t)slot < cap) ev[slot] = (p << 1); ++slot; }
-    if ((starts >> j) & 1u) { if ((int64_t)slot < cap) ev[slot] = (p << 1) | 1ull; ++slot; }
+  while (ends | starts) {
+    const int je = ends ? __ffs(ends) - 1 : 99, js = starts ? __ffs(starts) - 1 : 99;
+    if (je <= js) {  // END sorts before START at the same position anyway
+      if ((int64_t)slot < cap) ev[slot] = ((unsigned long long)(p0 + je) << 1);
+      ends &= ends - 1;
+    } else {
+      if ((int64_t)slot < cap) ev[slot] = ((unsigned long long)(p0 + js) << 1) | 1ull;
+      starts &= starts - 1;
+    }
+    ++slot;
+  }
+}
+
+// N-transition events of the whole buffer read as one string with N before
+// position 0 and at position total: START at p (first non-N byte after an N),
+// END at p (first N after a non-N byte).  16 bytes per step, persistent grid.
+__global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ seq, int64_t total,
+                                                  unsigned long long *__restrict__ ev,
+                                                  unsigned long long *__restrict__ ev_count, int64_t cap) {
+  const int64_t nunits = total / 16 + 1;  // covers position total
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t u0 = (int64_t)blockIdx.x * blockDim.x; u0 < nunits; u0 += stride) {
+    const int64_t u = u0 + threadIdx.x;
+    uint32_t starts = 0, ends = 0;
+    const int64_t p0 = u * 16;
+    if (u < nunits) {
+      uint32_t nm = 0xffffu;
+      if (p0 + 16 <= total) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(seq + p0);
+        nm = n_mask4(v.x) | (n_mask4(v.y) << 4) | (n_mask4(v.z) << 8) | (n_mask4(v.w) << 12);
+      } else {
+        for (int j = 0; j < 16; ++j)
+          if (p0 + j < total && !is_n(seq[p0 + j])) nm &= ~(1u << j);
+      }
+      const uint32_t prev_n = (p0 == 0) ? 1u : (is_n(seq[p0 - 1]) ? 1u : 0u);
+      const uint32_t non = ~nm & 0xffffu;
+      starts = non & ((nm << 1) | prev_n);
+      ends = nm & ((non << 1) | (prev_n ^ 1u)) & 0xffffu;
+      if (p0 + 16 > total) {  // no events past position total
+        const int keep = (int)(total - p0) + 1;
+        const uint32_t km = keep >= 16 ? 0xffffu : ((1u << keep) - 1u);
+        starts &= km;
+        ends &= km;
+      }
+    }
+    append_events(starts, ends, p0, ev, ev_count, cap);
+  }
+}
+
+// Interior sequence boundaries between two non-N bytes split a run: END and
+// START at the boundary (emitted once per distinct offset).
+__global__ void k_seq_events(const uint8_t *__restrict__ seq, int64_t total, const int64_t *__restrict__ offs,
+                             int32_t nseq, unsigned long long *__restrict__ ev,
+                             unsigned long long *__restrict__ ev_count, int64_t cap) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < 1 || q >= nseq) return;
+  const int64_t p = offs[q];
+  if (offs[q - 1] == p || p <= 0 || p >= total) return;
+  if (is_n(seq[p - 1]) || is_n(seq[p])) return;
+  const unsigned long long slot = atomicAdd(ev_count, 2ull);
+  if ((int64_t)slot + 1 < cap) {
+    ev[slot] = ((unsigned long long)p << 1);
+    ev[slot + 1] = ((unsigned long long)p << 1) | 1ull;
   }
 }
 
@@ -117,7 +136,6 @@ ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
   unsigned long long *d_count = reinterpret_cast<unsigned long long *>(scal);
-  const int64_t nblocks = (total + 1 + kTile - 1) / kTile;
   int64_t cap = 1 << 20;
   if (ctx->slots[SLOT_EVENTS].bytes / 8 > (size_t)cap) cap = ctx->slots[SLOT_EVENTS].bytes / 8;
   unsigned long long n_ev = 0;
@@ -125,9 +143,16 @@ ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs
     void *evp = nullptr;
     KS_TRY(ensure(ctx, SLOT_EVENTS, (size_t)cap * 8, &evp));
     KS_HIP(hipMemsetAsync(d_count, 0, 8, st));
-    hipLaunchKernelGGL(k_run_events, dim3((unsigned)nblocks), dim3(256), 0, st, s->seq, total,
-                       s->offsets_dev, s->nseq, (unsigned long long *)evp, d_count, cap);
+    const int64_t nunits = total / 16 + 1;
+    const unsigned grid = (unsigned)std::min<int64_t>((nunits + 255) / 256, (int64_t)ctx->num_cus * 16);
+    hipLaunchKernelGGL(k_n_events, dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp,
+                       d_count, cap);
     KS_HIP(hipGetLastError());
+    if (s->nseq > 1) {
+      hipLaunchKernelGGL(k_seq_events, dim3((unsigned)((s->nseq + 255) / 256)), dim3(256), 0, st, s->seq, total,
+                         s->offsets_dev, s->nseq, (unsigned long long *)evp, d_count, cap);
+      KS_HIP(hipGetLastError());
+    }
     KS_HIP(hipMemcpyAsync(&n_ev, d_count, 8, hipMemcpyDeviceToHost, st));
     KS_HIP(hipStreamSynchronize(st));
     if ((int64_t)n_ev <= cap) break;

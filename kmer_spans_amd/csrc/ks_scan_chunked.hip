@@ -60,10 +60,10 @@ struct P1 {  // per-chunk results of the gather pass
   uint8_t *special;      // a non-finite value occurred
 };
 
-struct Summ {  // binade-integer summaries (P2)
-  int32_t *e;  // binade exponent, INT32_MIN: no summary
-  long long *D, *M, *N;  // [2 * nch] (entry parity 0/1)
-  int32_t *A;            // [2 * nch]
+struct Summ {  // binade-integer summaries for the predicted binade (P2)
+  int32_t *e;             // binade, INT32_MIN: none
+  long long *D, *M, *N;   // [2 * nch] by entry parity
+  int32_t *A;             // [2 * nch]
 };
 
 struct Carry {  // P3/P4
@@ -125,18 +125,20 @@ __device__ __forceinline__ double value_at(const Chunks &g, const uint8_t *__res
 
 // ------------------------------------------------------------------- P0
 
-__global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__restrict__ rb,
-                              const int64_t *__restrict__ cbase, int64_t nruns, int k, Chunks g) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nruns) return;
-  const int64_t lo = ra[r] + k, hi = rb[r] - 1;
-  if (hi < lo) return;
-  int64_t c = cbase[r];
-  for (int64_t p = lo; p <= hi; p += CH, ++c) {
-    g.start[c] = p;
-    g.n[c] = (int32_t)min((int64_t)CH, hi - p + 1);
-    g.run[c] = (int32_t)r;
+__global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase, int64_t nruns,
+                              int k, const int64_t *__restrict__ rbnd, Chunks g) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= g.nch) return;
+  int64_t lo = 0, hi = nruns - 1;  // last run with cbase[r] <= c
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (cbase[mid] <= c) lo = mid; else hi = mid - 1;
   }
+  const int64_t first = ra[lo] + k + (c - cbase[lo]) * CH;
+  const int64_t last = rbnd[lo] - 1;
+  g.start[c] = first;
+  g.n[c] = (int32_t)min((int64_t)CH, last - first + 1);
+  g.run[c] = (int32_t)lo;
 }
 
 // ------------------------------------------------------------------- P1
@@ -265,66 +267,38 @@ __global__ void __launch_bounds__(256) k_pass1(Chunks g, const uint8_t *__restri
   }
 }
 
-// ------------------------------------------------------------------- P2
+// ------------------------------------------------------------------- P3
 
-// Approximate max-plus scan, one wave per run: chunk j maps x -> max(x + a, b)
-// (a = sum, b = clean exit); x~_j = composite of chunks < j applied to 0.
-__global__ void __launch_bounds__(64) k_approx_scan(const int64_t *__restrict__ cbase, int64_t nruns,
-                                                    P1 o, double *__restrict__ xt) {
-  const int64_t r = blockIdx.x;
-  if (r >= nruns) return;
-  const int lane = threadIdx.x;
-  const int64_t c0 = cbase[r], c1 = cbase[r + 1];
-  double carry = 0.0;
-  for (int64_t cb = c0; cb < c1; cb += 64) {
-    const int64_t c = cb + lane;
-    double a = 0.0, b = -INFINITY;  // identity
-    if (c < c1) {
-      a = o.special[c] ? -INFINITY : o.asum[c];
-      b = o.cexit[c];
-    }
-    // inclusive scan: (a1,b1) then (a2,b2) = (a1 + a2, max(b1 + a2, b2))
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const double pa = __shfl_up(a, d, 64), pb = __shfl_up(b, d, 64);
-      if (lane >= d) {
-        b = fmax(pb + a, b);
-        a = pa + a;
-      }
-    }
-    double ea = __shfl_up(a, 1, 64), eb = __shfl_up(b, 1, 64);
-    if (lane == 0) { ea = 0.0; eb = -INFINITY; }
-    if (c < c1) xt[c] = fmax(carry + ea, eb);
-    const double la = __shfl(a, 63, 64), lb = __shfl(b, 63, 64);
-    carry = fmax(carry + la, lb);
-    if (!(carry == carry)) carry = 0.0;  // NaN guard: only a prediction
-  }
+// Bits of a positive normal double in binade e: x = m * 2^(e-52), m in [2^52, 2^53).
+__device__ __forceinline__ int binade_of(double x) {
+  return (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
+}
+__device__ __forceinline__ long long mant_of(double x) {
+  return (__double_as_longlong(x) & ((1LL << 52) - 1)) | (1LL << 52);
+}
+__device__ __forceinline__ double from_mant(long long m, int e) {
+  return __longlong_as_double(((long long)(e + 1023) << 52) | (m - (1LL << 52)));
 }
 
-// Binade-integer summary of the chunk for the binade its predicted
-// trajectory lies in (lane per chunk).
+// Binade-integer summary of chunk c for binade e: with S = m * 2^(e-52) and
+// the whole trajectory inside [2^e, 2^(e+1)), fl(S + s) = S + RN(s * 2^(52-e))
+// with ties to even decided by the parity of m.  For both entry parities t:
+// total D, max M (first argmax A) and min N of the integer trajectory.
+// Returns false if a value is not representable (overflow, NaN, Inf).
 template <bool kCompressed>
-__global__ void __launch_bounds__(256) k_summaries(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
-                                                   int k, TableView tv, const uint16_t *__restrict__ codes,
-                                                   P1 o, const double *__restrict__ xt, Summ sm) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= g.nch) return;
-  sm.e[c] = INT32_MIN;
-  if (o.special[c]) return;
-  const double x = xt[c];
-  if (!(x >= 4096.0) || !(x < 1e18)) return;
-  int E;
-  frexp(x, &E);
-  const int e = E - 1;  // x in [2^e, 2^(e+1))
-  const double lo = fmin(x, x + o.pmin[c]), hi = fmax(x, x + o.pmax[c]);
-  const double slack = ldexp(1.0, e - 30) + o.sabs[c] * 1e-9;
-  if (!(lo - slack >= ldexp(1.0, e)) || !(hi + slack < ldexp(1.0, e + 1))) return;
+__device__ bool chunk_summary(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
+                              const TableView &tv, const uint16_t *__restrict__ codes, int64_t c, int e,
+                              long long D[2], long long M[2], int A[2], long long N[2]) {
   const int n = g.n[c];
   const int64_t start = g.start[c];
   const uint32_t mask = (1u << (2 * k)) - 1u;
+  const double scale = ldexp(1.0, 52 - e);
   uint32_t code = kCompressed ? 0u : prime_code(seq, start - k, k);
-  long long cur[2] = {0, 0}, M[2] = {LLONG_MIN, LLONG_MIN}, N[2] = {LLONG_MAX, LLONG_MAX};
-  int A[2] = {0, 0};
+  long long cur[2] = {0, 0};
+  M[0] = M[1] = LLONG_MIN;
+  N[0] = N[1] = LLONG_MAX;
+  A[0] = A[1] = 0;
+  bool ok = true;
   for (int b0 = 0; b0 < n; b0 += NB) {
     double v[NB];
     if (kCompressed) {
@@ -346,153 +320,234 @@ __global__ void __launch_bounds__(256) k_summaries(Chunks g, const uint8_t *__re
     for (int j = 0; j < NB; ++j) {
       const int i = b0 + j;
       if (i < n) {
-        const double y = ldexp(v[j], 52 - e);  // exact (power-of-two scaling)
+        const double y = v[j] * scale;  // exact: power-of-two scaling
+        ok &= fabs(y) < 4.0e18;         // also false for NaN / Inf
         const double fq = floor(y);
-        const double f = y - fq;               // exact fractional part
-        const long long q = (long long)fq;
-        const bool up = f > 0.5;
-        const bool tie = f == 0.5;
+        const double f = y - fq;        // exact fractional part
+        const long long q = ok ? (long long)fq : 0;
+        const bool up = f > 0.5, tie = f == 0.5;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const long long par = (t + cur[t]) & 1;            // parity of the current m
-          const long long d = q + ((up || (tie && ((par + q) & 1))) ? 1 : 0);
-          cur[t] += d;
+          const long long par = (t + cur[t]) & 1;
+          cur[t] += q + ((up || (tie && ((par + q) & 1))) ? 1 : 0);
           if (cur[t] > M[t]) { M[t] = cur[t]; A[t] = i; }
           N[t] = min(N[t], cur[t]);
         }
       }
     }
   }
+  D[0] = cur[0];
+  D[1] = cur[1];
+  return ok;
+}
+
+// ------------------------------------------------------------------- P2
+
+// Approximate max-plus scan, one wave per run: chunk j maps x -> max(x + a, b)
+// (a = sum, b = clean exit); x~_j = composite of chunks < j applied to 0.  Only
+// a prediction (which binade the exact carry will be in); never trusted.
+__global__ void __launch_bounds__(64) k_approx_scan(const int64_t *__restrict__ cbase, int64_t nruns, P1 o,
+                                                    double *__restrict__ xt) {
+  const int64_t r = blockIdx.x;
+  if (r >= nruns) return;
+  const int lane = threadIdx.x;
+  const int64_t c0 = cbase[r], c1 = cbase[r + 1];
+  double carry = 0.0;
+  for (int64_t cb = c0; cb < c1; cb += 64) {
+    const int64_t c = cb + lane;
+    double a = 0.0, b = -INFINITY;  // identity
+    if (c < c1) {
+      a = o.special[c] ? -INFINITY : o.asum[c];
+      b = o.cexit[c];
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {  // (a1,b1) then (a2,b2) = (a1+a2, max(b1+a2, b2))
+      const double pa = __shfl_up(a, d, 64), pb = __shfl_up(b, d, 64);
+      if (lane >= d) {
+        b = fmax(pb + a, b);
+        a = pa + a;
+      }
+    }
+    double ea = __shfl_up(a, 1, 64), eb = __shfl_up(b, 1, 64);
+    if (lane == 0) { ea = 0.0; eb = -INFINITY; }
+    if (c < c1) xt[c] = fmax(carry + ea, eb);
+    const double la = __shfl(a, 63, 64), lb = __shfl(b, 63, 64);
+    carry = fmax(carry + la, lb);
+    if (!(carry == carry)) carry = 0.0;
+  }
+}
+
+// Largest value of the predicted trajectory that keeps a binade summary
+// meaningful; below kLMin the trajectory crosses binades every few steps.
+constexpr double kLMin = 64.0;
+
+// Summary of each chunk for the binade of its predicted trajectory (lane per
+// chunk, full occupancy); chunks predicted to leave the binade or to approach
+// 0 get none.
+template <bool kCompressed>
+__global__ void __launch_bounds__(256) k_summaries(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
+                                                   TableView tv, const uint16_t *__restrict__ codes, P1 o,
+                                                   const double *__restrict__ xt, Summ sm) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= g.nch) return;
+  sm.e[c] = INT32_MIN;
+  if (o.special[c]) return;
+  const double x = xt[c];
+  if (!(x >= kLMin) || !(x < 1.0e18)) return;
+  const int e = (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
+  const double lo = fmin(x, x + o.pmin[c]), hi = fmax(x, x + o.pmax[c]);
+  const double slack = ldexp(1.0, e - 24) + o.sabs[c] * 1e-9;
+  if (!(lo - slack >= ldexp(1.0, e)) || !(hi + slack < ldexp(1.0, e + 1))) return;
+  long long D[2], M[2], N[2];
+  int A[2];
+  if (!chunk_summary<kCompressed>(g, seq, total, k, tv, codes, c, e, D, M, A, N)) return;
   sm.e[c] = e;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    sm.D[2 * c + t] = cur[t];
+    sm.D[2 * c + t] = D[t];
     sm.M[2 * c + t] = M[t];
     sm.N[2 * c + t] = N[t];
     sm.A[2 * c + t] = A[t];
   }
 }
 
-// ------------------------------------------------------------------- P3
-
-__device__ __forceinline__ bool summary_step(const Summ &sm, int64_t c, double x, long long *m0_out,
-                                             int *par_out) {
-  const int e = sm.e[c];
-  if (e == INT32_MIN) return false;
-  int E;
-  frexp(x, &E);
-  if (E - 1 != e) return false;
-  const long long m0 = (long long)ldexp(x, 52 - e);  // exact integer in [2^52, 2^53)
-  const int par = (int)(m0 & 1);
-  const long long lo = m0 + sm.N[2 * c + par], hi = m0 + sm.M[2 * c + par];
-  if (lo < (1LL << 52) + 1 || hi > (1LL << 53) - 2) return false;
-  *m0_out = m0;
-  *par_out = par;
-  return true;
+// Exact carry, one wave per run, walking 64-chunk tiles (lane j <-> chunk
+// cb + j).  Per chunk, in order: entry 0 -> clean exit (CLEAN); a binade
+// summary valid for the exact entry -> integer step (L; the summaries of the
+// tile's lanes are computed wave-parallel, once per binade); a certain clamp
+// (x + minprefix < -margin) -> clean exit (R); else exact replay (U).  The
+// chain is wave-uniform; L chunks also get their head (max/argmax) here.
+// Wave-uniform broadcast of lane j's value (v_readlane: a VALU op, unlike a
+// variable-lane __shfl which goes through ds_bpermute).
+__device__ __forceinline__ int rl32(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
+__device__ __forceinline__ long long rl64(long long v, int j) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(v & 0xffffffff), j);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(v >> 32), j);
+  return (long long)(((unsigned long long)hi << 32) | lo);
 }
+__device__ __forceinline__ double rld(double v, int j) { return __longlong_as_double(rl64(__double_as_longlong(v), j)); }
 
-// Exact carry, one wave per run.  The per-chunk inputs of 64 chunks are
-// staged in LDS by the whole wave (coalesced), then every lane walks the
-// chain redundantly (wave-uniform values; the lanes are needed together only
-// for the cooperative loads of a replayed chunk).
+// Exact carry, one wave per run, walking 64-chunk tiles (lane j <-> chunk
+// cb + j, its inputs in registers, broadcast with v_readlane).  Per chunk, in
+// order: entry 0 -> clean exit (CLEAN); the chunk's precomputed binade summary
+// is for the exact entry's binade and its integer trajectory stays inside ->
+// integer step (L, also yields the head); a certain clamp (x + minprefix <
+// -margin) -> clean exit (R); else exact replay (U): the wave loads the 256
+// values into registers (4 per lane) and walks them with readlane.
 template <bool kCompressed>
 __global__ void __launch_bounds__(64) k_carry(Chunks g, const int64_t *__restrict__ cbase, int64_t nruns,
-                                              const uint8_t *__restrict__ seq, int k, TableView tv,
+                                              const uint8_t *__restrict__ seq, int64_t total, int k, TableView tv,
                                               const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
-                                              unsigned long long *__restrict__ nreplay) {
-  __shared__ double vals[CH];
-  __shared__ double b_cexit[64], b_pmin[64], b_sabs[64];
-  __shared__ long long b_D[2][64], b_N[2][64], b_M[2][64];
-  __shared__ int b_e[64], b_spec[64];
-  __shared__ double b_x[64];
-  __shared__ uint8_t b_mode[64];
+                                              unsigned long long *__restrict__ nreplay,
+                                              long long *__restrict__ dbg) {
   const int64_t r = blockIdx.x;
   if (r >= nruns) return;
   const int lane = threadIdx.x;
   const int64_t c0 = cbase[r], c1 = cbase[r + 1];
   double x = 0.0;
   unsigned long long replays = 0;
+  const long long t_start = dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
+  long long n_l = 0, n_r = 0;
   for (int64_t cb = c0; cb < c1; cb += 64) {
-    {
-      const int64_t c = cb + lane;
-      if (c < c1) {
-        b_cexit[lane] = o.cexit[c];
-        b_pmin[lane] = o.pmin[c];
-        b_sabs[lane] = o.sabs[c];
-        b_spec[lane] = o.special[c];
-        const int e = sm.e[c];
-        b_e[lane] = e;
-        if (e != INT32_MIN) {
+    const int64_t c = cb + lane;
+    const bool live = c < c1;
+    const double l_exit = live ? o.cexit[c] : 0.0;
+    const double l_pmin = live ? o.pmin[c] : 0.0;
+    const double l_sabs = live ? o.sabs[c] : 0.0;
+    const int l_spec = live ? o.special[c] : 1;
+    const int l_n = live ? g.n[c] : 0;
+    const int se = live ? sm.e[c] : INT32_MIN;
+    long long D[2] = {0, 0}, M[2] = {0, 0}, N[2] = {0, 0};
+    int A[2] = {0, 0};
+    if (se != INT32_MIN) {
 #pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            b_D[t][lane] = sm.D[2 * c + t];
-            b_N[t][lane] = sm.N[2 * c + t];
-            b_M[t][lane] = sm.M[2 * c + t];
-          }
-        }
+      for (int t = 0; t < 2; ++t) {
+        D[t] = sm.D[2 * c + t];
+        M[t] = sm.M[2 * c + t];
+        N[t] = sm.N[2 * c + t];
+        A[t] = sm.A[2 * c + t];
       }
     }
-    __syncthreads();
     const int nb = (int)min((int64_t)64, c1 - cb);
+    double my_x = 0.0, my_hmax = -1.0;
+    int my_mode = kModeClean, my_harg = 0;
     for (int j = 0; j < nb; ++j) {
-      b_x[j] = x;
-      int mode;
+      const double cj_exit = rld(l_exit, j);
+      if (lane == j) my_x = x;
+      int mode = kModeU;
       bool done = false;
       if (x == 0.0) {
         mode = kModeClean;
-        x = b_cexit[j];
+        x = cj_exit;
         done = true;
-      }
-      if (!done && b_e[j] != INT32_MIN) {  // binade-integer summary
-        const int e = b_e[j];
-        int E;
-        frexp(x, &E);
-        if (E - 1 == e) {
-          const long long m0 = (long long)ldexp(x, 52 - e);
-          const int par = (int)(m0 & 1);
-          const long long lo = m0 + b_N[par][j], hi = m0 + b_M[par][j];
-          if (lo >= (1LL << 52) + 1 && hi <= (1LL << 53) - 2) {
-            mode = kModeL;
-            x = ldexp((double)(m0 + b_D[par][j]), e - 52);
-            done = true;
+      } else if (x >= kLMin && x < 1.0e18 && rl32(se, j) == binade_of(x)) {
+        const int e = binade_of(x);
+        const long long m0 = mant_of(x);
+        const int par = (int)(m0 & 1);
+        const long long Nj = rl64(par ? N[1] : N[0], j), Mj = rl64(par ? M[1] : M[0], j);
+        if (m0 + Nj >= (1LL << 52) + 1 && m0 + Mj <= (1LL << 53) - 2) {
+          const long long Dj = rl64(par ? D[1] : D[0], j);
+          mode = kModeL;
+          if (lane == j) {
+            my_hmax = from_mant(m0 + Mj, e);
+            my_harg = par ? A[1] : A[0];
           }
+          x = from_mant(m0 + Dj, e);
+          done = true;
         }
       }
-      if (!done && !b_spec[j] && x + b_pmin[j] < -ldexp(fabs(x) + b_sabs[j], -40)) {
+      if (!done && !rl32(l_spec, j) && x + rld(l_pmin, j) < -ldexp(fabs(x) + rld(l_sabs, j), -40)) {
         mode = kModeR;  // certain clamp -> coincides with the clean trajectory
-        x = b_cexit[j];
+        x = cj_exit;
         done = true;
       }
-      if (!done) {  // exact replay of the chunk from x
+      if (!done) {  // exact replay of chunk cb + j from x
         mode = kModeU;
         ++replays;
-        const int64_t c = cb + j;
-        const int n = g.n[c];
-        __syncthreads();
-        for (int i = lane; i < n; i += 64) vals[i] = value_at(g, seq, k, tv, kCompressed ? codes : nullptr, c, i);
-        __syncthreads();
+        const int64_t cj = cb + j;
+        const int n = rl32(l_n, j);
+        double v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = lane + 64 * q;
+          v[q] = i < n ? value_at(g, seq, k, tv, kCompressed ? codes : nullptr, cj, i) : 0.0;
+        }
         double T = x;
         bool clamped = false;
-        for (int i = 0; i < n; ++i) {
-          const double t = T + vals[i];
-          T = t > 0 ? t : 0.0;
-          if (T == 0.0) { clamped = true; break; }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          for (int i = 0; i < 64 && !clamped; ++i) {
+            if (64 * q + i >= n) break;
+            const double t = T + rld(v[q], i);
+            T = t > 0 ? t : 0.0;
+            clamped = T == 0.0;
+          }
         }
-        x = clamped ? b_cexit[j] : T;
+        x = clamped ? cj_exit : T;
       }
-      b_mode[j] = (uint8_t)mode;
+      if (lane == j) my_mode = mode;
+      n_l += mode == kModeL;
+      n_r += mode == kModeR;
     }
-    __syncthreads();
-    {
-      const int64_t c = cb + lane;
-      if (c < c1) {
-        cr.x[c] = b_x[lane];
-        cr.mode[c] = b_mode[lane];
+    if (live) {
+      cr.x[c] = my_x;
+      cr.mode[c] = (uint8_t)my_mode;
+      if (my_mode == kModeL) {
+        cr.hq[c] = -1;
+        cr.hmax[c] = my_hmax;
+        cr.harg[c] = my_harg;
       }
     }
-    __syncthreads();
   }
   if (lane == 0 && replays) atomicAdd(nreplay, replays);
+  if (dbg && lane == 0) {
+    dbg[6 * r + 0] = (long long)__builtin_amdgcn_s_memtime() - t_start;
+    dbg[6 * r + 1] = c1 - c0;
+    dbg[6 * r + 2] = (long long)replays;
+    dbg[6 * r + 3] = 0;
+    dbg[6 * r + 4] = n_l;
+    dbg[6 * r + 5] = n_r;
+  }
 }
 
 // ------------------------------------------------------------------- P4
@@ -500,23 +555,16 @@ __global__ void __launch_bounds__(64) k_carry(Chunks g, const int64_t *__restric
 template <bool kCompressed>
 __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
                                                int k, TableView tv, const uint16_t *__restrict__ codes,
-                                               Summ sm, Carry cr, unsigned int *__restrict__ err) {
+                                               Carry cr, unsigned int *__restrict__ err) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
   const int mode = cr.mode[c];
+  if (mode == kModeL) return;  // head written by the carry from the summary
   cr.hq[c] = -1;
   cr.hmax[c] = -1.0;
   cr.harg[c] = 0;
   if (mode == kModeClean) return;
   const double x = cr.x[c];
-  if (mode == kModeL) {
-    long long m0;
-    int par;
-    if (!summary_step(sm, c, x, &m0, &par)) { atomicOr(err, 1u); return; }
-    cr.hmax[c] = ldexp((double)(m0 + sm.M[2 * c + par]), sm.e[c] - 52);
-    cr.harg[c] = sm.A[2 * c + par];
-    return;
-  }
   const int n = g.n[c];
   const int64_t start = g.start[c];
   const uint32_t mask = (1u << (2 * k)) - 1u;
@@ -572,19 +620,57 @@ __device__ __forceinline__ void emit(const RegionBuf &rb, const Rescan &rs, int3
   }
 }
 
-// Stitch, one wave per run: the wave stages 64 chunks' fragments in LDS,
-// lane 0 walks them in order (candidates in begin order), emitting regions
-// and rescan ranges.
+// Stitch as a segmented scan, one wave per run.  Chunk c acts on the open
+// excursion state by one of: RESET(tail or none) -- an excursion closes in the
+// chunk and/or its clean tail opens a new one -- or EXTEND(head) -- the carried
+// excursion takes the chunk's head maximum (first argmax: a later head wins
+// only when strictly greater).  The operator is associative, so 64 chunks are
+// combined per step with shuffles; the chunk that closes an excursion emits it.
+struct XState {
+  int reset;  // 1: RESET to (open, xb, xm, xa); 0: EXTEND by (xm, xa)
+  int open;
+  long long xb, xa;
+  double xm;
+};
+
+__device__ __forceinline__ XState x_compose(const XState &f1, const XState &f2) {  // f1 then f2
+  if (f2.reset) return f2;
+  XState r = f1;
+  if (f2.xm > f1.xm) { r.xm = f2.xm; r.xa = f2.xa; }
+  return r;
+}
+
+__device__ __forceinline__ XState x_shfl_up(const XState &a, int d) {
+  XState r;
+  r.reset = __shfl_up(a.reset, d, 64);
+  r.open = __shfl_up(a.open, d, 64);
+  r.xb = __shfl_up(a.xb, d, 64);
+  r.xa = __shfl_up(a.xa, d, 64);
+  r.xm = __shfl_up(a.xm, d, 64);
+  return r;
+}
+
+__device__ __forceinline__ XState x_shfl(const XState &a, int l) {
+  XState r;
+  r.reset = __shfl(a.reset, l, 64);
+  r.open = __shfl(a.open, l, 64);
+  r.xb = __shfl(a.xb, l, 64);
+  r.xa = __shfl(a.xa, l, 64);
+  r.xm = __shfl(a.xm, l, 64);
+  return r;
+}
+
+// First scan index at which a candidate or tail of the chunk is valid: after
+// the carried head's clamp, or nowhere when the carried excursion spans it.
+__device__ __forceinline__ int64_t valid_from(int mode, int hq, int64_t st, int64_t en) {
+  if (mode == kModeClean) return st;
+  return hq >= 0 ? st + hq + 1 : en;
+}
+
 __global__ void __launch_bounds__(64) k_stitch(Chunks g, const int64_t *__restrict__ cbase, int64_t nruns,
                                                const int64_t *__restrict__ rb_end, const int32_t *__restrict__ rseq,
-                                               int k, P1 o, Carry cr, Cand cand, int64_t ncand,
-                                               const int32_t *__restrict__ corder, uint64_t mw,
-                                               double min_score, RegionBuf out, Rescan rs,
-                                               unsigned int *__restrict__ err) {
-  __shared__ int64_t b_st[64];
-  __shared__ int32_t b_n[64], b_hq[64], b_harg[64], b_tbeg[64], b_targ[64];
-  __shared__ double b_hmax[64], b_tmax[64];
-  __shared__ uint8_t b_mode[64];
+                                               int k, P1 o, Carry cr, uint64_t mw, double min_score, RegionBuf out,
+                                               Rescan rs, unsigned int *__restrict__ err) {
   const int64_t r = blockIdx.x;
   if (r >= nruns) return;
   const int lane = threadIdx.x;
@@ -592,74 +678,78 @@ __global__ void __launch_bounds__(64) k_stitch(Chunks g, const int64_t *__restri
   if (c0 == c1) return;
   const int32_t sid = rseq[r];
   const int64_t last = rb_end[r] - 1;
-  int64_t cp = 0;
-  if (lane == 0) {  // first candidate of this run (candidates sorted by begin)
-    const int64_t first_pos = g.start[c0];
-    int64_t lo = 0, hi = ncand;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (cand.beg[corder[mid]] < first_pos) lo = mid + 1; else hi = mid;
-    }
-    cp = lo;
-  }
-  bool open = false, bad = false;
-  int64_t xb = 0, xa = 0;
-  double xm = 0.0;
+  XState carry{1, 0, 0, 0, -1.0};  // state entering the tile: closed
   for (int64_t cb = c0; cb < c1; cb += 64) {
     const int64_t c = cb + lane;
-    if (c < c1) {
-      b_st[lane] = g.start[c];
-      b_n[lane] = g.n[c];
-      b_mode[lane] = cr.mode[c];
-      b_hq[lane] = cr.hq[c];
-      b_hmax[lane] = cr.hmax[c];
-      b_harg[lane] = cr.harg[c];
-      b_tbeg[lane] = o.tbeg[c];
-      b_tmax[lane] = o.tmax[c];
-      b_targ[lane] = o.targ[c];
-    }
-    __syncthreads();
-    if (lane == 0 && !bad) {
-      const int nb = (int)min((int64_t)64, c1 - cb);
-      for (int j = 0; j < nb && !bad; ++j) {
-        const int64_t st = b_st[j];
-        const int64_t en = st + b_n[j];
-        int64_t valid_from = st;  // candidates / tail must begin at or after this
-        bool tail_ok = true;
-        if (b_mode[j] != kModeClean) {
-          if (!open) { bad = true; atomicOr(err, 4u); break; }
-          const int hq = b_hq[j];
-          if (hq != 0 && b_hmax[j] > xm) { xm = b_hmax[j]; xa = st + b_harg[j]; }
-          if (hq >= 0) {
-            const int64_t rpos = st + hq;
-            if ((uint64_t)(xa - xb) >= mw && xm >= min_score) emit(out, rs, sid, k, xb, xa, xm, rpos);
-            open = false;
-            valid_from = rpos + 1;
-          } else {
-            valid_from = en;  // the carried excursion covers the whole chunk
-            tail_ok = false;
-          }
-        }
-        while (cp < ncand) {
-          const int32_t q = corder[cp];
-          const int64_t b = cand.beg[q];
-          if (b >= en) break;
-          if (b >= valid_from) emit(out, rs, sid, k, b, cand.arg[q], cand.best[q], cand.rst[q]);
-          ++cp;
-        }
-        if (tail_ok && b_tbeg[j] >= 0 && st + b_tbeg[j] >= valid_from) {
-          if (open) { bad = true; atomicOr(err, 8u); break; }
-          open = true;
-          xb = st + b_tbeg[j];
-          xa = st + b_targ[j];
-          xm = b_tmax[j];
-        }
+    const bool live = c < c1;
+    XState f{0, 0, 0, 0, -INFINITY};  // identity
+    bool closes = false;
+    int64_t st = 0, close_pos = 0;
+    double hmax = -INFINITY;
+    int64_t harg = 0;
+    if (live) {
+      st = g.start[c];
+      const int64_t en = st + g.n[c];
+      const int mode = cr.mode[c];
+      const int hq = cr.hq[c];
+      const int tb = o.tbeg[c];
+      const int64_t vf = valid_from(mode, hq, st, en);
+      if (mode != kModeClean && hq != 0) { hmax = cr.hmax[c]; harg = st + cr.harg[c]; }
+      closes = mode != kModeClean && hq >= 0;
+      close_pos = st + hq;
+      const bool opens = tb >= 0 && st + tb >= vf && !(mode != kModeClean && hq < 0);
+      if (opens) {
+        f = XState{1, 1, st + tb, st + o.targ[c], o.tmax[c]};
+      } else if (closes) {
+        f = XState{1, 0, 0, 0, -1.0};
+      } else if (mode != kModeClean) {
+        f = XState{0, 0, 0, harg, hmax};
       }
     }
-    __syncthreads();
+    // inclusive scan of the chunk operators
+    XState inc = f;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const XState p = x_shfl_up(inc, d);
+      if (lane >= d) inc = x_compose(p, inc);
+    }
+    XState exc = x_shfl_up(inc, 1);
+    if (lane == 0) exc = XState{0, 0, 0, 0, -INFINITY};
+    const XState in = x_compose(carry, exc);  // state entering chunk c (a RESET)
+    if (live && closes) {
+      if (!in.open) {
+        atomicOr(err, 4u);
+      } else {
+        double xm = in.xm;
+        long long xa = in.xa;
+        if (hmax > xm) { xm = hmax; xa = harg; }
+        if ((uint64_t)(xa - in.xb) >= mw && xm >= min_score) emit(out, rs, sid, k, in.xb, xa, xm, close_pos);
+      }
+    }
+    if (live && !closes && f.reset == 0 && (cr.mode[c] != kModeClean) && !in.open) atomicOr(err, 8u);
+    carry = x_compose(carry, x_shfl(inc, 63));
   }
-  if (lane == 0 && !bad && open && (uint64_t)(xa - xb) >= mw && xm >= min_score)
-    emit(out, rs, sid, k, xb, xa, xm, last);
+  if (lane == 0 && carry.open && (uint64_t)(carry.xa - carry.xb) >= mw && carry.xm >= min_score)
+    emit(out, rs, sid, k, carry.xb, carry.xa, carry.xm, last);
+}
+
+// Candidates (closed emittable excursions of the clean trajectories) are
+// valid when they begin at or after their chunk's valid_from.
+__global__ void k_candidates(Chunks g, const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase,
+                             int64_t nruns, const int32_t *__restrict__ rseq, int k, Cand cand, int64_t ncand,
+                             Carry cr, RegionBuf out, Rescan rs) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ncand) return;
+  const int64_t b = cand.beg[i];
+  int64_t lo = 0, hi = nruns - 1;  // last run with ra <= b
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (ra[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const int64_t c = cbase[lo] + (b - (ra[lo] + k)) / CH;
+  const int64_t st = g.start[c];
+  if (b >= valid_from(cr.mode[c], cr.hq[c], st, st + g.n[c]))
+    emit(out, rs, rseq[lo], k, b, cand.arg[i], cand.best[i], cand.rst[i]);
 }
 
 }  // namespace
@@ -741,8 +831,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
             cnts, ccap};
 
   KS_HIP(hipEventRecord(ctx->ev[7], st));
-  hipLaunchKernelGGL(k_make_chunks, dim3((unsigned)((nruns + 255) / 256)), dim3(256), 0, st, runs.a, runs.b,
-                     d_cbase, nruns, k, g);
+  hipLaunchKernelGGL(k_make_chunks, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, st, runs.a, d_cbase,
+                     nruns, k, runs.b, g);
   KS_HIP(hipGetLastError());
   const unsigned gch = (unsigned)((nch + 255) / 256);
   hipEvent_t e_p1a, e_p1b;
@@ -761,64 +851,71 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
 #undef KS_P1
   KS_HIP(hipGetLastError());
   KS_HIP(hipEventRecord(e_p1b, st));
+  // KS_DEBUG_CARRY=1: per-run carry statistics to stderr (diagnostics only)
+  static const bool dbg_on = getenv("KS_DEBUG_CARRY") != nullptr;
+  long long *dbg = nullptr;
+  if (dbg_on) KS_HIP(hipMalloc(&dbg, nruns * 6 * sizeof(long long)));
   hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)nruns), dim3(64), 0, st, d_cbase, nruns, p1, xt);
   KS_HIP(hipGetLastError());
   if (comp)
     hipLaunchKernelGGL(k_summaries<true>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, p1, xt, sm);
   else
-    hipLaunchKernelGGL(k_summaries<false>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, p1, xt,
-                       sm);
+    hipLaunchKernelGGL(k_summaries<false>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, p1, xt, sm);
   KS_HIP(hipGetLastError());
   if (comp)
-    hipLaunchKernelGGL(k_carry<true>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, k, tv,
-                       codes, p1, sm, cr, cnts + 2);
+    hipLaunchKernelGGL(k_carry<true>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, total, k,
+                       tv, codes, p1, sm, cr, cnts + 2, dbg);
   else
-    hipLaunchKernelGGL(k_carry<false>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, k, tv,
-                       codes, p1, sm, cr, cnts + 2);
+    hipLaunchKernelGGL(k_carry<false>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, total, k,
+                       tv, codes, p1, sm, cr, cnts + 2, dbg);
   KS_HIP(hipGetLastError());
   unsigned int *d_err = reinterpret_cast<unsigned int *>(cnts + 3);
   if (comp)
-    hipLaunchKernelGGL(k_heads<true>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, sm, cr, d_err);
+    hipLaunchKernelGGL(k_heads<true>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, cr, d_err);
   else
-    hipLaunchKernelGGL(k_heads<false>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, sm, cr,
-                       d_err);
+    hipLaunchKernelGGL(k_heads<false>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, cr, d_err);
   KS_HIP(hipGetLastError());
-  // candidates: order by begin position
   unsigned long long hc[4] = {0, 0, 0, 0};
   KS_HIP(hipMemcpyAsync(hc, cnts, 32, hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
+  if (dbg) {
+    std::vector<long long> h(nruns * 6);
+    KS_HIP(hipMemcpy(h.data(), dbg, nruns * 6 * sizeof(long long), hipMemcpyDeviceToHost));
+    KS_HIP(hipFree(dbg));
+    std::vector<int64_t> idx(nruns);
+    for (int64_t i = 0; i < nruns; ++i) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return h[6 * a] > h[6 * b]; });
+    long long tot[6] = {0, 0, 0, 0, 0, 0};
+    for (int64_t i = 0; i < nruns; ++i)
+      for (int q = 0; q < 6; ++q) tot[q] += h[6 * i + q];
+    fprintf(stderr, "[carry] runs %lld chunks %lld replays %lld recomputes %lld L %lld R %lld\n", (long long)nruns,
+            tot[1], tot[2], tot[3], tot[4], tot[5]);
+    for (int64_t i = 0; i < std::min<int64_t>(nruns, 8); ++i) {
+      const long long *d = &h[6 * idx[i]];
+      fprintf(stderr, "[carry] run %lld cycles %lld chunks %lld replays %lld recomputes %lld L %lld R %lld\n",
+              (long long)idx[i], d[0], d[1], d[2], d[3], d[4], d[5]);
+    }
+  }
   if ((int64_t)hc[0] > ccap) {
     KS_HIP(hipEventDestroy(e_p1a));
     KS_HIP(hipEventDestroy(e_p1b));
     return fail(KS_ERR_INTERNAL, "candidate buffer overflow (%llu > %lld)", hc[0], (long long)ccap);
   }
   const int64_t ncand = (int64_t)hc[0];
-  void *sbuf = nullptr;
-  KS_TRY(ensure(ctx, SLOT_CHUNK_D, (size_t)std::max<int64_t>(ncand, 1) * 32 + 1024, &sbuf));
-  unsigned long long *kin = reinterpret_cast<unsigned long long *>(sbuf);
-  unsigned long long *kout = kin + std::max<int64_t>(ncand, 1);
-  int32_t *vin = reinterpret_cast<int32_t *>(kout + std::max<int64_t>(ncand, 1));
-  int32_t *vout = vin + std::max<int64_t>(ncand, 1);
-  if (ncand > 0) {
-    std::vector<int32_t> iota(ncand);
-    for (int64_t i = 0; i < ncand; ++i) iota[i] = (int32_t)i;
-    KS_HIP(hipMemcpyAsync(kin, cand.beg, ncand * 8, hipMemcpyDeviceToDevice, st));
-    KS_HIP(hipMemcpyAsync(vin, iota.data(), ncand * 4, hipMemcpyHostToDevice, st));
-    size_t tb = 0;
-    KS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin, vout, (int)ncand, 0, 64, st));
-    void *tmp = nullptr;
-    KS_TRY(ensure(ctx, SLOT_SORT_TMP, tb, &tmp));
-    KS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout, (int)ncand, 0, 64, st));
-  }
   // rescan buffer
   int64_t rcap = std::max<int64_t>(rb.cap, 4096);
   void *rsb = nullptr;
   KS_TRY(ensure(ctx, SLOT_WORK_A, (size_t)rcap * 20 + 1024, &rsb));
   Rescan rs{reinterpret_cast<int64_t *>(rsb), reinterpret_cast<int64_t *>(rsb) + rcap,
             reinterpret_cast<int32_t *>(reinterpret_cast<int64_t *>(rsb) + 2 * rcap), cnts + 1, rcap};
-  hipLaunchKernelGGL(k_stitch, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, runs.b,
-                     runs.seq, k, p1, cr, cand, ncand, vout, mw, min_score, rb, rs, d_err);
+  hipLaunchKernelGGL(k_stitch, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, runs.b, runs.seq, k, p1, cr,
+                     mw, min_score, rb, rs, d_err);
   KS_HIP(hipGetLastError());
+  if (ncand > 0) {
+    hipLaunchKernelGGL(k_candidates, dim3((unsigned)((ncand + 255) / 256)), dim3(256), 0, st, g, runs.a, d_cbase,
+                       nruns, runs.seq, k, cand, ncand, cr, rb, rs);
+    KS_HIP(hipGetLastError());
+  }
   KS_HIP(hipMemcpyAsync(hc, cnts, 32, hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
   const unsigned int errbits = (unsigned int)(hc[3] & 0xffffffffu);
@@ -850,6 +947,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
     stats->ms_rescan = ms_res;
     stats->ms_finish += ms_all - ms_p1;
     stats->n_rescan = nres;
+    stats->n_replay = (int64_t)hc[2];
   }
   return KS_OK;
 }

@@ -471,7 +471,46 @@ __global__ void __launch_bounds__(64) k_carry(Chunks g, const int64_t *__restric
     const int nb = (int)min((int64_t)64, c1 - cb);
     double my_x = 0.0, my_hmax = -1.0;
     int my_mode = kModeClean, my_harg = 0;
-    for (int j = 0; j < nb; ++j) {
+    // Tile fast path: every chunk has a summary for the binade of the tile's
+    // exact entry -> compose the 64 integer maps m -> m + D[m & 1] with a wave
+    // scan, then check each chunk's trajectory bounds at its exact entry.
+    bool tile_done = false;
+    if (x >= kLMin && x < 1.0e18) {
+      const int e = binade_of(x);
+      if (__all(!live || se == e)) {
+        long long i0 = live ? D[0] : 0, i1 = live ? D[1] : 0;  // inclusive composed map
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const long long p0 = __shfl_up(i0, d, 64), p1 = __shfl_up(i1, d, 64);
+          if (lane >= d) {
+            const long long n0 = p0 + ((p0 & 1) ? i1 : i0);          // entry parity 0
+            const long long n1 = p1 + (((1 + p1) & 1) ? i1 : i0);    // entry parity 1
+            i0 = n0;
+            i1 = n1;
+          }
+        }
+        long long x0 = __shfl_up(i0, 1, 64), x1 = __shfl_up(i1, 1, 64);
+        if (lane == 0) { x0 = 0; x1 = 0; }
+        const long long m0 = mant_of(x);
+        const long long mj = m0 + ((m0 & 1) ? x1 : x0);  // exact entry of this lane's chunk
+        const int pj = (int)(mj & 1);
+        const bool ok = !live || (mj + (pj ? N[1] : N[0]) >= (1LL << 52) + 1 &&
+                                  mj + (pj ? M[1] : M[0]) <= (1LL << 53) - 2);
+        if (__all(ok)) {
+          if (live) {
+            my_x = from_mant(mj, e);
+            my_mode = kModeL;
+            my_hmax = from_mant(mj + (pj ? M[1] : M[0]), e);
+            my_harg = pj ? A[1] : A[0];
+          }
+          const long long last = rl64(mj + (pj ? D[1] : D[0]), nb - 1);
+          x = from_mant(last, e);
+          tile_done = true;
+          n_l += nb;
+        }
+      }
+    }
+    for (int j = 0; j < nb && !tile_done; ++j) {
       const double cj_exit = rld(l_exit, j);
       if (lane == j) my_x = x;
       int mode = kModeU;

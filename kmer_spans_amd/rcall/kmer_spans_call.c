@@ -1,0 +1,202 @@
+/*
+ * kmer_spans_call.c -- the R .Call entry points of lmjakt/kmer_spans
+ * (kmer_spans.c:452-808) re-implemented over the C ABI of libkmerspans
+ * (include/kmer_spans.h).  Build with R CMD SHLIB (see Makevars) into
+ * src/kmer_spans.so next to kmer_spans.R; kmer_spans.R then works unchanged.
+ *
+ * Every routine keeps the reference's name, arity, argument checks, error
+ * strings and return layout; the span scan, counting and table work runs on
+ * the GPU through ks_*().  Arguments are validated completely before any
+ * allocation because error() longjmps (kmer_spans.c:454-457, 491-511,
+ * 549-568, 624-628).  HIP is initialised lazily inside the calling process,
+ * so forked workers (parallel::mclapply, test.R:550-567) each get their own
+ * context.
+ */
+#include <R.h>
+#include <R_ext/Rdynload.h>
+#include <Rinternals.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "kmer_spans.h"
+
+#define MAX_K 16 /* the reference's MAX_K (kmer_spans.c:37); 16 itself is rejected by ks_* */
+
+/* Marshal a STRSXP into (pointer, length) arrays; R strings hold no NUL. */
+typedef struct {
+  const char **ptrs;
+  int64_t *lens;
+  int n;
+} seq_view;
+
+static seq_view view_seqs(SEXP seq_r) {
+  seq_view v;
+  v.n = length(seq_r);
+  v.ptrs = (const char **)R_alloc((size_t)v.n, sizeof(char *));
+  v.lens = (int64_t *)R_alloc((size_t)v.n, sizeof(int64_t));
+  for (int i = 0; i < v.n; ++i) {
+    SEXP s = STRING_ELT(seq_r, i);
+    v.ptrs[i] = CHAR(s);
+    v.lens[i] = (int64_t)length(s);
+  }
+  return v;
+}
+
+static void ks_check(ks_status st) {
+  if (st != KS_OK) error("%s", ks_last_error());
+}
+
+/* Copy a ks_regions into R's (3 x n int, 2 x n double) matrices. */
+static void regions_to_r(ks_regions *reg, SEXP ret, int i_ints, int i_dbls) {
+  SET_VECTOR_ELT(ret, i_ints, allocMatrix(INTSXP, 3, (int)reg->n));
+  SET_VECTOR_ELT(ret, i_dbls, allocMatrix(REALSXP, 2, (int)reg->n));
+  int *ip = INTEGER(VECTOR_ELT(ret, i_ints));
+  double *dp = REAL(VECTOR_ELT(ret, i_dbls));
+  for (int64_t j = 0; j < reg->n; ++j) {
+    ip[3 * j] = reg->seq_id[j];
+    ip[3 * j + 1] = reg->beg[j];
+    ip[3 * j + 2] = reg->end[j];
+    dp[2 * j] = reg->score[j];
+    dp[2 * j + 1] = 0.0;
+  }
+  ks_regions_free(reg);
+}
+
+/* kmer_counts(seq_r, k_r)  -- kmer_spans.c:453-487 */
+SEXP kmer_counts(SEXP seq_r, SEXP k_r) {
+  if (TYPEOF(seq_r) != STRSXP || length(seq_r) < 1)
+    error("seq_r must be a character vector of length at least one");
+  if (TYPEOF(k_r) != INTSXP || length(k_r) < 1)
+    error("k_r must be an integer vector of length at least one");
+  int k = INTEGER(k_r)[0];
+  if (k < 1 || k > MAX_K)
+    error("k must be a positive integer less than 1+MAX_K");
+  if (k > KS_MAX_K) error("k must be a positive integer less than 1+MAX_K");
+  seq_view v = view_seqs(seq_r);
+  size_t counts_size = (size_t)1 << (2 * k);
+  SEXP ret = PROTECT(allocVector(VECSXP, 2));
+  SET_VECTOR_ELT(ret, 0, allocVector(REALSXP, 1));
+  SET_VECTOR_ELT(ret, 1, allocVector(INTSXP, (R_xlen_t)counts_size));
+  double n = 0;
+  ks_status st = ks_kmer_counts(NULL, v.ptrs, v.lens, v.n, k, INTEGER(VECTOR_ELT(ret, 1)), &n);
+  if (st != KS_OK) { UNPROTECT(1); ks_check(st); }
+  REAL(VECTOR_ELT(ret, 0))[0] = n;
+  UNPROTECT(1);
+  return ret;
+}
+
+/* kmer_regions_r(seq_r, k_r, kmer_w_r, min_width_r, min_score_r)  -- :490-546 */
+SEXP kmer_regions_r(SEXP seq_r, SEXP k_r, SEXP kmer_w_r, SEXP min_width_r, SEXP min_score_r) {
+  if (TYPEOF(seq_r) != STRSXP || length(seq_r) < 1)
+    error("seq_r must be a character vector of length at least one");
+  if (TYPEOF(k_r) != INTSXP || length(k_r) < 1)
+    error("k_r must be an integer vector of length at least one");
+  if (TYPEOF(kmer_w_r) != REALSXP)
+    error("kmer_w_r must be a double vector of length k^4");
+  if (TYPEOF(min_width_r) != INTSXP || length(min_width_r) != 1)
+    error("the minimum width must be an integer vector of length 1");
+  if (TYPEOF(min_score_r) != REALSXP || length(min_score_r) != 1)
+    error("the minimum score must be a REAL vector of length 1");
+  int k = INTEGER(k_r)[0];
+  if (k >= MAX_K)
+    error("kmer sizes larger than or equal to %d not currently supported", MAX_K);
+  if (k < 1) error("k must be a positive integer");
+  int kmer_n = length(kmer_w_r);
+  if ((unsigned int)kmer_n != (1u << (2 * k)))
+    error("kmer_w contains %d elements but should have %d", kmer_n, (1 << (2 * k)));
+  seq_view v = view_seqs(seq_r);
+  SEXP ret = PROTECT(allocVector(VECSXP, 4));
+  SET_VECTOR_ELT(ret, 0, allocVector(REALSXP, 1));
+  SET_VECTOR_ELT(ret, 1, allocVector(INTSXP, kmer_n));
+  double n = 0;
+  ks_regions reg;
+  ks_status st = ks_kmer_regions(NULL, v.ptrs, v.lens, v.n, k, REAL(kmer_w_r), kmer_n,
+                                 INTEGER(min_width_r)[0], REAL(min_score_r)[0],
+                                 INTEGER(VECTOR_ELT(ret, 1)), &n, &reg);
+  if (st != KS_OK) { UNPROTECT(1); ks_check(st); }
+  REAL(VECTOR_ELT(ret, 0))[0] = n;
+  regions_to_r(&reg, ret, 2, 3);
+  UNPROTECT(1);
+  return ret;
+}
+
+/* kmer_low_comp_regions(seq_r, k_r, min_width_r, min_score_r, threshold_r) -- :548-621 */
+SEXP kmer_low_comp_regions(SEXP seq_r, SEXP k_r, SEXP min_width_r, SEXP min_score_r, SEXP threshold_r) {
+  if (TYPEOF(seq_r) != STRSXP || length(seq_r) < 1)
+    error("seq_r must be a character vector of length at least one");
+  if (TYPEOF(k_r) != INTSXP || length(k_r) < 1)
+    error("k_r must be an integer vector of length at least one");
+  if (TYPEOF(min_width_r) != INTSXP || length(min_width_r) != 1)
+    error("the minimum width must be an integer vector of length 1");
+  if (TYPEOF(min_score_r) != REALSXP || length(min_score_r) != 1)
+    error("the minimum score must be a REAL vector of length 1");
+  if (TYPEOF(threshold_r) != REALSXP || length(threshold_r) != 1)
+    error("the threshold must be a REAL vector of length 1");
+  int k = INTEGER(k_r)[0];
+  double threshold = REAL(threshold_r)[0];
+  if (threshold <= 0 || threshold >= 1)
+    error("the threshold must be between 0 and 1");
+  if (k < 1 || k > KS_MAX_K) /* unchecked in the reference (Q7) */
+    error("k must be a positive integer less than 1+MAX_K");
+  seq_view v = view_seqs(seq_r);
+  size_t counts_size = (size_t)1 << (2 * k);
+  SEXP ret = PROTECT(allocVector(VECSXP, 5));
+  SET_VECTOR_ELT(ret, 0, allocVector(REALSXP, 2));
+  SET_VECTOR_ELT(ret, 1, allocVector(INTSXP, (R_xlen_t)counts_size));
+  SET_VECTOR_ELT(ret, 2, allocVector(REALSXP, (R_xlen_t)counts_size));
+  ks_regions reg;
+  ks_status st = ks_low_comp_regions(NULL, v.ptrs, v.lens, v.n, k, INTEGER(min_width_r)[0],
+                                     REAL(min_score_r)[0], threshold, INTEGER(VECTOR_ELT(ret, 1)),
+                                     REAL(VECTOR_ELT(ret, 2)), REAL(VECTOR_ELT(ret, 0)), &reg);
+  if (st != KS_OK) { UNPROTECT(1); ks_check(st); }
+  regions_to_r(&reg, ret, 3, 4);
+  UNPROTECT(1);
+  return ret;
+}
+
+/* kmer_seq_r(k_r)  -- :623-639 */
+SEXP kmer_seq_r(SEXP k_r) {
+  if (TYPEOF(k_r) != INTSXP || length(k_r) != 1)
+    error("k_r should be an integer of length 1");
+  unsigned int k = (unsigned int)(INTEGER(k_r)[0]);
+  if (k > MAX_K || k < 1)
+    error("k_r (%d) should be smaller than MAX_K (%d) and larger than 0", k, MAX_K);
+  if (k > KS_MAX_K) error("k_r (%d) should be smaller than MAX_K (%d) and larger than 0", k, MAX_K);
+  size_t n = (size_t)1 << (2 * k);
+  char *buf = (char *)malloc(n * (k + 1));
+  if (!buf) error("out of memory");
+  ks_status st = ks_kmer_seq((int32_t)k, buf, n * (k + 1));
+  if (st != KS_OK) { free(buf); ks_check(st); }
+  SEXP ret = PROTECT(allocVector(STRSXP, (R_xlen_t)n));
+  for (size_t i = 0; i < n; ++i) SET_STRING_ELT(ret, (R_xlen_t)i, mkChar(buf + i * (k + 1)));
+  free(buf);
+  UNPROTECT(1);
+  return ret;
+}
+
+/* Out of the span-scan path: not provided by this
+ * build.  They stay registered so that a package that registers all six
+ * names loads; calling them reports that the routine lives in the reference. */
+SEXP tr_lr_regions_r(SEXP seq_r, SEXP params_r, SEXP kmers_r, SEXP kmer_scores_r, SEXP trans_scores_r) {
+  (void)seq_r; (void)params_r; (void)kmers_r; (void)kmer_scores_r; (void)trans_scores_r;
+  error("tr_lr_regions_r is not part of the MI355X span-scan build (out of scope, see DESIGN.md)");
+  return R_NilValue;
+}
+
+SEXP windowed_kmer_count_distributions_r(SEXP seq_r, SEXP kmers_r, SEXP k_r, SEXP window_r, SEXP ret_flag_r) {
+  (void)seq_r; (void)kmers_r; (void)k_r; (void)window_r; (void)ret_flag_r;
+  error("windowed_kmer_count_distributions_r is not part of the MI355X span-scan build (out of scope, see DESIGN.md)");
+  return R_NilValue;
+}
+
+static const R_CallMethodDef callMethods[] = {
+    {"kmer_counts", (DL_FUNC)&kmer_counts, 2},
+    {"kmer_regions_r", (DL_FUNC)&kmer_regions_r, 5},
+    {"kmer_low_comp_regions", (DL_FUNC)&kmer_low_comp_regions, 5},
+    {"kmer_seq_r", (DL_FUNC)&kmer_seq_r, 1},
+    {"tr_lr_regions_r", (DL_FUNC)&tr_lr_regions_r, 5},
+    {"windowed_kmer_count_distributions_r", (DL_FUNC)&windowed_kmer_count_distributions_r, 5},
+    {NULL, NULL, 0}};
+
+void R_init_kmer_spans(DllInfo *info) { R_registerRoutines(info, NULL, callMethods, NULL, NULL); }

@@ -151,7 +151,7 @@ __global__ void __launch_bounds__(256) k_pass1(Chunks g, const uint8_t *__restri
                                                int k, TableView tv, uint16_t *__restrict__ codes,
                                                uint64_t mw, double min_score, uint32_t *__restrict__ visits,
                                                P1 o, Cand cand) {
-  constexpr int G = (J == 1) ? 16 : 8;  // table reads in flight per lane and batch
+  constexpr int G = (J == 1) ? 16 : (J == 4 ? 4 : 8);  // table reads in flight per lane and batch
   constexpr int PB = G * J;             // scan indices per batch (16, 16, 24, 32)
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
@@ -285,10 +285,11 @@ __device__ __forceinline__ double from_mant(long long m, int e) {
 // with ties to even decided by the parity of m.  For both entry parities t:
 // total D, max M (first argmax A) and min N of the integer trajectory.
 // Returns false if a value is not representable (overflow, NaN, Inf).
-template <bool kCompressed>
-__device__ bool chunk_summary(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
-                              const TableView &tv, const uint16_t *__restrict__ codes, int64_t c, int e,
-                              long long D[2], long long M[2], int A[2], long long N[2]) {
+template <bool kCompressed, bool kDual>
+__device__ int chunk_summary_impl(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
+                                  const TableView &tv, const uint16_t *__restrict__ codes, int64_t c, int e,
+                                  long long D[2], long long M[2], int A[2], long long N[2]) {
+  // returns 1 ok, 0 not representable, -1 (single-trajectory mode only) a tie occurred
   const int n = g.n[c];
   const int64_t start = g.start[c];
   const uint32_t mask = (1u << (2 * k)) - 1u;
@@ -298,7 +299,7 @@ __device__ bool chunk_summary(const Chunks &g, const uint8_t *__restrict__ seq, 
   M[0] = M[1] = LLONG_MIN;
   N[0] = N[1] = LLONG_MAX;
   A[0] = A[1] = 0;
-  bool ok = true;
+  bool ok = true, tie_seen = false;
   for (int b0 = 0; b0 < n; b0 += NB) {
     double v[NB];
     if (kCompressed) {
@@ -324,21 +325,48 @@ __device__ bool chunk_summary(const Chunks &g, const uint8_t *__restrict__ seq, 
         ok &= fabs(y) < 4.0e18;         // also false for NaN / Inf
         const double fq = floor(y);
         const double f = y - fq;        // exact fractional part
-        const long long q = ok ? (long long)fq : 0;
         const bool up = f > 0.5, tie = f == 0.5;
+        if (kDual) {
+          const long long q = ok ? (long long)fq : 0;
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const long long par = (t + cur[t]) & 1;
-          cur[t] += q + ((up || (tie && ((par + q) & 1))) ? 1 : 0);
-          if (cur[t] > M[t]) { M[t] = cur[t]; A[t] = i; }
-          N[t] = min(N[t], cur[t]);
+          for (int t = 0; t < 2; ++t) {
+            const long long par = (t + cur[t]) & 1;
+            cur[t] += q + ((up || (tie && ((par + q) & 1))) ? 1 : 0);
+            if (cur[t] > M[t]) { M[t] = cur[t]; A[t] = i; }
+            N[t] = min(N[t], cur[t]);
+          }
+        } else {  // no tie: the increment does not depend on the parity
+          tie_seen |= tie;
+          const long long q = ok ? (long long)(up ? fq + 1.0 : fq) : 0;
+          cur[0] += q;
+          if (cur[0] > M[0]) { M[0] = cur[0]; A[0] = i; }
+          N[0] = min(N[0], cur[0]);
         }
       }
     }
   }
+  if (!ok) return 0;
+  if (!kDual) {
+    if (tie_seen) return -1;
+    cur[1] = cur[0]; M[1] = M[0]; N[1] = N[0]; A[1] = A[0];
+  }
   D[0] = cur[0];
   D[1] = cur[1];
-  return ok;
+  return 1;
+}
+
+// Binade-integer summary of chunk c for binade e: with S = m * 2^(e-52) and
+// the whole trajectory inside [2^e, 2^(e+1)), fl(S + s) = S + RN(s * 2^(52-e))
+// with ties to even decided by the parity of m.  For both entry parities t:
+// total D, max M (first argmax A) and min N of the integer trajectory.  One
+// trajectory is tracked unless an exact tie occurs (then both parities).
+template <bool kCompressed>
+__device__ bool chunk_summary(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
+                              const TableView &tv, const uint16_t *__restrict__ codes, int64_t c, int e,
+                              long long D[2], long long M[2], int A[2], long long N[2]) {
+  const int rc = chunk_summary_impl<kCompressed, false>(g, seq, total, k, tv, codes, c, e, D, M, A, N);
+  if (rc >= 0) return rc == 1;
+  return chunk_summary_impl<kCompressed, true>(g, seq, total, k, tv, codes, c, e, D, M, A, N) == 1;
 }
 
 // ------------------------------------------------------------------- P2

@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--cpu-sample", type=float, default=2.0e8, help="bases in the CPU-baseline sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-expand", action="store_true", help="do not build the expanded (k+J-1)-mer table")
+    p.add_argument("--ncontigs", type=int, default=24, help="1 = the chr1-like single contig of config 2")
+    p.add_argument("--host-path", action="store_true",
+                   help="also time the host-pointer entry point (ks_kmer_regions: staging + PCIe + scan)")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
     return p.parse_args()
 
@@ -78,7 +81,8 @@ def main():
 
     # ---- synthetic genome (device-resident) + score table from its counts
     t0 = time.time()
-    parts, lens = genome.human_like(scale=args.scale, seed=args.seed + 1000 * rank, device=dev)
+    parts, lens = genome.human_like(scale=args.scale, seed=args.seed + 1000 * rank, device=dev,
+                                    ncontigs=args.ncontigs)
     ds = D.from_parts(parts, lens, dev)
     del parts
     torch.cuda.synchronize()
@@ -143,6 +147,19 @@ def main():
                 "kernel": "k_scan_lane" if stats[-1]["scan_algo"] == 0 else "k_chunk_pass1",
                 "kernel_ms": round(ms_kernel, 3), "algo_bytes_per_base": ALGO_BYTES_PER_BASE}
 
+    # ---- PCIe-inclusive rate of the host entry point (reported, never `value`)
+    host_path = None
+    if args.host_path and rank == 0:
+        hs = [ds.host_seq(q) for q in range(ds.nseq)]
+        t0 = time.perf_counter()
+        hr = api.kmer_regions(hs, k, w, args.min_width, args.min_score, visits=False) if thr == 0.0 else None
+        t_host = time.perf_counter() - t0
+        if hr is not None:
+            host_path = {"seconds": round(t_host, 4), "Gbases_per_s": round(n_bases / t_host / 1e9, 3),
+                         "regions_equal": bool(np.array_equal(hr["pos"], pos)),
+                         "note": "ks_kmer_regions from host memory: pinned staging + H2D + table upload/compress + scan"}
+        del hs
+
     # ---- CPU baseline: the oracle (single thread) on a bounded sample
     cpu = None
     parity = None
@@ -177,7 +194,7 @@ def main():
         "value": round(value, 4), "unit": "Gbases/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": f"human-shaped synthetic genome ({n_bases} bp, 24 contigs, scale {args.scale}), "
+        "config": {"workload": f"human-shaped synthetic genome ({n_bases} bp, {ds.nseq} contigs, scale {args.scale}), "
                                f"k={k}, {args.score} score from its own counts, min_width {args.min_width}, "
                                f"min_score {args.min_score}, device-resident",
                    "k": k, "score": args.score, "genome_bp": n_bases, "parallelism": f"contig-shard x{world}",
@@ -188,6 +205,7 @@ def main():
         "parity_sample": parity,
         "regions": n_regions_all,
         "replayed_chunks": int(stats[-1]["n_replay"]),
+        "host_path": host_path,
         "phase_ms": {key: round(float(np.mean([s[key] for s in stats])), 3)
                      for key in ("ms_runs", "ms_scan", "ms_rescan", "ms_finish", "ms_total")},
         "setup_s": {"genome": round(t_gen, 2), "count": round(t_count, 3), "table": round(t_table, 3)},

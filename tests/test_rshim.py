@@ -1,0 +1,69 @@
+"""The R .Call shim (kmer_spans_amd/rcall/kmer_spans_call.c) through the
+tests/rstub R C-API emulation: the six registered routines of the reference
+(kmer_spans.c:795-802) with their arities, error strings, and -- on a GPU --
+results equal to the oracle."""
+import numpy as np
+import pytest
+
+
+@pytest.fixture(scope="module")
+def R():
+    from tests.rshim import RShim
+    return RShim()
+
+
+def test_registration_table(R):
+    assert R.routines() == {"kmer_counts": 2, "kmer_regions_r": 5, "kmer_low_comp_regions": 5,
+                            "kmer_seq_r": 1, "tr_lr_regions_r": 5, "windowed_kmer_count_distributions_r": 5}
+
+
+def test_reference_error_strings(R):
+    cases = [
+        (("kmer_counts", R.int_([1]), R.int_([2])), "seq_r must be a character vector of length at least one"),
+        (("kmer_counts", R.str_(["ACGT"]), R.real([2.0])), "k_r must be an integer vector of length at least one"),
+        (("kmer_counts", R.str_(["ACGT"]), R.int_([17])), "k must be a positive integer less than 1+MAX_K"),
+        (("kmer_regions_r", R.str_(["ACGT"]), R.int_([1]), R.int_([1, 2, 3, 4]), R.int_([0]), R.real([0.0])),
+         "kmer_w_r must be a double vector of length k^4"),
+        (("kmer_regions_r", R.str_(["ACGT"]), R.int_([1]), R.real([1.0] * 4), R.int_([0, 1]), R.real([0.0])),
+         "the minimum width must be an integer vector of length 1"),
+        (("kmer_regions_r", R.str_(["ACGT"]), R.int_([1]), R.real([1.0] * 4), R.int_([0]), R.int_([0])),
+         "the minimum score must be a REAL vector of length 1"),
+        (("kmer_regions_r", R.str_(["ACGT"]), R.int_([16]), R.real([1.0] * 4), R.int_([0]), R.real([0.0])),
+         "kmer sizes larger than or equal to 16 not currently supported"),
+        (("kmer_regions_r", R.str_(["ACGT"]), R.int_([2]), R.real([1.0] * 4), R.int_([0]), R.real([0.0])),
+         "kmer_w contains 4 elements but should have 16"),
+        (("kmer_low_comp_regions", R.str_(["ACGT"]), R.int_([2]), R.int_([0]), R.real([0.0]), R.real([1.5])),
+         "the threshold must be between 0 and 1"),
+        (("kmer_low_comp_regions", R.str_(["ACGT"]), R.int_([2]), R.int_([0]), R.real([0.0]), R.int_([0])),
+         "the threshold must be a REAL vector of length 1"),
+        (("kmer_seq_r", R.int_([0])), "k_r (0) should be smaller than MAX_K (16) and larger than 0"),
+        (("kmer_seq_r", R.int_([1, 2])), "k_r should be an integer of length 1"),
+        (("tr_lr_regions_r", *[R.int_([0])] * 5), "not part of the MI355X span-scan build"),
+    ]
+    for args, msg in cases:
+        with pytest.raises(RuntimeError, match=msg.replace("^", "\\^").replace("+", "\\+").replace("(", "\\(").replace(")", "\\)")):
+            R.call(*args)
+
+
+def test_kmer_seq_r(R, oracle):
+    for k in (1, 3):
+        assert R.to_py(R.call("kmer_seq_r", R.int_([k]))) == oracle.kmer_seq(k)
+
+
+@pytest.mark.gpu
+def test_shim_results_vs_oracle(R, oracle):
+    rng = np.random.default_rng(2)
+    seqs = ["".join(rng.choice(list("ACGTN"), 3000, p=[.24, .24, .24, .24, .04])), "CAAAAAATCAACCCCCC", "AC"]
+    n, c = oracle.kmer_counts(seqs, 4)
+    got = R.to_py(R.call("kmer_counts", R.str_(seqs), R.int_([4])))
+    assert got[0][0] == n and np.array_equal(got[1], c)
+    w = rng.normal(size=4 ** 4)
+    o = oracle.kmer_regions(seqs, 4, w, 3, 1.0)
+    got = R.to_py(R.call("kmer_regions_r", R.str_(seqs), R.int_([4]), R.real(w), R.int_([3]), R.real([1.0])))
+    assert got[0][0] == o["n"] and np.array_equal(got[1], o["counts"])
+    assert np.array_equal(np.asarray(got[2]).reshape(3, -1), o["pos"])
+    lc = oracle.low_comp_regions(seqs, 3, 5, 2.0, 0.6)
+    got = R.to_py(R.call("kmer_low_comp_regions", R.str_(seqs), R.int_([3]), R.int_([5]), R.real([2.0]), R.real([0.6])))
+    assert np.array_equal(got[0], lc["n"]) and np.array_equal(got[1], lc["counts"])
+    assert np.array_equal(got[2], lc["w_rank"])
+    assert np.array_equal(np.asarray(got[3]).reshape(3, -1), lc["pos"])

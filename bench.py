@@ -62,19 +62,24 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1)  # ranks > GPUs only when rehearsing N>1 on a small box
     if dist:
         import torch.distributed as tdist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if ndev >= world:  # one process per GPU: RCCL over xGMI
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:              # rehearsal with shared GPUs: RCCL refuses duplicate GPUs
+            tdist.init_process_group("gloo")
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     from kmer_spans_amd import _lib, api, genome
     from kmer_spans_amd import device as D
 
     k = args.k
-    ctx = _lib.context(local)
+    ctx = _lib.context(gpu)
     D.bind_torch_stream(ctx)
     if args.algo >= 0:
         ctx.set_scan_algo(args.algo)
@@ -123,7 +128,7 @@ def main():
         tdist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev if tdist.get_backend() == "nccl" else "cpu")
         tdist.all_reduce(e, op=tdist.ReduceOp.MAX)
         elapsed = float(e.item())
 

@@ -13,6 +13,11 @@
 
 namespace ks {
 
+// Internal status (never returned through the C ABI): the region buffer was
+// too small for a pass whose partial results cannot be kept; grow and rerun.
+constexpr ks_status KS_INTERNAL_RETRY = static_cast<ks_status>(100);
+
+
 // ---------------------------------------------------------------- errors
 void set_error(const char *fmt, ...);
 ks_status fail(ks_status st, const char *fmt, ...);

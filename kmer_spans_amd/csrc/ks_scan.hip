@@ -10,6 +10,8 @@
 // one lane per run; it is the correctness baseline and the path for short
 // runs.  The chunked carry scan (ks_scan_chunked.hip) parallelises inside
 // long runs.
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <numeric>
 
@@ -93,6 +95,31 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
   }
 }
 
+__global__ void k_region_keys(const int64_t *__restrict__ beg, int64_t n, unsigned long long *__restrict__ keys,
+                              int32_t *__restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    keys[i] = (unsigned long long)beg[i];
+    idx[i] = (int32_t)i;
+  }
+}
+
+// Regions in (seq_id, beg) order == global begin order; local coordinates.
+__global__ void k_region_gather(RegionBuf rb, const int32_t *__restrict__ perm, int64_t n,
+                                const int64_t *__restrict__ offs, int32_t *__restrict__ o_seq,
+                                int32_t *__restrict__ o_beg, int32_t *__restrict__ o_end,
+                                double *__restrict__ o_score) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int32_t i = perm[j];
+  const int32_t q = rb.seq[i];
+  const int64_t base = offs[q];
+  o_seq[j] = q;
+  o_beg[j] = (int32_t)(rb.beg[i] - base);
+  o_end[j] = (int32_t)(rb.end[i] - base);
+  o_score[j] = rb.score[i];
+}
+
 __global__ void k_add_hist(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     dst[i] += src[i];
@@ -147,14 +174,15 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
   if (algo < 0) algo = (longest > (1 << 15)) ? 1 : 0;
   S->scan_algo = algo;
 
-  int64_t cap = std::max<int64_t>(4096, (int64_t)(ctx->slots[SLOT_REGIONS].bytes / 28));
+  int64_t cap = std::max<int64_t>(std::max<int64_t>(65536, scored / 2048), (int64_t)(ctx->slots[SLOT_REGIONS].bytes / 28));
   unsigned long long n_reg = 0;
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
   unsigned long long *d_rcount = reinterpret_cast<unsigned long long *>(scal) + 2;
   RegionBuf rb{};
   uint32_t *vis = reinterpret_cast<uint32_t *>(visits_dev);
-  for (int attempt = 0; attempt < 3; ++attempt) {
+  bool complete = false;
+  for (int attempt = 0; attempt < 4 && !complete; ++attempt) {
     void *rp = nullptr;
     KS_TRY(ensure(ctx, SLOT_REGIONS, (size_t)cap * 28 + 64, &rp));
     rb.beg = reinterpret_cast<int64_t *>(rp);
@@ -177,6 +205,12 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
         KS_HIP(hipMemsetAsync(vscr, 0, nb, st));
       }
       ks_status rc = scan_chunked(ctx, s, runs, k, tv, mw, min_score, vscr, rb, S);
+      if (rc == KS_INTERNAL_RETRY) {  // rescans did not fit: grow, rerun, visits untouched
+        KS_HIP(hipMemcpyAsync(&n_reg, d_rcount, 8, hipMemcpyDeviceToHost, st));
+        KS_HIP(hipStreamSynchronize(st));
+        cap = std::max<int64_t>(2 * cap, (int64_t)n_reg + 1024);
+        continue;
+      }
       if (rc == KS_OK) {
         if (vis) {
           const int64_t n = (int64_t)1 << (2 * k);
@@ -202,29 +236,19 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     float ms = 0;
     KS_HIP(hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[4]));
     if (algo == 0) S->ms_scan = ms;
-    if ((int64_t)n_reg <= cap) break;
+    if ((int64_t)n_reg <= cap) {
+      complete = true;
+      break;
+    }
     cap = (int64_t)n_reg + 1024;
     vis = nullptr;  // visits were complete on the first pass
   }
-  if ((int64_t)n_reg > cap) return fail(KS_ERR_INTERNAL, "region buffer overflow");
+  if (!complete) return fail(KS_ERR_INTERNAL, "region buffer overflow");
 
-  // Order regions by global begin == (seq_id, beg); convert to local coords.
+  // Order regions by global begin == (seq_id, beg) on the device (radix sort),
+  // convert to sequence-local coordinates, copy out.
   KS_HIP(hipEventRecord(ctx->ev[5], st));
   const int64_t n = (int64_t)n_reg;
-  std::vector<int64_t> gb(n), ge(n);
-  std::vector<double> sc(n);
-  std::vector<int32_t> sq(n);
-  if (n) {
-    KS_HIP(hipMemcpyAsync(gb.data(), rb.beg, n * 8, hipMemcpyDeviceToHost, st));
-    KS_HIP(hipMemcpyAsync(ge.data(), rb.end, n * 8, hipMemcpyDeviceToHost, st));
-    KS_HIP(hipMemcpyAsync(sc.data(), rb.score, n * 8, hipMemcpyDeviceToHost, st));
-    KS_HIP(hipMemcpyAsync(sq.data(), rb.seq, n * 4, hipMemcpyDeviceToHost, st));
-  }
-  KS_HIP(hipEventRecord(ctx->ev[6], st));
-  KS_HIP(hipStreamSynchronize(st));
-  std::vector<int64_t> order(n);
-  std::iota(order.begin(), order.end(), 0);
-  std::sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return gb[x] < gb[y]; });
   out->n = n;
   out->seq_id = (int32_t *)malloc(std::max<int64_t>(n, 1) * 4);
   out->beg = (int32_t *)malloc(std::max<int64_t>(n, 1) * 4);
@@ -234,14 +258,39 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     ks_regions_free(out);
     return fail(KS_ERR_NOMEM, "out of host memory for %lld regions", (long long)n);
   }
-  for (int64_t j = 0; j < n; ++j) {
-    const int64_t o = order[j];
-    const int64_t base = s->offsets_host[sq[o]];
-    out->seq_id[j] = sq[o];
-    out->beg[j] = (int32_t)(gb[o] - base);
-    out->end[j] = (int32_t)(ge[o] - base);
-    out->score[j] = sc[o];
+  if (n > 0) {
+    void *tmpb = nullptr;
+    const size_t nn = (size_t)n;
+    KS_TRY(ensure(ctx, SLOT_REG_TMP, nn * (8 + 8 + 4 + 4) + nn * 20 + 1024, &tmpb));
+    unsigned long long *k_in = static_cast<unsigned long long *>(tmpb);
+    unsigned long long *k_out = k_in + nn;
+    int32_t *v_in = reinterpret_cast<int32_t *>(k_out + nn);
+    int32_t *v_out = v_in + nn;
+    int32_t *o_seq = v_out + nn;
+    int32_t *o_beg = o_seq + nn;
+    int32_t *o_end = o_beg + nn;
+    double *o_score = reinterpret_cast<double *>((reinterpret_cast<uintptr_t>(o_end + nn) + 7) & ~(uintptr_t)7);
+    const unsigned g = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(k_region_keys, dim3(g), dim3(256), 0, st, rb.beg, n, k_in, v_in);
+    KS_HIP(hipGetLastError());
+    const int64_t total = s->offsets_host[s->nseq];
+    int end_bit = 1;
+    while (end_bit < 64 && ((unsigned long long)total >> end_bit)) ++end_bit;
+    size_t tb = 0;
+    KS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k_in, k_out, v_in, v_out, (int)n, 0, end_bit, st));
+    void *tmp = nullptr;
+    KS_TRY(ensure(ctx, SLOT_SORT_TMP, tb, &tmp));
+    KS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k_in, k_out, v_in, v_out, (int)n, 0, end_bit, st));
+    hipLaunchKernelGGL(k_region_gather, dim3(g), dim3(256), 0, st, rb, v_out, n, s->offsets_dev, o_seq, o_beg,
+                       o_end, o_score);
+    KS_HIP(hipGetLastError());
+    KS_HIP(hipMemcpyAsync(out->seq_id, o_seq, nn * 4, hipMemcpyDeviceToHost, st));
+    KS_HIP(hipMemcpyAsync(out->beg, o_beg, nn * 4, hipMemcpyDeviceToHost, st));
+    KS_HIP(hipMemcpyAsync(out->end, o_end, nn * 4, hipMemcpyDeviceToHost, st));
+    KS_HIP(hipMemcpyAsync(out->score, o_score, nn * 8, hipMemcpyDeviceToHost, st));
   }
+  KS_HIP(hipEventRecord(ctx->ev[6], st));
+  KS_HIP(hipStreamSynchronize(st));
   S->n_regions = n;
   float ms_fin = 0, ms_tot = 0;
   KS_HIP(hipEventElapsedTime(&ms_fin, ctx->ev[5], ctx->ev[6]));

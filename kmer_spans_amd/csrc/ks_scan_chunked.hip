@@ -114,13 +114,33 @@ __device__ __forceinline__ size_t code_slot(int64_t c, int i) {
   return ((((size_t)(c >> 6) * (CH / 8) + (size_t)(i >> 3)) * 64 + (size_t)(c & 63)) << 3) + (size_t)(i & 7);
 }
 
-// Value of scan index i of chunk c, computed from scratch (rare paths).
-__device__ __forceinline__ double value_at(const Chunks &g, const uint8_t *__restrict__ seq, int k,
-                                           const TableView &tv, const uint16_t *__restrict__ codes,
-                                           int64_t c, int i) {
-  if (codes) return tv.lut[codes[code_slot(c, i)]];
-  const int64_t p = g.start[c] + i;
-  return tv_get(tv, prime_code(seq, p - k, k));
+// Values of scan indices i0 .. i0+3 of chunk c (0 past n): one 8-byte code
+// load (compressed) or one k-mer prime plus three rolls.
+__device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restrict__ seq, int k,
+                                        const TableView &tv, const uint16_t *__restrict__ codes, int64_t c,
+                                        int i0, int n, double v[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = 0.0;
+  if (i0 >= n) return;
+  if (codes) {
+    const uint2 w = *reinterpret_cast<const uint2 *>(codes + code_slot(c, i0));
+    const uint32_t cw[2] = {w.x, w.y};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (i0 + q < n) v[q] = tv.lut[(cw[q >> 1] >> (16 * (q & 1))) & 0xffffu];
+    return;
+  }
+  const int64_t p = g.start[c] + i0;
+  const uint32_t mask = (1u << (2 * k)) - 1u;
+  uint32_t code = prime_code(seq, p - k, k);
+  v[0] = tv_get(tv, code);
+#pragma unroll
+  for (int q = 1; q < 4; ++q) {
+    if (i0 + q < n) {
+      code = ((code << 2) | enc(seq[p + q - 1])) & mask;
+      v[q] = tv_get(tv, code);
+    }
+  }
 }
 
 // ------------------------------------------------------------------- P0
@@ -439,6 +459,31 @@ __global__ void __launch_bounds__(256) k_summaries(Chunks g, const uint8_t *__re
   }
 }
 
+// Segment starts: every run start, and after the first chunk of each
+// 64-chunk window that is predicted to clamp by a wide margin (so that the
+// exact entry, which differs from x~ by rounding only, clamps too).
+__global__ void __launch_bounds__(64) k_seg_marks(Chunks g, P1 o, const double *__restrict__ xt,
+                                                  uint8_t *__restrict__ flag) {
+  const int64_t e = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  bool elig = false, next_run = false;
+  if (e + 1 < g.nch) {
+    next_run = g.run[e + 1] != g.run[e];
+    if (!next_run && !o.special[e]) {
+      const double x = xt[e];
+      elig = x + o.pmin[e] < -ldexp(fabs(x) + o.sabs[e], -20);  // false for NaN
+    }
+  }
+  const unsigned long long b = __ballot(elig);
+  const int f = b ? __ffsll((long long)b) - 1 : 64;
+  if (e + 1 < g.nch) flag[e + 1] = (next_run || (int)threadIdx.x == f) ? 1 : 0;
+  if (e == 0) flag[0] = 1;
+}
+
+__global__ void k_seg_sentinel(int64_t *__restrict__ seg, const unsigned long long *__restrict__ d_nseg,
+                               int64_t nch) {
+  seg[*d_nseg] = nch;
+}
+
 // Exact carry, one wave per run, walking 64-chunk tiles (lane j <-> chunk
 // cb + j).  Per chunk, in order: entry 0 -> clean exit (CLEAN); a binade
 // summary valid for the exact entry -> integer step (L; the summaries of the
@@ -462,17 +507,26 @@ __device__ __forceinline__ double rld(double v, int j) { return __longlong_as_do
 // integer step (L, also yields the head); a certain clamp (x + minprefix <
 // -margin) -> clean exit (R); else exact replay (U): the wave loads the 256
 // values into registers (4 per lane) and walks them with readlane.
+//
+// Segments: a run's chain is cut after chunks predicted (x~ from P2, with a
+// wide margin) to clamp: the chunk after one starts a segment whose entry is
+// assumed to be that chunk's clean exit, and the segments run in parallel.
+// The wave of the preceding segment checks the assumption against its exact
+// exit (bit 16 of err on mismatch; the host then redoes the carry per run).
 template <bool kCompressed>
-__global__ void __launch_bounds__(64) k_carry(Chunks g, const int64_t *__restrict__ cbase, int64_t nruns,
+__global__ void __launch_bounds__(64) k_carry(Chunks g, const int64_t *__restrict__ seg, int64_t nseg_max,
+                                              const unsigned long long *__restrict__ d_nseg,
                                               const uint8_t *__restrict__ seq, int64_t total, int k, TableView tv,
                                               const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
-                                              unsigned long long *__restrict__ nreplay,
+                                              unsigned long long *__restrict__ nreplay, unsigned int *__restrict__ err,
                                               long long *__restrict__ dbg) {
   const int64_t r = blockIdx.x;
-  if (r >= nruns) return;
+  const int64_t nseg = d_nseg ? (int64_t)*d_nseg : nseg_max;
+  if (r >= nseg) return;
   const int lane = threadIdx.x;
-  const int64_t c0 = cbase[r], c1 = cbase[r + 1];
-  double x = 0.0;
+  const int64_t c0 = seg[r], c1 = seg[r + 1];
+  if (c0 >= c1) return;
+  double x = (c0 > 0 && g.run[c0] == g.run[c0 - 1]) ? o.cexit[c0 - 1] : 0.0;
   unsigned long long replays = 0;
   const long long t_start = dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
   long long n_l = 0, n_r = 0;
@@ -498,7 +552,7 @@ __global__ void __launch_bounds__(64) k_carry(Chunks g, const int64_t *__restric
     }
     const int nb = (int)min((int64_t)64, c1 - cb);
     double my_x = 0.0, my_hmax = -1.0;
-    int my_mode = kModeClean, my_harg = 0;
+    int my_mode = kModeClean, my_harg = 0, my_hq = -1;
     // Tile fast path: every chunk has a summary for the binade of the tile's
     // exact entry -> compose the 64 integer maps m -> m + D[m & 1] with a wave
     // scan, then check each chunk's trajectory bounds at its exact entry.
@@ -568,29 +622,34 @@ __global__ void __launch_bounds__(64) k_carry(Chunks g, const int64_t *__restric
         x = cj_exit;
         done = true;
       }
-      if (!done) {  // exact replay of chunk cb + j from x
+      if (!done) {  // exact replay of chunk cb + j from x; also yields its head
         mode = kModeU;
         ++replays;
         const int64_t cj = cb + j;
         const int n = rl32(l_n, j);
         double v[4];
+        values4(g, seq, k, tv, kCompressed ? codes : nullptr, cj, 4 * lane, n, v);
+        double T = x, hmax = -1.0;
+        int hq = -1, harg = 0;
+        for (int i = 0; i < 64 && hq < 0; ++i) {
+          if (4 * i >= n) break;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int i = lane + 64 * q;
-          v[q] = i < n ? value_at(g, seq, k, tv, kCompressed ? codes : nullptr, cj, i) : 0.0;
-        }
-        double T = x;
-        bool clamped = false;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          for (int i = 0; i < 64 && !clamped; ++i) {
-            if (64 * q + i >= n) break;
-            const double t = T + rld(v[q], i);
-            T = t > 0 ? t : 0.0;
-            clamped = T == 0.0;
+          for (int q = 0; q < 4; ++q) {
+            const int idx = 4 * i + q;
+            if (idx < n && hq < 0) {
+              const double t = T + rld(v[q], i);
+              T = t > 0 ? t : 0.0;
+              if (T == 0.0) hq = idx;
+              else if (T > hmax) { hmax = T; harg = idx; }
+            }
           }
         }
-        x = clamped ? cj_exit : T;
+        if (lane == j) {
+          my_hq = hq;
+          my_hmax = hmax;
+          my_harg = harg;
+        }
+        x = hq >= 0 ? cj_exit : T;
       }
       if (lane == j) my_mode = mode;
       n_l += mode == kModeL;
@@ -599,14 +658,17 @@ __global__ void __launch_bounds__(64) k_carry(Chunks g, const int64_t *__restric
     if (live) {
       cr.x[c] = my_x;
       cr.mode[c] = (uint8_t)my_mode;
-      if (my_mode == kModeL) {
-        cr.hq[c] = -1;
+      if (my_mode == kModeL || my_mode == kModeU) {
+        cr.hq[c] = my_hq;
         cr.hmax[c] = my_hmax;
         cr.harg[c] = my_harg;
       }
     }
   }
   if (lane == 0 && replays) atomicAdd(nreplay, replays);
+  if (lane == 0 && c1 < g.nch && g.run[c1] == g.run[c1 - 1] &&
+      __double_as_longlong(x) != __double_as_longlong(o.cexit[c1 - 1]))
+    atomicOr(err, 16u);  // the next segment assumed a different entry
   if (dbg && lane == 0) {
     dbg[6 * r + 0] = (long long)__builtin_amdgcn_s_memtime() - t_start;
     dbg[6 * r + 1] = c1 - c0;
@@ -619,14 +681,17 @@ __global__ void __launch_bounds__(64) k_carry(Chunks g, const int64_t *__restric
 
 // ------------------------------------------------------------------- P4
 
-template <bool kCompressed>
+// Heads of the R chunks (the carried excursion up to its certain clamp):
+// lane per chunk, from the exact entry.  Uncompressed tables read the
+// expanded table (J indices per read) like P1.
+template <int J, bool kCompressed>
 __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
                                                int k, TableView tv, const uint16_t *__restrict__ codes,
                                                Carry cr, unsigned int *__restrict__ err) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
   const int mode = cr.mode[c];
-  if (mode == kModeL) return;  // head written by the carry from the summary
+  if (mode == kModeL || mode == kModeU) return;  // head written by the carry (summary / replay)
   cr.hq[c] = -1;
   cr.hmax[c] = -1.0;
   cr.harg[c] = 0;
@@ -634,39 +699,79 @@ __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restri
   const double x = cr.x[c];
   const int n = g.n[c];
   const int64_t start = g.start[c];
-  const uint32_t mask = (1u << (2 * k)) - 1u;
-  uint32_t code = kCompressed ? 0u : prime_code(seq, start - k, k);
   double T = x, hmax = -1.0;
   int harg = 0, hq = -1;
-  for (int b0 = 0; b0 < n && hq < 0; b0 += NB) {
-    double v[NB];
-    if (kCompressed) {
+  if (kCompressed) {
+    for (int b0 = 0; b0 < n && hq < 0; b0 += NB) {
+      double v[NB];
       const uint4 w0 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0));
       const uint4 w1 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0 + 8));
       const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
       for (int j = 0; j < NB; ++j) v[j] = tv.lut[(w[j >> 1] >> (16 * (j & 1))) & 0xffffu];
-    } else {
-      uint8_t by[16];
-      load16(seq, start + b0, total, by);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        v[j] = (b0 + j < n) ? tv.vals[code] : 0.0;
-        code = roll(code, by[j], mask);
+        const int i = b0 + j;
+        if (i < n && hq < 0) {
+          const double t = T + v[j];
+          T = t > 0 ? t : 0.0;
+          if (T == 0.0) hq = i;
+          else if (T > hmax) { hmax = T; harg = i; }
+        }
       }
     }
+  } else {
+    constexpr int G = (J == 1) ? 16 : (J == 4 ? 4 : 8);
+    constexpr int PB = G * J;
+    const int kx = k + J - 1;
+    const uint32_t xmask = (kx >= 16) ? 0xffffffffu : ((1u << (2 * kx)) - 1u);
+    uint32_t gcode = prime_code_guarded(seq, start - k, kx, total);
+    for (int b0 = 0; b0 < n && hq < 0; b0 += PB) {
+      uint8_t by[32];
+      load16(seq, start + b0 + J - 1, total, by);
+      if (PB > 16) load16(seq, start + b0 + J - 1 + 16, total, by + 16);
+      uint32_t gc[G];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int i = b0 + j;
-      if (i < n && hq < 0) {
-        const double t = T + v[j];
-        T = t > 0 ? t : 0.0;
-        if (T == 0.0) hq = i;
-        else if (T > hmax) { hmax = T; harg = i; }
+      for (int gi = 0; gi < G; ++gi) {
+        gc[gi] = gcode;
+#pragma unroll
+        for (int t = 0; t < J; ++t) gcode = ((gcode << 2) | enc(by[gi * J + t])) & xmask;
+      }
+      double v[PB];
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi) {
+        const bool live = b0 + gi * J < n;
+        if (J == 1) {
+          v[gi] = live ? tv.vals[gc[gi]] : 0.0;
+        } else {
+          double2 e0 = make_double2(0.0, 0.0), e1 = e0;
+          if (live) {
+            const double2 *E = reinterpret_cast<const double2 *>(tv.ext);
+            if (J <= 2) {
+              e0 = E[gc[gi]];
+            } else {
+              e0 = E[2 * (size_t)gc[gi]];
+              e1 = E[2 * (size_t)gc[gi] + 1];
+            }
+          }
+          const double ev[4] = {e0.x, e0.y, e1.x, e1.y};
+#pragma unroll
+          for (int t = 0; t < J; ++t) v[gi * J + t] = ev[t];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < PB; ++j) {
+        const int i = b0 + j;
+        if (i < n && hq < 0) {
+          const double t = T + v[j];
+          T = t > 0 ? t : 0.0;
+          if (T == 0.0) hq = i;
+          else if (T > hmax) { hmax = T; harg = i; }
+        }
       }
     }
   }
-  if (mode == kModeR && hq < 0) atomicOr(err, 2u);  // predicted clamp did not happen
+  if (hq < 0) atomicOr(err, 2u);  // predicted clamp did not happen
   cr.hq[c] = hq;
   cr.hmax[c] = hmax;
   cr.harg[c] = harg;
@@ -734,70 +839,161 @@ __device__ __forceinline__ int64_t valid_from(int mode, int hq, int64_t st, int6
   return hq >= 0 ? st + hq + 1 : en;
 }
 
-__global__ void __launch_bounds__(64) k_stitch(Chunks g, const int64_t *__restrict__ cbase, int64_t nruns,
-                                               const int64_t *__restrict__ rb_end, const int32_t *__restrict__ rseq,
-                                               int k, P1 o, Carry cr, uint64_t mw, double min_score, RegionBuf out,
-                                               Rescan rs, unsigned int *__restrict__ err) {
+// The operator of chunk c on the open-excursion state, plus what the chunk
+// needs to emit a closing excursion.
+struct ChunkOp {
+  XState f;
+  bool closes;
+  int64_t close_pos;
+  double hmax;
+  int64_t harg;
+  int mode;
+};
+
+__device__ __forceinline__ ChunkOp chunk_op(const Chunks &g, const P1 &o, const Carry &cr, int64_t c) {
+  ChunkOp r;
+  r.f = XState{0, 0, 0, 0, -INFINITY};  // identity
+  r.closes = false;
+  r.close_pos = 0;
+  r.hmax = -INFINITY;
+  r.harg = 0;
+  const int64_t st = g.start[c];
+  const int64_t en = st + g.n[c];
+  const int mode = cr.mode[c];
+  const int hq = cr.hq[c];
+  const int tb = o.tbeg[c];
+  r.mode = mode;
+  const int64_t vf = valid_from(mode, hq, st, en);
+  if (mode != kModeClean && hq != 0) { r.hmax = cr.hmax[c]; r.harg = st + cr.harg[c]; }
+  r.closes = mode != kModeClean && hq >= 0;
+  r.close_pos = st + hq;
+  const bool opens = tb >= 0 && st + tb >= vf && !(mode != kModeClean && hq < 0);
+  if (opens) {
+    r.f = XState{1, 1, st + tb, st + o.targ[c], o.tmax[c]};
+  } else if (r.closes) {
+    r.f = XState{1, 0, 0, 0, -1.0};
+  } else if (mode != kModeClean) {
+    r.f = XState{0, 0, 0, r.harg, r.hmax};
+  }
+  return r;
+}
+
+__device__ __forceinline__ XState wave_inclusive(XState inc, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const XState p = x_shfl_up(inc, d);
+    if (lane >= d) inc = x_compose(p, inc);
+  }
+  return inc;
+}
+
+// Tile t (64 chunks of one run, aligned to the run's first chunk) -> run id
+// and first chunk.
+__device__ __forceinline__ void tile_of(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
+                                        int64_t nruns, int64_t t, int64_t &r, int64_t &c0, int64_t &c1) {
+  int64_t lo = 0, hi = nruns - 1;  // last run with tbase[r] <= t
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (tbase[mid] <= t) lo = mid; else hi = mid - 1;
+  }
+  r = lo;
+  c0 = cbase[lo] + (t - tbase[lo]) * 64;
+  c1 = min(c0 + 64, cbase[lo + 1]);
+}
+
+// Stitch as a three-phase segmented scan (tile aggregates in parallel, a
+// short per-run scan of the aggregates, then every tile again with its
+// carry-in).  Chunk c acts on the open excursion state by one of:
+// RESET(tail or none) -- an excursion closes in the chunk and/or its clean
+// tail opens a new one -- or EXTEND(head) -- the carried excursion takes the
+// chunk's head maximum (first argmax: a later head wins only when strictly
+// greater).  The operator is associative; the chunk that closes an excursion
+// emits it.
+struct XTiles {
+  int32_t *reset, *open;
+  long long *xb, *xa;
+  double *xm;
+};
+
+__device__ __forceinline__ void xt_store(const XTiles &a, int64_t t, const XState &v) {
+  a.reset[t] = v.reset; a.open[t] = v.open; a.xb[t] = v.xb; a.xa[t] = v.xa; a.xm[t] = v.xm;
+}
+__device__ __forceinline__ XState xt_load(const XTiles &a, int64_t t) {
+  return XState{a.reset[t], a.open[t], a.xb[t], a.xa[t], a.xm[t]};
+}
+
+__global__ void __launch_bounds__(64) k_stitch_tiles(Chunks g, const int64_t *__restrict__ tbase,
+                                                     const int64_t *__restrict__ cbase, int64_t nruns, P1 o,
+                                                     Carry cr, XTiles agg) {
+  const int64_t t = blockIdx.x;
+  const int lane = threadIdx.x;
+  int64_t r, c0, c1;
+  tile_of(tbase, cbase, nruns, t, r, c0, c1);
+  const int64_t c = c0 + lane;
+  XState f{0, 0, 0, 0, -INFINITY};
+  if (c < c1) f = chunk_op(g, o, cr, c).f;
+  const XState inc = wave_inclusive(f, lane);
+  if (lane == 63) xt_store(agg, t, inc);
+}
+
+// Per run: exclusive scan of its tile aggregates (64 tiles per step) -> the
+// state entering each tile; the excursion still open at the run end is
+// emitted here.
+__global__ void __launch_bounds__(64) k_stitch_runs(const int64_t *__restrict__ tbase, int64_t nruns,
+                                                    const int64_t *__restrict__ rb_end,
+                                                    const int32_t *__restrict__ rseq, int k, uint64_t mw,
+                                                    double min_score, XTiles agg, XTiles tin, RegionBuf out,
+                                                    Rescan rs) {
   const int64_t r = blockIdx.x;
   if (r >= nruns) return;
   const int lane = threadIdx.x;
-  const int64_t c0 = cbase[r], c1 = cbase[r + 1];
-  if (c0 == c1) return;
-  const int32_t sid = rseq[r];
-  const int64_t last = rb_end[r] - 1;
-  XState carry{1, 0, 0, 0, -1.0};  // state entering the tile: closed
-  for (int64_t cb = c0; cb < c1; cb += 64) {
-    const int64_t c = cb + lane;
-    const bool live = c < c1;
-    XState f{0, 0, 0, 0, -INFINITY};  // identity
-    bool closes = false;
-    int64_t st = 0, close_pos = 0;
-    double hmax = -INFINITY;
-    int64_t harg = 0;
-    if (live) {
-      st = g.start[c];
-      const int64_t en = st + g.n[c];
-      const int mode = cr.mode[c];
-      const int hq = cr.hq[c];
-      const int tb = o.tbeg[c];
-      const int64_t vf = valid_from(mode, hq, st, en);
-      if (mode != kModeClean && hq != 0) { hmax = cr.hmax[c]; harg = st + cr.harg[c]; }
-      closes = mode != kModeClean && hq >= 0;
-      close_pos = st + hq;
-      const bool opens = tb >= 0 && st + tb >= vf && !(mode != kModeClean && hq < 0);
-      if (opens) {
-        f = XState{1, 1, st + tb, st + o.targ[c], o.tmax[c]};
-      } else if (closes) {
-        f = XState{1, 0, 0, 0, -1.0};
-      } else if (mode != kModeClean) {
-        f = XState{0, 0, 0, harg, hmax};
-      }
-    }
-    // inclusive scan of the chunk operators
-    XState inc = f;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const XState p = x_shfl_up(inc, d);
-      if (lane >= d) inc = x_compose(p, inc);
-    }
+  const int64_t t0 = tbase[r], t1 = tbase[r + 1];
+  if (t0 == t1) return;
+  XState carry{1, 0, 0, 0, -1.0};  // closed
+  for (int64_t tb = t0; tb < t1; tb += 64) {
+    const int64_t t = tb + lane;
+    XState f{0, 0, 0, 0, -INFINITY};
+    if (t < t1) f = xt_load(agg, t);
+    const XState inc = wave_inclusive(f, lane);
     XState exc = x_shfl_up(inc, 1);
     if (lane == 0) exc = XState{0, 0, 0, 0, -INFINITY};
-    const XState in = x_compose(carry, exc);  // state entering chunk c (a RESET)
-    if (live && closes) {
-      if (!in.open) {
-        atomicOr(err, 4u);
-      } else {
-        double xm = in.xm;
-        long long xa = in.xa;
-        if (hmax > xm) { xm = hmax; xa = harg; }
-        if ((uint64_t)(xa - in.xb) >= mw && xm >= min_score) emit(out, rs, sid, k, in.xb, xa, xm, close_pos);
-      }
-    }
-    if (live && !closes && f.reset == 0 && (cr.mode[c] != kModeClean) && !in.open) atomicOr(err, 8u);
+    if (t < t1) xt_store(tin, t, x_compose(carry, exc));
     carry = x_compose(carry, x_shfl(inc, 63));
   }
   if (lane == 0 && carry.open && (uint64_t)(carry.xa - carry.xb) >= mw && carry.xm >= min_score)
-    emit(out, rs, sid, k, carry.xb, carry.xa, carry.xm, last);
+    emit(out, rs, rseq[r], k, carry.xb, carry.xa, carry.xm, rb_end[r] - 1);
+}
+
+__global__ void __launch_bounds__(64) k_stitch_emit(Chunks g, const int64_t *__restrict__ tbase,
+                                                    const int64_t *__restrict__ cbase, int64_t nruns,
+                                                    const int32_t *__restrict__ rseq, int k, P1 o, Carry cr,
+                                                    uint64_t mw, double min_score, XTiles tin, RegionBuf out,
+                                                    Rescan rs, unsigned int *__restrict__ err) {
+  const int64_t t = blockIdx.x;
+  const int lane = threadIdx.x;
+  int64_t r, c0, c1;
+  tile_of(tbase, cbase, nruns, t, r, c0, c1);
+  const int64_t c = c0 + lane;
+  const bool live = c < c1;
+  ChunkOp op;
+  op.f = XState{0, 0, 0, 0, -INFINITY};
+  op.closes = false;
+  if (live) op = chunk_op(g, o, cr, c);
+  const XState inc = wave_inclusive(op.f, lane);
+  XState exc = x_shfl_up(inc, 1);
+  if (lane == 0) exc = XState{0, 0, 0, 0, -INFINITY};
+  const XState in = x_compose(xt_load(tin, t), exc);  // state entering chunk c
+  if (live && op.closes) {
+    if (!in.open) {
+      atomicOr(err, 4u);
+    } else {
+      double xm = in.xm;
+      long long xa = in.xa;
+      if (op.hmax > xm) { xm = op.hmax; xa = op.harg; }
+      if ((uint64_t)(xa - in.xb) >= mw && xm >= min_score) emit(out, rs, rseq[r], k, in.xb, xa, xm, op.close_pos);
+    }
+  }
+  if (live && !op.closes && op.f.reset == 0 && op.mode != kModeClean && !in.open) atomicOr(err, 8u);
 }
 
 // Candidates (closed emittable excursions of the clean trajectories) are
@@ -839,6 +1035,9 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
   }
   const int64_t nch = cb[nruns];
   if (nch == 0) return KS_OK;
+  std::vector<int64_t> tbv(nruns + 1, 0);  // stitch tiles: 64 chunks, aligned to each run's first chunk
+  for (int64_t r = 0; r < nruns; ++r) tbv[r + 1] = tbv[r] + (cb[r + 1] - cb[r] + 63) / 64;
+  const int64_t ntiles = tbv[nruns];
   const bool comp = tv.compressed != 0;
 
   // ---- workspace
@@ -860,6 +1059,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
   const size_t o_hq = off; off += al(nch * 4 * 2);
   const size_t o_hmax = off; off += al(nch * 8);
   const size_t o_cnt = off; off += al(64);
+  const size_t o_tbase = off; off += al((nruns + 1) * 8);
+  const size_t o_xagg = off; off += al(ntiles * 32) * 2;
   void *wsp = nullptr;
   KS_TRY(ensure(ctx, SLOT_CHUNK_A, off, &wsp));
   char *W = static_cast<char *>(wsp);
@@ -878,15 +1079,23 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
   Carry cr{reinterpret_cast<double *>(W + o_x), reinterpret_cast<uint8_t *>(W + o_mode), hqp,
            reinterpret_cast<double *>(W + o_hmax), hqp + nch};
   unsigned long long *cnts = reinterpret_cast<unsigned long long *>(W + o_cnt);
+  int64_t *d_tbase = reinterpret_cast<int64_t *>(W + o_tbase);
+  auto xtiles = [&](char *p) {
+    return XTiles{reinterpret_cast<int32_t *>(p), reinterpret_cast<int32_t *>(p) + ntiles,
+                  reinterpret_cast<long long *>(p + ntiles * 8), reinterpret_cast<long long *>(p + ntiles * 16),
+                  reinterpret_cast<double *>(p + ntiles * 24)};
+  };
+  const XTiles xagg = xtiles(W + o_xagg), xtin = xtiles(W + o_xagg + al(ntiles * 32));
   // cnts: [0] candidates, [1] rescans, [2] replays, [3] error bits (u32)
   KS_HIP(hipMemsetAsync(cnts, 0, 64, st));
   KS_HIP(hipMemcpyAsync(d_cbase, cb.data(), (nruns + 1) * 8, hipMemcpyHostToDevice, st));
+  KS_HIP(hipMemcpyAsync(d_tbase, tbv.data(), (nruns + 1) * 8, hipMemcpyHostToDevice, st));
 
   uint16_t *codes = nullptr;
   if (comp) {
     void *cp = nullptr;
-    const int64_t ntiles = (nch + 63) / 64;
-    KS_TRY(ensure(ctx, SLOT_CHUNK_B, (size_t)ntiles * 64 * CH * 2, &cp));
+    const int64_t ctiles = (nch + 63) / 64;  // code store tiles (global chunk index / 64)
+    KS_TRY(ensure(ctx, SLOT_CHUNK_B, (size_t)ctiles * 64 * CH * 2, &cp));
     codes = static_cast<uint16_t *>(cp);
   }
   int64_t ccap = std::max<int64_t>(1 << 16, nch / 4);
@@ -918,46 +1127,89 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
 #undef KS_P1
   KS_HIP(hipGetLastError());
   KS_HIP(hipEventRecord(e_p1b, st));
-  // KS_DEBUG_CARRY=1: per-run carry statistics to stderr (diagnostics only)
+  // segments of the carry chain (k_seg_marks) -> seg[0..nseg], seg[nseg] = nch
+  const int64_t nwin = (nch + 63) / 64;
+  const int64_t nseg_max = nwin + nruns;
+  unsigned long long *d_nseg = cnts + 4;
+  void *segp = nullptr;
+  KS_TRY(ensure(ctx, SLOT_CHUNK_D, (size_t)(nseg_max + 2) * 8 + (size_t)nch + 256, &segp));
+  int64_t *d_seg = static_cast<int64_t *>(segp);
+  uint8_t *d_flag = reinterpret_cast<uint8_t *>(d_seg + nseg_max + 2);
+  // KS_DEBUG_CARRY=1: per-segment carry statistics to stderr (diagnostics only)
   static const bool dbg_on = getenv("KS_DEBUG_CARRY") != nullptr;
   long long *dbg = nullptr;
-  if (dbg_on) KS_HIP(hipMalloc(&dbg, nruns * 6 * sizeof(long long)));
+  if (dbg_on) KS_HIP(hipMalloc(&dbg, std::max(nseg_max, nruns) * 6 * sizeof(long long)));
   hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)nruns), dim3(64), 0, st, d_cbase, nruns, p1, xt);
   KS_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_seg_marks, dim3((unsigned)nwin), dim3(64), 0, st, g, p1, xt, d_flag);
+  KS_HIP(hipGetLastError());
+  {
+    size_t tb = 0;
+    hipcub::CountingInputIterator<int64_t> it(0);
+    KS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, it, d_flag, d_seg, d_nseg, (int)nch, st));
+    void *tmp = nullptr;
+    KS_TRY(ensure(ctx, SLOT_SORT_TMP, tb, &tmp));
+    KS_HIP(hipcub::DeviceSelect::Flagged(tmp, tb, it, d_flag, d_seg, d_nseg, (int)nch, st));
+    hipLaunchKernelGGL(k_seg_sentinel, dim3(1), dim3(1), 0, st, d_seg, d_nseg, nch);
+    KS_HIP(hipGetLastError());
+  }
   if (comp)
     hipLaunchKernelGGL(k_summaries<true>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, p1, xt, sm);
   else
     hipLaunchKernelGGL(k_summaries<false>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, p1, xt, sm);
   KS_HIP(hipGetLastError());
-  if (comp)
-    hipLaunchKernelGGL(k_carry<true>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, total, k,
-                       tv, codes, p1, sm, cr, cnts + 2, dbg);
-  else
-    hipLaunchKernelGGL(k_carry<false>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, total, k,
-                       tv, codes, p1, sm, cr, cnts + 2, dbg);
-  KS_HIP(hipGetLastError());
   unsigned int *d_err = reinterpret_cast<unsigned int *>(cnts + 3);
-  if (comp)
-    hipLaunchKernelGGL(k_heads<true>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, cr, d_err);
-  else
-    hipLaunchKernelGGL(k_heads<false>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, cr, d_err);
-  KS_HIP(hipGetLastError());
-  unsigned long long hc[4] = {0, 0, 0, 0};
-  KS_HIP(hipMemcpyAsync(hc, cnts, 32, hipMemcpyDeviceToHost, st));
+  // per segment (seg_mode) or per run (fallback: the whole chain of a run in one wave)
+  auto carry_and_heads = [&](bool seg_mode) -> ks_status {
+    const int64_t *sg = seg_mode ? d_seg : d_cbase;
+    const int64_t nb = seg_mode ? nseg_max : nruns;
+    const unsigned long long *dn = seg_mode ? d_nseg : nullptr;
+    if (comp)
+      hipLaunchKernelGGL(k_carry<true>, dim3((unsigned)nb), dim3(64), 0, st, g, sg, nb, dn, s->seq, total, k, tv,
+                         codes, p1, sm, cr, cnts + 2, d_err, dbg);
+    else
+      hipLaunchKernelGGL(k_carry<false>, dim3((unsigned)nb), dim3(64), 0, st, g, sg, nb, dn, s->seq, total, k, tv,
+                         codes, p1, sm, cr, cnts + 2, d_err, dbg);
+    KS_HIP(hipGetLastError());
+#define KS_HEADS(J, C) \
+  hipLaunchKernelGGL((k_heads<J, C>), dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, cr, d_err)
+    if (comp) KS_HEADS(1, true);
+    else if (J == 4) KS_HEADS(4, false);
+    else if (J == 3) KS_HEADS(3, false);
+    else if (J == 2) KS_HEADS(2, false);
+    else KS_HEADS(1, false);
+#undef KS_HEADS
+    KS_HIP(hipGetLastError());
+    return KS_OK;
+  };
+  KS_TRY(carry_and_heads(true));
+  unsigned long long hc[5] = {0, 0, 0, 0, 0};
+  KS_HIP(hipMemcpyAsync(hc, cnts, 40, hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
+  const int64_t nseg = (int64_t)hc[4];
+  // KS_TEST_SEG_FALLBACK=1 takes the fallback path unconditionally (tests)
+  const bool seg_failed = (hc[3] & 16u) != 0 || getenv("KS_TEST_SEG_FALLBACK") != nullptr;
+  if (seg_failed) {  // a segment entry assumption failed: redo the carry run by run
+    if (hc[3] & 16u) fprintf(stderr, "kmer_spans_amd: carry segment check failed; redoing the carry per run\n");
+    KS_HIP(hipMemsetAsync(cnts + 2, 0, 16, st));
+    KS_TRY(carry_and_heads(false));
+    KS_HIP(hipMemcpyAsync(hc, cnts, 40, hipMemcpyDeviceToHost, st));
+    KS_HIP(hipStreamSynchronize(st));
+  }
   if (dbg) {
-    std::vector<long long> h(nruns * 6);
-    KS_HIP(hipMemcpy(h.data(), dbg, nruns * 6 * sizeof(long long), hipMemcpyDeviceToHost));
+    const int64_t nd = seg_failed ? nruns : nseg;
+    std::vector<long long> h(nd * 6);
+    KS_HIP(hipMemcpy(h.data(), dbg, nd * 6 * sizeof(long long), hipMemcpyDeviceToHost));
     KS_HIP(hipFree(dbg));
-    std::vector<int64_t> idx(nruns);
-    for (int64_t i = 0; i < nruns; ++i) idx[i] = i;
+    std::vector<int64_t> idx(nd);
+    for (int64_t i = 0; i < nd; ++i) idx[i] = i;
     std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return h[6 * a] > h[6 * b]; });
     long long tot[6] = {0, 0, 0, 0, 0, 0};
-    for (int64_t i = 0; i < nruns; ++i)
+    for (int64_t i = 0; i < nd; ++i)
       for (int q = 0; q < 6; ++q) tot[q] += h[6 * i + q];
-    fprintf(stderr, "[carry] runs %lld chunks %lld replays %lld recomputes %lld L %lld R %lld\n", (long long)nruns,
-            tot[1], tot[2], tot[3], tot[4], tot[5]);
-    for (int64_t i = 0; i < std::min<int64_t>(nruns, 8); ++i) {
+    fprintf(stderr, "[carry] segments %lld (runs %lld) chunks %lld replays %lld recomputes %lld L %lld R %lld\n",
+            (long long)nd, (long long)nruns, tot[1], tot[2], tot[3], tot[4], tot[5]);
+    for (int64_t i = 0; i < std::min<int64_t>(nd, 8); ++i) {
       const long long *d = &h[6 * idx[i]];
       fprintf(stderr, "[carry] run %lld cycles %lld chunks %lld replays %lld recomputes %lld L %lld R %lld\n",
               (long long)idx[i], d[0], d[1], d[2], d[3], d[4], d[5]);
@@ -975,15 +1227,21 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
   KS_TRY(ensure(ctx, SLOT_WORK_A, (size_t)rcap * 20 + 1024, &rsb));
   Rescan rs{reinterpret_cast<int64_t *>(rsb), reinterpret_cast<int64_t *>(rsb) + rcap,
             reinterpret_cast<int32_t *>(reinterpret_cast<int64_t *>(rsb) + 2 * rcap), cnts + 1, rcap};
-  hipLaunchKernelGGL(k_stitch, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, runs.b, runs.seq, k, p1, cr,
-                     mw, min_score, rb, rs, d_err);
+  hipLaunchKernelGGL(k_stitch_tiles, dim3((unsigned)ntiles), dim3(64), 0, st, g, d_tbase, d_cbase, nruns, p1, cr,
+                     xagg);
+  KS_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_stitch_runs, dim3((unsigned)nruns), dim3(64), 0, st, d_tbase, nruns, runs.b, runs.seq, k, mw,
+                     min_score, xagg, xtin, rb, rs);
+  KS_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_stitch_emit, dim3((unsigned)ntiles), dim3(64), 0, st, g, d_tbase, d_cbase, nruns, runs.seq, k,
+                     p1, cr, mw, min_score, xtin, rb, rs, d_err);
   KS_HIP(hipGetLastError());
   if (ncand > 0) {
     hipLaunchKernelGGL(k_candidates, dim3((unsigned)((ncand + 255) / 256)), dim3(256), 0, st, g, runs.a, d_cbase,
                        nruns, runs.seq, k, cand, ncand, cr, rb, rs);
     KS_HIP(hipGetLastError());
   }
-  KS_HIP(hipMemcpyAsync(hc, cnts, 32, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipMemcpyAsync(hc, cnts, 40, hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
   const unsigned int errbits = (unsigned int)(hc[3] & 0xffffffffu);
   float ms_p1 = 0;
@@ -991,7 +1249,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
   KS_HIP(hipEventDestroy(e_p1a));
   KS_HIP(hipEventDestroy(e_p1b));
   if (errbits) return fail(KS_ERR_INTERNAL, "chunked scan consistency check failed (bits %u)", errbits);
-  if ((int64_t)hc[1] > rcap) return fail(KS_ERR_INTERNAL, "rescan buffer overflow");
+  if ((int64_t)hc[1] > rcap) return KS_INTERNAL_RETRY;  // regions overflowed too: the caller grows and reruns
   float ms_all = 0;
   KS_HIP(hipEventRecord(ctx->ev[6], st));
   KS_HIP(hipEventSynchronize(ctx->ev[6]));

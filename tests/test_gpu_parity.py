@@ -297,3 +297,55 @@ def test_expanded_table_edges(K, oracle, ctx, k, compress):
         _assert_same_regions(pos, sc, o["pos"], o["score"], ("ext", k, algo))
         assert np.array_equal(vis.cpu().numpy(), o["counts"])
     ctx.set_scan_algo(-1)
+
+
+def test_many_regions_retry(K, oracle):
+    """More regions (and rescans) than the initial region buffer holds: the
+    chunked path grows the buffer and reruns with visits counted once; one
+    long run so that the carry is cut into many segments."""
+    import torch
+    from kmer_spans_amd import _lib, device as D
+    ctx = _lib.Context(0)  # fresh workspace: the initial region buffer is the minimum
+    k = 6
+    rng = np.random.default_rng(5)
+    seq = "".join(rng.choice(list("ACGT"), 4_000_000))
+    w = rng.normal(size=4 ** k) - 0.05
+    ds = D.from_host([seq], "cuda")
+    D.bind_torch_stream(ctx)
+    tab = D.DeviceTable(ctx, w, k, 0.0, expand=True)
+    o = oracle.scan([seq], k, w, 0.0, 0, 0.5, visits=True)
+    assert o["pos"].shape[1] > 150_000
+    for algo in ALGOS:
+        ctx.set_scan_algo(algo)
+        vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+        pos, sc, st = D.scan(ctx, ds, k, tab, 0, 0.5, vis)
+        _assert_same_regions(pos, sc, o["pos"], o["score"], ("many", algo))
+        assert np.array_equal(vis.cpu().numpy(), o["counts"])
+    del tab
+    ctx.close()
+
+
+def test_carry_segment_fallback(K, oracle, ctx, monkeypatch):
+    """The per-run carry that replaces a failed segment assumption gives the
+    same results (KS_TEST_SEG_FALLBACK forces that path)."""
+    import torch
+    from kmer_spans_amd import device as D, genome
+    s = genome.contig(2_000_000, 33, device="cuda", repeats=True)
+    ds = D.from_parts([s], [s.numel()], "cuda")
+    host = [ds.host_seq(0)]
+    k = 9
+    n, oc = oracle.kmer_counts(host, k)
+    w = K.rank_table(oc, k, n)
+    D.bind_torch_stream(ctx)
+    tab = D.DeviceTable(ctx, w, k, 0.75, expand=True)
+    o = oracle.scan(host, k, w, 0.75, 20, 5.0, visits=True)
+    ctx.set_scan_algo(1)
+    for forced in (False, True):
+        if forced:
+            monkeypatch.setenv("KS_TEST_SEG_FALLBACK", "1")
+        vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+        pos, sc, st = D.scan(ctx, ds, k, tab, 20, 5.0, vis)
+        _assert_same_regions(pos, sc, o["pos"], o["score"], ("segfb", forced))
+        assert np.array_equal(vis.cpu().numpy(), o["counts"])
+    monkeypatch.delenv("KS_TEST_SEG_FALLBACK")
+    ctx.set_scan_algo(-1)

@@ -107,8 +107,9 @@ def check(rc: int) -> None:
 def regions_to_numpy(r: Regions):
     """Copy a ks_regions into (pos int32[3, n], score float64[2, n]) and free it."""
     n = int(r.n)
-    pos = np.zeros((3, n), dtype=np.int32)
-    score = np.zeros((2, n), dtype=np.float64)
+    pos = np.empty((3, n), dtype=np.int32)
+    score = np.empty((2, n), dtype=np.float64)
+    score[1] = 0.0
     if n:
         pos[0] = np.ctypeslib.as_array(r.seq_id, shape=(n,))
         pos[1] = np.ctypeslib.as_array(r.beg, shape=(n,))

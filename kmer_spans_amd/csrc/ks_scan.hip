@@ -13,6 +13,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstring>
 #include <numeric>
 
 #include "ks_scan_common.h"
@@ -25,46 +26,56 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
 
 namespace {
 
-// Values of a batch of kBatch consecutive scan indices are gathered before
-// the sequential state machine consumes them, so a lane keeps kBatch random
+// Values of a batch of consecutive scan indices are gathered before the
+// sequential state machine consumes them, so a lane keeps several random
 // table reads in flight instead of one (the gathers do not depend on S).
-constexpr int kBatch = 16;
-
-__global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ seq,
+// With an expanded table one read serves J consecutive indices (the
+// (k+J-1)-mer spanning them), as in the chunked gather pass.
+template <int J, bool kCompressed>
+__global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ seq, int64_t total,
                                                   const int64_t *__restrict__ ra,
                                                   const int64_t *__restrict__ rbnd,
                                                   const int32_t *__restrict__ rseq, int64_t nruns,
                                                   int k, TableView tv, uint64_t mw, double min_score,
                                                   uint32_t *__restrict__ visits, RegionBuf out) {
+  constexpr int G = (J == 1) ? 16 : (J == 4 ? 4 : (J == 3 ? 6 : 8));  // reads per batch
+  constexpr int PB = G * J;                                           // indices per batch (16, 16, 18, 16)
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= nruns) return;
   const int64_t a = ra[r], b = rbnd[r];
   if (b - a <= k) return;
   const int32_t sid = rseq[r];
-  const uint32_t mask = (1u << (2 * k)) - 1u;
+  const int kx = k + J - 1;
+  const uint32_t xmask = (kx >= 16) ? 0xffffffffu : ((1u << (2 * kx)) - 1u);
+  const uint32_t kmask = (1u << (2 * k)) - 1u;
   int64_t i = a;  // priming point
   for (;;) {
-    uint32_t code = prime_code(seq, i, k);  // k-mer scored at index i + k
+    // (k+J-1)-mer of the group starting at scan index i + k
+    uint32_t gcode = prime_code_guarded(seq, i, kx, total);
     double S = 0.0, prev = 0.0, best = 0.0;
     int64_t beg = 0, arg = 0;
     bool restart = false;
-    for (int64_t p0 = i + k; p0 < b && !restart; p0 += kBatch) {
-      const int n = (int)((b - p0) < kBatch ? (b - p0) : kBatch);
-      double v[kBatch];
-      uint32_t c[kBatch];
-      uint32_t cc = code;
+    for (int64_t p0 = i + k; p0 < b && !restart; p0 += PB) {
+      const int n = (int)((b - p0) < PB ? (b - p0) : PB);
+      double v[PB];
+      uint32_t gc[G];
 #pragma unroll
-      for (int j = 0; j < kBatch; ++j) {
-        c[j] = cc;
-        if (j < n) v[j] = tv_get(tv, cc);
-        if (j < n) cc = ((cc << 2) | enc(seq[p0 + j])) & mask;
+      for (int g = 0; g < G; ++g) {
+        gc[g] = gcode;
+        if (g * J < n) {
+          gather_group<J, kCompressed>(tv, gcode, v + g * J);
+#pragma unroll
+          for (int t = 0; t < J; ++t) {
+            const int64_t q = p0 + g * J + J - 1 + t;
+            gcode = ((gcode << 2) | enc(q < total ? seq[q] : (uint8_t)'N')) & xmask;
+          }
+        }
       }
-      code = cc;
 #pragma unroll
-      for (int j = 0; j < kBatch; ++j) {  // fully unrolled: v[]/c[] stay in registers
+      for (int j = 0; j < PB; ++j) {  // fully unrolled: v[]/gc[] stay in registers
         if (j < n && !restart) {
           const int64_t p = p0 + j;
-          if (visits) atomicAdd(&visits[c[j]], 1u);
+          if (visits) atomicAdd(&visits[(gc[j / J] >> (2 * (J - 1 - j % J))) & kmask], 1u);
           const double t = prev + v[j];
           S = t > 0 ? t : 0.0;
           if (prev == 0 && S > 0) { beg = p; arg = p; best = S; }
@@ -127,12 +138,20 @@ __global__ void k_add_hist(uint32_t *__restrict__ dst, const uint32_t *__restric
 
 }  // namespace
 
-ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, const int64_t *ra, const int64_t *rb,
+ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const int64_t *ra, const int64_t *rb,
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out) {
   if (n <= 0) return KS_OK;
-  hipLaunchKernelGGL(k_scan_lane, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, ra, rb, rs, n, k,
-                     tv, mw, min_score, visits, out);
+  const int J = tv.ext ? tv.ext_J : 1;
+#define KS_LANE(J, C)                                                                                   \
+  hipLaunchKernelGGL((k_scan_lane<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, total, \
+                     ra, rb, rs, n, k, tv, mw, min_score, visits, out)
+  if (tv.compressed) {
+    if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
+  } else {
+    if (J == 4) KS_LANE(4, false); else if (J == 3) KS_LANE(3, false); else if (J == 2) KS_LANE(2, false); else KS_LANE(1, false);
+  }
+#undef KS_LANE
   KS_HIP(hipGetLastError());
   return KS_OK;
 }
@@ -228,7 +247,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
       }
     }
     if (algo == 0) {
-      if (runs.n) KS_TRY(launch_scan_lane(ctx, s->seq, runs.a, runs.b, runs.seq, runs.n, k, tv, mw, min_score, vis, rb));
+      if (runs.n) KS_TRY(launch_scan_lane(ctx, s->seq, total, runs.a, runs.b, runs.seq, runs.n, k, tv, mw, min_score, vis, rb));
     }
     KS_HIP(hipEventRecord(ctx->ev[4], st));
     KS_HIP(hipMemcpyAsync(&n_reg, d_rcount, 8, hipMemcpyDeviceToHost, st));
@@ -273,7 +292,6 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     const unsigned g = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(k_region_keys, dim3(g), dim3(256), 0, st, rb.beg, n, k_in, v_in);
     KS_HIP(hipGetLastError());
-    const int64_t total = s->offsets_host[s->nseq];
     int end_bit = 1;
     while (end_bit < 64 && ((unsigned long long)total >> end_bit)) ++end_bit;
     size_t tb = 0;
@@ -284,13 +302,23 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     hipLaunchKernelGGL(k_region_gather, dim3(g), dim3(256), 0, st, rb, v_out, n, s->offsets_dev, o_seq, o_beg,
                        o_end, o_score);
     KS_HIP(hipGetLastError());
-    KS_HIP(hipMemcpyAsync(out->seq_id, o_seq, nn * 4, hipMemcpyDeviceToHost, st));
-    KS_HIP(hipMemcpyAsync(out->beg, o_beg, nn * 4, hipMemcpyDeviceToHost, st));
-    KS_HIP(hipMemcpyAsync(out->end, o_end, nn * 4, hipMemcpyDeviceToHost, st));
-    KS_HIP(hipMemcpyAsync(out->score, o_score, nn * 8, hipMemcpyDeviceToHost, st));
+    // one D2H of the contiguous [seq | beg | end | score] block into pinned
+    // staging, then host copies into the caller-owned arrays
+    const size_t blk = (size_t)(reinterpret_cast<char *>(o_score + nn) - reinterpret_cast<char *>(o_seq));
+    void *hp = nullptr;
+    KS_TRY(ensure_pinned(ctx, blk, &hp));
+    KS_HIP(hipMemcpyAsync(hp, o_seq, blk, hipMemcpyDeviceToHost, st));
+    KS_HIP(hipEventRecord(ctx->ev[6], st));
+    KS_HIP(hipStreamSynchronize(st));
+    const char *h = static_cast<const char *>(hp);
+    memcpy(out->seq_id, h, nn * 4);
+    memcpy(out->beg, h + (reinterpret_cast<char *>(o_beg) - reinterpret_cast<char *>(o_seq)), nn * 4);
+    memcpy(out->end, h + (reinterpret_cast<char *>(o_end) - reinterpret_cast<char *>(o_seq)), nn * 4);
+    memcpy(out->score, h + (reinterpret_cast<char *>(o_score) - reinterpret_cast<char *>(o_seq)), nn * 8);
+  } else {
+    KS_HIP(hipEventRecord(ctx->ev[6], st));
+    KS_HIP(hipStreamSynchronize(st));
   }
-  KS_HIP(hipEventRecord(ctx->ev[6], st));
-  KS_HIP(hipStreamSynchronize(st));
   S->n_regions = n;
   float ms_fin = 0, ms_tot = 0;
   KS_HIP(hipEventElapsedTime(&ms_fin, ctx->ev[5], ctx->ev[6]));

@@ -37,7 +37,7 @@
 
 namespace ks {
 
-ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, const int64_t *ra, const int64_t *rb,
+ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const int64_t *ra, const int64_t *rb,
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out);
 
@@ -792,6 +792,44 @@ __device__ __forceinline__ void emit(const RegionBuf &rb, const Rescan &rs, int3
   }
 }
 
+// emit() for a whole wave (every lane calls it; lanes with want set emit):
+// one atomic per wave and buffer instead of one per region, so that millions
+// of regions do not serialise on the two counters.
+__device__ __forceinline__ void emit_wave(bool want, const RegionBuf &rb, const Rescan &rs, int32_t sid, int k,
+                                          int64_t beg, int64_t arg, double best, int64_t end) {
+  const unsigned long long m = __ballot(want);
+  if (m == 0) return;
+  const bool wr = want && arg + 1 <= end;
+  const unsigned long long mr = __ballot(wr);
+  const int lane = (int)(threadIdx.x & 63);
+  const int leader = __ffsll((long long)m) - 1;
+  unsigned long long base = 0, rbase = 0;
+  if (lane == leader) {
+    base = atomicAdd(rb.count, (unsigned long long)__popcll(m));
+    if (mr) rbase = atomicAdd(rs.count, (unsigned long long)__popcll(mr));
+  }
+  base = __shfl(base, leader, 64);
+  rbase = __shfl(rbase, leader, 64);
+  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  if (want) {
+    const unsigned long long slot = base + (unsigned long long)__popcll(m & below);
+    if ((int64_t)slot < rb.cap) {
+      rb.seq[slot] = sid;
+      rb.beg[slot] = beg;
+      rb.end[slot] = arg;
+      rb.score[slot] = best;
+    }
+  }
+  if (wr) {
+    const unsigned long long slot = rbase + (unsigned long long)__popcll(mr & below);
+    if ((int64_t)slot < rs.cap) {
+      rs.a[slot] = arg + 1 - k;
+      rs.b[slot] = end + 1;
+      rs.seq[slot] = sid;
+    }
+  }
+}
+
 // Stitch as a segmented scan, one wave per run.  Chunk c acts on the open
 // excursion state by one of: RESET(tail or none) -- an excursion closes in the
 // chunk and/or its clean tail opens a new one -- or EXTEND(head) -- the carried
@@ -983,16 +1021,18 @@ __global__ void __launch_bounds__(64) k_stitch_emit(Chunks g, const int64_t *__r
   XState exc = x_shfl_up(inc, 1);
   if (lane == 0) exc = XState{0, 0, 0, 0, -INFINITY};
   const XState in = x_compose(xt_load(tin, t), exc);  // state entering chunk c
+  bool want = false;
+  double xm = in.xm;
+  long long xa = in.xa;
   if (live && op.closes) {
     if (!in.open) {
       atomicOr(err, 4u);
     } else {
-      double xm = in.xm;
-      long long xa = in.xa;
       if (op.hmax > xm) { xm = op.hmax; xa = op.harg; }
-      if ((uint64_t)(xa - in.xb) >= mw && xm >= min_score) emit(out, rs, rseq[r], k, in.xb, xa, xm, op.close_pos);
+      want = (uint64_t)(xa - in.xb) >= mw && xm >= min_score;
     }
   }
+  emit_wave(want, out, rs, rseq[r], k, in.xb, xa, xm, op.close_pos);
   if (live && !op.closes && op.f.reset == 0 && op.mode != kModeClean && !in.open) atomicOr(err, 8u);
 }
 
@@ -1002,17 +1042,27 @@ __global__ void k_candidates(Chunks g, const int64_t *__restrict__ ra, const int
                              int64_t nruns, const int32_t *__restrict__ rseq, int k, Cand cand, int64_t ncand,
                              Carry cr, RegionBuf out, Rescan rs) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ncand) return;
-  const int64_t b = cand.beg[i];
-  int64_t lo = 0, hi = nruns - 1;  // last run with ra <= b
-  while (lo < hi) {
-    const int64_t mid = (lo + hi + 1) >> 1;
-    if (ra[mid] <= b) lo = mid; else hi = mid - 1;
+  if ((int64_t)blockIdx.x * blockDim.x >= ncand) return;  // whole block idle
+  bool want = false;
+  int64_t b = 0, arg = 0, rst = 0;
+  double best = 0.0;
+  int32_t sid = 0;
+  if (i < ncand) {
+    b = cand.beg[i];
+    int64_t lo = 0, hi = nruns - 1;  // last run with ra <= b
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (ra[mid] <= b) lo = mid; else hi = mid - 1;
+    }
+    const int64_t c = cbase[lo] + (b - (ra[lo] + k)) / CH;
+    const int64_t st = g.start[c];
+    want = b >= valid_from(cr.mode[c], cr.hq[c], st, st + g.n[c]);
+    sid = rseq[lo];
+    arg = cand.arg[i];
+    best = cand.best[i];
+    rst = cand.rst[i];
   }
-  const int64_t c = cbase[lo] + (b - (ra[lo] + k)) / CH;
-  const int64_t st = g.start[c];
-  if (b >= valid_from(cr.mode[c], cr.hq[c], st, st + g.n[c]))
-    emit(out, rs, rseq[lo], k, b, cand.arg[i], cand.best[i], cand.rst[i]);
+  emit_wave(want, out, rs, sid, k, b, arg, best, rst);
 }
 
 }  // namespace
@@ -1256,11 +1306,29 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
   KS_HIP(hipEventElapsedTime(&ms_all, ctx->ev[7], ctx->ev[6]));
   // rescans: the lane kernel on virtual runs
   const int64_t nres = (int64_t)hc[1];
+  if (dbg_on && nres > 0) {  // rescan length histogram (log2 buckets)
+    std::vector<int64_t> a(nres), b(nres);
+    KS_HIP(hipMemcpy(a.data(), rs.a, nres * 8, hipMemcpyDeviceToHost));
+    KS_HIP(hipMemcpy(b.data(), rs.b, nres * 8, hipMemcpyDeviceToHost));
+    long long hist[40] = {0}, tot = 0, mx = 0;
+    for (int64_t i = 0; i < nres; ++i) {
+      const long long L = b[i] - a[i] - k;
+      tot += L;
+      mx = std::max(mx, L);
+      int e = 0;
+      while (e < 39 && (1LL << (e + 1)) <= L) ++e;
+      ++hist[L > 0 ? e : 0];
+    }
+    fprintf(stderr, "[rescan] n %lld indices %lld max %lld |", (long long)nres, tot, mx);
+    for (int e = 0; e < 40; ++e)
+      if (hist[e]) fprintf(stderr, " 2^%d:%lld", e, hist[e]);
+    fprintf(stderr, "\n");
+  }
   hipEvent_t e_ra, e_rb;
   KS_HIP(hipEventCreate(&e_ra));
   KS_HIP(hipEventCreate(&e_rb));
   KS_HIP(hipEventRecord(e_ra, st));
-  if (nres > 0) KS_TRY(launch_scan_lane(ctx, s->seq, rs.a, rs.b, rs.seq, nres, k, tv, mw, min_score, visits, rb));
+  if (nres > 0) KS_TRY(launch_scan_lane(ctx, s->seq, total, rs.a, rs.b, rs.seq, nres, k, tv, mw, min_score, visits, rb));
   KS_HIP(hipEventRecord(e_rb, st));
   KS_HIP(hipEventSynchronize(e_rb));
   float ms_res = 0;

@@ -20,6 +20,32 @@ __device__ __forceinline__ double tv_get(const TableView &t, uint32_t code) {
   return t.compressed ? t.lut[t.codes[code]] : t.vals[code];
 }
 
+// The J values of one expanded-table read: scan indices served by the
+// (k+J-1)-mer `gcode` (J = 1: the base table entry of the k-mer).
+template <int J, bool kCompressed>
+__device__ __forceinline__ void gather_group(const TableView &t, uint32_t gcode, double v[J]) {
+  if (J == 1) {
+    v[0] = kCompressed ? t.lut[t.codes[gcode]] : t.vals[gcode];
+  } else if (kCompressed) {
+    const uint64_t e = (J <= 2) ? (uint64_t)reinterpret_cast<const uint32_t *>(t.ext)[gcode]
+                                : reinterpret_cast<const uint64_t *>(t.ext)[gcode];
+#pragma unroll
+    for (int q = 0; q < J; ++q) v[q] = t.lut[(uint16_t)(e >> (16 * q))];
+  } else {
+    const double2 *E = reinterpret_cast<const double2 *>(t.ext);
+    double2 e0, e1 = make_double2(0.0, 0.0);
+    if (J <= 2) {
+      e0 = E[gcode];
+    } else {
+      e0 = E[2 * (size_t)gcode];
+      e1 = E[2 * (size_t)gcode + 1];
+    }
+    const double ev[4] = {e0.x, e0.y, e1.x, e1.y};
+#pragma unroll
+    for (int q = 0; q < J; ++q) v[q] = ev[q];
+  }
+}
+
 // Append one region record (global coordinates); drops it (but counts it)
 // when the buffer is full so the host can retry with a larger one.
 __device__ __forceinline__ void push_region(const RegionBuf &rb, int32_t seq, int64_t beg, int64_t end,

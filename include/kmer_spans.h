@@ -70,7 +70,9 @@ void ks_regions_free(ks_regions *r);
 typedef struct ks_ctx ks_ctx;
 ks_status ks_ctx_create(int32_t device, ks_ctx **out);
 void ks_ctx_destroy(ks_ctx *ctx);
-/* Use an external HIP stream (hipStream_t as void*); NULL = the ctx's own. */
+/* Run the ctx's work on an external HIP stream (hipStream_t as void*).
+ * NULL is HIP's default (null) stream, e.g. torch's default stream; a new
+ * ctx starts on a non-blocking stream of its own. */
 ks_status ks_ctx_set_stream(ks_ctx *ctx, void *hip_stream);
 /* Process-wide default context on device 0 (what the .Call shim uses). */
 ks_ctx *ks_default_ctx(void);

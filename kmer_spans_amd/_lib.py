@@ -133,6 +133,7 @@ class Context:
         return self._h
 
     def set_stream(self, stream_ptr: int | None):
+        """hipStream_t as an int; 0/None = HIP's default (null) stream."""
         check(load().ks_ctx_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
 
     def set_scan_algo(self, algo: int):

@@ -169,7 +169,7 @@ extern "C" ks_status ks_ctx_create(int32_t device, ks_ctx **out) {
 extern "C" void ks_ctx_destroy(ks_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamSynchronize(c->stream);
   for (auto &b : c->slots)
     if (b.ptr) (void)hipFree(b.ptr);
   if (c->pinned) (void)hipHostFree(c->pinned);
@@ -187,13 +187,7 @@ extern "C" ks_status ks_ctx_set_stream(ks_ctx *c, void *stream) {
     c->own_stream = false;
     c->stream = nullptr;
   }
-  if (stream) {
-    c->stream = static_cast<hipStream_t>(stream);
-  } else {
-    KS_HIP(hipSetDevice(c->device));
-    KS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    c->own_stream = true;
-  }
+  c->stream = static_cast<hipStream_t>(stream);  // nullptr: the default (null) stream
   return KS_OK;
 }
 

@@ -227,7 +227,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
       if (rc == KS_INTERNAL_RETRY) {  // rescans did not fit: grow, rerun, visits untouched
         KS_HIP(hipMemcpyAsync(&n_reg, d_rcount, 8, hipMemcpyDeviceToHost, st));
         KS_HIP(hipStreamSynchronize(st));
-        cap = std::max<int64_t>(2 * cap, (int64_t)n_reg + 1024);
+        if ((int64_t)n_reg > cap) cap = (int64_t)n_reg + 1024;
         continue;
       }
       if (rc == KS_OK) {

@@ -1265,10 +1265,12 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
               (long long)idx[i], d[0], d[1], d[2], d[3], d[4], d[5]);
     }
   }
-  if ((int64_t)hc[0] > ccap) {
+  if ((int64_t)hc[0] > ccap) {  // grow the candidate buffer and rerun the pass
     KS_HIP(hipEventDestroy(e_p1a));
     KS_HIP(hipEventDestroy(e_p1b));
-    return fail(KS_ERR_INTERNAL, "candidate buffer overflow (%llu > %lld)", hc[0], (long long)ccap);
+    void *grown = nullptr;
+    KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)(hc[0] + hc[0] / 4 + 1024) * 40 + 1024, &grown));
+    return KS_INTERNAL_RETRY;
   }
   const int64_t ncand = (int64_t)hc[0];
   // rescan buffer

@@ -321,6 +321,7 @@ def test_many_regions_retry(K, oracle):
         pos, sc, st = D.scan(ctx, ds, k, tab, 0, 0.5, vis)
         _assert_same_regions(pos, sc, o["pos"], o["score"], ("many", algo))
         assert np.array_equal(vis.cpu().numpy(), o["counts"])
+        assert st["scan_algo"] == algo  # no fallback: buffers grew instead
     del tab
     ctx.close()
 
@@ -349,3 +350,22 @@ def test_carry_segment_fallback(K, oracle, ctx, monkeypatch):
         assert np.array_equal(vis.cpu().numpy(), o["counts"])
     monkeypatch.delenv("KS_TEST_SEG_FALLBACK")
     ctx.set_scan_algo(-1)
+
+
+def test_torch_stream_ordering(K, oracle, ctx):
+    """A ctx bound to torch's current (default, null) stream is ordered after
+    pending torch work: a zero-fill queued behind a long sleep must land
+    before the count kernel adds into the tensor."""
+    import torch
+    from kmer_spans_amd import device as D, genome
+    s = genome.contig(2_000_000, 3, device="cuda", repeats=True)
+    ds = D.from_parts([s], [s.numel()], "cuda")
+    D.bind_torch_stream(ctx)
+    k = 12
+    counts = torch.full((4 ** k,), 7, dtype=torch.int32, device="cuda")
+    torch.cuda._sleep(200_000_000)  # keep the stream busy
+    counts.zero_()
+    words = D.count(ctx, ds, k, counts)
+    assert int(counts.sum(dtype=torch.int64)) == int(words)
+    n, oc = oracle.kmer_counts([ds.host_seq(0)], k)
+    assert np.array_equal(counts.cpu().numpy(), oc) and n == words

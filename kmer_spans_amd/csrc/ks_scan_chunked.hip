@@ -166,13 +166,20 @@ __global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__r
 // J = scan indices served by one table read: 1 reads the base table
 // (uint16 code or FP64 value per index); J >= 2 reads the expanded table
 // entry of the (k+J-1)-mer that spans J consecutive indices.
-template <int J, bool kCompressed>
-__global__ void __launch_bounds__(256) k_pass1(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
-                                               int k, TableView tv, uint16_t *__restrict__ codes,
-                                               uint64_t mw, double min_score, uint32_t *__restrict__ visits,
-                                               P1 o, Cand cand) {
+// kLds: the compressed LUT is copied to LDS once per 1024-lane block
+// (random LUT reads hit LDS banks instead of the L1/L2 path).
+template <int J, bool kCompressed, bool kLds>
+__global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
+                                                int k, TableView tv, uint16_t *__restrict__ codes,
+                                                uint64_t mw, double min_score, uint32_t *__restrict__ visits,
+                                                P1 o, Cand cand) {
   constexpr int G = (J == 1) ? 16 : (J == 4 ? 4 : 8);  // table reads in flight per lane and batch
   constexpr int PB = G * J;             // scan indices per batch (16, 16, 24, 32)
+  __shared__ double s_lut[kLds ? kLdsLutMax : 1];
+  if (kLds) {
+    for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
+    __syncthreads();
+  }
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
   const int kx = k + J - 1;
@@ -228,7 +235,7 @@ __global__ void __launch_bounds__(256) k_pass1(Chunks g, const uint8_t *__restri
     }
     if (kCompressed) {
 #pragma unroll
-      for (int j = 0; j < PB; ++j) v[j] = tv.lut[q[j]];
+      for (int j = 0; j < PB; ++j) v[j] = kLds ? s_lut[q[j]] : tv.lut[q[j]];
 #pragma unroll
       for (int r8 = 0; r8 < PB / 8; ++r8) {
         if (b0 + 8 * r8 < CH) {
@@ -380,11 +387,73 @@ __device__ int chunk_summary_impl(const Chunks &g, const uint8_t *__restrict__ s
 // with ties to even decided by the parity of m.  For both entry parities t:
 // total D, max M (first argmax A) and min N of the integer trajectory.  One
 // trajectory is tracked unless an exact tie occurs (then both parities).
-template <bool kCompressed>
+// Single-trajectory binade summary in FP64 integer arithmetic: with
+// |y| < 2^51, (y + 1.5*2^52) - 1.5*2^52 is y rounded half-to-even, an exact
+// integer; partial sums stay exact while |sum| < 2^53 (checked through the
+// extremes).  Returns 1 ok, 0 not representable, -1 a tie occurred (the
+// increment then depends on the parity: the dual-parity path is used).
+template <bool kCompressed, bool kLds>
+__device__ int chunk_summary_fast(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
+                                  const TableView &tv, const uint16_t *__restrict__ codes, int64_t c, int e,
+                                  long long D[2], long long M[2], int A[2], long long N[2],
+                                  const double *s_lut) {
+  const int n = g.n[c];
+  const int64_t start = g.start[c];
+  const uint32_t mask = (1u << (2 * k)) - 1u;
+  const double scale = ldexp(1.0, 52 - e);
+  constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
+  uint32_t code = kCompressed ? 0u : prime_code(seq, start - k, k);
+  double cur = 0.0, mx = -INFINITY, mn = INFINITY;
+  int arg = 0;
+  bool ok = true, tie_seen = false;
+  for (int b0 = 0; b0 < n; b0 += NB) {
+    double v[NB];
+    if (kCompressed) {
+      const uint4 w0 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0));
+      const uint4 w1 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0 + 8));
+      const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const uint32_t q = (w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+        v[j] = kLds ? s_lut[q] : tv.lut[q];
+      }
+    } else {
+      uint8_t by[16];
+      load16(seq, start + b0, total, by);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        v[j] = (b0 + j < n) ? tv.vals[code] : 0.0;
+        code = roll(code, by[j], mask);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (b0 + j < n) {
+        const double y = v[j] * scale;  // exact: power-of-two scaling
+        ok &= fabs(y) < 2251799813685248.0;  // 2^51; false for NaN / Inf
+        const double r = (y + kMagic) - kMagic;
+        tie_seen |= fabs(r - y) == 0.5;
+        cur += r;
+        if (cur > mx) { mx = cur; arg = b0 + j; }
+        mn = fmin(mn, cur);
+      }
+    }
+  }
+  ok &= mx < 4503599627370496.0 && mn > -4503599627370496.0;  // |partial sums| < 2^52: all exact
+  if (!ok) return 0;
+  if (tie_seen) return -1;
+  D[0] = D[1] = (long long)cur;
+  M[0] = M[1] = (long long)mx;
+  N[0] = N[1] = (long long)mn;
+  A[0] = A[1] = arg;
+  return 1;
+}
+
+template <bool kCompressed, bool kLds>
 __device__ bool chunk_summary(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
                               const TableView &tv, const uint16_t *__restrict__ codes, int64_t c, int e,
-                              long long D[2], long long M[2], int A[2], long long N[2]) {
-  const int rc = chunk_summary_impl<kCompressed, false>(g, seq, total, k, tv, codes, c, e, D, M, A, N);
+                              long long D[2], long long M[2], int A[2], long long N[2], const double *s_lut) {
+  const int rc = chunk_summary_fast<kCompressed, kLds>(g, seq, total, k, tv, codes, c, e, D, M, A, N, s_lut);
   if (rc >= 0) return rc == 1;
   return chunk_summary_impl<kCompressed, true>(g, seq, total, k, tv, codes, c, e, D, M, A, N) == 1;
 }
@@ -432,10 +501,15 @@ constexpr double kLMin = 64.0;
 // Summary of each chunk for the binade of its predicted trajectory (lane per
 // chunk, full occupancy); chunks predicted to leave the binade or to approach
 // 0 get none.
-template <bool kCompressed>
-__global__ void __launch_bounds__(256) k_summaries(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
-                                                   TableView tv, const uint16_t *__restrict__ codes, P1 o,
-                                                   const double *__restrict__ xt, Summ sm) {
+template <bool kCompressed, bool kLds>
+__global__ void __launch_bounds__(1024) k_summaries(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
+                                                    int k, TableView tv, const uint16_t *__restrict__ codes, P1 o,
+                                                    const double *__restrict__ xt, Summ sm) {
+  __shared__ double s_lut[kLds ? kLdsLutMax : 1];
+  if (kLds) {
+    for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
+    __syncthreads();
+  }
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
   sm.e[c] = INT32_MIN;
@@ -448,7 +522,7 @@ __global__ void __launch_bounds__(256) k_summaries(Chunks g, const uint8_t *__re
   if (!(lo - slack >= ldexp(1.0, e)) || !(hi + slack < ldexp(1.0, e + 1))) return;
   long long D[2], M[2], N[2];
   int A[2];
-  if (!chunk_summary<kCompressed>(g, seq, total, k, tv, codes, c, e, D, M, A, N)) return;
+  if (!chunk_summary<kCompressed, kLds>(g, seq, total, k, tv, codes, c, e, D, M, A, N, s_lut)) return;
   sm.e[c] = e;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -1165,14 +1239,18 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
   KS_HIP(hipEventCreate(&e_p1a));
   KS_HIP(hipEventCreate(&e_p1b));
   KS_HIP(hipEventRecord(e_p1a, st));
-#define KS_P1(J, C)                                                                                   \
-  hipLaunchKernelGGL((k_pass1<J, C>), dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, mw, min_score, \
-                     visits, p1, cand)
+  const unsigned gch1k = (unsigned)((nch + 1023) / 1024);
+  const bool lds_lut = comp && tv.nlut <= kLdsLutMax && getenv("KS_NO_LDS_LUT") == nullptr;
+#define KS_P1(J, C, L)                                                                                       \
+  hipLaunchKernelGGL((k_pass1<J, C, L>), dim3(J == 1 ? gch : gch1k), dim3(J == 1 ? 256 : 1024), 0, st, g, s->seq, \
+                     total, k, tv, codes, mw, min_score, visits, p1, cand)
   const int J = (tv.ext != nullptr) ? tv.ext_J : 1;
-  if (comp) {
-    if (J == 4) KS_P1(4, true); else if (J == 3) KS_P1(3, true); else if (J == 2) KS_P1(2, true); else KS_P1(1, true);
+  if (comp && lds_lut) {
+    if (J == 4) KS_P1(4, true, true); else if (J == 3) KS_P1(3, true, true); else if (J == 2) KS_P1(2, true, true); else KS_P1(1, true, false);
+  } else if (comp) {
+    if (J == 4) KS_P1(4, true, false); else if (J == 3) KS_P1(3, true, false); else if (J == 2) KS_P1(2, true, false); else KS_P1(1, true, false);
   } else {
-    if (J == 4) KS_P1(4, false); else if (J == 3) KS_P1(3, false); else if (J == 2) KS_P1(2, false); else KS_P1(1, false);
+    if (J == 4) KS_P1(4, false, false); else if (J == 3) KS_P1(3, false, false); else if (J == 2) KS_P1(2, false, false); else KS_P1(1, false, false);
   }
 #undef KS_P1
   KS_HIP(hipGetLastError());
@@ -1203,10 +1281,15 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
     hipLaunchKernelGGL(k_seg_sentinel, dim3(1), dim3(1), 0, st, d_seg, d_nseg, nch);
     KS_HIP(hipGetLastError());
   }
-  if (comp)
-    hipLaunchKernelGGL(k_summaries<true>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, p1, xt, sm);
+  if (lds_lut)
+    hipLaunchKernelGGL((k_summaries<true, true>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes, p1,
+                       xt, sm);
+  else if (comp)
+    hipLaunchKernelGGL((k_summaries<true, false>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes, p1,
+                       xt, sm);
   else
-    hipLaunchKernelGGL(k_summaries<false>, dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, p1, xt, sm);
+    hipLaunchKernelGGL((k_summaries<false, false>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes,
+                       p1, xt, sm);
   KS_HIP(hipGetLastError());
   unsigned int *d_err = reinterpret_cast<unsigned int *>(cnts + 3);
   // per segment (seg_mode) or per run (fallback: the whole chain of a run in one wave)

@@ -14,7 +14,11 @@ struct TableView {
   int compressed;
   const void *ext;  // expanded table (see ks_table), nullptr if absent
   int ext_J;
+  int nlut;         // compressed: LUT entries (distinct values)
 };
+
+// LUT entries that fit the LDS copy used by the streaming passes (64 KiB).
+constexpr int kLdsLutMax = 8192;
 
 __device__ __forceinline__ double tv_get(const TableView &t, uint32_t code) {
   return t.compressed ? t.lut[t.codes[code]] : t.vals[code];

@@ -106,7 +106,7 @@ def main():
     else:
         w, thr = api.rank_table(hc, k, words), 0.75
     t0 = time.time()
-    table = D.DeviceTable(ctx, w, k, thr, compress=True, expand=not args.no_expand)
+    table = D.DeviceTable(ctx, w, k, thr, compress=True, expand=not args.no_expand, freq=counts)
     torch.cuda.synchronize()
     t_table = time.time() - t0
 
@@ -204,7 +204,8 @@ def main():
                                f"min_score {args.min_score}, device-resident",
                    "k": k, "score": args.score, "genome_bp": n_bases, "parallelism": f"contig-shard x{world}",
                    "scan_algo": int(stats[-1]["scan_algo"]), "table_compressed": table.compressed,
-                   "table_distinct": table.distinct, "positions_per_read": table.positions_per_read},
+                   "table_distinct": table.distinct, "positions_per_read": table.positions_per_read,
+                   "code_bits": table.code_bits, "escape_fraction": round(table.escape_fraction, 6)},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "parity_sample": parity,

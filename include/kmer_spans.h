@@ -142,14 +142,22 @@ typedef struct ks_dev_seqs {
  *                     (exact: the LUT holds the very same doubles);
  *  KS_TABLE_EXPAND    also build the expanded table: one entry per
  *                     (k+J-1)-mer holding the J codes/values of its J
- *                     consecutive k-mers (J <= 4, <= 32 GiB), so the scan
- *                     issues one random read per J scan indices.  Skipped
- *                     when it does not fit. */
+ *                     consecutive k-mers (J <= 5, up to 128 GiB of the
+ *                     GPU's HBM), so the scan issues one random read per J
+ *                     scan indices.  J = 5 uses 12-bit codes for the 4095
+ *                     values covering most positions and an escape to the
+ *                     base table for the rest.  Skipped when it does not fit. */
 #define KS_TABLE_COMPRESS 1
 #define KS_TABLE_EXPAND 2
 typedef struct ks_table ks_table;
 ks_status ks_table_create(ks_ctx *ctx, const double *w_host, int32_t k, double thr,
                           int32_t flags, ks_table **out);
+/* As ks_table_create, with the k-mer counts of the sequences to be scanned
+ * (device pointer, 4^k int32; NULL = none) as a position-frequency hint:
+ * it only decides which values get the short codes of the expanded table,
+ * never the results. */
+ks_status ks_table_create_hint(ks_ctx *ctx, const double *w_host, int32_t k, double thr,
+                               int32_t flags, const int32_t *freq_dev, ks_table **out);
 void ks_table_destroy(ks_table *t);
 /* 1 if the table is stored compressed (uint16 codes + LUT), else 0. */
 int32_t ks_table_is_compressed(const ks_table *t);
@@ -157,6 +165,12 @@ int64_t ks_table_distinct(const ks_table *t);
 /* Scan indices served per random table read (J of the expanded table, 1 if
  * it was not built). */
 int32_t ks_table_positions_per_read(const ks_table *t);
+/* Bits per value code in the expanded table (12 or 16), 16 for a compressed
+ * table without one, 64 for an FP64 table. */
+int32_t ks_table_code_bits(const ks_table *t);
+/* Share of positions (by the hint, else by k-mer multiplicity) whose value
+ * escapes the 12-bit codes; 0 unless code bits are 12. */
+double ks_table_escape_fraction(const ks_table *t);
 
 /* Scan statistics of the last ks_scan_dev call (device time of each phase,
  * measured with hipEvents on the ctx stream). */

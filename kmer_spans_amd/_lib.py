@@ -50,7 +50,7 @@ EXPORTS = [
     "ks_ctx_set_stream", "ks_default_ctx", "ks_kmer_counts", "ks_kmer_regions",
     "ks_low_comp_regions", "ks_kmer_seq", "ks_rank_table", "ks_log2_table", "ks_pm1_table",
     "ks_table_create", "ks_table_destroy", "ks_table_is_compressed", "ks_table_distinct",
-    "ks_table_positions_per_read",
+    "ks_table_positions_per_read", "ks_table_create_hint", "ks_table_code_bits", "ks_table_escape_fraction",
     "ks_scan_dev", "ks_count_dev", "ks_ctx_set_scan_algo",
 ]
 
@@ -87,6 +87,9 @@ def load():
         "ks_table_is_compressed": ([P], I32),
         "ks_table_distinct": ([P], I64),
         "ks_table_positions_per_read": ([P], I32),
+        "ks_table_create_hint": ([P, P, I32, D, I32, P, P], I32),
+        "ks_table_code_bits": ([P], I32),
+        "ks_table_escape_fraction": ([P], D),
         "ks_scan_dev": ([P, P, I32, P, I32, D, P, P, P], I32),
         "ks_count_dev": ([P, P, I32, P, P], I32),
     }

@@ -96,6 +96,14 @@ struct ks_table {
   void *d_ext = nullptr;        // uint64 (J <= 4 codes) or double[4] (J <= 3 values)
   size_t ext_bytes = 0;
   double ms_ext = 0;            // build time
+  // Narrow codes (ext_bits = 12, J = 5): the 4095 values covering most
+  // positions get a 12-bit code (d_map12 -> uint16 code, d_lut12 -> value);
+  // code 0xFFF escapes to the base uint16 table for that index.
+  int ext_bits = 16;
+  uint16_t *d_map12 = nullptr;  // [4096]
+  double *d_lut12 = nullptr;    // [4096]
+  double escape_frac = 0.0;     // estimated share of positions that escape
+  uint16_t *d_rank12_tmp = nullptr;  // build-time uint16 -> 12-bit map
 };
 
 namespace ks {
@@ -136,7 +144,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
                     ks_scan_stats *stats);
 
 // Build the expanded table of t (no-op if it exists or does not fit).
-ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes);
+ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t *freq_dev);
 
 // Host table builders (ks_tables.cpp).
 ks_status rank_table_host(const int32_t *counts, int k, double total, double *ranks);

@@ -13,6 +13,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstring>
 #include <numeric>
 
@@ -38,32 +39,33 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
                                                   const int32_t *__restrict__ rseq, int64_t nruns,
                                                   int k, TableView tv, uint64_t mw, double min_score,
                                                   uint32_t *__restrict__ visits, RegionBuf out) {
-  constexpr int G = (J == 1) ? 16 : (J == 4 ? 4 : (J == 3 ? 6 : 8));  // reads per batch
-  constexpr int PB = G * J;                                           // indices per batch (16, 16, 18, 16)
+  constexpr int G = (J == 1) ? 16 : (J >= 4 ? 4 : (J == 3 ? 6 : 8));  // reads per batch
+  constexpr int PB = G * J;                                           // indices per batch (16, 16, 18, 16, 20)
+  using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;  // (k+J-1)-mer code
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= nruns) return;
   const int64_t a = ra[r], b = rbnd[r];
   if (b - a <= k) return;
   const int32_t sid = rseq[r];
   const int kx = k + J - 1;
-  const uint32_t xmask = (kx >= 16) ? 0xffffffffu : ((1u << (2 * kx)) - 1u);
+  const GC xmask = (2 * kx >= 8 * (int)sizeof(GC)) ? ~(GC)0 : (((GC)1 << (2 * kx)) - 1);
   const uint32_t kmask = (1u << (2 * k)) - 1u;
   int64_t i = a;  // priming point
   for (;;) {
     // (k+J-1)-mer of the group starting at scan index i + k
-    uint32_t gcode = prime_code_guarded(seq, i, kx, total);
+    GC gcode = (GC)prime_code_guarded64(seq, i, kx, total);
     double S = 0.0, prev = 0.0, best = 0.0;
     int64_t beg = 0, arg = 0;
     bool restart = false;
     for (int64_t p0 = i + k; p0 < b && !restart; p0 += PB) {
       const int n = (int)((b - p0) < PB ? (b - p0) : PB);
       double v[PB];
-      uint32_t gc[G];
+      GC gc[G];
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         gc[g] = gcode;
         if (g * J < n) {
-          gather_group<J, kCompressed>(tv, gcode, v + g * J);
+          gather_group<J, kCompressed>(tv, gcode, kmask, v + g * J);
 #pragma unroll
           for (int t = 0; t < J; ++t) {
             const int64_t q = p0 + g * J + J - 1 + t;
@@ -75,7 +77,7 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
       for (int j = 0; j < PB; ++j) {  // fully unrolled: v[]/gc[] stay in registers
         if (j < n && !restart) {
           const int64_t p = p0 + j;
-          if (visits) atomicAdd(&visits[(gc[j / J] >> (2 * (J - 1 - j % J))) & kmask], 1u);
+          if (visits) atomicAdd(&visits[(uint32_t)(gc[j / J] >> (2 * (J - 1 - j % J))) & kmask], 1u);
           const double t = prev + v[j];
           S = t > 0 ? t : 0.0;
           if (prev == 0 && S > 0) { beg = p; arg = p; best = S; }
@@ -147,7 +149,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
   hipLaunchKernelGGL((k_scan_lane<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, total, \
                      ra, rb, rs, n, k, tv, mw, min_score, visits, out)
   if (tv.compressed) {
-    if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
+    if (J == 5) KS_LANE(5, true); else if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
   } else {
     if (J == 4) KS_LANE(4, false); else if (J == 3) KS_LANE(3, false); else if (J == 2) KS_LANE(2, false); else KS_LANE(1, false);
   }
@@ -187,7 +189,8 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     if (L >= k) S->n_bases += L;
   }
 
-  TableView tv{t->d_vals, t->d_codes, t->d_lut, t->compressed ? 1 : 0, t->d_ext, t->ext_J, (int)t->distinct};
+  TableView tv{t->d_vals,  t->d_codes,   t->d_lut,     t->compressed ? 1 : 0, t->d_ext,
+               t->ext_J, (int)t->distinct, t->ext_bits, t->d_lut12, t->d_map12};
   const uint64_t mw = (uint64_t)(int64_t)min_width;
   int algo = ctx->scan_algo;
   if (algo < 0) algo = (longest > (1 << 15)) ? 1 : 0;

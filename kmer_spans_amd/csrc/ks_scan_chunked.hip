@@ -31,6 +31,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "ks_scan_common.h"
@@ -110,8 +111,18 @@ __device__ __forceinline__ void load16(const uint8_t *__restrict__ seq, int64_t 
 }
 
 __device__ __forceinline__ size_t code_slot(int64_t c, int i) {
-  // [tile = c/64][i/8][lane = c%64][i%8]: a wave's lanes store 16 B each, contiguous
-  return ((((size_t)(c >> 6) * (CH / 8) + (size_t)(i >> 3)) * 64 + (size_t)(c & 63)) << 3) + (size_t)(i & 7);
+  // [tile = c/64][i/4][lane = c%64][i%4]: a wave's lanes store 8 B each, contiguous
+  return ((((size_t)(c >> 6) * (CH / 4) + (size_t)(i >> 2)) * 64 + (size_t)(c & 63)) << 2) + (size_t)(i & 3);
+}
+
+// The 16 codes of indices b0 .. b0+15 (b0 % 4 == 0) as 8 words of 2 codes.
+__device__ __forceinline__ void load_codes16(const uint16_t *__restrict__ codes, int64_t c, int b0, uint32_t w[8]) {
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const uint2 x = *reinterpret_cast<const uint2 *>(codes + code_slot(c, b0 + 4 * h));
+    w[2 * h] = x.x;
+    w[2 * h + 1] = x.y;
+  }
 }
 
 // Values of scan indices i0 .. i0+3 of chunk c (0 past n): one 8-byte code
@@ -173,21 +184,31 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
                                                 int k, TableView tv, uint16_t *__restrict__ codes,
                                                 uint64_t mw, double min_score, uint32_t *__restrict__ visits,
                                                 P1 o, Cand cand) {
-  constexpr int G = (J == 1) ? 16 : (J == 4 ? 4 : 8);  // table reads in flight per lane and batch
-  constexpr int PB = G * J;             // scan indices per batch (16, 16, 24, 32)
+  constexpr int G = (J == 1) ? 16 : (J >= 3 ? 4 : 8);  // table reads in flight per lane and batch
+  constexpr int PB = G * J;             // scan indices per batch (16, 16, 12, 16, 20)
+  constexpr bool k12 = (J == 5);        // 12-bit codes with escapes (kCompressed only)
+  using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;  // (k+J-1)-mer code
   __shared__ double s_lut[kLds ? kLdsLutMax : 1];
+  __shared__ double s_lut12[k12 ? 4096 : 1];
+  __shared__ uint16_t s_map12[k12 ? 4096 : 1];
   if (kLds) {
     for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
-    __syncthreads();
   }
+  if (k12) {
+    for (int i = threadIdx.x; i < 4096; i += blockDim.x) {
+      s_lut12[i] = tv.lut12[i];
+      s_map12[i] = tv.map12[i];
+    }
+  }
+  if (kLds || k12) __syncthreads();
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
   const int kx = k + J - 1;
-  const uint32_t xmask = (kx >= 16) ? 0xffffffffu : ((1u << (2 * kx)) - 1u);
+  const GC xmask = (2 * kx >= 8 * (int)sizeof(GC)) ? ~(GC)0 : (((GC)1 << (2 * kx)) - 1);
   const uint32_t kmask = (1u << (2 * k)) - 1u;
   const int64_t start = g.start[c];
   const int n = g.n[c];
-  uint32_t gcode = prime_code_guarded(seq, start - k, kx, total);  // (k+J-1)-mer of group 0
+  GC gcode = (GC)prime_code_guarded64(seq, start - k, kx, total);  // (k+J-1)-mer of group 0
   double prev = 0.0, best = 0.0;
   int beg = -1, arg = 0;
   double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
@@ -196,7 +217,7 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
     uint8_t by[32];  // bytes rolled in by groups 1..G: start + b0 + J - 1 + [0, PB)
     load16(seq, start + b0 + J - 1, total, by);
     if (PB > 16) load16(seq, start + b0 + J - 1 + 16, total, by + 16);
-    uint32_t gc[G];
+    GC gc[G];
 #pragma unroll
     for (int gi = 0; gi < G; ++gi) {
       gc[gi] = gcode;
@@ -211,6 +232,20 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
       if (J == 1) {
         if (kCompressed) q[gi] = live ? tv.codes[gc[gi]] : (uint16_t)0;
         else v[gi] = live ? tv.vals[gc[gi]] : 0.0;
+      } else if (kCompressed && k12) {
+        const uint64_t e = live ? reinterpret_cast<const uint64_t *>(tv.ext)[gc[gi]] : 0ull;
+#pragma unroll
+        for (int t = 0; t < J; ++t) {
+          const uint32_t c12 = (uint32_t)(e >> (12 * t)) & 0xfffu;
+          if (c12 != 0xfffu) {
+            q[gi * J + t] = s_map12[c12];
+            v[gi * J + t] = s_lut12[c12];
+          } else {  // value outside the 12-bit set: base table
+            const uint16_t qe = tv.codes[(uint32_t)(gc[gi] >> (2 * (J - 1 - t))) & kmask];
+            q[gi * J + t] = qe;
+            v[gi * J + t] = tv.lut[qe];
+          }
+        }
       } else if (kCompressed) {
         uint64_t e = 0;
         if (live) e = (J <= 2) ? (uint64_t)reinterpret_cast<const uint32_t *>(tv.ext)[gc[gi]]
@@ -235,16 +270,15 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
     }
     if (kCompressed) {
 #pragma unroll
-      for (int j = 0; j < PB; ++j) v[j] = kLds ? s_lut[q[j]] : tv.lut[q[j]];
+      for (int j = 0; j < PB; ++j)
+        if (!k12) v[j] = kLds ? s_lut[q[j]] : tv.lut[q[j]];
 #pragma unroll
-      for (int r8 = 0; r8 < PB / 8; ++r8) {
-        if (b0 + 8 * r8 < CH) {
-          uint4 w;
-          w.x = q[8 * r8 + 0] | ((uint32_t)q[8 * r8 + 1] << 16);
-          w.y = q[8 * r8 + 2] | ((uint32_t)q[8 * r8 + 3] << 16);
-          w.z = q[8 * r8 + 4] | ((uint32_t)q[8 * r8 + 5] << 16);
-          w.w = q[8 * r8 + 6] | ((uint32_t)q[8 * r8 + 7] << 16);
-          *reinterpret_cast<uint4 *>(codes + code_slot(c, b0 + 8 * r8)) = w;
+      for (int r4 = 0; r4 < PB / 4; ++r4) {
+        if (b0 + 4 * r4 < CH) {
+          uint2 w;
+          w.x = q[4 * r4 + 0] | ((uint32_t)q[4 * r4 + 1] << 16);
+          w.y = q[4 * r4 + 2] | ((uint32_t)q[4 * r4 + 3] << 16);
+          *reinterpret_cast<uint2 *>(codes + code_slot(c, b0 + 4 * r4)) = w;
         }
       }
     }
@@ -252,7 +286,7 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
     for (int j = 0; j < PB; ++j) {
       const int i = b0 + j;
       if (i < n) {
-        if (visits) atomicAdd(&visits[(gc[j / J] >> (2 * (J - 1 - j % J))) & kmask], 1u);
+        if (visits) atomicAdd(&visits[(uint32_t)(gc[j / J] >> (2 * (J - 1 - j % J))) & kmask], 1u);
         const double s = v[j];
         asum += s;
         pmin = fmin(pmin, asum);
@@ -330,9 +364,8 @@ __device__ int chunk_summary_impl(const Chunks &g, const uint8_t *__restrict__ s
   for (int b0 = 0; b0 < n; b0 += NB) {
     double v[NB];
     if (kCompressed) {
-      const uint4 w0 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0));
-      const uint4 w1 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0 + 8));
-      const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      uint32_t w[8];
+      load_codes16(codes, c, b0, w);
 #pragma unroll
       for (int j = 0; j < NB; ++j) v[j] = tv.lut[(w[j >> 1] >> (16 * (j & 1))) & 0xffffu];
     } else {
@@ -409,9 +442,8 @@ __device__ int chunk_summary_fast(const Chunks &g, const uint8_t *__restrict__ s
   for (int b0 = 0; b0 < n; b0 += NB) {
     double v[NB];
     if (kCompressed) {
-      const uint4 w0 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0));
-      const uint4 w1 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0 + 8));
-      const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      uint32_t w[8];
+      load_codes16(codes, c, b0, w);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const uint32_t q = (w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
@@ -778,9 +810,8 @@ __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restri
   if (kCompressed) {
     for (int b0 = 0; b0 < n && hq < 0; b0 += NB) {
       double v[NB];
-      const uint4 w0 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0));
-      const uint4 w1 = *reinterpret_cast<const uint4 *>(codes + code_slot(c, b0 + 8));
-      const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      uint32_t w[8];
+      load_codes16(codes, c, b0, w);
 #pragma unroll
       for (int j = 0; j < NB; ++j) v[j] = tv.lut[(w[j >> 1] >> (16 * (j & 1))) & 0xffffu];
 #pragma unroll
@@ -1245,7 +1276,9 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
   hipLaunchKernelGGL((k_pass1<J, C, L>), dim3(J == 1 ? gch : gch1k), dim3(J == 1 ? 256 : 1024), 0, st, g, s->seq, \
                      total, k, tv, codes, mw, min_score, visits, p1, cand)
   const int J = (tv.ext != nullptr) ? tv.ext_J : 1;
-  if (comp && lds_lut) {
+  if (comp && J == 5) {
+    KS_P1(5, true, false);  // 12-bit codes: value LUT of the short codes in LDS
+  } else if (comp && lds_lut) {
     if (J == 4) KS_P1(4, true, true); else if (J == 3) KS_P1(3, true, true); else if (J == 2) KS_P1(2, true, true); else KS_P1(1, true, false);
   } else if (comp) {
     if (J == 4) KS_P1(4, true, false); else if (J == 3) KS_P1(3, true, false); else if (J == 2) KS_P1(2, true, false); else KS_P1(1, true, false);

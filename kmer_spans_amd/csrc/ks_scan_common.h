@@ -15,6 +15,9 @@ struct TableView {
   const void *ext;  // expanded table (see ks_table), nullptr if absent
   int ext_J;
   int nlut;         // compressed: LUT entries (distinct values)
+  int ext_bits;     // 12: J = 5 narrow codes (lut12 / map12, 0xFFF escapes)
+  const double *lut12;
+  const uint16_t *map12;
 };
 
 // LUT entries that fit the LDS copy used by the streaming passes (64 KiB).
@@ -25,11 +28,19 @@ __device__ __forceinline__ double tv_get(const TableView &t, uint32_t code) {
 }
 
 // The J values of one expanded-table read: scan indices served by the
-// (k+J-1)-mer `gcode` (J = 1: the base table entry of the k-mer).
-template <int J, bool kCompressed>
-__device__ __forceinline__ void gather_group(const TableView &t, uint32_t gcode, double v[J]) {
+// (k+J-1)-mer `gcode` (J = 1: the base table entry of the k-mer).  J = 5
+// (compressed) holds 12-bit codes; 0xFFF escapes to the base table.
+template <int J, bool kCompressed, typename GC>
+__device__ __forceinline__ void gather_group(const TableView &t, GC gcode, uint32_t kmask, double v[J]) {
   if (J == 1) {
     v[0] = kCompressed ? t.lut[t.codes[gcode]] : t.vals[gcode];
+  } else if (kCompressed && J == 5) {
+    const uint64_t e = reinterpret_cast<const uint64_t *>(t.ext)[gcode];
+#pragma unroll
+    for (int q = 0; q < J; ++q) {
+      const uint32_t c12 = (uint32_t)(e >> (12 * q)) & 0xfffu;
+      v[q] = (c12 != 0xfffu) ? t.lut12[c12] : t.lut[t.codes[(uint32_t)(gcode >> (2 * (J - 1 - q))) & kmask]];
+    }
   } else if (kCompressed) {
     const uint64_t e = (J <= 2) ? (uint64_t)reinterpret_cast<const uint32_t *>(t.ext)[gcode]
                                 : reinterpret_cast<const uint64_t *>(t.ext)[gcode];
@@ -46,7 +57,7 @@ __device__ __forceinline__ void gather_group(const TableView &t, uint32_t gcode,
     }
     const double ev[4] = {e0.x, e0.y, e1.x, e1.y};
 #pragma unroll
-    for (int q = 0; q < J; ++q) v[q] = ev[q];
+    for (int q = 0; q < J && q < 4; ++q) v[q] = ev[q];
   }
 }
 
@@ -68,6 +79,14 @@ __device__ __forceinline__ void push_region(const RegionBuf &rb, int32_t seq, in
 __device__ __forceinline__ uint32_t prime_code_guarded(const uint8_t *__restrict__ seq, int64_t p, int n,
                                                        int64_t total) {
   uint32_t c = 0;
+  for (int j = 0; j < n; ++j) c = (c << 2) | enc(p + j < total ? seq[p + j] : (uint8_t)'N');
+  return c;
+}
+
+// 64-bit form for (k+J-1)-mers of up to 32 bases.
+__device__ __forceinline__ uint64_t prime_code_guarded64(const uint8_t *__restrict__ seq, int64_t p, int n,
+                                                         int64_t total) {
+  uint64_t c = 0;
   for (int j = 0; j < n; ++j) c = (c << 2) | enc(p + j < total ? seq[p + j] : (uint8_t)'N');
   return c;
 }

@@ -9,6 +9,10 @@
 // 256 MiB Infinity Cache while the sequence streams past.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
 #include "ks_internal.h"
 
 namespace ks {
@@ -53,6 +57,32 @@ __global__ void k_build_ext_u16(const uint16_t *__restrict__ codes, int k, uint6
   }
 }
 
+// Position weight of every uint16 code: number of k-mers with that code, or
+// (with a frequency hint) the number of positions scoring them.
+__global__ void k_code_hist(const uint16_t *__restrict__ codes, const int32_t *__restrict__ freq, int64_t n,
+                            unsigned long long *__restrict__ hist) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long wgt = freq ? (unsigned long long)(uint32_t)freq[i] : 1ull;
+    if (wgt) atomicAdd(&hist[codes[i]], wgt);
+  }
+}
+
+// Expanded table, 12-bit codes: J = 5 codes per uint64 entry (rank12 maps a
+// uint16 code to its 12-bit code or the escape 0xFFF).
+__global__ void k_build_ext_c12(const uint16_t *__restrict__ codes, const uint16_t *__restrict__ rank12, int k,
+                                uint64_t nent, uint64_t *__restrict__ ext) {
+  constexpr int J = 5;
+  const uint64_t mk = ((uint64_t)1 << (2 * k)) - 1;
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nent;
+       e += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int t = 0; t < J; ++t) v |= (uint64_t)rank12[codes[(e >> (2 * (J - 1 - t))) & mk]] << (12 * t);
+    ext[e] = v;
+  }
+}
+
 // Expanded table, FP64 values: J values per entry (double2 / double4).
 template <int J>
 __global__ void k_build_ext_f64(const double *__restrict__ vals, int k, uint64_t nent, double *__restrict__ ext) {
@@ -80,32 +110,107 @@ static size_t ext_entry_bytes(bool u16, int J) {
   return J <= 2 ? 16 : 32;
 }
 
-ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes) {
+// 12-bit code assignment for J = 5: the 4095 heaviest uint16 codes (by
+// position weight) get codes 0..4094, the rest escape.  Returns false if the
+// escape share is above max_escape.
+static ks_status assign_code12(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev, double max_escape, bool *use) {
+  *use = false;
+  hipStream_t st = ctx->stream;
+  const int64_t n = (int64_t)1 << (2 * t->k);
+  const int64_t nu = t->distinct;
+  unsigned long long *d_hist = nullptr;
+  KS_HIP(hipMalloc(&d_hist, 65536 * 8));
+  KS_HIP(hipMemsetAsync(d_hist, 0, 65536 * 8, st));
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ctx->num_cus * 16);
+  hipLaunchKernelGGL(k_code_hist, dim3(grid), dim3(256), 0, st, t->d_codes, freq_dev, n, d_hist);
+  std::vector<unsigned long long> h(65536);
+  std::vector<double> lut(nu);
+  KS_HIP(hipMemcpyAsync(h.data(), d_hist, 65536 * 8, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipMemcpyAsync(lut.data(), t->d_lut, nu * 8, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipStreamSynchronize(st));
+  KS_HIP(hipFree(d_hist));
+  std::vector<int32_t> order(nu);
+  for (int64_t i = 0; i < nu; ++i) order[i] = (int32_t)i;
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return h[a] > h[b]; });
+  const int64_t ndirect = std::min<int64_t>(nu, 4095);
+  long double tot = 0, cov = 0;
+  for (int64_t i = 0; i < nu; ++i) tot += h[order[i]];
+  for (int64_t i = 0; i < ndirect; ++i) cov += h[order[i]];
+  t->escape_frac = tot > 0 ? (double)(1.0L - cov / tot) : 0.0;
+  if (t->escape_frac > max_escape) return KS_OK;
+  std::vector<uint16_t> rank12(65536, 0xFFF), map12(4096, 0);
+  std::vector<double> lut12(4096, 0.0);
+  for (int64_t i = 0; i < ndirect; ++i) {
+    rank12[order[i]] = (uint16_t)i;
+    map12[i] = (uint16_t)order[i];
+    lut12[i] = lut[order[i]];
+  }
+  KS_HIP(hipMalloc(&t->d_map12, 4096 * 2));
+  KS_HIP(hipMalloc(&t->d_lut12, 4096 * 8));
+  KS_HIP(hipMemcpyAsync(t->d_map12, map12.data(), 4096 * 2, hipMemcpyHostToDevice, st));
+  KS_HIP(hipMemcpyAsync(t->d_lut12, lut12.data(), 4096 * 8, hipMemcpyHostToDevice, st));
+  uint16_t *d_rank = nullptr;
+  KS_HIP(hipMalloc(&d_rank, 65536 * 2));
+  KS_HIP(hipMemcpyAsync(d_rank, rank12.data(), 65536 * 2, hipMemcpyHostToDevice, st));
+  KS_HIP(hipStreamSynchronize(st));
+  t->d_rank12_tmp = d_rank;
+  *use = true;
+  return KS_OK;
+}
+
+ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t *freq_dev) {
   if (t->d_ext || t->ext_J > 1) return KS_OK;
   const bool u16 = t->compressed;
-  int J = 0;
-  for (int cand = 4; cand >= 2; --cand) {
-    const int kx = t->k + cand - 1;
-    if (kx > 16) continue;  // (k+J-1)-mer codes are 32-bit
-    const size_t bytes = ((size_t)1 << (2 * kx)) * ext_entry_bytes(u16, cand);
-    if (bytes <= max_bytes) { J = cand; break; }
+  size_t free_b = 0, total_b = 0;
+  KS_HIP(hipMemGetInfo(&free_b, &total_b));
+  // leave room for the sequences and the scan workspace
+  const size_t reserve = std::max<size_t>((size_t)32 << 30, total_b / 4);
+  const size_t budget = std::min(max_bytes, free_b > reserve ? free_b - reserve : (size_t)0);
+  // candidates, best first: (J, code bits); (k+J-1)-mer indices up to 34 bits
+  struct Cand { int J, bits; };
+  const Cand cands_u16[] = {{5, 12}, {4, 16}, {3, 16}, {2, 16}};
+  const Cand cands_f64[] = {{4, 64}, {3, 64}, {2, 64}};
+  const Cand *cands = u16 ? cands_u16 : cands_f64;
+  const int ncand = u16 ? 4 : 3;
+  const char *esc_env = getenv("KS_EXT_ESCAPE_MAX");
+  const double max_escape = esc_env ? atof(esc_env) : 0.01;
+  int J = 0, bits = 16;
+  for (int i = 0; i < ncand; ++i) {
+    const Cand c = cands[i];
+    const int kx = t->k + c.J - 1;
+    if (kx > 17) continue;
+    if (!u16 && kx > 16) continue;
+    const size_t bytes = ((size_t)1 << (2 * kx)) * ext_entry_bytes(u16, c.J);
+    if (bytes > budget) continue;
+    if (c.bits == 12) {
+      if (getenv("KS_NO_CODE12")) continue;
+      bool use = false;
+      KS_TRY(assign_code12(ctx, t, freq_dev, max_escape, &use));
+      if (!use) continue;
+    }
+    J = c.J;
+    bits = c.bits;
+    break;
   }
   if (J == 0) return KS_OK;
   const int kx = t->k + J - 1;
   const uint64_t nent = (uint64_t)1 << (2 * kx);
   const size_t bytes = nent * ext_entry_bytes(u16, J);
-  size_t free_b = 0, total_b = 0;
-  KS_HIP(hipMemGetInfo(&free_b, &total_b));
-  if (bytes > free_b / 10 * 4) return KS_OK;  // leave room for the scan workspace
   hipStream_t st = ctx->stream;
   void *ext = nullptr;
-  if (hipMalloc(&ext, bytes) != hipSuccess) { (void)hipGetLastError(); return KS_OK; }
+  if (hipMalloc(&ext, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return KS_OK;
+  }
   hipEvent_t a, b;
   KS_HIP(hipEventCreate(&a));
   KS_HIP(hipEventCreate(&b));
   KS_HIP(hipEventRecord(a, st));
   const unsigned grid = (unsigned)std::min<uint64_t>((nent + 255) / 256, (uint64_t)ctx->num_cus * 32);
-  if (u16) {
+  if (u16 && bits == 12) {
+    hipLaunchKernelGGL(k_build_ext_c12, dim3(grid), dim3(256), 0, st, t->d_codes, t->d_rank12_tmp, t->k, nent,
+                       (uint64_t *)ext);
+  } else if (u16) {
     if (J == 4) hipLaunchKernelGGL((k_build_ext_u16<4, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
     else if (J == 3) hipLaunchKernelGGL((k_build_ext_u16<3, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
     else hipLaunchKernelGGL((k_build_ext_u16<2, uint32_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint32_t *)ext);
@@ -121,8 +226,19 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes) {
   KS_HIP(hipEventElapsedTime(&ms, a, b));
   KS_HIP(hipEventDestroy(a));
   KS_HIP(hipEventDestroy(b));
+  if (t->d_rank12_tmp) {
+    KS_HIP(hipFree(t->d_rank12_tmp));
+    t->d_rank12_tmp = nullptr;
+  }
+  if (bits != 12) {  // a 12-bit assignment that was not used
+    if (t->d_map12) (void)hipFree(t->d_map12);
+    if (t->d_lut12) (void)hipFree(t->d_lut12);
+    t->d_map12 = nullptr;
+    t->d_lut12 = nullptr;
+  }
   t->d_ext = ext;
   t->ext_J = J;
+  t->ext_bits = bits;
   t->ext_bytes = bytes;
   t->ms_ext = ms;
   return KS_OK;
@@ -134,6 +250,11 @@ using namespace ks;
 
 extern "C" ks_status ks_table_create(ks_ctx *ctx, const double *w_host, int32_t k, double thr,
                                      int32_t flags, ks_table **out) {
+  return ks_table_create_hint(ctx, w_host, k, thr, flags, nullptr, out);
+}
+
+extern "C" ks_status ks_table_create_hint(ks_ctx *ctx, const double *w_host, int32_t k, double thr,
+                                          int32_t flags, const int32_t *freq_dev, ks_table **out) {
   const int32_t allow_compress = flags & KS_TABLE_COMPRESS;
   if (!ctx || !w_host || !out) return fail(KS_ERR_ARG, "ks_table_create: null argument");
   if (k < 1 || k > KS_MAX_K) return fail(KS_ERR_ARG, "k must be between 1 and %d", KS_MAX_K);
@@ -202,7 +323,7 @@ extern "C" ks_status ks_table_create(ks_ctx *ctx, const double *w_host, int32_t 
 #undef KS_TBL_HIP
   cleanup();
   if (flags & KS_TABLE_EXPAND) {
-    const ks_status rc = table_expand(ctx, t, (size_t)32 << 30);
+    const ks_status rc = table_expand(ctx, t, (size_t)160 << 30, freq_dev);
     if (rc != KS_OK) { ks_table_destroy(t); return rc; }
   }
   *out = t;
@@ -215,9 +336,20 @@ extern "C" void ks_table_destroy(ks_table *t) {
   if (t->d_codes) (void)hipFree(t->d_codes);
   if (t->d_lut) (void)hipFree(t->d_lut);
   if (t->d_ext) (void)hipFree(t->d_ext);
+  if (t->d_map12) (void)hipFree(t->d_map12);
+  if (t->d_lut12) (void)hipFree(t->d_lut12);
+  if (t->d_rank12_tmp) (void)hipFree(t->d_rank12_tmp);
   delete t;
 }
 
 extern "C" int32_t ks_table_is_compressed(const ks_table *t) { return t && t->compressed ? 1 : 0; }
 extern "C" int64_t ks_table_distinct(const ks_table *t) { return t ? t->distinct : -1; }
 extern "C" int32_t ks_table_positions_per_read(const ks_table *t) { return t ? t->ext_J : 0; }
+extern "C" int32_t ks_table_code_bits(const ks_table *t) {
+  if (!t) return 0;
+  if (t->ext_J > 1 && t->compressed) return t->ext_bits;
+  return t->compressed ? 16 : 64;
+}
+extern "C" double ks_table_escape_fraction(const ks_table *t) {
+  return (t && t->ext_bits == 12) ? t->escape_frac : 0.0;
+}

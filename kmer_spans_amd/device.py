@@ -78,14 +78,28 @@ class DeviceTable:
     """A score table s = w - thr on the device (ks_table)."""
 
     def __init__(self, ctx: _lib.Context, w, k: int, thr: float = 0.0, compress: bool = True,
-                 expand: bool = False):
+                 expand: bool = False, freq: torch.Tensor | None = None):
+        """freq: optional k-mer counts (int32[4^k], cuda) of the sequences to be
+        scanned -- a hint for the expanded table's short codes, never the results."""
         w = np.ascontiguousarray(w, dtype=np.float64)
         if w.size != 4 ** k:
             raise _lib.KmerSpansError(f"kmer_w contains {w.size} elements but should have {4 ** k}")
+        if freq is not None and (freq.dtype != torch.int32 or freq.numel() != 4 ** k or not freq.is_cuda):
+            raise _lib.KmerSpansError("freq must be an int32 cuda tensor of 4^k counts")
         self.k = k
         self._h = C.c_void_p()
         flags = (1 if compress else 0) | (2 if expand else 0)
-        check(load().ks_table_create(ctx.handle, w.ctypes.data, k, float(thr), flags, C.byref(self._h)))
+        check(load().ks_table_create_hint(ctx.handle, w.ctypes.data, k, float(thr), flags,
+                                          C.c_void_p(freq.data_ptr()) if freq is not None else None,
+                                          C.byref(self._h)))
+
+    @property
+    def code_bits(self) -> int:
+        return int(load().ks_table_code_bits(self._h))
+
+    @property
+    def escape_fraction(self) -> float:
+        return float(load().ks_table_escape_fraction(self._h))
 
     @property
     def compressed(self) -> bool:

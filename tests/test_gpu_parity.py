@@ -369,3 +369,34 @@ def test_torch_stream_ordering(K, oracle, ctx):
     assert int(counts.sum(dtype=torch.int64)) == int(words)
     n, oc = oracle.kmer_counts([ds.host_seq(0)], k)
     assert np.array_equal(counts.cpu().numpy(), oc) and n == words
+
+
+@pytest.mark.parametrize("k,ndist,force", [(9, 6000, True), (13, 3000, False), (7, 5000, True)])
+def test_code12_tables(K, oracle, ctx, monkeypatch, k, ndist, force):
+    """J = 5 expanded tables with 12-bit codes: escapes to the base table
+    (forced on with KS_EXT_ESCAPE_MAX=1 when more than 4095 values), and
+    (k+4)-mer indices beyond 32 bits at k=13."""
+    import torch
+    from kmer_spans_amd import device as D, genome
+    if force:
+        monkeypatch.setenv("KS_EXT_ESCAPE_MAX", "1.0")
+    rng = np.random.default_rng(k + ndist)
+    vals = np.round(rng.normal(size=ndist) * 64) / 64 + rng.normal(size=ndist) * 1e-3
+    w = vals[rng.integers(0, ndist, size=4 ** k)]
+    s = genome.contig(1_500_000, k, device="cuda", repeats=True)
+    ds = D.from_parts([s], [s.numel()], "cuda")
+    host = [ds.host_seq(0)]
+    D.bind_torch_stream(ctx)
+    tab = D.DeviceTable(ctx, w, k, 0.02, compress=True, expand=True)
+    assert tab.positions_per_read == 5 and tab.code_bits == 12, (tab.positions_per_read, tab.code_bits)
+    if ndist > 4095:
+        assert tab.escape_fraction > 0
+    o = oracle.scan(host, k, w, 0.02, 30, 3.0, visits=True)
+    for algo in ALGOS:
+        ctx.set_scan_algo(algo)
+        vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+        pos, sc, st = D.scan(ctx, ds, k, tab, 30, 3.0, vis)
+        _assert_same_regions(pos, sc, o["pos"], o["score"], ("c12", k, algo))
+        assert np.array_equal(vis.cpu().numpy(), o["counts"])
+    ctx.set_scan_algo(-1)
+    tab.close()

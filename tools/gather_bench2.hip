@@ -1,5 +1,5 @@
 // gather_bench2.hip -- rates for the expanded (k+j)-mer table design:
-// random gathers of 8/16/32-byte entries from 4-32 GiB tables, and the cost
+// random gathers of 8/16/32-byte entries from 4-128 GiB tables, and the cost
 // of the dependent uint16 -> FP64 LUT lookups (global memory vs LDS).
 #include <hip/hip_runtime.h>
 
@@ -81,8 +81,15 @@ void gw(const char *name, int log2n, int64_t n, int grid) {
 struct B16 { uint4 a; };
 struct B32 { uint4 a, b; };
 
-int main() {
+int main(int argc, char **argv) {
   const int64_t n = 1LL << 30;
+  if (argc > 1 && argv[1][0] == 'b') {  // "big": 32 / 64 / 128 GiB tables of u64 entries
+    gw<uint64_t, 8>("u64_4G_entries", 32, n, 4096);
+    gw<uint64_t, 8>("u64_8G_entries", 33, n, 4096);
+    gw<uint64_t, 8>("u64_16G_entries", 34, n, 4096);
+    gw<uint64_t, 16>("u64_16G_entries", 34, n, 8192);
+    return 0;
+  }
   gw<uint64_t, 8>("u64_4G_entries", 32, n, 4096);   // 32 GiB
   gw<uint64_t, 16>("u64_4G_entries", 32, n, 4096);
   gw<uint64_t, 8>("u64_1G_entries", 30, n, 4096);   // 8 GiB

@@ -57,6 +57,7 @@ enum Slot : int {
   SLOT_WORK_A,      // rescan work lists
   SLOT_WORK_B,
   SLOT_TABLE_TMP,
+  SLOT_LAYOUT,      // run layout (chunk / tile bases)
   SLOT_COUNT
 };
 
@@ -77,7 +78,7 @@ struct ks_ctx {
   // pinned host staging
   void *pinned = nullptr;
   size_t pinned_bytes = 0;
-  hipEvent_t ev[8] = {};
+  hipEvent_t ev[16] = {};
 };
 
 struct ks_table {
@@ -124,6 +125,22 @@ struct Runs {
   int32_t *seq = nullptr;
   int64_t n = 0;
 };
+
+// Scan indices per chunk of the chunked scan, chunks per stitch tile.
+constexpr int kChunk = 256;
+constexpr int kTileChunks = 64;
+
+// Chunk layout of the runs, computed on the device (run_layout): chunk and
+// tile bases per run (device, n + 1 entries) and host totals.
+struct RunLayout {
+  int64_t *cbase = nullptr;
+  int64_t *tbase = nullptr;
+  int64_t nch = 0, ntiles = 0;
+  int64_t scored = 0;   // scan indices (sum over runs of len - k)
+  int64_t nscan = 0;    // runs longer than k
+  int64_t longest = 0;  // longest run (bases)
+};
+ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay);
 
 // Region record buffer written by scan kernels.
 struct RegionBuf {

@@ -128,7 +128,75 @@ __global__ void k_pair_runs(const unsigned long long *__restrict__ ev, int64_t n
   rs[r] = lo;
 }
 
+// Chunks and stitch tiles of every run, plus (wave-aggregated) totals.
+__global__ void k_run_counts(const int64_t *__restrict__ ra, const int64_t *__restrict__ rb, int64_t n, int k,
+                             int64_t *__restrict__ cnt_c, int64_t *__restrict__ cnt_t,
+                             unsigned long long *__restrict__ agg) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long sc = 0, ns = 0, lo = 0;
+  if (r < n) {
+    const int64_t L = rb[r] - ra[r];
+    const int64_t P = L - k;
+    const int64_t ch = P > 0 ? (P + kChunk - 1) / kChunk : 0;
+    cnt_c[r] = ch;
+    cnt_t[r] = (ch + kTileChunks - 1) / kTileChunks;
+    if (P > 0) { sc = (unsigned long long)P; ns = 1; lo = (unsigned long long)L; }
+  } else if (r == n) {
+    cnt_c[r] = 0;
+    cnt_t[r] = 0;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    sc += __shfl_down(sc, d, 64);
+    ns += __shfl_down(ns, d, 64);
+    const unsigned long long o = __shfl_down(lo, d, 64);
+    lo = o > lo ? o : lo;
+  }
+  if ((threadIdx.x & 63) == 0 && (sc | ns | lo)) {
+    atomicAdd(&agg[0], sc);
+    atomicAdd(&agg[1], ns);
+    atomicMax(&agg[2], lo);
+  }
+}
+
 }  // namespace
+
+ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay) {
+  hipStream_t st = ctx->stream;
+  const int64_t n = runs.n;
+  *lay = RunLayout{};
+  void *buf = nullptr;
+  KS_TRY(ensure(ctx, SLOT_LAYOUT, (size_t)(n + 1) * 8 * 4 + 256, &buf));
+  int64_t *cnt_c = static_cast<int64_t *>(buf);
+  int64_t *cnt_t = cnt_c + (n + 1);
+  lay->cbase = cnt_t + (n + 1);
+  lay->tbase = lay->cbase + (n + 1);
+  void *scal = nullptr;
+  KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
+  unsigned long long *agg = reinterpret_cast<unsigned long long *>(scal) + 8;
+  KS_HIP(hipMemsetAsync(agg, 0, 24, st));
+  hipLaunchKernelGGL(k_run_counts, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st, runs.a, runs.b, n, k,
+                     cnt_c, cnt_t, agg);
+  KS_HIP(hipGetLastError());
+  size_t tb = 0;
+  KS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt_c, lay->cbase, (int)(n + 1), st));
+  void *tmp = nullptr;
+  KS_TRY(ensure(ctx, SLOT_SORT_TMP, tb, &tmp));
+  KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt_c, lay->cbase, (int)(n + 1), st));
+  KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt_t, lay->tbase, (int)(n + 1), st));
+  int64_t h[2] = {0, 0};
+  unsigned long long ha[3] = {0, 0, 0};
+  KS_HIP(hipMemcpyAsync(&h[0], lay->cbase + n, 8, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipMemcpyAsync(&h[1], lay->tbase + n, 8, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipMemcpyAsync(ha, agg, 24, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipStreamSynchronize(st));
+  lay->nch = h[0];
+  lay->ntiles = h[1];
+  lay->scored = (int64_t)ha[0];
+  lay->nscan = (int64_t)ha[1];
+  lay->longest = (int64_t)ha[2];
+  return KS_OK;
+}
 
 ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs, float *ms) {
   hipStream_t st = ctx->stream;

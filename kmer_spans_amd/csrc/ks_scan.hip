@@ -21,9 +21,13 @@
 
 namespace ks {
 
-ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int k, const TableView &tv,
-                       uint64_t mw, double min_score, uint32_t *visits, const RegionBuf &rb,
+ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, const RunLayout &lay, int k,
+                       const TableView &tv, uint64_t mw, double min_score, uint32_t *visits, const RegionBuf &rb,
                        ks_scan_stats *stats);
+ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const int64_t *ra, const int64_t *rb,
+                           const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
+                           double min_score, uint32_t *visits, const RegionBuf &out,
+                           const unsigned long long *d_n = nullptr);
 
 namespace {
 
@@ -38,11 +42,13 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
                                                   const int64_t *__restrict__ rbnd,
                                                   const int32_t *__restrict__ rseq, int64_t nruns,
                                                   int k, TableView tv, uint64_t mw, double min_score,
-                                                  uint32_t *__restrict__ visits, RegionBuf out) {
+                                                  uint32_t *__restrict__ visits, RegionBuf out,
+                                                  const unsigned long long *__restrict__ d_n) {
   constexpr int G = (J == 1) ? 16 : (J >= 4 ? 4 : (J == 3 ? 6 : 8));  // reads per batch
   constexpr int PB = G * J;                                           // indices per batch (16, 16, 18, 16, 20)
   using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;  // (k+J-1)-mer code
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d_n && (int64_t)*d_n < nruns) nruns = (int64_t)*d_n;  // count known on the device only
   if (r >= nruns) return;
   const int64_t a = ra[r], b = rbnd[r];
   if (b - a <= k) return;
@@ -142,12 +148,13 @@ __global__ void k_add_hist(uint32_t *__restrict__ dst, const uint32_t *__restric
 
 ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const int64_t *ra, const int64_t *rb,
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
-                           double min_score, uint32_t *visits, const RegionBuf &out) {
+                           double min_score, uint32_t *visits, const RegionBuf &out,
+                           const unsigned long long *d_n) {
   if (n <= 0) return KS_OK;
   const int J = tv.ext ? tv.ext_J : 1;
 #define KS_LANE(J, C)                                                                                   \
   hipLaunchKernelGGL((k_scan_lane<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, total, \
-                     ra, rb, rs, n, k, tv, mw, min_score, visits, out)
+                     ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_n)
   if (tv.compressed) {
     if (J == 5) KS_LANE(5, true); else if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
   } else {
@@ -170,20 +177,12 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
   float ms_runs = 0;
   KS_TRY(find_runs(ctx, s, total, &runs, &ms_runs));
   S->ms_runs = ms_runs;
-  // host view of runs for statistics and algorithm choice
-  std::vector<int64_t> ha(runs.n), hb(runs.n);
-  if (runs.n) {
-    KS_HIP(hipMemcpyAsync(ha.data(), runs.a, runs.n * 8, hipMemcpyDeviceToHost, st));
-    KS_HIP(hipMemcpyAsync(hb.data(), runs.b, runs.n * 8, hipMemcpyDeviceToHost, st));
-    KS_HIP(hipStreamSynchronize(st));
-  }
-  int64_t longest = 0, scored = 0, nscan = 0;
-  for (int64_t r = 0; r < runs.n; ++r) {
-    const int64_t L = hb[r] - ha[r];
-    if (L > k) { scored += L - k; ++nscan; longest = std::max(longest, L); }
-  }
+  // chunk layout, statistics and algorithm choice (device-side, one sync)
+  RunLayout lay;
+  if (runs.n) KS_TRY(run_layout(ctx, runs, k, &lay));
+  const int64_t longest = lay.longest, scored = lay.scored;
   S->n_scored = scored;
-  S->n_runs = nscan;
+  S->n_runs = lay.nscan;
   for (int32_t q = 0; q < s->nseq; ++q) {
     const int64_t L = s->offsets_host[q + 1] - s->offsets_host[q];
     if (L >= k) S->n_bases += L;
@@ -196,7 +195,11 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
   if (algo < 0) algo = (longest > (1 << 15)) ? 1 : 0;
   S->scan_algo = algo;
 
-  int64_t cap = std::max<int64_t>(std::max<int64_t>(65536, scored / 2048), (int64_t)(ctx->slots[SLOT_REGIONS].bytes / 28));
+  // region capacity: what the (grow-only) slot already holds, so that the
+  // slot is not reallocated on every call
+  const size_t reg_bytes = ctx->slots[SLOT_REGIONS].bytes;
+  int64_t cap = std::max<int64_t>(std::max<int64_t>(65536, scored / 2048),
+                                  reg_bytes > 64 ? (int64_t)((reg_bytes - 64) / 28) : 0);
   unsigned long long n_reg = 0;
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
@@ -226,7 +229,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
         vscr = static_cast<uint32_t *>(vp);
         KS_HIP(hipMemsetAsync(vscr, 0, nb, st));
       }
-      ks_status rc = scan_chunked(ctx, s, runs, k, tv, mw, min_score, vscr, rb, S);
+      ks_status rc = scan_chunked(ctx, s, runs, lay, k, tv, mw, min_score, vscr, rb, S);
       if (rc == KS_INTERNAL_RETRY) {  // rescans did not fit: grow, rerun, visits untouched
         KS_HIP(hipMemcpyAsync(&n_reg, d_rcount, 8, hipMemcpyDeviceToHost, st));
         KS_HIP(hipStreamSynchronize(st));

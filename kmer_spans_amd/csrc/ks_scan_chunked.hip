@@ -40,7 +40,8 @@ namespace ks {
 
 ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const int64_t *ra, const int64_t *rb,
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
-                           double min_score, uint32_t *visits, const RegionBuf &out);
+                           double min_score, uint32_t *visits, const RegionBuf &out,
+                           const unsigned long long *d_n = nullptr);
 
 namespace {
 
@@ -328,6 +329,170 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
   }
 }
 
+// Software-pipelined gather pass for expanded compressed tables (J >= 2):
+// the reads of batch b+1 (and the sequence bytes of batch b+2) are issued
+// before batch b is consumed, so every wave keeps its next table reads in
+// flight while it runs the trajectory, and the escape reads of batch b (J = 5,
+// issued first) complete without waiting for them (in-order vmcnt).  All
+// loads are unconditional (dead groups read entry 0) so the wait counts stay
+// static.  Results are identical to k_pass1.
+template <int J, bool kLds>
+__global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
+                                                 TableView tv, uint16_t *__restrict__ codes, uint64_t mw,
+                                                 double min_score, uint32_t *__restrict__ visits, P1 o, Cand cand) {
+  constexpr int G = 4;                  // table reads per batch
+  constexpr int PB = G * J;             // scan indices per batch (8, 12, 16, 20)
+  constexpr bool k12 = (J == 5);        // 12-bit codes with escapes
+  using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;
+  using EW = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;  // entry word
+  __shared__ double s_lut[kLds ? kLdsLutMax : 1];
+  __shared__ double s_lut12[k12 ? 4096 : 1];
+  __shared__ uint16_t s_map12[k12 ? 4096 : 1];
+  if (kLds)
+    for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
+  if (k12)
+    for (int i = threadIdx.x; i < 4096; i += blockDim.x) {
+      s_lut12[i] = tv.lut12[i];
+      s_map12[i] = tv.map12[i];
+    }
+  if (kLds || k12) __syncthreads();
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= g.nch) return;
+  const EW *__restrict__ ext = reinterpret_cast<const EW *>(tv.ext);
+  const int kx = k + J - 1;
+  const GC xmask = (2 * kx >= 8 * (int)sizeof(GC)) ? ~(GC)0 : (((GC)1 << (2 * kx)) - 1);
+  const uint32_t kmask = (1u << (2 * k)) - 1u;
+  const int64_t start = g.start[c];
+  const int n = g.n[c];
+  GC gcode = (GC)prime_code_guarded64(seq, start - k, kx, total);  // (k+J-1)-mer of group 0
+  uint8_t by[32];
+  // prologue: codes + reads of batch 0, bytes of batch 1
+  load16(seq, start + J - 1, total, by);
+  if (PB > 16) load16(seq, start + J - 1 + 16, total, by + 16);
+  GC gc[G];
+  EW e[G];
+#pragma unroll
+  for (int gi = 0; gi < G; ++gi) {
+    gc[gi] = gcode;
+#pragma unroll
+    for (int t = 0; t < J; ++t) gcode = ((gcode << 2) | enc(by[gi * J + t])) & xmask;
+  }
+#pragma unroll
+  for (int gi = 0; gi < G; ++gi) e[gi] = ext[(gi * J < n) ? gc[gi] : (GC)0];
+  load16(seq, start + PB + J - 1, total, by);
+  if (PB > 16) load16(seq, start + PB + J - 1 + 16, total, by + 16);
+  double prev = 0.0, best = 0.0;
+  int beg = -1, arg = 0;
+  double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
+  bool special = false;
+  for (int b0 = 0; b0 < n; b0 += PB) {
+    // 1. escape reads of batch b first (one per group: its first escaped
+    //    slot; further escapes in the same group, ~1e-5 of groups, read inline)
+    uint16_t qe[k12 ? G : 1];
+    int tesc[k12 ? G : 1];
+    if (k12) {
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi) {
+        int te = J;
+#pragma unroll
+        for (int t = J - 1; t >= 0; --t)
+          if (((uint32_t)(e[gi] >> (12 * t)) & 0xfffu) == 0xfffu) te = t;
+        tesc[gi] = te;
+        const uint32_t km = (uint32_t)(gc[gi] >> (2 * (J - 1 - (te < J ? te : 0)))) & kmask;
+        qe[gi] = tv.codes[te < J ? km : 0u];
+      }
+    }
+    // 2. reads of batch b+1 (entry 0 where the group is past the chunk end)
+    GC gn[G];
+    EW en[G];
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+      gn[gi] = gcode;
+#pragma unroll
+      for (int t = 0; t < J; ++t) gcode = ((gcode << 2) | enc(by[gi * J + t])) & xmask;
+    }
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) en[gi] = ext[(b0 + PB + gi * J < n) ? gn[gi] : (GC)0];
+    // 3. bytes of batch b+2
+    load16(seq, start + b0 + 2 * PB + J - 1, total, by);
+    if (PB > 16) load16(seq, start + b0 + 2 * PB + J - 1 + 16, total, by + 16);
+    // 4. batch b group by group: values, packed codes, trajectory
+    uint32_t cw[PB / 2];
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+#pragma unroll
+      for (int t = 0; t < J; ++t) {
+        const int j = gi * J + t;
+        uint32_t qq;
+        double s;
+        if (k12) {
+          const uint32_t c12 = (uint32_t)(e[gi] >> (12 * t)) & 0xfffu;
+          if (c12 != 0xfffu) {
+            qq = s_map12[c12];
+            s = s_lut12[c12];
+          } else {
+            qq = (t == tesc[gi]) ? qe[gi] : tv.codes[(uint32_t)(gc[gi] >> (2 * (J - 1 - t))) & kmask];
+            s = kLds ? s_lut[qq] : tv.lut[qq];
+          }
+        } else {
+          qq = (uint32_t)(e[gi] >> (16 * t)) & 0xffffu;
+          s = kLds ? s_lut[qq] : tv.lut[qq];
+        }
+        if (j & 1) cw[j >> 1] |= qq << 16;
+        else cw[j >> 1] = qq;
+        const int i = b0 + j;
+        if (i < n) {
+          if (visits) atomicAdd(&visits[(uint32_t)(gc[gi] >> (2 * (J - 1 - t))) & kmask], 1u);
+          asum += s;
+          pmin = fmin(pmin, asum);
+          pmax = fmax(pmax, asum);
+          sabs += fabs(s);
+          special |= !isfinite(s);
+          const double tt = prev + s;
+          const double S = tt > 0 ? tt : 0.0;
+          if (prev == 0 && S > 0) {
+            beg = i; arg = i; best = S;
+          } else if (prev > 0 && S == 0) {
+            if ((uint64_t)(arg - beg) >= mw && best >= min_score) {
+              const unsigned long long slot = atomicAdd(cand.count, 1ull);
+              if ((int64_t)slot < cand.cap) {
+                cand.beg[slot] = start + beg;
+                cand.arg[slot] = start + arg;
+                cand.rst[slot] = start + i;
+                cand.best[slot] = best;
+              }
+            }
+            beg = -1;
+          } else if (S > best) {
+            best = S; arg = i;
+          }
+          prev = S;
+        }
+      }
+    }
+#pragma unroll
+    for (int r4 = 0; r4 < PB / 4; ++r4)
+      if (b0 + 4 * r4 < CH)
+        *reinterpret_cast<uint2 *>(codes + code_slot(c, b0 + 4 * r4)) = make_uint2(cw[2 * r4], cw[2 * r4 + 1]);
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+      gc[gi] = gn[gi];
+      e[gi] = en[gi];
+    }
+  }
+  o.cexit[c] = prev;
+  o.asum[c] = asum;
+  o.pmin[c] = pmin;
+  o.pmax[c] = pmax;
+  o.sabs[c] = sabs;
+  o.special[c] = special ? 1 : 0;
+  if (prev > 0) {
+    o.tbeg[c] = beg; o.tmax[c] = best; o.targ[c] = arg;
+  } else {
+    o.tbeg[c] = -1; o.tmax[c] = 0.0; o.targ[c] = 0;
+  }
+}
+
 // ------------------------------------------------------------------- P3
 
 // Bits of a positive normal double in binade e: x = m * 2^(e-52), m in [2^52, 2^53).
@@ -585,10 +750,6 @@ __global__ void __launch_bounds__(64) k_seg_marks(Chunks g, P1 o, const double *
   if (e == 0) flag[0] = 1;
 }
 
-__global__ void k_seg_sentinel(int64_t *__restrict__ seg, const unsigned long long *__restrict__ d_nseg,
-                               int64_t nch) {
-  seg[*d_nseg] = nch;
-}
 
 // Exact carry, one wave per run, walking 64-chunk tiles (lane j <-> chunk
 // cb + j).  Per chunk, in order: entry 0 -> clean exit (CLEAN); a binade
@@ -620,18 +781,13 @@ __device__ __forceinline__ double rld(double v, int j) { return __longlong_as_do
 // The wave of the preceding segment checks the assumption against its exact
 // exit (bit 16 of err on mismatch; the host then redoes the carry per run).
 template <bool kCompressed>
-__global__ void __launch_bounds__(64) k_carry(Chunks g, const int64_t *__restrict__ seg, int64_t nseg_max,
-                                              const unsigned long long *__restrict__ d_nseg,
-                                              const uint8_t *__restrict__ seq, int64_t total, int k, TableView tv,
-                                              const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
-                                              unsigned long long *__restrict__ nreplay, unsigned int *__restrict__ err,
-                                              long long *__restrict__ dbg) {
-  const int64_t r = blockIdx.x;
-  const int64_t nseg = d_nseg ? (int64_t)*d_nseg : nseg_max;
-  if (r >= nseg) return;
+__device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64_t c1, const uint8_t *__restrict__ seq,
+                                              int64_t total, int k, const TableView &tv,
+                                              const uint16_t *__restrict__ codes, const P1 &o, const Summ &sm,
+                                              const Carry &cr, unsigned long long *__restrict__ nreplay,
+                                              unsigned int *__restrict__ err, long long *__restrict__ dbg,
+                                              int64_t r) {
   const int lane = threadIdx.x;
-  const int64_t c0 = seg[r], c1 = seg[r + 1];
-  if (c0 >= c1) return;
   double x = (c0 > 0 && g.run[c0] == g.run[c0 - 1]) ? o.cexit[c0 - 1] : 0.0;
   unsigned long long replays = 0;
   const long long t_start = dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
@@ -775,15 +931,74 @@ __global__ void __launch_bounds__(64) k_carry(Chunks g, const int64_t *__restric
   if (lane == 0 && c1 < g.nch && g.run[c1] == g.run[c1 - 1] &&
       __double_as_longlong(x) != __double_as_longlong(o.cexit[c1 - 1]))
     atomicOr(err, 16u);  // the next segment assumed a different entry
-  if (dbg && lane == 0) {
-    dbg[6 * r + 0] = (long long)__builtin_amdgcn_s_memtime() - t_start;
-    dbg[6 * r + 1] = c1 - c0;
-    dbg[6 * r + 2] = (long long)replays;
-    dbg[6 * r + 3] = 0;
-    dbg[6 * r + 4] = n_l;
-    dbg[6 * r + 5] = n_r;
+  if (dbg && lane == 0) {  // accumulated per block (several segments per window)
+    dbg[6 * r + 0] += (long long)__builtin_amdgcn_s_memtime() - t_start;
+    dbg[6 * r + 1] += c1 - c0;
+    dbg[6 * r + 2] += (long long)replays;
+    dbg[6 * r + 3] += 1;
+    dbg[6 * r + 4] += n_l;
+    dbg[6 * r + 5] += n_r;
   }
 }
+
+// Carry by window: block w runs the segments that start in chunks
+// [64w, 64w + 64) (segment starts flagged by k_seg_marks; a segment ends at
+// the next flagged chunk, possibly windows later).
+template <bool kCompressed>
+__global__ void __launch_bounds__(64) k_carry_win(Chunks g, const uint8_t *__restrict__ flag,
+                                                  const uint8_t *__restrict__ seq, int64_t total, int k, TableView tv,
+                                                  const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
+                                                  unsigned long long *__restrict__ nreplay,
+                                                  unsigned int *__restrict__ err, long long *__restrict__ dbg) {
+  const int64_t w = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t base = w * 64;
+  unsigned long long m = __ballot(base + lane < g.nch && flag[base + lane]);
+  while (m) {
+    const int b = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const int64_t c0 = base + b;
+    int64_t c1 = g.nch;
+    if (m) {
+      c1 = base + __ffsll((long long)m) - 1;
+    } else {
+      for (int64_t nb = base + 64; nb < g.nch; nb += 64) {
+        const unsigned long long mm = __ballot(nb + lane < g.nch && flag[nb + lane]);
+        if (mm) {
+          c1 = nb + __ffsll((long long)mm) - 1;
+          break;
+        }
+      }
+    }
+    carry_segment<kCompressed>(g, c0, c1, seq, total, k, tv, codes, o, sm, cr, nreplay, err, dbg, w);
+  }
+}
+
+// Carry by run (the fallback when a segment assumption failed): gated on
+// bit 16 of err, so it can be queued unconditionally.
+template <bool kCompressed>
+__global__ void __launch_bounds__(64) k_carry_run(Chunks g, const int64_t *__restrict__ cbase, int64_t nruns,
+                                                  const uint8_t *__restrict__ seq, int64_t total, int k, TableView tv,
+                                                  const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
+                                                  unsigned long long *__restrict__ nreplay,
+                                                  unsigned int *__restrict__ err, long long *__restrict__ dbg) {
+  const int64_t r = blockIdx.x;
+  if (r >= nruns || !(*(volatile unsigned int *)err & 16u)) return;
+  const int64_t c0 = cbase[r], c1 = cbase[r + 1];
+  if (c0 < c1) carry_segment<kCompressed>(g, c0, c1, seq, total, k, tv, codes, o, sm, cr, nreplay, err, nullptr, r);
+}
+
+// Fallback preparation: after a failed segment check, the first heads pass
+// may have flagged clamps against the wrong carry; clear everything but 16.
+__global__ void k_fallback_prep(unsigned int *__restrict__ err, unsigned long long *__restrict__ nreplay,
+                                int force) {
+  if (force) *err |= 16u;
+  if (*err & 16u) {
+    *err = 16u;
+    *nreplay = 0;
+  }
+}
+
 
 // ------------------------------------------------------------------- P4
 
@@ -793,9 +1008,10 @@ __global__ void __launch_bounds__(64) k_carry(Chunks g, const int64_t *__restric
 template <int J, bool kCompressed>
 __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
                                                int k, TableView tv, const uint16_t *__restrict__ codes,
-                                               Carry cr, unsigned int *__restrict__ err) {
+                                               Carry cr, unsigned int *__restrict__ err, int gated) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
+  if (gated && !(*(volatile unsigned int *)err & 16u)) return;  // second pass only after a fallback
   const int mode = cr.mode[c];
   if (mode == kModeL || mode == kModeU) return;  // head written by the carry (summary / replay)
   cr.hq[c] = -1;
@@ -1144,8 +1360,9 @@ __global__ void __launch_bounds__(64) k_stitch_emit(Chunks g, const int64_t *__r
 // Candidates (closed emittable excursions of the clean trajectories) are
 // valid when they begin at or after their chunk's valid_from.
 __global__ void k_candidates(Chunks g, const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase,
-                             int64_t nruns, const int32_t *__restrict__ rseq, int k, Cand cand, int64_t ncand,
-                             Carry cr, RegionBuf out, Rescan rs) {
+                             int64_t nruns, const int32_t *__restrict__ rseq, int k, Cand cand,
+                             const unsigned long long *__restrict__ d_ncand, Carry cr, RegionBuf out, Rescan rs) {
+  const int64_t ncand = min((int64_t)*d_ncand, cand.cap);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if ((int64_t)blockIdx.x * blockDim.x >= ncand) return;  // whole block idle
   bool want = false;
@@ -1172,33 +1389,21 @@ __global__ void k_candidates(Chunks g, const int64_t *__restrict__ ra, const int
 
 }  // namespace
 
-ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int k, const TableView &tv,
-                       uint64_t mw, double min_score, uint32_t *visits, const RegionBuf &rb,
+ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, const RunLayout &lay, int k,
+                       const TableView &tv, uint64_t mw, double min_score, uint32_t *visits, const RegionBuf &rb,
                        ks_scan_stats *stats) {
   hipStream_t st = ctx->stream;
   const int64_t total = s->offsets_host[s->nseq];
   const int64_t nruns = runs.n;
-  if (nruns == 0) return KS_OK;
-  // chunk bases (host prefix over runs)
-  std::vector<int64_t> ha(nruns), hb(nruns), cb(nruns + 1, 0);
-  KS_HIP(hipMemcpyAsync(ha.data(), runs.a, nruns * 8, hipMemcpyDeviceToHost, st));
-  KS_HIP(hipMemcpyAsync(hb.data(), runs.b, nruns * 8, hipMemcpyDeviceToHost, st));
-  KS_HIP(hipStreamSynchronize(st));
-  for (int64_t r = 0; r < nruns; ++r) {
-    const int64_t P = hb[r] - ha[r] - k;
-    cb[r + 1] = cb[r] + (P > 0 ? (P + CH - 1) / CH : 0);
-  }
-  const int64_t nch = cb[nruns];
-  if (nch == 0) return KS_OK;
-  std::vector<int64_t> tbv(nruns + 1, 0);  // stitch tiles: 64 chunks, aligned to each run's first chunk
-  for (int64_t r = 0; r < nruns; ++r) tbv[r + 1] = tbv[r] + (cb[r + 1] - cb[r] + 63) / 64;
-  const int64_t ntiles = tbv[nruns];
+  const int64_t nch = lay.nch, ntiles = lay.ntiles;
+  if (nruns == 0 || nch == 0) return KS_OK;
+  const int64_t *d_cbase = lay.cbase, *d_tbase = lay.tbase;
   const bool comp = tv.compressed != 0;
 
   // ---- workspace
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const int64_t nwin = (nch + 63) / 64;
   size_t off = 0;
-  const size_t o_cbase = off; off += al((nruns + 1) * 8);
   const size_t o_start = off; off += al(nch * 8);
   const size_t o_n = off; off += al(nch * 4);
   const size_t o_run = off; off += al(nch * 4);
@@ -1214,12 +1419,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
   const size_t o_hq = off; off += al(nch * 4 * 2);
   const size_t o_hmax = off; off += al(nch * 8);
   const size_t o_cnt = off; off += al(64);
-  const size_t o_tbase = off; off += al((nruns + 1) * 8);
+  const size_t o_flag = off; off += al(nch + 64);
   const size_t o_xagg = off; off += al(ntiles * 32) * 2;
   void *wsp = nullptr;
   KS_TRY(ensure(ctx, SLOT_CHUNK_A, off, &wsp));
   char *W = static_cast<char *>(wsp);
-  int64_t *d_cbase = reinterpret_cast<int64_t *>(W + o_cbase);
   Chunks g{reinterpret_cast<int64_t *>(W + o_start), reinterpret_cast<int32_t *>(W + o_n),
            reinterpret_cast<int32_t *>(W + o_run), nch};
   double *p1d = reinterpret_cast<double *>(W + o_p1d);
@@ -1234,7 +1438,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
   Carry cr{reinterpret_cast<double *>(W + o_x), reinterpret_cast<uint8_t *>(W + o_mode), hqp,
            reinterpret_cast<double *>(W + o_hmax), hqp + nch};
   unsigned long long *cnts = reinterpret_cast<unsigned long long *>(W + o_cnt);
-  int64_t *d_tbase = reinterpret_cast<int64_t *>(W + o_tbase);
+  uint8_t *d_flag = reinterpret_cast<uint8_t *>(W + o_flag);
   auto xtiles = [&](char *p) {
     return XTiles{reinterpret_cast<int32_t *>(p), reinterpret_cast<int32_t *>(p) + ntiles,
                   reinterpret_cast<long long *>(p + ntiles * 8), reinterpret_cast<long long *>(p + ntiles * 16),
@@ -1243,8 +1447,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
   const XTiles xagg = xtiles(W + o_xagg), xtin = xtiles(W + o_xagg + al(ntiles * 32));
   // cnts: [0] candidates, [1] rescans, [2] replays, [3] error bits (u32)
   KS_HIP(hipMemsetAsync(cnts, 0, 64, st));
-  KS_HIP(hipMemcpyAsync(d_cbase, cb.data(), (nruns + 1) * 8, hipMemcpyHostToDevice, st));
-  KS_HIP(hipMemcpyAsync(d_tbase, tbv.data(), (nruns + 1) * 8, hipMemcpyHostToDevice, st));
+  unsigned int *d_err = reinterpret_cast<unsigned int *>(cnts + 3);
 
   uint16_t *codes = nullptr;
   if (comp) {
@@ -1254,29 +1457,50 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
     codes = static_cast<uint16_t *>(cp);
   }
   int64_t ccap = std::max<int64_t>(1 << 16, nch / 4);
-  if (ctx->slots[SLOT_CHUNK_C].bytes / 40 > (size_t)ccap) ccap = ctx->slots[SLOT_CHUNK_C].bytes / 40;
+  const size_t cand_bytes = ctx->slots[SLOT_CHUNK_C].bytes;  // use what the grow-only slot holds
+  if (cand_bytes > 1024 && (cand_bytes - 1024) / 40 > (size_t)ccap) ccap = (int64_t)((cand_bytes - 1024) / 40);
   void *cbuf = nullptr;
   KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)ccap * 40 + 1024, &cbuf));
   Cand cand{reinterpret_cast<long long *>(cbuf), reinterpret_cast<long long *>(cbuf) + ccap,
             reinterpret_cast<long long *>(cbuf) + 2 * ccap, reinterpret_cast<double *>(cbuf) + 3 * ccap,
             cnts, ccap};
+  const int64_t rcap = std::max<int64_t>(rb.cap, 4096);
+  void *rsb = nullptr;
+  KS_TRY(ensure(ctx, SLOT_WORK_A, (size_t)rcap * 20 + 1024, &rsb));
+  Rescan rs{reinterpret_cast<int64_t *>(rsb), reinterpret_cast<int64_t *>(rsb) + rcap,
+            reinterpret_cast<int32_t *>(reinterpret_cast<int64_t *>(rsb) + 2 * rcap), cnts + 1, rcap};
+  // KS_DEBUG_CARRY=1: per-window carry statistics to stderr (diagnostics only)
+  static const bool dbg_on = getenv("KS_DEBUG_CARRY") != nullptr;
+  long long *dbg = nullptr;
+  if (dbg_on) {
+    KS_HIP(hipMalloc(&dbg, nwin * 6 * sizeof(long long)));
+    KS_HIP(hipMemsetAsync(dbg, 0, nwin * 6 * sizeof(long long), st));
+  }
 
+  // ---- P0 chunks, P1 gather pass
   KS_HIP(hipEventRecord(ctx->ev[7], st));
   hipLaunchKernelGGL(k_make_chunks, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, st, runs.a, d_cbase,
                      nruns, k, runs.b, g);
   KS_HIP(hipGetLastError());
   const unsigned gch = (unsigned)((nch + 255) / 256);
-  hipEvent_t e_p1a, e_p1b;
-  KS_HIP(hipEventCreate(&e_p1a));
-  KS_HIP(hipEventCreate(&e_p1b));
-  KS_HIP(hipEventRecord(e_p1a, st));
   const unsigned gch1k = (unsigned)((nch + 1023) / 1024);
+  KS_HIP(hipEventRecord(ctx->ev[8], st));
   const bool lds_lut = comp && tv.nlut <= kLdsLutMax && getenv("KS_NO_LDS_LUT") == nullptr;
 #define KS_P1(J, C, L)                                                                                       \
   hipLaunchKernelGGL((k_pass1<J, C, L>), dim3(J == 1 ? gch : gch1k), dim3(J == 1 ? 256 : 1024), 0, st, g, s->seq, \
                      total, k, tv, codes, mw, min_score, visits, p1, cand)
   const int J = (tv.ext != nullptr) ? tv.ext_J : 1;
-  if (comp && J == 5) {
+  const bool pipelined = getenv("KS_NO_PIPELINED_P1") == nullptr;
+#define KS_P1P(J, L)                                                                                           \
+  hipLaunchKernelGGL((k_pass1p<J, L>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes, mw,       \
+                     min_score, visits, p1, cand)
+  if (comp && J >= 2 && pipelined) {
+    if (lds_lut) {
+      if (J == 5) KS_P1P(5, true); else if (J == 4) KS_P1P(4, true); else if (J == 3) KS_P1P(3, true); else KS_P1P(2, true);
+    } else {
+      if (J == 5) KS_P1P(5, false); else if (J == 4) KS_P1P(4, false); else if (J == 3) KS_P1P(3, false); else KS_P1P(2, false);
+    }
+  } else if (comp && J == 5) {
     KS_P1(5, true, false);  // 12-bit codes: value LUT of the short codes in LDS
   } else if (comp && lds_lut) {
     if (J == 4) KS_P1(4, true, true); else if (J == 3) KS_P1(3, true, true); else if (J == 2) KS_P1(2, true, true); else KS_P1(1, true, false);
@@ -1286,34 +1510,15 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
     if (J == 4) KS_P1(4, false, false); else if (J == 3) KS_P1(3, false, false); else if (J == 2) KS_P1(2, false, false); else KS_P1(1, false, false);
   }
 #undef KS_P1
+#undef KS_P1P
   KS_HIP(hipGetLastError());
-  KS_HIP(hipEventRecord(e_p1b, st));
-  // segments of the carry chain (k_seg_marks) -> seg[0..nseg], seg[nseg] = nch
-  const int64_t nwin = (nch + 63) / 64;
-  const int64_t nseg_max = nwin + nruns;
-  unsigned long long *d_nseg = cnts + 4;
-  void *segp = nullptr;
-  KS_TRY(ensure(ctx, SLOT_CHUNK_D, (size_t)(nseg_max + 2) * 8 + (size_t)nch + 256, &segp));
-  int64_t *d_seg = static_cast<int64_t *>(segp);
-  uint8_t *d_flag = reinterpret_cast<uint8_t *>(d_seg + nseg_max + 2);
-  // KS_DEBUG_CARRY=1: per-segment carry statistics to stderr (diagnostics only)
-  static const bool dbg_on = getenv("KS_DEBUG_CARRY") != nullptr;
-  long long *dbg = nullptr;
-  if (dbg_on) KS_HIP(hipMalloc(&dbg, std::max(nseg_max, nruns) * 6 * sizeof(long long)));
+  KS_HIP(hipEventRecord(ctx->ev[9], st));
+
+  // ---- P2 prediction, segment starts, summaries
   hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)nruns), dim3(64), 0, st, d_cbase, nruns, p1, xt);
   KS_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_seg_marks, dim3((unsigned)nwin), dim3(64), 0, st, g, p1, xt, d_flag);
   KS_HIP(hipGetLastError());
-  {
-    size_t tb = 0;
-    hipcub::CountingInputIterator<int64_t> it(0);
-    KS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, it, d_flag, d_seg, d_nseg, (int)nch, st));
-    void *tmp = nullptr;
-    KS_TRY(ensure(ctx, SLOT_SORT_TMP, tb, &tmp));
-    KS_HIP(hipcub::DeviceSelect::Flagged(tmp, tb, it, d_flag, d_seg, d_nseg, (int)nch, st));
-    hipLaunchKernelGGL(k_seg_sentinel, dim3(1), dim3(1), 0, st, d_seg, d_nseg, nch);
-    KS_HIP(hipGetLastError());
-  }
   if (lds_lut)
     hipLaunchKernelGGL((k_summaries<true, true>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes, p1,
                        xt, sm);
@@ -1324,77 +1529,41 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
     hipLaunchKernelGGL((k_summaries<false, false>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes,
                        p1, xt, sm);
   KS_HIP(hipGetLastError());
-  unsigned int *d_err = reinterpret_cast<unsigned int *>(cnts + 3);
-  // per segment (seg_mode) or per run (fallback: the whole chain of a run in one wave)
-  auto carry_and_heads = [&](bool seg_mode) -> ks_status {
-    const int64_t *sg = seg_mode ? d_seg : d_cbase;
-    const int64_t nb = seg_mode ? nseg_max : nruns;
-    const unsigned long long *dn = seg_mode ? d_nseg : nullptr;
-    if (comp)
-      hipLaunchKernelGGL(k_carry<true>, dim3((unsigned)nb), dim3(64), 0, st, g, sg, nb, dn, s->seq, total, k, tv,
-                         codes, p1, sm, cr, cnts + 2, d_err, dbg);
-    else
-      hipLaunchKernelGGL(k_carry<false>, dim3((unsigned)nb), dim3(64), 0, st, g, sg, nb, dn, s->seq, total, k, tv,
-                         codes, p1, sm, cr, cnts + 2, d_err, dbg);
-    KS_HIP(hipGetLastError());
-#define KS_HEADS(J, C) \
-  hipLaunchKernelGGL((k_heads<J, C>), dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, cr, d_err)
-    if (comp) KS_HEADS(1, true);
-    else if (J == 4) KS_HEADS(4, false);
-    else if (J == 3) KS_HEADS(3, false);
-    else if (J == 2) KS_HEADS(2, false);
-    else KS_HEADS(1, false);
-#undef KS_HEADS
-    KS_HIP(hipGetLastError());
-    return KS_OK;
+
+  // ---- P3 carry by segments + P4 heads; then the gated per-run fallback
+  if (comp)
+    hipLaunchKernelGGL(k_carry_win<true>, dim3((unsigned)nwin), dim3(64), 0, st, g, d_flag, s->seq, total, k, tv,
+                       codes, p1, sm, cr, cnts + 2, d_err, dbg);
+  else
+    hipLaunchKernelGGL(k_carry_win<false>, dim3((unsigned)nwin), dim3(64), 0, st, g, d_flag, s->seq, total, k, tv,
+                       codes, p1, sm, cr, cnts + 2, d_err, dbg);
+  KS_HIP(hipGetLastError());
+#define KS_HEADS(J, C, GATED)                                                                                 \
+  hipLaunchKernelGGL((k_heads<J, C>), dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, cr, d_err, \
+                     GATED)
+  auto heads = [&](int gated) {
+    if (comp) KS_HEADS(1, true, gated);
+    else if (J == 4) KS_HEADS(4, false, gated);
+    else if (J == 3) KS_HEADS(3, false, gated);
+    else if (J == 2) KS_HEADS(2, false, gated);
+    else KS_HEADS(1, false, gated);
   };
-  KS_TRY(carry_and_heads(true));
-  unsigned long long hc[5] = {0, 0, 0, 0, 0};
-  KS_HIP(hipMemcpyAsync(hc, cnts, 40, hipMemcpyDeviceToHost, st));
-  KS_HIP(hipStreamSynchronize(st));
-  const int64_t nseg = (int64_t)hc[4];
-  // KS_TEST_SEG_FALLBACK=1 takes the fallback path unconditionally (tests)
-  const bool seg_failed = (hc[3] & 16u) != 0 || getenv("KS_TEST_SEG_FALLBACK") != nullptr;
-  if (seg_failed) {  // a segment entry assumption failed: redo the carry run by run
-    if (hc[3] & 16u) fprintf(stderr, "kmer_spans_amd: carry segment check failed; redoing the carry per run\n");
-    KS_HIP(hipMemsetAsync(cnts + 2, 0, 16, st));
-    KS_TRY(carry_and_heads(false));
-    KS_HIP(hipMemcpyAsync(hc, cnts, 40, hipMemcpyDeviceToHost, st));
-    KS_HIP(hipStreamSynchronize(st));
-  }
-  if (dbg) {
-    const int64_t nd = seg_failed ? nruns : nseg;
-    std::vector<long long> h(nd * 6);
-    KS_HIP(hipMemcpy(h.data(), dbg, nd * 6 * sizeof(long long), hipMemcpyDeviceToHost));
-    KS_HIP(hipFree(dbg));
-    std::vector<int64_t> idx(nd);
-    for (int64_t i = 0; i < nd; ++i) idx[i] = i;
-    std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return h[6 * a] > h[6 * b]; });
-    long long tot[6] = {0, 0, 0, 0, 0, 0};
-    for (int64_t i = 0; i < nd; ++i)
-      for (int q = 0; q < 6; ++q) tot[q] += h[6 * i + q];
-    fprintf(stderr, "[carry] segments %lld (runs %lld) chunks %lld replays %lld recomputes %lld L %lld R %lld\n",
-            (long long)nd, (long long)nruns, tot[1], tot[2], tot[3], tot[4], tot[5]);
-    for (int64_t i = 0; i < std::min<int64_t>(nd, 8); ++i) {
-      const long long *d = &h[6 * idx[i]];
-      fprintf(stderr, "[carry] run %lld cycles %lld chunks %lld replays %lld recomputes %lld L %lld R %lld\n",
-              (long long)idx[i], d[0], d[1], d[2], d[3], d[4], d[5]);
-    }
-  }
-  if ((int64_t)hc[0] > ccap) {  // grow the candidate buffer and rerun the pass
-    KS_HIP(hipEventDestroy(e_p1a));
-    KS_HIP(hipEventDestroy(e_p1b));
-    void *grown = nullptr;
-    KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)(hc[0] + hc[0] / 4 + 1024) * 40 + 1024, &grown));
-    return KS_INTERNAL_RETRY;
-  }
-  const int64_t ncand = (int64_t)hc[0];
-  // rescan buffer
-  int64_t rcap = std::max<int64_t>(rb.cap, 4096);
-  void *rsb = nullptr;
-  KS_TRY(ensure(ctx, SLOT_WORK_A, (size_t)rcap * 20 + 1024, &rsb));
-  Rescan rs{reinterpret_cast<int64_t *>(rsb), reinterpret_cast<int64_t *>(rsb) + rcap,
-            reinterpret_cast<int32_t *>(reinterpret_cast<int64_t *>(rsb) + 2 * rcap), cnts + 1, rcap};
+#undef KS_HEADS
+  heads(0);
+  KS_HIP(hipGetLastError());
+  // KS_TEST_SEG_FALLBACK=1 forces the fallback path (tests)
+  const int force_fb = getenv("KS_TEST_SEG_FALLBACK") != nullptr ? 1 : 0;
+  hipLaunchKernelGGL(k_fallback_prep, dim3(1), dim3(1), 0, st, d_err, cnts + 2, force_fb);
+  if (comp)
+    hipLaunchKernelGGL(k_carry_run<true>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, total,
+                       k, tv, codes, p1, sm, cr, cnts + 2, d_err, nullptr);
+  else
+    hipLaunchKernelGGL(k_carry_run<false>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, total,
+                       k, tv, codes, p1, sm, cr, cnts + 2, d_err, nullptr);
+  heads(1);
+  KS_HIP(hipGetLastError());
+
+  // ---- P5 stitch, candidates (count read on the device), rescans
   hipLaunchKernelGGL(k_stitch_tiles, dim3((unsigned)ntiles), dim3(64), 0, st, g, d_tbase, d_cbase, nruns, p1, cr,
                      xagg);
   KS_HIP(hipGetLastError());
@@ -1404,25 +1573,45 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
   hipLaunchKernelGGL(k_stitch_emit, dim3((unsigned)ntiles), dim3(64), 0, st, g, d_tbase, d_cbase, nruns, runs.seq, k,
                      p1, cr, mw, min_score, xtin, rb, rs, d_err);
   KS_HIP(hipGetLastError());
-  if (ncand > 0) {
-    hipLaunchKernelGGL(k_candidates, dim3((unsigned)((ncand + 255) / 256)), dim3(256), 0, st, g, runs.a, d_cbase,
-                       nruns, runs.seq, k, cand, ncand, cr, rb, rs);
-    KS_HIP(hipGetLastError());
-  }
-  KS_HIP(hipMemcpyAsync(hc, cnts, 40, hipMemcpyDeviceToHost, st));
+  hipLaunchKernelGGL(k_candidates, dim3((unsigned)((ccap + 255) / 256)), dim3(256), 0, st, g, runs.a, d_cbase,
+                     nruns, runs.seq, k, cand, cnts, cr, rb, rs);
+  KS_HIP(hipGetLastError());
+  KS_HIP(hipEventRecord(ctx->ev[10], st));
+  KS_TRY(launch_scan_lane(ctx, s->seq, total, rs.a, rs.b, rs.seq, rcap, k, tv, mw, min_score, visits, rb,
+                          rs.count));
+  KS_HIP(hipEventRecord(ctx->ev[11], st));
+  unsigned long long hc[4] = {0, 0, 0, 0};
+  KS_HIP(hipMemcpyAsync(hc, cnts, 32, hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
+
   const unsigned int errbits = (unsigned int)(hc[3] & 0xffffffffu);
-  float ms_p1 = 0;
-  KS_HIP(hipEventElapsedTime(&ms_p1, e_p1a, e_p1b));
-  KS_HIP(hipEventDestroy(e_p1a));
-  KS_HIP(hipEventDestroy(e_p1b));
-  if (errbits) return fail(KS_ERR_INTERNAL, "chunked scan consistency check failed (bits %u)", errbits);
+  if ((errbits & 16u) && !force_fb)
+    fprintf(stderr, "kmer_spans_amd: carry segment check failed; the carry was redone per run\n");
+  if (dbg) {
+    std::vector<long long> h(nwin * 6);
+    KS_HIP(hipMemcpy(h.data(), dbg, nwin * 6 * sizeof(long long), hipMemcpyDeviceToHost));
+    KS_HIP(hipFree(dbg));
+    std::vector<int64_t> idx(nwin);
+    for (int64_t i = 0; i < nwin; ++i) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return h[6 * a] > h[6 * b]; });
+    long long tot[6] = {0, 0, 0, 0, 0, 0};
+    for (int64_t i = 0; i < nwin; ++i)
+      for (int q = 0; q < 6; ++q) tot[q] += h[6 * i + q];
+    fprintf(stderr, "[carry] windows %lld (runs %lld) chunks %lld replays %lld segments %lld L %lld R %lld\n",
+            (long long)nwin, (long long)nruns, tot[1], tot[2], tot[3], tot[4], tot[5]);
+    for (int64_t i = 0; i < std::min<int64_t>(nwin, 8); ++i) {
+      const long long *d = &h[6 * idx[i]];
+      fprintf(stderr, "[carry] window %lld cycles %lld chunks %lld replays %lld segments %lld L %lld R %lld\n",
+              (long long)idx[i], d[0], d[1], d[2], d[3], d[4], d[5]);
+    }
+  }
+  if (errbits & ~16u) return fail(KS_ERR_INTERNAL, "chunked scan consistency check failed (bits %u)", errbits);
+  if ((int64_t)hc[0] > ccap) {  // grow the candidate buffer and rerun the pass
+    void *grown = nullptr;
+    KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)(hc[0] + hc[0] / 4 + 1024) * 40 + 1024, &grown));
+    return KS_INTERNAL_RETRY;
+  }
   if ((int64_t)hc[1] > rcap) return KS_INTERNAL_RETRY;  // regions overflowed too: the caller grows and reruns
-  float ms_all = 0;
-  KS_HIP(hipEventRecord(ctx->ev[6], st));
-  KS_HIP(hipEventSynchronize(ctx->ev[6]));
-  KS_HIP(hipEventElapsedTime(&ms_all, ctx->ev[7], ctx->ev[6]));
-  // rescans: the lane kernel on virtual runs
   const int64_t nres = (int64_t)hc[1];
   if (dbg_on && nres > 0) {  // rescan length histogram (log2 buckets)
     std::vector<int64_t> a(nres), b(nres);
@@ -1442,18 +1631,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, int 
       if (hist[e]) fprintf(stderr, " 2^%d:%lld", e, hist[e]);
     fprintf(stderr, "\n");
   }
-  hipEvent_t e_ra, e_rb;
-  KS_HIP(hipEventCreate(&e_ra));
-  KS_HIP(hipEventCreate(&e_rb));
-  KS_HIP(hipEventRecord(e_ra, st));
-  if (nres > 0) KS_TRY(launch_scan_lane(ctx, s->seq, total, rs.a, rs.b, rs.seq, nres, k, tv, mw, min_score, visits, rb));
-  KS_HIP(hipEventRecord(e_rb, st));
-  KS_HIP(hipEventSynchronize(e_rb));
-  float ms_res = 0;
-  KS_HIP(hipEventElapsedTime(&ms_res, e_ra, e_rb));
-  KS_HIP(hipEventDestroy(e_ra));
-  KS_HIP(hipEventDestroy(e_rb));
   if (stats) {
+    float ms_p1 = 0, ms_all = 0, ms_res = 0;
+    KS_HIP(hipEventElapsedTime(&ms_p1, ctx->ev[8], ctx->ev[9]));
+    KS_HIP(hipEventElapsedTime(&ms_all, ctx->ev[7], ctx->ev[10]));
+    KS_HIP(hipEventElapsedTime(&ms_res, ctx->ev[10], ctx->ev[11]));
     stats->ms_scan = ms_p1;
     stats->ms_rescan = ms_res;
     stats->ms_finish += ms_all - ms_p1;

@@ -172,11 +172,14 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   const Cand cands_f64[] = {{4, 64}, {3, 64}, {2, 64}};
   const Cand *cands = u16 ? cands_u16 : cands_f64;
   const int ncand = u16 ? 4 : 3;
+  const char *jmax_env = getenv("KS_EXT_MAX_J");  // tests: cap J to exercise every table form
+  const int jmax = jmax_env ? atoi(jmax_env) : 5;
   const char *esc_env = getenv("KS_EXT_ESCAPE_MAX");
   const double max_escape = esc_env ? atof(esc_env) : 0.01;
   int J = 0, bits = 16;
   for (int i = 0; i < ncand; ++i) {
     const Cand c = cands[i];
+    if (c.J > jmax) continue;
     const int kx = t->k + c.J - 1;
     if (kx > 17) continue;
     if (!u16 && kx > 16) continue;

@@ -271,12 +271,15 @@ def test_long_drift_run(K, oracle, ctx, k):
     ctx.set_scan_algo(-1)
 
 
-@pytest.mark.parametrize("k,compress", [(3, False), (7, False), (5, True), (10, True)])
-def test_expanded_table_edges(K, oracle, ctx, k, compress):
-    """Expanded tables (FP64 and uint16 entries) on ragged inputs: runs
-    shorter than J, N runs, sequence ends inside a read group."""
+@pytest.mark.parametrize("k,compress,jmax", [(3, False, 5), (7, False, 5), (7, False, 3), (7, False, 2),
+                                             (5, True, 5), (10, True, 5), (10, True, 4), (6, True, 3),
+                                             (11, True, 2)])
+def test_expanded_table_edges(K, oracle, ctx, monkeypatch, k, compress, jmax):
+    """Expanded tables (FP64 and uint16/12-bit entries, every J) on ragged
+    inputs: runs shorter than J, N runs, sequence ends inside a read group."""
     import torch
     from kmer_spans_amd import device as D
+    monkeypatch.setenv("KS_EXT_MAX_J", str(jmax))
     rng = np.random.default_rng(k)
     w = rng.normal(size=4 ** k) - 0.1
     if compress:
@@ -288,7 +291,7 @@ def test_expanded_table_edges(K, oracle, ctx, k, compress):
     ds = D.from_host(seqs, "cuda")
     D.bind_torch_stream(ctx)
     tab = D.DeviceTable(ctx, w, k, 0.05, compress=compress, expand=True)
-    assert tab.positions_per_read >= 2
+    assert tab.positions_per_read == (jmax if compress else min(jmax, 4))
     o = oracle.scan(seqs, k, w, 0.05, 0, 0.5, visits=True)
     for algo in ALGOS:
         ctx.set_scan_algo(algo)

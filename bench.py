@@ -149,8 +149,21 @@ def main():
     achieved = ALGO_BYTES_PER_BASE * n_bases / (ms_kernel * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": "k_scan_lane" if stats[-1]["scan_algo"] == 0 else "k_chunk_pass1",
+                "kernel": "k_scan_lane" if stats[-1]["scan_algo"] == 0 else "k_pass1p",
                 "kernel_ms": round(ms_kernel, 3), "algo_bytes_per_base": ALGO_BYTES_PER_BASE}
+    # HBM traffic per launch of the dominant kernel: rocprofv3 PMC passes of this
+    # same workload (tools/gpu_pmc.sh), committed under profiles/
+    pmc_path = os.path.join(ROOT, "profiles", "r1_pmc_summary.json")
+    if os.path.exists(pmc_path) and stats[-1]["scan_algo"] == 1:
+        pmc = json.load(open(pmc_path))
+        wl = pmc.get("workload", {})
+        if (wl.get("k") == k and wl.get("score") == args.score and wl.get("scale") == args.scale
+                and wl.get("ncontigs") == args.ncontigs and not args.no_expand):
+            for name, cs in pmc.get("kernels", {}).items():
+                if name.startswith("k_pass1") and "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+                    roofline["traffic"] = round((cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1e3)  # KB -> B
+                    roofline["traffic_source"] = f"profiles/r1_pmc_summary.json ({name}, FETCH+WRITE)"
+                    break
 
     # ---- PCIe-inclusive rate of the host entry point (reported, never `value`)
     host_path = None

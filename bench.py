@@ -34,6 +34,16 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 ALGO_BYTES_PER_BASE = 9.0      # 1 B sequence + 8 B FP64 table entry (k >= 8)
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -197,7 +207,7 @@ def main():
         t_cpu = time.perf_counter() - t0
         cpu = {"value": round(acc / t_cpu / 1e9, 5), "unit": "Gbases/s", "cores": 1, "kind": "port",
                "sample": f"oracle/ks_oracle.c scan of {len(ids)} contigs ({acc} bp) of the same genome, same table",
-               "seconds": round(t_cpu, 3)}
+               "seconds": round(t_cpu, 3), "host_cpu": cpu_model(), "host_nproc": os.cpu_count()}
         # parity of the sampled contigs: GPU records vs oracle records
         sel = np.isin(pos[0], ids)
         gp = pos[:, sel].copy()

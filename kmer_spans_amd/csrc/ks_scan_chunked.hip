@@ -792,24 +792,56 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
   unsigned long long replays = 0;
   const long long t_start = dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
   long long n_l = 0, n_r = 0;
-  for (int64_t cb = c0; cb < c1; cb += 64) {
+  // per-lane inputs of one 64-chunk tile; the next tile's are loaded before
+  // the current one is processed (all loads independent: hides their latency
+  // behind the tile's scan)
+  struct TileIn {
+    double exit, pmin, sabs;
+    int spec, n, se;
+    long long D[2], M[2], N[2];
+    int A[2];
+  };
+  auto load_tile = [&](int64_t cb, TileIn &t) {
     const int64_t c = cb + lane;
     const bool live = c < c1;
-    const double l_exit = live ? o.cexit[c] : 0.0;
-    const double l_pmin = live ? o.pmin[c] : 0.0;
-    const double l_sabs = live ? o.sabs[c] : 0.0;
-    const int l_spec = live ? o.special[c] : 1;
-    const int l_n = live ? g.n[c] : 0;
-    const int se = live ? sm.e[c] : INT32_MIN;
+    const int64_t cc = live ? c : c0;  // dead lanes read a valid chunk, values unused
+    t.exit = o.cexit[cc];
+    t.pmin = o.pmin[cc];
+    t.sabs = o.sabs[cc];
+    t.spec = live ? o.special[cc] : 1;
+    t.n = live ? g.n[cc] : 0;
+    const int se = sm.e[cc];
+    t.se = live ? se : INT32_MIN;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      t.D[q] = sm.D[2 * cc + q];
+      t.M[q] = sm.M[2 * cc + q];
+      t.N[q] = sm.N[2 * cc + q];
+      t.A[q] = sm.A[2 * cc + q];
+    }
+  };
+  TileIn cur;
+  load_tile(c0, cur);
+  for (int64_t cb = c0; cb < c1; cb += 64) {
+    TileIn nxt = cur;
+    if (cb + 64 < c1) load_tile(cb + 64, nxt);
+    const int64_t c = cb + lane;
+    const bool live = c < c1;
+    const double l_exit = live ? cur.exit : 0.0;
+    const double l_pmin = live ? cur.pmin : 0.0;
+    const double l_sabs = live ? cur.sabs : 0.0;
+    const int l_spec = cur.spec;
+    const int l_n = cur.n;
+    const int se = cur.se;
     long long D[2] = {0, 0}, M[2] = {0, 0}, N[2] = {0, 0};
     int A[2] = {0, 0};
     if (se != INT32_MIN) {
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        D[t] = sm.D[2 * c + t];
-        M[t] = sm.M[2 * c + t];
-        N[t] = sm.N[2 * c + t];
-        A[t] = sm.A[2 * c + t];
+        D[t] = cur.D[t];
+        M[t] = cur.M[t];
+        N[t] = cur.N[t];
+        A[t] = cur.A[t];
       }
     }
     const int nb = (int)min((int64_t)64, c1 - cb);
@@ -926,6 +958,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
         cr.harg[c] = my_harg;
       }
     }
+    cur = nxt;
   }
   if (lane == 0 && replays) atomicAdd(nreplay, replays);
   if (lane == 0 && c1 < g.nch && g.run[c1] == g.run[c1 - 1] &&

@@ -143,13 +143,19 @@ struct RunLayout {
 ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay);
 
 // Region record buffer written by scan kernels.
+// Append buffers (regions, rescans, candidates) are split into kSegs
+// segments of segcap slots, each with its own counter, so that appends from
+// thousands of waves do not serialise on one address; slot s*segcap + i.
+constexpr int kSegs = 64;
+
 struct RegionBuf {
   int32_t *seq;
   int64_t *beg;
   int64_t *end;
   double *score;
-  unsigned long long *count;  // device counter
-  int64_t cap;
+  unsigned long long *count;  // [kSegs] device counters
+  int64_t cap;                // kSegs * segcap
+  int64_t segcap;
 };
 
 // Launch wrappers (defined in the .hip files).

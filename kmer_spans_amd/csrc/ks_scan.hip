@@ -27,7 +27,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
 ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const int64_t *ra, const int64_t *rb,
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
-                           const unsigned long long *d_n = nullptr);
+                           const unsigned long long *d_cnt = nullptr, int64_t segcap = 0);
 
 namespace {
 
@@ -43,13 +43,13 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
                                                   const int32_t *__restrict__ rseq, int64_t nruns,
                                                   int k, TableView tv, uint64_t mw, double min_score,
                                                   uint32_t *__restrict__ visits, RegionBuf out,
-                                                  const unsigned long long *__restrict__ d_n) {
+                                                  const unsigned long long *__restrict__ d_cnt, int64_t segcap) {
   constexpr int G = (J == 1) ? 16 : (J >= 4 ? 4 : (J == 3 ? 6 : 8));  // reads per batch
   constexpr int PB = G * J;                                           // indices per batch (16, 16, 18, 16, 20)
   using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;  // (k+J-1)-mer code
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (d_n && (int64_t)*d_n < nruns) nruns = (int64_t)*d_n;  // count known on the device only
   if (r >= nruns) return;
+  if (d_cnt && (r % segcap) >= (int64_t)d_cnt[r / segcap]) return;  // segmented list: unused slot
   const int64_t a = ra[r], b = rbnd[r];
   if (b - a <= k) return;
   const int32_t sid = rseq[r];
@@ -114,13 +114,24 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
   }
 }
 
-__global__ void k_region_keys(const int64_t *__restrict__ beg, int64_t n, unsigned long long *__restrict__ keys,
-                              int32_t *__restrict__ idx) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    keys[i] = (unsigned long long)beg[i];
-    idx[i] = (int32_t)i;
+// Compacted index j -> slot of the segmented region buffer.
+struct SegPrefix {
+  int64_t p[kSegs + 1];
+  int64_t segcap;
+};
+
+__global__ void k_region_keys(const int64_t *__restrict__ beg, int64_t n, SegPrefix pre,
+                              unsigned long long *__restrict__ keys, int32_t *__restrict__ idx) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  int lo = 0, hi = kSegs - 1;  // segment with p[s] <= j < p[s + 1]
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pre.p[mid] <= j) lo = mid; else hi = mid - 1;
   }
+  const int64_t slot = (int64_t)lo * pre.segcap + (j - pre.p[lo]);
+  keys[j] = (unsigned long long)beg[slot];
+  idx[j] = (int32_t)slot;
 }
 
 // Regions in (seq_id, beg) order == global begin order; local coordinates.
@@ -149,12 +160,12 @@ __global__ void k_add_hist(uint32_t *__restrict__ dst, const uint32_t *__restric
 ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const int64_t *ra, const int64_t *rb,
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
-                           const unsigned long long *d_n) {
+                           const unsigned long long *d_cnt, int64_t segcap) {
   if (n <= 0) return KS_OK;
   const int J = tv.ext ? tv.ext_J : 1;
 #define KS_LANE(J, C)                                                                                   \
   hipLaunchKernelGGL((k_scan_lane<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, total, \
-                     ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_n)
+                     ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap)
   if (tv.compressed) {
     if (J == 5) KS_LANE(5, true); else if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
   } else {
@@ -196,18 +207,29 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
   S->scan_algo = algo;
 
   // region capacity: what the (grow-only) slot already holds, so that the
-  // slot is not reallocated on every call
+  // slot is not reallocated on every call; kSegs segments of segcap slots
   const size_t reg_bytes = ctx->slots[SLOT_REGIONS].bytes;
-  int64_t cap = std::max<int64_t>(std::max<int64_t>(65536, scored / 2048),
-                                  reg_bytes > 64 ? (int64_t)((reg_bytes - 64) / 28) : 0);
-  unsigned long long n_reg = 0;
+  int64_t segcap = std::max<int64_t>(std::max<int64_t>(65536, scored / 2048),
+                                     reg_bytes > 64 ? (int64_t)((reg_bytes - 64) / 28) : 0) / kSegs;
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
-  unsigned long long *d_rcount = reinterpret_cast<unsigned long long *>(scal) + 2;
+  unsigned long long *d_rcount = reinterpret_cast<unsigned long long *>(scal) + 16;  // [kSegs]
+  std::vector<unsigned long long> hcnt(kSegs, 0);
+  auto read_counts = [&]() -> ks_status {  // -> hcnt; sync
+    KS_HIP(hipMemcpyAsync(hcnt.data(), d_rcount, 8 * kSegs, hipMemcpyDeviceToHost, st));
+    KS_HIP(hipStreamSynchronize(st));
+    return KS_OK;
+  };
+  auto max_count = [&]() {
+    unsigned long long m = 0;
+    for (auto c : hcnt) m = std::max(m, c);
+    return (int64_t)m;
+  };
   RegionBuf rb{};
   uint32_t *vis = reinterpret_cast<uint32_t *>(visits_dev);
   bool complete = false;
   for (int attempt = 0; attempt < 4 && !complete; ++attempt) {
+    const int64_t cap = segcap * kSegs;
     void *rp = nullptr;
     KS_TRY(ensure(ctx, SLOT_REGIONS, (size_t)cap * 28 + 64, &rp));
     rb.beg = reinterpret_cast<int64_t *>(rp);
@@ -216,7 +238,8 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     rb.seq = reinterpret_cast<int32_t *>(rb.score + cap);
     rb.count = d_rcount;
     rb.cap = cap;
-    KS_HIP(hipMemsetAsync(d_rcount, 0, 8, st));
+    rb.segcap = segcap;
+    KS_HIP(hipMemsetAsync(d_rcount, 0, 8 * kSegs, st));
     KS_HIP(hipEventRecord(ctx->ev[3], st));
     if (algo == 1) {
       // visits of the chunked path go to a scratch histogram first, so that a
@@ -230,10 +253,10 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
         KS_HIP(hipMemsetAsync(vscr, 0, nb, st));
       }
       ks_status rc = scan_chunked(ctx, s, runs, lay, k, tv, mw, min_score, vscr, rb, S);
-      if (rc == KS_INTERNAL_RETRY) {  // rescans did not fit: grow, rerun, visits untouched
-        KS_HIP(hipMemcpyAsync(&n_reg, d_rcount, 8, hipMemcpyDeviceToHost, st));
-        KS_HIP(hipStreamSynchronize(st));
-        if ((int64_t)n_reg > cap) cap = (int64_t)n_reg + 1024;
+      if (rc == KS_INTERNAL_RETRY) {  // a buffer did not fit: grow, rerun, visits untouched
+        KS_TRY(read_counts());
+        const int64_t m = max_count();
+        if (m > segcap) segcap = m + m / 4 + 64;
         continue;
       }
       if (rc == KS_OK) {
@@ -247,7 +270,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
         fprintf(stderr, "kmer_spans_amd: chunked scan fell back to the lane kernel: %s\n", ks_last_error());
         algo = 0;
         S->scan_algo = 0;
-        KS_HIP(hipMemsetAsync(d_rcount, 0, 8, st));
+        KS_HIP(hipMemsetAsync(d_rcount, 0, 8 * kSegs, st));
       } else {
         return rc;
       }
@@ -256,16 +279,16 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
       if (runs.n) KS_TRY(launch_scan_lane(ctx, s->seq, total, runs.a, runs.b, runs.seq, runs.n, k, tv, mw, min_score, vis, rb));
     }
     KS_HIP(hipEventRecord(ctx->ev[4], st));
-    KS_HIP(hipMemcpyAsync(&n_reg, d_rcount, 8, hipMemcpyDeviceToHost, st));
-    KS_HIP(hipStreamSynchronize(st));
+    KS_TRY(read_counts());
     float ms = 0;
     KS_HIP(hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[4]));
     if (algo == 0) S->ms_scan = ms;
-    if ((int64_t)n_reg <= cap) {
+    const int64_t m = max_count();
+    if (m <= segcap) {
       complete = true;
       break;
     }
-    cap = (int64_t)n_reg + 1024;
+    segcap = m + m / 4 + 64;
     vis = nullptr;  // visits were complete on the first pass
   }
   if (!complete) return fail(KS_ERR_INTERNAL, "region buffer overflow");
@@ -273,7 +296,11 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
   // Order regions by global begin == (seq_id, beg) on the device (radix sort),
   // convert to sequence-local coordinates, copy out.
   KS_HIP(hipEventRecord(ctx->ev[5], st));
-  const int64_t n = (int64_t)n_reg;
+  SegPrefix pre;
+  pre.p[0] = 0;
+  for (int q = 0; q < kSegs; ++q) pre.p[q + 1] = pre.p[q] + (int64_t)hcnt[q];
+  pre.segcap = segcap;
+  const int64_t n = pre.p[kSegs];
   out->n = n;
   out->seq_id = (int32_t *)malloc(std::max<int64_t>(n, 1) * 4);
   out->beg = (int32_t *)malloc(std::max<int64_t>(n, 1) * 4);
@@ -296,7 +323,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     int32_t *o_end = o_beg + nn;
     double *o_score = reinterpret_cast<double *>((reinterpret_cast<uintptr_t>(o_end + nn) + 7) & ~(uintptr_t)7);
     const unsigned g = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(k_region_keys, dim3(g), dim3(256), 0, st, rb.beg, n, k_in, v_in);
+    hipLaunchKernelGGL(k_region_keys, dim3(g), dim3(256), 0, st, rb.beg, n, pre, k_in, v_in);
     KS_HIP(hipGetLastError());
     int end_bit = 1;
     while (end_bit < 64 && ((unsigned long long)total >> end_bit)) ++end_bit;

@@ -41,7 +41,7 @@ namespace ks {
 ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const int64_t *ra, const int64_t *rb,
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
-                           const unsigned long long *d_n = nullptr);
+                           const unsigned long long *d_cnt = nullptr, int64_t segcap = 0);
 
 namespace {
 
@@ -76,18 +76,18 @@ struct Carry {  // P3/P4
   int32_t *harg;
 };
 
-struct Cand {  // closed emittable excursions of the clean trajectories
+struct Cand {  // closed emittable excursions of the clean trajectories (segmented append)
   long long *beg, *arg, *rst;
   double *best;
-  unsigned long long *count;
-  int64_t cap;
+  unsigned long long *count;  // [kSegs]
+  int64_t cap, segcap;
 };
 
 struct Rescan {
-  int64_t *a, *b;  // virtual runs [a, b) for the lane kernel
+  int64_t *a, *b;  // virtual runs [a, b) for the lane kernel (segmented append)
   int32_t *seq;
-  unsigned long long *count;
-  int64_t cap;
+  unsigned long long *count;  // [kSegs]
+  int64_t cap, segcap;
 };
 
 __device__ __forceinline__ uint32_t roll(uint32_t c, uint8_t b, uint32_t mask) {
@@ -128,7 +128,7 @@ __device__ __forceinline__ void load_codes16(const uint16_t *__restrict__ codes,
 
 // Values of scan indices i0 .. i0+3 of chunk c (0 past n): one 8-byte code
 // load (compressed) or one k-mer prime plus three rolls.
-__device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restrict__ seq, int k,
+__device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
                                         const TableView &tv, const uint16_t *__restrict__ codes, int64_t c,
                                         int i0, int n, double v[4]) {
 #pragma unroll
@@ -143,6 +143,16 @@ __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restri
     return;
   }
   const int64_t p = g.start[c] + i0;
+  if (tv.ext && tv.ext_J == 4) {  // FP64 expanded table: the 4 values in one 32-B entry
+    const uint64_t gcode = prime_code_guarded64(seq, p - k, k + 3, total);
+    const double2 *E = reinterpret_cast<const double2 *>(tv.ext);
+    const double2 e0 = E[2 * gcode], e1 = E[2 * gcode + 1];
+    const double ev[4] = {e0.x, e0.y, e1.x, e1.y};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (i0 + q < n) v[q] = ev[q];
+    return;
+  }
   const uint32_t mask = (1u << (2 * k)) - 1u;
   uint32_t code = prime_code(seq, p - k, k);
   v[0] = tv_get(tv, code);
@@ -300,8 +310,8 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
           beg = i; arg = i; best = S;
         } else if (prev > 0 && S == 0) {
           if ((uint64_t)(arg - beg) >= mw && best >= min_score) {
-            const unsigned long long slot = atomicAdd(cand.count, 1ull);
-            if ((int64_t)slot < cand.cap) {
+            const int64_t slot = append_one(cand.count, cand.segcap);
+            if (slot >= 0) {
               cand.beg[slot] = start + beg;
               cand.arg[slot] = start + arg;
               cand.rst[slot] = start + i;
@@ -454,8 +464,8 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
             beg = i; arg = i; best = S;
           } else if (prev > 0 && S == 0) {
             if ((uint64_t)(arg - beg) >= mw && best >= min_score) {
-              const unsigned long long slot = atomicAdd(cand.count, 1ull);
-              if ((int64_t)slot < cand.cap) {
+              const int64_t slot = append_one(cand.count, cand.segcap);
+              if (slot >= 0) {
                 cand.beg[slot] = start + beg;
                 cand.arg[slot] = start + arg;
                 cand.rst[slot] = start + i;
@@ -613,6 +623,27 @@ __device__ int chunk_summary_fast(const Chunks &g, const uint8_t *__restrict__ s
       for (int j = 0; j < NB; ++j) {
         const uint32_t q = (w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
         v[j] = kLds ? s_lut[q] : tv.lut[q];
+      }
+    } else if (tv.ext && tv.ext_J == 4) {  // FP64 expanded table: 4 values per 32-B read
+      uint8_t by[16];
+      load16(seq, start + b0, total, by);
+      const double2 *E = reinterpret_cast<const double2 *>(tv.ext);
+#pragma unroll
+      for (int gq = 0; gq < NB / 4; ++gq) {
+        // (k+3)-mer of indices b0+4gq .. +3: the k-mer of the first, then 3 bytes
+        const uint64_t gx = ((uint64_t)code << 6) | ((uint64_t)enc(by[4 * gq]) << 4) |
+                            ((uint64_t)enc(by[4 * gq + 1]) << 2) | (uint64_t)enc(by[4 * gq + 2]);
+        double2 e0 = make_double2(0.0, 0.0), e1 = e0;
+        if (b0 + 4 * gq < n) {
+          e0 = E[2 * gx];
+          e1 = E[2 * gx + 1];
+        }
+        v[4 * gq] = e0.x;
+        v[4 * gq + 1] = e0.y;
+        v[4 * gq + 2] = e1.x;
+        v[4 * gq + 3] = e1.y;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) code = roll(code, by[4 * gq + t], mask);
       }
     } else {
       uint8_t by[16];
@@ -922,7 +953,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
         const int64_t cj = cb + j;
         const int n = rl32(l_n, j);
         double v[4];
-        values4(g, seq, k, tv, kCompressed ? codes : nullptr, cj, 4 * lane, n, v);
+        values4(g, seq, total, k, tv, kCompressed ? codes : nullptr, cj, 4 * lane, n, v);
         double T = x, hmax = -1.0;
         int hq = -1, harg = 0;
         for (int i = 0; i < 64 && hq < 0; ++i) {
@@ -1137,8 +1168,8 @@ __device__ __forceinline__ void emit(const RegionBuf &rb, const Rescan &rs, int3
                                      int64_t arg, double best, int64_t end) {
   push_region(rb, sid, beg, arg, best);
   if (arg + 1 <= end) {
-    const unsigned long long slot = atomicAdd(rs.count, 1ull);
-    if ((int64_t)slot < rs.cap) {
+    const int64_t slot = append_one(rs.count, rs.segcap);
+    if (slot >= 0) {
       rs.a[slot] = arg + 1 - k;  // virtual run: scan indices arg+1 .. end
       rs.b[slot] = end + 1;
       rs.seq[slot] = sid;
@@ -1157,17 +1188,19 @@ __device__ __forceinline__ void emit_wave(bool want, const RegionBuf &rb, const 
   const unsigned long long mr = __ballot(wr);
   const int lane = (int)(threadIdx.x & 63);
   const int leader = __ffsll((long long)m) - 1;
+  const int sg = append_seg();
   unsigned long long base = 0, rbase = 0;
   if (lane == leader) {
-    base = atomicAdd(rb.count, (unsigned long long)__popcll(m));
-    if (mr) rbase = atomicAdd(rs.count, (unsigned long long)__popcll(mr));
+    base = atomicAdd(&rb.count[sg], (unsigned long long)__popcll(m));
+    if (mr) rbase = atomicAdd(&rs.count[sg], (unsigned long long)__popcll(mr));
   }
   base = __shfl(base, leader, 64);
   rbase = __shfl(rbase, leader, 64);
   const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   if (want) {
-    const unsigned long long slot = base + (unsigned long long)__popcll(m & below);
-    if ((int64_t)slot < rb.cap) {
+    const unsigned long long i = base + (unsigned long long)__popcll(m & below);
+    if ((int64_t)i < rb.segcap) {
+      const int64_t slot = (int64_t)sg * rb.segcap + (int64_t)i;
       rb.seq[slot] = sid;
       rb.beg[slot] = beg;
       rb.end[slot] = arg;
@@ -1175,8 +1208,9 @@ __device__ __forceinline__ void emit_wave(bool want, const RegionBuf &rb, const 
     }
   }
   if (wr) {
-    const unsigned long long slot = rbase + (unsigned long long)__popcll(mr & below);
-    if ((int64_t)slot < rs.cap) {
+    const unsigned long long i = rbase + (unsigned long long)__popcll(mr & below);
+    if ((int64_t)i < rs.segcap) {
+      const int64_t slot = (int64_t)sg * rs.segcap + (int64_t)i;
       rs.a[slot] = arg + 1 - k;
       rs.b[slot] = end + 1;
       rs.seq[slot] = sid;
@@ -1394,15 +1428,13 @@ __global__ void __launch_bounds__(64) k_stitch_emit(Chunks g, const int64_t *__r
 // valid when they begin at or after their chunk's valid_from.
 __global__ void k_candidates(Chunks g, const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase,
                              int64_t nruns, const int32_t *__restrict__ rseq, int k, Cand cand,
-                             const unsigned long long *__restrict__ d_ncand, Carry cr, RegionBuf out, Rescan rs) {
-  const int64_t ncand = min((int64_t)*d_ncand, cand.cap);
+                             Carry cr, RegionBuf out, Rescan rs) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if ((int64_t)blockIdx.x * blockDim.x >= ncand) return;  // whole block idle
   bool want = false;
   int64_t b = 0, arg = 0, rst = 0;
   double best = 0.0;
   int32_t sid = 0;
-  if (i < ncand) {
+  if (i < cand.cap && (i % cand.segcap) < (int64_t)cand.count[i / cand.segcap]) {
     b = cand.beg[i];
     int64_t lo = 0, hi = nruns - 1;  // last run with ra <= b
     while (lo < hi) {
@@ -1451,7 +1483,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const size_t o_mode = off; off += al(nch);
   const size_t o_hq = off; off += al(nch * 4 * 2);
   const size_t o_hmax = off; off += al(nch * 8);
-  const size_t o_cnt = off; off += al(64);
+  const size_t o_cnt = off; off += al(8 * (2 * kSegs + 8));
   const size_t o_flag = off; off += al(nch + 64);
   const size_t o_xagg = off; off += al(ntiles * 32) * 2;
   void *wsp = nullptr;
@@ -1478,9 +1510,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                   reinterpret_cast<double *>(p + ntiles * 24)};
   };
   const XTiles xagg = xtiles(W + o_xagg), xtin = xtiles(W + o_xagg + al(ntiles * 32));
-  // cnts: [0] candidates, [1] rescans, [2] replays, [3] error bits (u32)
-  KS_HIP(hipMemsetAsync(cnts, 0, 64, st));
-  unsigned int *d_err = reinterpret_cast<unsigned int *>(cnts + 3);
+  // cnts: [0, kSegs) candidate counters, [kSegs, 2 kSegs) rescan counters,
+  // [2 kSegs] replays, [2 kSegs + 1] error bits (u32)
+  KS_HIP(hipMemsetAsync(cnts, 0, 8 * (2 * kSegs + 8), st));
+  unsigned long long *d_replays = cnts + 2 * kSegs;
+  unsigned int *d_err = reinterpret_cast<unsigned int *>(cnts + 2 * kSegs + 1);
 
   uint16_t *codes = nullptr;
   if (comp) {
@@ -1492,16 +1526,19 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   int64_t ccap = std::max<int64_t>(1 << 16, nch / 4);
   const size_t cand_bytes = ctx->slots[SLOT_CHUNK_C].bytes;  // use what the grow-only slot holds
   if (cand_bytes > 1024 && (cand_bytes - 1024) / 40 > (size_t)ccap) ccap = (int64_t)((cand_bytes - 1024) / 40);
+  const int64_t csegcap = ccap / kSegs;
+  ccap = csegcap * kSegs;
   void *cbuf = nullptr;
   KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)ccap * 40 + 1024, &cbuf));
   Cand cand{reinterpret_cast<long long *>(cbuf), reinterpret_cast<long long *>(cbuf) + ccap,
             reinterpret_cast<long long *>(cbuf) + 2 * ccap, reinterpret_cast<double *>(cbuf) + 3 * ccap,
-            cnts, ccap};
-  const int64_t rcap = std::max<int64_t>(rb.cap, 4096);
+            cnts, ccap, csegcap};
+  const int64_t rcap = rb.cap;  // a rescan accompanies a region in the same segment
   void *rsb = nullptr;
   KS_TRY(ensure(ctx, SLOT_WORK_A, (size_t)rcap * 20 + 1024, &rsb));
   Rescan rs{reinterpret_cast<int64_t *>(rsb), reinterpret_cast<int64_t *>(rsb) + rcap,
-            reinterpret_cast<int32_t *>(reinterpret_cast<int64_t *>(rsb) + 2 * rcap), cnts + 1, rcap};
+            reinterpret_cast<int32_t *>(reinterpret_cast<int64_t *>(rsb) + 2 * rcap), cnts + kSegs, rcap,
+            rb.segcap};
   // KS_DEBUG_CARRY=1: per-window carry statistics to stderr (diagnostics only)
   static const bool dbg_on = getenv("KS_DEBUG_CARRY") != nullptr;
   long long *dbg = nullptr;
@@ -1566,10 +1603,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // ---- P3 carry by segments + P4 heads; then the gated per-run fallback
   if (comp)
     hipLaunchKernelGGL(k_carry_win<true>, dim3((unsigned)nwin), dim3(64), 0, st, g, d_flag, s->seq, total, k, tv,
-                       codes, p1, sm, cr, cnts + 2, d_err, dbg);
+                       codes, p1, sm, cr, d_replays, d_err, dbg);
   else
     hipLaunchKernelGGL(k_carry_win<false>, dim3((unsigned)nwin), dim3(64), 0, st, g, d_flag, s->seq, total, k, tv,
-                       codes, p1, sm, cr, cnts + 2, d_err, dbg);
+                       codes, p1, sm, cr, d_replays, d_err, dbg);
   KS_HIP(hipGetLastError());
 #define KS_HEADS(J, C, GATED)                                                                                 \
   hipLaunchKernelGGL((k_heads<J, C>), dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, cr, d_err, \
@@ -1586,13 +1623,13 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   KS_HIP(hipGetLastError());
   // KS_TEST_SEG_FALLBACK=1 forces the fallback path (tests)
   const int force_fb = getenv("KS_TEST_SEG_FALLBACK") != nullptr ? 1 : 0;
-  hipLaunchKernelGGL(k_fallback_prep, dim3(1), dim3(1), 0, st, d_err, cnts + 2, force_fb);
+  hipLaunchKernelGGL(k_fallback_prep, dim3(1), dim3(1), 0, st, d_err, d_replays, force_fb);
   if (comp)
     hipLaunchKernelGGL(k_carry_run<true>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, total,
-                       k, tv, codes, p1, sm, cr, cnts + 2, d_err, nullptr);
+                       k, tv, codes, p1, sm, cr, d_replays, d_err, nullptr);
   else
     hipLaunchKernelGGL(k_carry_run<false>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, total,
-                       k, tv, codes, p1, sm, cr, cnts + 2, d_err, nullptr);
+                       k, tv, codes, p1, sm, cr, d_replays, d_err, nullptr);
   heads(1);
   KS_HIP(hipGetLastError());
 
@@ -1607,15 +1644,23 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                      p1, cr, mw, min_score, xtin, rb, rs, d_err);
   KS_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_candidates, dim3((unsigned)((ccap + 255) / 256)), dim3(256), 0, st, g, runs.a, d_cbase,
-                     nruns, runs.seq, k, cand, cnts, cr, rb, rs);
+                     nruns, runs.seq, k, cand, cr, rb, rs);
   KS_HIP(hipGetLastError());
   KS_HIP(hipEventRecord(ctx->ev[10], st));
   KS_TRY(launch_scan_lane(ctx, s->seq, total, rs.a, rs.b, rs.seq, rcap, k, tv, mw, min_score, visits, rb,
-                          rs.count));
+                          rs.count, rs.segcap));
   KS_HIP(hipEventRecord(ctx->ev[11], st));
-  unsigned long long hc[4] = {0, 0, 0, 0};
-  KS_HIP(hipMemcpyAsync(hc, cnts, 32, hipMemcpyDeviceToHost, st));
+  std::vector<unsigned long long> hcv(2 * kSegs + 2);
+  KS_HIP(hipMemcpyAsync(hcv.data(), cnts, 8 * (2 * kSegs + 2), hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
+  unsigned long long cand_max = 0, res_max = 0, res_tot = 0;
+  for (int q = 0; q < kSegs; ++q) {
+    cand_max = std::max(cand_max, hcv[q]);
+    res_max = std::max(res_max, hcv[kSegs + q]);
+    res_tot += std::min<unsigned long long>(hcv[kSegs + q], (unsigned long long)rs.segcap);
+  }
+  // hc: [0] largest candidate segment, [1] rescans, [2] replays, [3] error bits
+  const unsigned long long hc[4] = {cand_max, res_tot, hcv[2 * kSegs], hcv[2 * kSegs + 1]};
 
   const unsigned int errbits = (unsigned int)(hc[3] & 0xffffffffu);
   if ((errbits & 16u) && !force_fb)
@@ -1639,19 +1684,21 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     }
   }
   if (errbits & ~16u) return fail(KS_ERR_INTERNAL, "chunked scan consistency check failed (bits %u)", errbits);
-  if ((int64_t)hc[0] > ccap) {  // grow the candidate buffer and rerun the pass
+  if ((int64_t)cand_max > csegcap) {  // grow the candidate buffer and rerun the pass
     void *grown = nullptr;
-    KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)(hc[0] + hc[0] / 4 + 1024) * 40 + 1024, &grown));
+    const size_t seg = (size_t)(cand_max + cand_max / 4 + 64);
+    KS_TRY(ensure(ctx, SLOT_CHUNK_C, seg * kSegs * 40 + 1024, &grown));
     return KS_INTERNAL_RETRY;
   }
-  if ((int64_t)hc[1] > rcap) return KS_INTERNAL_RETRY;  // regions overflowed too: the caller grows and reruns
+  if ((int64_t)res_max > rs.segcap) return KS_INTERNAL_RETRY;  // regions overflowed too: the caller grows
   const int64_t nres = (int64_t)hc[1];
   if (dbg_on && nres > 0) {  // rescan length histogram (log2 buckets)
-    std::vector<int64_t> a(nres), b(nres);
-    KS_HIP(hipMemcpy(a.data(), rs.a, nres * 8, hipMemcpyDeviceToHost));
-    KS_HIP(hipMemcpy(b.data(), rs.b, nres * 8, hipMemcpyDeviceToHost));
+    std::vector<int64_t> a(rcap), b(rcap);
+    KS_HIP(hipMemcpy(a.data(), rs.a, rcap * 8, hipMemcpyDeviceToHost));
+    KS_HIP(hipMemcpy(b.data(), rs.b, rcap * 8, hipMemcpyDeviceToHost));
     long long hist[40] = {0}, tot = 0, mx = 0;
-    for (int64_t i = 0; i < nres; ++i) {
+    for (int64_t i = 0; i < rcap; ++i) {
+      if ((i % rs.segcap) >= (int64_t)hcv[kSegs + i / rs.segcap]) continue;
       const long long L = b[i] - a[i] - k;
       tot += L;
       mx = std::max(mx, L);

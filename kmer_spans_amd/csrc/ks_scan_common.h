@@ -61,12 +61,24 @@ __device__ __forceinline__ void gather_group(const TableView &t, GC gcode, uint3
   }
 }
 
-// Append one region record (global coordinates); drops it (but counts it)
-// when the buffer is full so the host can retry with a larger one.
+// Segment of the append buffers used by the calling wave.
+__device__ __forceinline__ int append_seg() {
+  return (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kSegs - 1));
+}
+
+// Slot for one appended element, or -1 when its segment is full (the
+// element is still counted so the host can retry with larger segments).
+__device__ __forceinline__ int64_t append_one(unsigned long long *count, int64_t segcap) {
+  const int s = append_seg();
+  const unsigned long long i = atomicAdd(&count[s], 1ull);
+  return (int64_t)i < segcap ? (int64_t)s * segcap + (int64_t)i : -1;
+}
+
+// Append one region record (global coordinates).
 __device__ __forceinline__ void push_region(const RegionBuf &rb, int32_t seq, int64_t beg, int64_t end,
                                             double score) {
-  const unsigned long long slot = atomicAdd(rb.count, 1ull);
-  if ((int64_t)slot < rb.cap) {
+  const int64_t slot = append_one(rb.count, rb.segcap);
+  if (slot >= 0) {
     rb.seq[slot] = seq;
     rb.beg[slot] = beg;
     rb.end[slot] = end;

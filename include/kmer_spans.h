@@ -106,6 +106,20 @@ ks_status ks_low_comp_regions(ks_ctx *ctx, const char *const *seqs, const int64_
                               double thr, int32_t *counts, double *ranks, double *n,
                               ks_regions *out);
 
+/* tr_lr_regions_r(seq_r, params_r = (k, min_length), kmers_r, kmer_scores_r,
+ * trans_scores_r) -- replaces kmer_spans.c:649-713 (find_kmer_tr_lr_regions
+ * :329-395).  kmers[i] spells the k-mer of entry i of kmer_scores and
+ * trans_scores (n_scores = 4^k entries, user order); they are remapped to
+ * 2-bit code order as the reference does (:677-690; entries no string maps
+ * to are 0 here, uninitialised there).  spectra (optional, 2 x 4^k,
+ * column-major) receives the remapped kmer then transition scores.  Regions
+ * are 1-based like the reference's: seq_id = sequence index + 1, beg and end
+ * = 1 + region begin / max position, score = region maximum. */
+ks_status ks_tr_lr_regions(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq,
+                           int32_t k, int32_t min_length, const char *const *kmers,
+                           const double *kmer_scores, const double *trans_scores, int64_t n_scores,
+                           double *spectra, ks_regions *out);
+
 /* kmer_seq_r(k_r) -- replaces kmer_spans.c:623-639.  out: 4^k * (k+1) bytes,
  * NUL-terminated k-char strings in internal code order. Host only. */
 ks_status ks_kmer_seq(int32_t k, char *out, size_t out_len);
@@ -195,6 +209,14 @@ typedef struct ks_scan_stats {
 ks_status ks_scan_dev(ks_ctx *ctx, const ks_dev_seqs *seqs, int32_t k, const ks_table *table,
                       int32_t min_width, double min_score, int32_t *visits_dev,
                       ks_regions *out, ks_scan_stats *stats);
+
+/* tr_lr scan of device-resident sequences: trans = transition scores, init
+ * = first-k-mer scores, both ks_tables in 2-bit code order built with
+ * threshold 0 (init without KS_TABLE_COMPRESS).  Tables with non-finite
+ * values are scanned by the literal per-run kernel (the reference keeps NaN
+ * through its clamp); all others by the chunked scan. */
+ks_status ks_tr_lr_dev(ks_ctx *ctx, const ks_dev_seqs *seqs, int32_t k, const ks_table *trans,
+                       const ks_table *init, int32_t min_length, ks_regions *out, ks_scan_stats *stats);
 
 /* k-mer counting of device-resident sequences into counts_dev (int32[4^k],
  * accumulated: the caller zeroes it).  *n_words as in ks_kmer_counts. */

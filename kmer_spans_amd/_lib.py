@@ -51,7 +51,7 @@ EXPORTS = [
     "ks_low_comp_regions", "ks_kmer_seq", "ks_rank_table", "ks_log2_table", "ks_pm1_table",
     "ks_table_create", "ks_table_destroy", "ks_table_is_compressed", "ks_table_distinct",
     "ks_table_positions_per_read", "ks_table_create_hint", "ks_table_code_bits", "ks_table_escape_fraction",
-    "ks_scan_dev", "ks_count_dev", "ks_ctx_set_scan_algo",
+    "ks_scan_dev", "ks_count_dev", "ks_ctx_set_scan_algo", "ks_tr_lr_regions", "ks_tr_lr_dev",
 ]
 
 _lib = None
@@ -92,6 +92,8 @@ def load():
         "ks_table_escape_fraction": ([P], D),
         "ks_scan_dev": ([P, P, I32, P, I32, D, P, P, P], I32),
         "ks_count_dev": ([P, P, I32, P, P], I32),
+        "ks_tr_lr_regions": ([P, P, P, I32, I32, I32, P, P, P, I64, P, P], I32),
+        "ks_tr_lr_dev": ([P, P, I32, P, P, I32, P, P], I32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -7,6 +7,7 @@ layout and error behaviour as /root/reference/kmer_spans.R:
   kmer_regions(seq, k, kmer_scores, min_width, min_score)   :41-52
   kmer_low_comp_regions(seq, k, min_w, min_score, thr=0.75) :72-79
   kmer_seq(k)                                     :84-86
+  lr_regions(seq, params, kmers, kmer_scores, trans_scores)  :88-99
 
 Sequences are a str/bytes or a list of them (R character vectors).  Results
 come from libkmerspans.so on the GPU; nothing here computes a result on the
@@ -133,6 +134,33 @@ def kmer_low_comp_regions(seq, k: int, min_w: int, min_score: float, thr: float 
                                      ranks.ctypes.data, n.ctypes.data, C.byref(r)))
     pos, score = regions_to_numpy(r)
     return {"n": n, "counts": counts, "w_rank": ranks, "pos": pos.T.copy(), "score": score.T.copy()}
+
+
+def lr_regions(seq, params, kmers, kmer_scores, trans_scores, device: int = 0) -> dict:
+    """lr.regions (kmer_spans.R:88-99) -> tr_lr_regions_r (kmer_spans.c:649-713):
+    {'kmer_scores': float64[4^k, 2] (the scores remapped to 2-bit code order,
+    rows named by kmer_seq(k)), 'reg': {'seq_i', 'beg', 'end', 'score', 'null'}}
+    with 1-based sequence indices and positions, as the reference returns them.
+    params = (k, min_length); kmers[i] spells entry i of both score vectors."""
+    if len(params) != 2:
+        raise KmerSpansError("params_r should have two integers (k, and min_length)")
+    k, min_length = int(params[0]), int(params[1])
+    hs = _HostSeqs(seq)
+    ks_in = np.ascontiguousarray(kmer_scores, dtype=np.float64).ravel()
+    tr_in = np.ascontiguousarray(trans_scores, dtype=np.float64).ravel()
+    n = len(kmers)
+    if ks_in.size != n or tr_in.size != n:
+        raise KmerSpansError("kmers_r, freq_a, freq_b should all be 4^k long")
+    bufs = [C.create_string_buffer(x.encode("latin-1") if isinstance(x, str) else bytes(x)) for x in kmers]
+    kptrs = (C.c_char_p * max(n, 1))(*[C.cast(b, C.c_char_p) for b in bufs])
+    nk = 4 ** k if 1 <= k <= _lib.KS_MAX_K else 1
+    spectra = np.zeros(2 * nk, dtype=np.float64)
+    r = Regions()
+    check(load().ks_tr_lr_regions(_ctx(device), hs.ptrs, hs.lens.ctypes.data, hs.n, k, min_length, kptrs,
+                                  ks_in.ctypes.data, tr_in.ctypes.data, n, spectra.ctypes.data, C.byref(r)))
+    pos, score = regions_to_numpy(r)
+    reg = {"seq_i": pos[0], "beg": pos[1], "end": pos[2], "score": score[0], "null": score[1]}
+    return {"kmer_scores": spectra.reshape(2, nk).T.copy(), "reg": reg, "pos": pos, "score": score}
 
 
 # ------------------------------------------------------------ table builders

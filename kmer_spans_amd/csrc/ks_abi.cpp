@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 #include <mutex>
 
 #include "ks_internal.h"
@@ -261,6 +262,100 @@ extern "C" ks_status ks_scan_dev(ks_ctx *ctx, const ks_dev_seqs *s, int32_t k, c
   memset(out, 0, sizeof(*out));
   KS_TRY(activate(ctx));
   return scan_impl(ctx, s, s->offsets_host[s->nseq], k, t, min_width, min_score, visits_dev, out, stats);
+}
+
+extern "C" ks_status ks_tr_lr_dev(ks_ctx *ctx, const ks_dev_seqs *s, int32_t k, const ks_table *trans,
+                                  const ks_table *init, int32_t min_length, ks_regions *out, ks_scan_stats *stats) {
+  if (!ctx || !trans || !init || !out) return fail(KS_ERR_ARG, "null argument");
+  KS_TRY(check_dev_seqs(s));
+  if (k < 1 || k > KS_MAX_K) return fail(KS_ERR_ARG, "k should be a positive value less than MAX_K");
+  if (min_length < 0) return fail(KS_ERR_ARG, "min_length should be a positive integer");
+  if (trans->k != k || init->k != k) return fail(KS_ERR_ARG, "tables built for another k");
+  if (!init->d_vals || init->thr != 0.0 || trans->thr != 0.0)
+    return fail(KS_ERR_ARG, "tr_lr tables need threshold 0 and an uncompressed init table");
+  memset(out, 0, sizeof(*out));
+  KS_TRY(activate(ctx));
+  ScanMode mode;
+  mode.trlr = 1;
+  mode.ks = init->d_vals;
+  mode.min_len = min_length;
+  mode.finite = trans->all_finite && init->all_finite;
+  mode.maxabs = std::max(trans->max_abs, init->max_abs);
+  return scan_impl(ctx, s, s->offsets_host[s->nseq], k, trans, 0, 0.0, nullptr, out, stats, mode);
+}
+
+// init_kmer (kmer_spans.c:119-132) on a NUL-terminated string from index 0:
+// the code of the first k consecutive non-N bytes; returns the index past them
+// (!= k when N bytes were skipped or the string is short).
+static int64_t prime_string(const char *str, int k, uint64_t *code) {
+  const unsigned char *s = (const unsigned char *)str;
+  int64_t i = 0, j = 0;
+  while (s[i]) {
+    uint64_t c = 0;
+    for (j = 0; j < k && s[i + j] && !is_n(s[i + j]); ++j) c = (c << 2) | enc(s[i + j]);
+    *code = c;
+    if (!s[i + j] || j == k) break;
+    i += j;
+    while (s[i] && is_n(s[i])) ++i;
+    j = 0;
+  }
+  return i + j;
+}
+
+extern "C" ks_status ks_tr_lr_regions(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq,
+                                      int32_t k, int32_t min_length, const char *const *kmers,
+                                      const double *kmer_scores, const double *trans_scores, int64_t n_scores,
+                                      double *spectra, ks_regions *out) {
+  if (nseq < 1 || !seqs || !lens)                             // :653-654
+    return fail(KS_ERR_ARG, "seq_r should be a character vector of of positive length");
+  KS_TRY(check_seqs(seqs, lens, nseq));
+  if (!kmers) return fail(KS_ERR_ARG, "kmers_r should be a character vector");              // :657-658
+  if (!kmer_scores || !trans_scores) return fail(KS_ERR_ARG, "freq_a and freq_b should be double vectors");
+  if (k < 1 || k > KS_MAX_K + 1)                              // :663-664 (MAX_K = 16 allowed there)
+    return fail(KS_ERR_ARG, "k should be a positive value less than MAX_K");
+  if (k > KS_MAX_K) return fail(KS_ERR_ARG, "k = 16 overflows the reference's int shift; not supported");
+  if (min_length < 0) return fail(KS_ERR_ARG, "min_length should be a positive integer");  // :665-666
+  const int64_t nk = (int64_t)1 << (2 * k);
+  if (n_scores != nk) return fail(KS_ERR_ARG, "kmers_r, freq_a, freq_b should all be 4^k long");  // :668-671
+  if (!out) return fail(KS_ERR_ARG, "null output");
+  memset(out, 0, sizeof(*out));
+  // remap to 2-bit code order (:677-690)
+  std::vector<double> ks((size_t)nk, 0.0), tr((size_t)nk, 0.0);
+  int64_t bad = 0;
+  for (int64_t i = 0; i < nk; ++i) {
+    if (!kmers[i]) return fail(KS_ERR_ARG, "kmers_r should be a character vector");
+    uint64_t code = 0;
+    if (prime_string(kmers[i], k, &code) != k) ++bad;
+    ks[code] = kmer_scores[i];
+    tr[code] = trans_scores[i];
+  }
+  if (bad) fprintf(stderr, "kmer_spans_amd: %lld k-mer strings of tr_lr_regions do not spell %d bases\n",
+                   (long long)bad, k);
+  if (spectra) {
+    memcpy(spectra, ks.data(), (size_t)nk * 8);
+    memcpy(spectra + nk, tr.data(), (size_t)nk * 8);
+  }
+  if (!ctx) ctx = ks_default_ctx();
+  if (!ctx) return fail(KS_ERR_DEVICE, "no HIP device available");
+  KS_TRY(activate(ctx));
+  Staged st;
+  KS_TRY(stage(ctx, seqs, lens, nseq, &st));
+  ks_table *t_tr = nullptr, *t_ks = nullptr;
+  KS_TRY(ks_table_create(ctx, tr.data(), k, 0.0, k >= 9 ? KS_TABLE_COMPRESS : 0, &t_tr));
+  ks_status rc = ks_table_create(ctx, ks.data(), k, 0.0, 0, &t_ks);
+  if (rc == KS_OK) {
+    ScanMode mode;
+    mode.trlr = 1;
+    mode.ks = t_ks->d_vals;
+    mode.min_len = min_length;
+    mode.finite = t_tr->all_finite && t_ks->all_finite;
+    mode.maxabs = std::max(t_tr->max_abs, t_ks->max_abs);
+    rc = scan_impl(ctx, &st.dev, st.total, k, t_tr, 0, 0.0, nullptr, out, nullptr, mode);
+  }
+  ks_table_destroy(t_tr);
+  ks_table_destroy(t_ks);
+  if (rc != KS_OK) ks_regions_free(out);
+  return rc;
 }
 
 extern "C" ks_status ks_kmer_counts(ks_ctx *ctx, const char *const *seqs, const int64_t *lens,

@@ -97,6 +97,8 @@ struct ks_table {
   void *d_ext = nullptr;        // uint64 (J <= 4 codes) or double[4] (J <= 3 values)
   size_t ext_bytes = 0;
   double ms_ext = 0;            // build time
+  bool all_finite = true;       // every s is finite
+  double max_abs = 0.0;         // max |s|
   // Narrow codes (ext_bits = 12, J = 5): the 4095 values covering most
   // positions get a 12-bit code (d_map12 -> uint16 code, d_lut12 -> value);
   // code 0xFFF escapes to the base uint16 table for that index.
@@ -140,7 +142,10 @@ struct RunLayout {
   int64_t nscan = 0;    // runs longer than k
   int64_t longest = 0;  // longest run (bases)
 };
-ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay);
+// trlr: one more scan index per run (the first k-mer's own step) and the
+// :341 skip of runs whose first k-mer ends within two bytes of the string end.
+ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int trlr = 0,
+                     const int64_t *offs_dev = nullptr);
 
 // Region record buffer written by scan kernels.
 // Append buffers (regions, rescans, candidates) are split into kSegs
@@ -162,9 +167,25 @@ struct RegionBuf {
 ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs, float *ms);
 ks_status launch_count(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const Runs &runs, int k,
                        int32_t *counts_dev, double *n_words);
+// Which span scan a call performs.  trlr = 0: kmer_regions (kmer_spans.c:
+// 243-307).  trlr = 1: find_kmer_tr_lr_regions (:329-395): the table holds the
+// transition scores, ks the first-k-mer scores, regions need
+// (max_pos - begin) >= min_len, every closed excursion restarts, output is
+// 1-based.  finite / maxabs describe both tr_lr tables: the chunked path
+// needs finite scores whose partial sums cannot overflow (the reference's
+// clamp keeps NaN, the chunked path's does not); otherwise the literal lane
+// kernel runs.
+struct ScanMode {
+  int trlr = 0;
+  const double *ks = nullptr;
+  int64_t min_len = 0;
+  int finite = 1;
+  double maxabs = 0.0;
+};
+
 ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, const ks_table *t,
                     int32_t min_width, double min_score, int32_t *visits_dev, ks_regions *out,
-                    ks_scan_stats *stats);
+                    ks_scan_stats *stats, const ScanMode &mode = ScanMode());
 
 // Build the expanded table of t (no-op if it exists or does not fit).
 ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t *freq_dev);

@@ -129,14 +129,16 @@ __global__ void k_pair_runs(const unsigned long long *__restrict__ ev, int64_t n
 }
 
 // Chunks and stitch tiles of every run, plus (wave-aggregated) totals.
-__global__ void k_run_counts(const int64_t *__restrict__ ra, const int64_t *__restrict__ rb, int64_t n, int k,
-                             int64_t *__restrict__ cnt_c, int64_t *__restrict__ cnt_t,
+__global__ void k_run_counts(const int64_t *__restrict__ ra, const int64_t *__restrict__ rb,
+                             const int32_t *__restrict__ rs, const int64_t *__restrict__ offs, int64_t n, int k,
+                             int trlr, int64_t *__restrict__ cnt_c, int64_t *__restrict__ cnt_t,
                              unsigned long long *__restrict__ agg) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long sc = 0, ns = 0, lo = 0;
   if (r < n) {
     const int64_t L = rb[r] - ra[r];
-    const int64_t P = L - k;
+    int64_t P = L - k;
+    if (trlr) P = (L >= k && ra[r] + k + 1 < offs[rs[r] + 1]) ? P + 1 : 0;
     const int64_t ch = P > 0 ? (P + kChunk - 1) / kChunk : 0;
     cnt_c[r] = ch;
     cnt_t[r] = (ch + kTileChunks - 1) / kTileChunks;
@@ -161,7 +163,7 @@ __global__ void k_run_counts(const int64_t *__restrict__ ra, const int64_t *__re
 
 }  // namespace
 
-ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay) {
+ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int trlr, const int64_t *offs_dev) {
   hipStream_t st = ctx->stream;
   const int64_t n = runs.n;
   *lay = RunLayout{};
@@ -175,8 +177,9 @@ ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay) {
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
   unsigned long long *agg = reinterpret_cast<unsigned long long *>(scal) + 8;
   KS_HIP(hipMemsetAsync(agg, 0, 24, st));
-  hipLaunchKernelGGL(k_run_counts, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st, runs.a, runs.b, n, k,
-                     cnt_c, cnt_t, agg);
+  if (trlr && !offs_dev) return fail(KS_ERR_INTERNAL, "run_layout: tr_lr needs sequence offsets");
+  hipLaunchKernelGGL(k_run_counts, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st, runs.a, runs.b,
+                     runs.seq, offs_dev, n, k, trlr, cnt_c, cnt_t, agg);
   KS_HIP(hipGetLastError());
   size_t tb = 0;
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt_c, lay->cbase, (int)(n + 1), st));

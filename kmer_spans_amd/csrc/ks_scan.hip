@@ -23,11 +23,12 @@ namespace ks {
 
 ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, const RunLayout &lay, int k,
                        const TableView &tv, uint64_t mw, double min_score, uint32_t *visits, const RegionBuf &rb,
-                       ks_scan_stats *stats);
+                       ks_scan_stats *stats, const ScanMode &mode);
 ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const int64_t *ra, const int64_t *rb,
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
-                           const unsigned long long *d_cnt = nullptr, int64_t segcap = 0);
+                           const unsigned long long *d_cnt = nullptr, int64_t segcap = 0,
+                           const ScanMode &mode = ScanMode(), int init_step = 1, const int64_t *offs = nullptr);
 
 namespace {
 
@@ -114,6 +115,90 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
   }
 }
 
+// find_kmer_tr_lr_regions (kmer_spans.c:329-395), literally, one lane per run
+// (init_step = 1: real N-free runs, with the first k-mer's own step and the
+// :341 skip) or per rescan range (init_step = 0: positions [a + k, b),
+// transitions only, fresh state).  Position p adds the transition score of the
+// k-mer ending at p; the maximum is tested before the clamp
+// `s < 0 ? 0 : s` (NaN kept, as in the reference); every return to 0 restarts
+// at max_pos + 1; an open region at the end is pushed without a restart.
+// Positions are global; the caller converts them to 1-based local ones.
+template <int J, bool kCompressed>
+__global__ void __launch_bounds__(64) k_scan_lane_trlr(const uint8_t *__restrict__ seq, int64_t total,
+                                                       const int64_t *__restrict__ ra,
+                                                       const int64_t *__restrict__ rbnd,
+                                                       const int32_t *__restrict__ rseq, int64_t nruns, int k,
+                                                       TableView tv, const double *__restrict__ ks,
+                                                       int64_t min_len, RegionBuf out,
+                                                       const unsigned long long *__restrict__ d_cnt,
+                                                       int64_t segcap, int init_step,
+                                                       const int64_t *__restrict__ offs) {
+  constexpr int G = (J == 1) ? 16 : (J >= 4 ? 4 : (J == 3 ? 6 : 8));  // reads per batch
+  constexpr int PB = G * J;
+  using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nruns) return;
+  if (d_cnt && (r % segcap) >= (int64_t)d_cnt[r / segcap]) return;  // segmented list: unused slot
+  const int64_t a = ra[r], b = rbnd[r];
+  if (b - a < k) return;
+  const int32_t sid = rseq[r];
+  const int kx = k + J - 1;
+  const GC xmask = (2 * kx >= 8 * (int)sizeof(GC)) ? ~(GC)0 : (((GC)1 << (2 * kx)) - 1);
+  const uint32_t kmask = (1u << (2 * k)) - 1u;
+  double last = 0.0, best = 0.0;
+  int64_t beg = 0, arg = 0;
+  if (init_step) {
+    if (a + k + 1 >= offs[sid + 1]) return;  // the string ends within a base of the first k-mer (:341)
+    double sc = ks[prime_code(seq, a, k)];
+    sc = sc < 0 ? 0 : sc;
+    if (sc > 0) { best = sc; arg = a + k; beg = a + k; }
+    last = sc;
+  }
+  int64_t ps = a + k;  // first transition position
+  const int64_t pe = b;
+  for (;;) {
+    // position p reads the k-mer ending at p: the (k+J-1)-mer of group 0 starts at ps + 1 - k
+    GC gcode = (GC)prime_code_guarded64(seq, ps + 1 - k, kx, total);
+    bool restart = false;
+    for (int64_t p0 = ps; p0 < pe && !restart; p0 += PB) {
+      const int n = (int)((pe - p0) < PB ? (pe - p0) : PB);
+      double v[PB];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        if (g * J < n) {
+          gather_group<J, kCompressed>(tv, gcode, kmask, v + g * J);
+#pragma unroll
+          for (int t = 0; t < J; ++t) {
+            const int64_t q = p0 + 1 + g * J + J - 1 + t;
+            gcode = ((gcode << 2) | enc(q < total ? seq[q] : (uint8_t)'N')) & xmask;
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < PB; ++j) {
+        if (j < n && !restart) {
+          const int64_t p = p0 + j;
+          double sc = last + v[j];
+          if (sc > best) { best = sc; arg = p; }
+          sc = sc < 0 ? 0 : sc;
+          if (last == 0 && sc > 0) { best = sc; arg = p; beg = p; }
+          if (sc == 0 && last > 0) {
+            if (arg - beg >= min_len) push_region(out, sid, beg, arg, best);
+            ps = arg + 1;
+            beg = arg;
+            last = best = 0.0;
+            restart = true;
+          } else {
+            last = sc;
+          }
+        }
+      }
+    }
+    if (!restart) break;
+  }
+  if (best > 0 && arg - beg >= min_len) push_region(out, sid, beg, arg, best);
+}
+
 // Compacted index j -> slot of the segmented region buffer.
 struct SegPrefix {
   int64_t p[kSegs + 1];
@@ -135,8 +220,9 @@ __global__ void k_region_keys(const int64_t *__restrict__ beg, int64_t n, SegPre
 }
 
 // Regions in (seq_id, beg) order == global begin order; local coordinates.
+// one = 1: tr_lr's 1-based sequence ids and positions (kmer_spans.c:378,:699).
 __global__ void k_region_gather(RegionBuf rb, const int32_t *__restrict__ perm, int64_t n,
-                                const int64_t *__restrict__ offs, int32_t *__restrict__ o_seq,
+                                const int64_t *__restrict__ offs, int one, int32_t *__restrict__ o_seq,
                                 int32_t *__restrict__ o_beg, int32_t *__restrict__ o_end,
                                 double *__restrict__ o_score) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -144,9 +230,9 @@ __global__ void k_region_gather(RegionBuf rb, const int32_t *__restrict__ perm, 
   const int32_t i = perm[j];
   const int32_t q = rb.seq[i];
   const int64_t base = offs[q];
-  o_seq[j] = q;
-  o_beg[j] = (int32_t)(rb.beg[i] - base);
-  o_end[j] = (int32_t)(rb.end[i] - base);
+  o_seq[j] = q + one;
+  o_beg[j] = (int32_t)(rb.beg[i] - base + one);
+  o_end[j] = (int32_t)(rb.end[i] - base + one);
   o_score[j] = rb.score[i];
 }
 
@@ -160,9 +246,23 @@ __global__ void k_add_hist(uint32_t *__restrict__ dst, const uint32_t *__restric
 ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const int64_t *ra, const int64_t *rb,
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
-                           const unsigned long long *d_cnt, int64_t segcap) {
+                           const unsigned long long *d_cnt, int64_t segcap, const ScanMode &mode, int init_step,
+                           const int64_t *offs) {
   if (n <= 0) return KS_OK;
   const int J = tv.ext ? tv.ext_J : 1;
+  if (mode.trlr) {
+#define KS_LANE_T(J, C)                                                                                   \
+  hipLaunchKernelGGL((k_scan_lane_trlr<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, \
+                     total, ra, rb, rs, n, k, tv, mode.ks, mode.min_len, out, d_cnt, segcap, init_step, offs)
+    if (tv.compressed) {
+      if (J == 5) KS_LANE_T(5, true); else if (J == 4) KS_LANE_T(4, true); else if (J == 3) KS_LANE_T(3, true); else if (J == 2) KS_LANE_T(2, true); else KS_LANE_T(1, true);
+    } else {
+      if (J == 4) KS_LANE_T(4, false); else if (J == 3) KS_LANE_T(3, false); else if (J == 2) KS_LANE_T(2, false); else KS_LANE_T(1, false);
+    }
+#undef KS_LANE_T
+    KS_HIP(hipGetLastError());
+    return KS_OK;
+  }
 #define KS_LANE(J, C)                                                                                   \
   hipLaunchKernelGGL((k_scan_lane<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, total, \
                      ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap)
@@ -178,7 +278,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
 
 ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, const ks_table *t,
                     int32_t min_width, double min_score, int32_t *visits_dev, ks_regions *out,
-                    ks_scan_stats *stats) {
+                    ks_scan_stats *stats, const ScanMode &mode) {
   hipStream_t st = ctx->stream;
   ks_scan_stats local{};
   ks_scan_stats *S = stats ? stats : &local;
@@ -190,7 +290,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
   S->ms_runs = ms_runs;
   // chunk layout, statistics and algorithm choice (device-side, one sync)
   RunLayout lay;
-  if (runs.n) KS_TRY(run_layout(ctx, runs, k, &lay));
+  if (runs.n) KS_TRY(run_layout(ctx, runs, k, &lay, mode.trlr, s->offsets_dev));
   const int64_t longest = lay.longest, scored = lay.scored;
   S->n_scored = scored;
   S->n_runs = lay.nscan;
@@ -204,6 +304,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
   const uint64_t mw = (uint64_t)(int64_t)min_width;
   int algo = ctx->scan_algo;
   if (algo < 0) algo = (longest > (1 << 15)) ? 1 : 0;
+  if (mode.trlr && !(mode.finite && mode.maxabs * (double)(longest + 2) < 1e300)) algo = 0;  // literal NaN rules
   S->scan_algo = algo;
 
   // region capacity: what the (grow-only) slot already holds, so that the
@@ -252,7 +353,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
         vscr = static_cast<uint32_t *>(vp);
         KS_HIP(hipMemsetAsync(vscr, 0, nb, st));
       }
-      ks_status rc = scan_chunked(ctx, s, runs, lay, k, tv, mw, min_score, vscr, rb, S);
+      ks_status rc = scan_chunked(ctx, s, runs, lay, k, tv, mw, min_score, vscr, rb, S, mode);
       if (rc == KS_INTERNAL_RETRY) {  // a buffer did not fit: grow, rerun, visits untouched
         KS_TRY(read_counts());
         const int64_t m = max_count();
@@ -276,7 +377,9 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
       }
     }
     if (algo == 0) {
-      if (runs.n) KS_TRY(launch_scan_lane(ctx, s->seq, total, runs.a, runs.b, runs.seq, runs.n, k, tv, mw, min_score, vis, rb));
+      if (runs.n)
+        KS_TRY(launch_scan_lane(ctx, s->seq, total, runs.a, runs.b, runs.seq, runs.n, k, tv, mw, min_score, vis, rb,
+                                nullptr, 0, mode, 1, s->offsets_dev));
     }
     KS_HIP(hipEventRecord(ctx->ev[4], st));
     KS_TRY(read_counts());
@@ -332,7 +435,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     void *tmp = nullptr;
     KS_TRY(ensure(ctx, SLOT_SORT_TMP, tb, &tmp));
     KS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k_in, k_out, v_in, v_out, (int)n, 0, end_bit, st));
-    hipLaunchKernelGGL(k_region_gather, dim3(g), dim3(256), 0, st, rb, v_out, n, s->offsets_dev, o_seq, o_beg,
+    hipLaunchKernelGGL(k_region_gather, dim3(g), dim3(256), 0, st, rb, v_out, n, s->offsets_dev, mode.trlr, o_seq, o_beg,
                        o_end, o_score);
     KS_HIP(hipGetLastError());
     // one D2H of the contiguous [seq | beg | end | score] block into pinned

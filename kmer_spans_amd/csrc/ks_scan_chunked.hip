@@ -41,7 +41,8 @@ namespace ks {
 ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const int64_t *ra, const int64_t *rb,
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
-                           const unsigned long long *d_cnt = nullptr, int64_t segcap = 0);
+                           const unsigned long long *d_cnt = nullptr, int64_t segcap = 0,
+                           const ScanMode &mode = ScanMode(), int init_step = 1, const int64_t *offs = nullptr);
 
 namespace {
 
@@ -89,6 +90,56 @@ struct Rescan {
   unsigned long long *count;  // [kSegs]
   int64_t cap, segcap;
 };
+
+// Emission rules of the scan (kmer_regions or tr_lr, see ScanMode).
+struct EmitCfg {
+  int trlr;
+  uint64_t mw;          // kmer_regions: (size_t)min_width
+  double min_score;     // kmer_regions
+  int64_t min_len;      // tr_lr
+  const double *ks;     // tr_lr: score of each run's first k-mer
+  int k;
+};
+
+// tr_lr position of scan index j in a run whose first scan index is f: the
+// first k-mer's step sits at f, the transition of the k-mer ending at p at
+// index p + 1.  kmer_regions reports scan indices.
+__device__ __forceinline__ int64_t pos_of(const EmitCfg &ec, int64_t j, int64_t f) {
+  return (ec.trlr && j != f) ? j - 1 : j;
+}
+
+// What an excursion (beg, first argmax arg, max best, ending at scan index
+// end; closed = it returned to 0 there, else open at the run end) produces:
+// a region record and/or a rescan range (virtual run [res_a, res_b) for the
+// lane kernel).  f = the run's first scan index.
+struct Emission {
+  bool reg, res;
+  int64_t rbeg, rend;    // region record (positions)
+  int64_t res_a, res_b;
+};
+
+__device__ __forceinline__ Emission decide(const EmitCfg &ec, int64_t f, int64_t beg, int64_t arg, double best,
+                                           int64_t end, bool closed) {
+  Emission e;
+  if (!ec.trlr) {  // kmer_regions: emitted excursions rescan (arg, end], open ones included
+    e.reg = (uint64_t)(arg - beg) >= ec.mw && best >= ec.min_score;
+    e.res = e.reg && arg + 1 <= end;
+    e.rbeg = beg;
+    e.rend = arg;
+    e.res_a = arg + 1 - ec.k;
+    e.res_b = end + 1;
+  } else {  // tr_lr: positions; every closed excursion rescans (pos(arg), pos(end)]
+    const int64_t pb = pos_of(ec, beg, f), pa = pos_of(ec, arg, f), pe = pos_of(ec, end, f);
+    e.reg = pa - pb >= ec.min_len;
+    e.res = closed && pe >= pa + 2;  // a one-position tail cannot hold an excursion
+    e.rbeg = pb;
+    e.rend = pa;
+    e.res_a = pa + 1 - ec.k;  // lane kernel (tr_lr): positions [res_a + k, res_b)
+    e.res_b = pe + 1;
+  }
+  (void)best;
+  return e;
+}
 
 __device__ __forceinline__ uint32_t roll(uint32_t c, uint8_t b, uint32_t mask) {
   return ((c << 2) | enc(b)) & mask;
@@ -168,7 +219,7 @@ __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restri
 // ------------------------------------------------------------------- P0
 
 __global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase, int64_t nruns,
-                              int k, const int64_t *__restrict__ rbnd, Chunks g) {
+                              int k, const int64_t *__restrict__ rbnd, int extra, Chunks g) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
   int64_t lo = 0, hi = nruns - 1;  // last run with cbase[r] <= c
@@ -177,13 +228,24 @@ __global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__r
     if (cbase[mid] <= c) lo = mid; else hi = mid - 1;
   }
   const int64_t first = ra[lo] + k + (c - cbase[lo]) * CH;
-  const int64_t last = rbnd[lo] - 1;
+  const int64_t last = rbnd[lo] - 1 + extra;  // tr_lr: one more index (the first k-mer's own step)
   g.start[c] = first;
   g.n[c] = (int32_t)min((int64_t)CH, last - first + 1);
   g.run[c] = (int32_t)lo;
 }
 
 // ------------------------------------------------------------------- P1
+
+// A closed excursion of a chunk's clean trajectory (chunk-relative beg, arg,
+// end) is kept as a candidate if it could emit a region or (tr_lr) needs a
+// rescan; first = the chunk starts its run.
+__device__ __forceinline__ bool cand_wanted(const EmitCfg &ec, bool first, int64_t start, int beg, int arg, int end,
+                                            double best) {
+  const int64_t f = first ? start : -1;
+  const Emission e = decide(ec, f, start + beg, start + arg, best, start + end, true);
+  return e.reg || e.res;
+}
+
 
 // J = scan indices served by one table read: 1 reads the base table
 // (uint16 code or FP64 value per index); J >= 2 reads the expanded table
@@ -193,8 +255,7 @@ __global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__r
 template <int J, bool kCompressed, bool kLds>
 __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
                                                 int k, TableView tv, uint16_t *__restrict__ codes,
-                                                uint64_t mw, double min_score, uint32_t *__restrict__ visits,
-                                                P1 o, Cand cand) {
+                                                EmitCfg ec, uint32_t *__restrict__ visits, P1 o, Cand cand) {
   constexpr int G = (J == 1) ? 16 : (J >= 3 ? 4 : 8);  // table reads in flight per lane and batch
   constexpr int PB = G * J;             // scan indices per batch (16, 16, 12, 16, 20)
   constexpr bool k12 = (J == 5);        // 12-bit codes with escapes (kCompressed only)
@@ -219,7 +280,10 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
   const uint32_t kmask = (1u << (2 * k)) - 1u;
   const int64_t start = g.start[c];
   const int n = g.n[c];
+  const bool first = c == 0 || g.run[c - 1] != g.run[c];  // the chunk starts its run
   GC gcode = (GC)prime_code_guarded64(seq, start - k, kx, total);  // (k+J-1)-mer of group 0
+  // tr_lr: the run's first scan index scores the first k-mer's own score
+  const double first_val = (ec.trlr && first) ? ec.ks[(uint32_t)(gcode >> (2 * (J - 1))) & kmask] : 0.0;
   double prev = 0.0, best = 0.0;
   int beg = -1, arg = 0;
   double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
@@ -293,6 +357,7 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
         }
       }
     }
+    if (ec.trlr && first && b0 == 0) v[0] = first_val;
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
       const int i = b0 + j;
@@ -309,7 +374,7 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
         if (prev == 0 && S > 0) {
           beg = i; arg = i; best = S;
         } else if (prev > 0 && S == 0) {
-          if ((uint64_t)(arg - beg) >= mw && best >= min_score) {
+          if (cand_wanted(ec, first, start, beg, arg, i, best)) {
             const int64_t slot = append_one(cand.count, cand.segcap);
             if (slot >= 0) {
               cand.beg[slot] = start + beg;
@@ -348,8 +413,8 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
 // static.  Results are identical to k_pass1.
 template <int J, bool kLds>
 __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
-                                                 TableView tv, uint16_t *__restrict__ codes, uint64_t mw,
-                                                 double min_score, uint32_t *__restrict__ visits, P1 o, Cand cand) {
+                                                 TableView tv, uint16_t *__restrict__ codes, EmitCfg ec,
+                                                 uint32_t *__restrict__ visits, P1 o, Cand cand) {
   constexpr int G = 4;                  // table reads per batch
   constexpr int PB = G * J;             // scan indices per batch (8, 12, 16, 20)
   constexpr bool k12 = (J == 5);        // 12-bit codes with escapes
@@ -374,7 +439,10 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
   const uint32_t kmask = (1u << (2 * k)) - 1u;
   const int64_t start = g.start[c];
   const int n = g.n[c];
+  const bool first = c == 0 || g.run[c - 1] != g.run[c];  // the chunk starts its run
   GC gcode = (GC)prime_code_guarded64(seq, start - k, kx, total);  // (k+J-1)-mer of group 0
+  // tr_lr: the run's first scan index scores the first k-mer's own score
+  const double first_val = (ec.trlr && first) ? ec.ks[(uint32_t)(gcode >> (2 * (J - 1))) & kmask] : 0.0;
   uint8_t by[32];
   // prologue: codes + reads of batch 0, bytes of batch 1
   load16(seq, start + J - 1, total, by);
@@ -450,6 +518,7 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
         }
         if (j & 1) cw[j >> 1] |= qq << 16;
         else cw[j >> 1] = qq;
+        if (ec.trlr && first && b0 == 0 && j == 0) s = first_val;
         const int i = b0 + j;
         if (i < n) {
           if (visits) atomicAdd(&visits[(uint32_t)(gc[gi] >> (2 * (J - 1 - t))) & kmask], 1u);
@@ -463,7 +532,7 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
           if (prev == 0 && S > 0) {
             beg = i; arg = i; best = S;
           } else if (prev > 0 && S == 0) {
-            if ((uint64_t)(arg - beg) >= mw && best >= min_score) {
+            if (cand_wanted(ec, first, start, beg, arg, i, best)) {
               const int64_t slot = append_one(cand.count, cand.segcap);
               if (slot >= 0) {
                 cand.beg[slot] = start + beg;
@@ -1164,55 +1233,54 @@ __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restri
 
 // ------------------------------------------------------------------- P5
 
-__device__ __forceinline__ void emit(const RegionBuf &rb, const Rescan &rs, int32_t sid, int k, int64_t beg,
-                                     int64_t arg, double best, int64_t end) {
-  push_region(rb, sid, beg, arg, best);
-  if (arg + 1 <= end) {
+// One lane's emission (sporadic callers).
+__device__ __forceinline__ void emit(const Emission &e, const RegionBuf &rb, const Rescan &rs, int32_t sid,
+                                     double best) {
+  if (e.reg) push_region(rb, sid, e.rbeg, e.rend, best);
+  if (e.res) {
     const int64_t slot = append_one(rs.count, rs.segcap);
     if (slot >= 0) {
-      rs.a[slot] = arg + 1 - k;  // virtual run: scan indices arg+1 .. end
-      rs.b[slot] = end + 1;
+      rs.a[slot] = e.res_a;
+      rs.b[slot] = e.res_b;
       rs.seq[slot] = sid;
     }
   }
 }
 
-// emit() for a whole wave (every lane calls it; lanes with want set emit):
-// one atomic per wave and buffer instead of one per region, so that millions
-// of regions do not serialise on the two counters.
-__device__ __forceinline__ void emit_wave(bool want, const RegionBuf &rb, const Rescan &rs, int32_t sid, int k,
-                                          int64_t beg, int64_t arg, double best, int64_t end) {
-  const unsigned long long m = __ballot(want);
-  if (m == 0) return;
-  const bool wr = want && arg + 1 <= end;
-  const unsigned long long mr = __ballot(wr);
+// emit() for a whole wave (every lane calls it): one atomic per wave and
+// buffer segment instead of one per record.
+__device__ __forceinline__ void emit_wave(const Emission &e, const RegionBuf &rb, const Rescan &rs, int32_t sid,
+                                          double best) {
+  const unsigned long long m = __ballot(e.reg);
+  const unsigned long long mr = __ballot(e.res);
+  if ((m | mr) == 0) return;
   const int lane = (int)(threadIdx.x & 63);
-  const int leader = __ffsll((long long)m) - 1;
+  const int leader = __ffsll((long long)(m | mr)) - 1;
   const int sg = append_seg();
   unsigned long long base = 0, rbase = 0;
   if (lane == leader) {
-    base = atomicAdd(&rb.count[sg], (unsigned long long)__popcll(m));
+    if (m) base = atomicAdd(&rb.count[sg], (unsigned long long)__popcll(m));
     if (mr) rbase = atomicAdd(&rs.count[sg], (unsigned long long)__popcll(mr));
   }
   base = __shfl(base, leader, 64);
   rbase = __shfl(rbase, leader, 64);
   const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  if (want) {
+  if (e.reg) {
     const unsigned long long i = base + (unsigned long long)__popcll(m & below);
     if ((int64_t)i < rb.segcap) {
       const int64_t slot = (int64_t)sg * rb.segcap + (int64_t)i;
       rb.seq[slot] = sid;
-      rb.beg[slot] = beg;
-      rb.end[slot] = arg;
+      rb.beg[slot] = e.rbeg;
+      rb.end[slot] = e.rend;
       rb.score[slot] = best;
     }
   }
-  if (wr) {
+  if (e.res) {
     const unsigned long long i = rbase + (unsigned long long)__popcll(mr & below);
     if ((int64_t)i < rs.segcap) {
       const int64_t slot = (int64_t)sg * rs.segcap + (int64_t)i;
-      rs.a[slot] = arg + 1 - k;
-      rs.b[slot] = end + 1;
+      rs.a[slot] = e.res_a;
+      rs.b[slot] = e.res_b;
       rs.seq[slot] = sid;
     }
   }
@@ -1366,10 +1434,9 @@ __global__ void __launch_bounds__(64) k_stitch_tiles(Chunks g, const int64_t *__
 // state entering each tile; the excursion still open at the run end is
 // emitted here.
 __global__ void __launch_bounds__(64) k_stitch_runs(const int64_t *__restrict__ tbase, int64_t nruns,
-                                                    const int64_t *__restrict__ rb_end,
-                                                    const int32_t *__restrict__ rseq, int k, uint64_t mw,
-                                                    double min_score, XTiles agg, XTiles tin, RegionBuf out,
-                                                    Rescan rs) {
+                                                    const int64_t *__restrict__ ra, const int64_t *__restrict__ rb_end,
+                                                    const int32_t *__restrict__ rseq, EmitCfg ec, XTiles agg,
+                                                    XTiles tin, RegionBuf out, Rescan rs) {
   const int64_t r = blockIdx.x;
   if (r >= nruns) return;
   const int lane = threadIdx.x;
@@ -1386,14 +1453,16 @@ __global__ void __launch_bounds__(64) k_stitch_runs(const int64_t *__restrict__ 
     if (t < t1) xt_store(tin, t, x_compose(carry, exc));
     carry = x_compose(carry, x_shfl(inc, 63));
   }
-  if (lane == 0 && carry.open && (uint64_t)(carry.xa - carry.xb) >= mw && carry.xm >= min_score)
-    emit(out, rs, rseq[r], k, carry.xb, carry.xa, carry.xm, rb_end[r] - 1);
+  if (lane == 0 && carry.open) {  // excursion open at the run end
+    const int64_t last = rb_end[r] - 1 + ec.trlr;  // last scan index of the run
+    emit(decide(ec, ra[r] + ec.k, carry.xb, carry.xa, carry.xm, last, false), out, rs, rseq[r], carry.xm);
+  }
 }
 
 __global__ void __launch_bounds__(64) k_stitch_emit(Chunks g, const int64_t *__restrict__ tbase,
                                                     const int64_t *__restrict__ cbase, int64_t nruns,
-                                                    const int32_t *__restrict__ rseq, int k, P1 o, Carry cr,
-                                                    uint64_t mw, double min_score, XTiles tin, RegionBuf out,
+                                                    const int64_t *__restrict__ ra, const int32_t *__restrict__ rseq,
+                                                    P1 o, Carry cr, EmitCfg ec, XTiles tin, RegionBuf out,
                                                     Rescan rs, unsigned int *__restrict__ err) {
   const int64_t t = blockIdx.x;
   const int lane = threadIdx.x;
@@ -1409,29 +1478,30 @@ __global__ void __launch_bounds__(64) k_stitch_emit(Chunks g, const int64_t *__r
   XState exc = x_shfl_up(inc, 1);
   if (lane == 0) exc = XState{0, 0, 0, 0, -INFINITY};
   const XState in = x_compose(xt_load(tin, t), exc);  // state entering chunk c
-  bool want = false;
   double xm = in.xm;
   long long xa = in.xa;
+  Emission e{false, false, 0, 0, 0, 0};
   if (live && op.closes) {
     if (!in.open) {
       atomicOr(err, 4u);
     } else {
       if (op.hmax > xm) { xm = op.hmax; xa = op.harg; }
-      want = (uint64_t)(xa - in.xb) >= mw && xm >= min_score;
+      e = decide(ec, ra[r] + ec.k, in.xb, xa, xm, op.close_pos, true);
     }
   }
-  emit_wave(want, out, rs, rseq[r], k, in.xb, xa, xm, op.close_pos);
+  emit_wave(e, out, rs, rseq[r], xm);
   if (live && !op.closes && op.f.reset == 0 && op.mode != kModeClean && !in.open) atomicOr(err, 8u);
 }
 
 // Candidates (closed emittable excursions of the clean trajectories) are
 // valid when they begin at or after their chunk's valid_from.
 __global__ void k_candidates(Chunks g, const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase,
-                             int64_t nruns, const int32_t *__restrict__ rseq, int k, Cand cand,
+                             int64_t nruns, const int32_t *__restrict__ rseq, EmitCfg ec, Cand cand,
                              Carry cr, RegionBuf out, Rescan rs) {
+  const int k = ec.k;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool want = false;
-  int64_t b = 0, arg = 0, rst = 0;
+  int64_t b = 0, arg = 0, rst = 0, f = 0;
   double best = 0.0;
   int32_t sid = 0;
   if (i < cand.cap && (i % cand.segcap) < (int64_t)cand.count[i / cand.segcap]) {
@@ -1448,15 +1518,19 @@ __global__ void k_candidates(Chunks g, const int64_t *__restrict__ ra, const int
     arg = cand.arg[i];
     best = cand.best[i];
     rst = cand.rst[i];
+    f = ra[lo] + k;
   }
-  emit_wave(want, out, rs, sid, k, b, arg, best, rst);
+  Emission e{false, false, 0, 0, 0, 0};
+  if (want) e = decide(ec, f, b, arg, best, rst, true);
+  emit_wave(e, out, rs, sid, best);
 }
 
 }  // namespace
 
 ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, const RunLayout &lay, int k,
                        const TableView &tv, uint64_t mw, double min_score, uint32_t *visits, const RegionBuf &rb,
-                       ks_scan_stats *stats) {
+                       ks_scan_stats *stats, const ScanMode &mode) {
+  const EmitCfg ec{mode.trlr, mw, min_score, mode.min_len, mode.ks, k};
   hipStream_t st = ctx->stream;
   const int64_t total = s->offsets_host[s->nseq];
   const int64_t nruns = runs.n;
@@ -1550,7 +1624,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // ---- P0 chunks, P1 gather pass
   KS_HIP(hipEventRecord(ctx->ev[7], st));
   hipLaunchKernelGGL(k_make_chunks, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, st, runs.a, d_cbase,
-                     nruns, k, runs.b, g);
+                     nruns, k, runs.b, mode.trlr, g);
   KS_HIP(hipGetLastError());
   const unsigned gch = (unsigned)((nch + 255) / 256);
   const unsigned gch1k = (unsigned)((nch + 1023) / 1024);
@@ -1558,12 +1632,12 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const bool lds_lut = comp && tv.nlut <= kLdsLutMax && getenv("KS_NO_LDS_LUT") == nullptr;
 #define KS_P1(J, C, L)                                                                                       \
   hipLaunchKernelGGL((k_pass1<J, C, L>), dim3(J == 1 ? gch : gch1k), dim3(J == 1 ? 256 : 1024), 0, st, g, s->seq, \
-                     total, k, tv, codes, mw, min_score, visits, p1, cand)
+                     total, k, tv, codes, ec, visits, p1, cand)
   const int J = (tv.ext != nullptr) ? tv.ext_J : 1;
   const bool pipelined = getenv("KS_NO_PIPELINED_P1") == nullptr;
 #define KS_P1P(J, L)                                                                                           \
-  hipLaunchKernelGGL((k_pass1p<J, L>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes, mw,       \
-                     min_score, visits, p1, cand)
+  hipLaunchKernelGGL((k_pass1p<J, L>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes, ec,       \
+                     visits, p1, cand)
   if (comp && J >= 2 && pipelined) {
     if (lds_lut) {
       if (J == 5) KS_P1P(5, true); else if (J == 4) KS_P1P(4, true); else if (J == 3) KS_P1P(3, true); else KS_P1P(2, true);
@@ -1637,18 +1711,18 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   hipLaunchKernelGGL(k_stitch_tiles, dim3((unsigned)ntiles), dim3(64), 0, st, g, d_tbase, d_cbase, nruns, p1, cr,
                      xagg);
   KS_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_stitch_runs, dim3((unsigned)nruns), dim3(64), 0, st, d_tbase, nruns, runs.b, runs.seq, k, mw,
-                     min_score, xagg, xtin, rb, rs);
+  hipLaunchKernelGGL(k_stitch_runs, dim3((unsigned)nruns), dim3(64), 0, st, d_tbase, nruns, runs.a, runs.b,
+                     runs.seq, ec, xagg, xtin, rb, rs);
   KS_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_stitch_emit, dim3((unsigned)ntiles), dim3(64), 0, st, g, d_tbase, d_cbase, nruns, runs.seq, k,
-                     p1, cr, mw, min_score, xtin, rb, rs, d_err);
+  hipLaunchKernelGGL(k_stitch_emit, dim3((unsigned)ntiles), dim3(64), 0, st, g, d_tbase, d_cbase, nruns, runs.a,
+                     runs.seq, p1, cr, ec, xtin, rb, rs, d_err);
   KS_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_candidates, dim3((unsigned)((ccap + 255) / 256)), dim3(256), 0, st, g, runs.a, d_cbase,
-                     nruns, runs.seq, k, cand, cr, rb, rs);
+                     nruns, runs.seq, ec, cand, cr, rb, rs);
   KS_HIP(hipGetLastError());
   KS_HIP(hipEventRecord(ctx->ev[10], st));
   KS_TRY(launch_scan_lane(ctx, s->seq, total, rs.a, rs.b, rs.seq, rcap, k, tv, mw, min_score, visits, rb,
-                          rs.count, rs.segcap));
+                          rs.count, rs.segcap, mode, 0));
   KS_HIP(hipEventRecord(ctx->ev[11], st));
   std::vector<unsigned long long> hcv(2 * kSegs + 2);
   KS_HIP(hipMemcpyAsync(hcv.data(), cnts, 8 * (2 * kSegs + 2), hipMemcpyDeviceToHost, st));

@@ -10,6 +10,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstring>
 #include <cstdlib>
 #include <vector>
 
@@ -25,6 +26,24 @@ __global__ void k_sub_thr(const double *__restrict__ w, double thr, double *__re
     const double v = w[i] - thr;
     s[i] = v;
     if (bits) bits[i] = (unsigned long long)__double_as_longlong(v);
+  }
+}
+
+// max |s| (as the bits of a non-negative double) and a non-finite flag.
+__global__ void k_absmax(const double *__restrict__ s, int64_t n, unsigned long long *__restrict__ out) {
+  unsigned long long m = 0, bad = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = s[i];
+    if (!isfinite(v)) bad = 1;
+    else m = max(m, (unsigned long long)__double_as_longlong(fabs(v)));
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    m = max(m, (unsigned long long)__shfl_down(m, d, 64));
+    bad |= __shfl_down(bad, d, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&out[0], m);
+    if (bad) atomicOr(&out[1], 1ull);
   }
 }
 
@@ -295,6 +314,19 @@ extern "C" ks_status ks_table_create_hint(ks_ctx *ctx, const double *w_host, int
   const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(k_sub_thr, dim3(grid), dim3(256), 0, st, d_w, thr, t->d_vals, d_bits, n);
   KS_TBL_HIP(hipGetLastError());
+  {  // finiteness and magnitude (tr_lr decides between the chunked and the literal path)
+    unsigned long long *d_am = nullptr, h_am[2] = {0, 0};
+    KS_TBL_HIP(hipMalloc(&d_am, 16));
+    KS_TBL_HIP(hipMemsetAsync(d_am, 0, 16, st));
+    hipLaunchKernelGGL(k_absmax, dim3(grid), dim3(256), 0, st, t->d_vals, n, d_am);
+    KS_TBL_HIP(hipMemcpyAsync(h_am, d_am, 16, hipMemcpyDeviceToHost, st));
+    KS_TBL_HIP(hipStreamSynchronize(st));
+    KS_TBL_HIP(hipFree(d_am));
+    t->all_finite = h_am[1] == 0;
+    double ma = 0;
+    memcpy(&ma, &h_am[0], 8);
+    t->max_abs = ma;
+  }
   t->distinct = -1;
   if (allow_compress) {
     KS_TBL_HIP(hipMalloc(&d_sorted, n * sizeof(unsigned long long)));

@@ -143,6 +143,19 @@ def scan(ctx: _lib.Context, ds: DeviceSeqs, k: int, table: DeviceTable, min_widt
     return pos, score, st.as_dict()
 
 
+def tr_lr(ctx: _lib.Context, ds: DeviceSeqs, k: int, trans: DeviceTable, init: DeviceTable, min_length: int):
+    """ks_tr_lr_dev: tr_lr regions (1-based, as tr_lr_regions_r) of
+    device-resident sequences; trans / init tables with threshold 0 (init
+    built with compress=False).  Returns (pos int32[3, R], score float64[2, R], stats)."""
+    st = ScanStats()
+    r = Regions()
+    s = ds.struct()
+    check(load().ks_tr_lr_dev(ctx.handle, C.byref(s), int(k), trans._h, init._h, int(min_length), C.byref(r),
+                              C.byref(st)))
+    pos, score = regions_to_numpy(r)
+    return pos, score, st.as_dict()
+
+
 def count(ctx: _lib.Context, ds: DeviceSeqs, k: int, counts: torch.Tensor) -> float:
     """ks_count_dev: accumulates into counts (int32[4^k] cuda); returns #words."""
     n = C.c_double(0)

@@ -175,15 +175,47 @@ SEXP kmer_seq_r(SEXP k_r) {
   return ret;
 }
 
-/* Out of the span-scan path: not provided by this
- * build.  They stay registered so that a package that registers all six
- * names loads; calling them reports that the routine lives in the reference. */
+/* tr_lr_regions_r(seq_r, params_r, kmers_r, kmer_scores_r, trans_scores_r)
+ * -- :649-713.  Returns list(spectra (4^k x 2: the remapped kmer and
+ * transition scores), pos (3 x n: 1-based seq_id, beg, end), scores (2 x n)).
+ * trans_scores_r is type-checked here (the reference reads it unchecked). */
 SEXP tr_lr_regions_r(SEXP seq_r, SEXP params_r, SEXP kmers_r, SEXP kmer_scores_r, SEXP trans_scores_r) {
-  (void)seq_r; (void)params_r; (void)kmers_r; (void)kmer_scores_r; (void)trans_scores_r;
-  error("tr_lr_regions_r is not part of the MI355X span-scan build (out of scope, see DESIGN.md)");
-  return R_NilValue;
+  if (TYPEOF(seq_r) != STRSXP || length(seq_r) < 1)
+    error("seq_r should be a character vector of of positive length");
+  if (TYPEOF(params_r) != INTSXP || length(params_r) != 2)
+    error("params_r should have two integers (k, and min_length)");
+  if (TYPEOF(kmers_r) != STRSXP)
+    error("kmers_r should be a character vector");
+  if (TYPEOF(kmer_scores_r) != REALSXP || TYPEOF(trans_scores_r) != REALSXP)
+    error("freq_a and freq_b should be double vectors");
+  int k = INTEGER(params_r)[0];
+  int min_length = INTEGER(params_r)[1];
+  if (k < 1 || k > MAX_K)
+    error("k should be a positive value less than MAX_K");
+  if (min_length < 0)
+    error("min_length should be a positive integer");
+  if (k > KS_MAX_K) error("k should be a positive value less than MAX_K");
+  size_t kmers_size = (size_t)1 << (2 * k);
+  if ((size_t)length(kmers_r) != kmers_size || (size_t)length(kmer_scores_r) != kmers_size ||
+      (size_t)length(trans_scores_r) != kmers_size)
+    error("kmers_r, freq_a, freq_b should all be 4^k long");
+  seq_view v = view_seqs(seq_r);
+  const char **kmers = (const char **)R_alloc(kmers_size, sizeof(char *));
+  for (size_t i = 0; i < kmers_size; ++i) kmers[i] = CHAR(STRING_ELT(kmers_r, (R_xlen_t)i));
+  SEXP ret = PROTECT(allocVector(VECSXP, 3));
+  SET_VECTOR_ELT(ret, 0, allocMatrix(REALSXP, (int)kmers_size, 2));
+  ks_regions reg;
+  ks_status st = ks_tr_lr_regions(NULL, v.ptrs, v.lens, v.n, k, min_length, kmers, REAL(kmer_scores_r),
+                                  REAL(trans_scores_r), (int64_t)kmers_size, REAL(VECTOR_ELT(ret, 0)), &reg);
+  if (st != KS_OK) { UNPROTECT(1); ks_check(st); }
+  regions_to_r(&reg, ret, 1, 2);
+  UNPROTECT(1);
+  return ret;
 }
 
+/* Out of the span-scan path: not provided by this build.
+ * It stays registered so that a package that registers all six names loads;
+ * calling it reports that the routine lives in the reference. */
 SEXP windowed_kmer_count_distributions_r(SEXP seq_r, SEXP kmers_r, SEXP k_r, SEXP window_r, SEXP ret_flag_r) {
   (void)seq_r; (void)kmers_r; (void)k_r; (void)window_r; (void)ret_flag_r;
   error("windowed_kmer_count_distributions_r is not part of the MI355X span-scan build (out of scope, see DESIGN.md)");

@@ -311,3 +311,85 @@ int orc_kmer_seq(int32_t k, char *out) {
   }
   return 0;
 }
+
+/* ---------------------------------------------------------- tr_lr regions */
+
+/* tr_lr_regions_r's k-mer remap (kmer_spans.c:677-690): entry i of the input
+ * tables belongs to the k-mer spelled by kmers[i]; it is stored at the code
+ * init_kmer computes for that string (N-skipping, possibly short).  Entries
+ * never assigned are zero here (uninitialised in the reference).  Returns the
+ * number of strings whose primed length is not k (the reference prints them). */
+int orc_trlr_remap(const char *const *kmers, int32_t k, const double *ks_in, const double *tr_in,
+                   double *ks_out, double *tr_out) {
+  const size_t n = (size_t)1 << (2 * k);
+  memset(ks_out, 0, n * sizeof(double));
+  memset(tr_out, 0, n * sizeof(double));
+  int bad = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const unsigned char *s = (const unsigned char *)kmers[i];
+    const int64_t len = (int64_t)strlen(kmers[i]);
+    uint64_t code = 0;
+    const int64_t ii = orc_prime(s, len, 0, k, &code);
+    if (ii != k) ++bad;
+    ks_out[code] = ks_in[i];
+    tr_out[code] = tr_in[i];
+  }
+  return bad;
+}
+
+/* find_kmer_tr_lr_regions (kmer_spans.c:329-395) for one sequence.  Per
+ * N-free run: the first k-mer's kmer score, clamped at 0 (`s < 0 ? 0 : s`,
+ * NaN kept), is attributed to the position just past it; then at each later
+ * position the k-mer ending there adds its transition score.  The maximum is
+ * tested before the clamp; a region opens where the score turns positive;
+ * when it returns to 0 the region is pushed if (max_pos - begin) >=
+ * min_length and the scan ALWAYS restarts at max_pos + 1 with fresh state.
+ * A region still open at the end of the run is pushed without a restart.
+ * The run is skipped when the string ends within one base after its first
+ * k-mer (:341).  Records are 1-based: (seq_id, 1 + begin, 1 + max_pos). */
+void orc_trlr_one(const char *str, int64_t len, int32_t seq_id, int32_t k, int32_t min_len,
+                  const double *ks, const double *tr, orc_regions *out) {
+  const unsigned char *s = (const unsigned char *)str;
+  const uint64_t mask = (((uint64_t)1) << (2 * k)) - 1;
+  uint64_t code = 0;
+  int64_t i = 0;
+  while (i < len) {
+    i = orc_prime(s, len, i, k, &code);
+    if (i >= len || i + 1 >= len) break;
+    code &= mask;
+    double last, best = 0.0, score = ks[code];
+    int64_t best_pos = 0, beg = 0;
+    score = score < 0 ? 0 : score;
+    if (score > 0) { best = score; best_pos = i; beg = i; }
+    last = score;
+    while (i < len && !orc_is_n(s[i])) {
+      code = mask & ((code << 2) | orc_code(s[i]));
+      score = last + tr[code];
+      if (score > best) { best = score; best_pos = i; }
+      score = score < 0 ? 0 : score;
+      if (last == 0 && score > 0) { best = score; best_pos = i; beg = i; }
+      if (score == 0 && last > 0) {
+        if (best_pos - beg >= min_len) orc_push(out, seq_id, 1 + beg, 1 + best_pos, best);
+        i = best_pos;
+        score = last = best = 0;
+        beg = i;
+        best_pos = 0;
+        orc_prime(s, len, 1 + i - k, k, &code); /* k-mer ending at i */
+      }
+      last = score;
+      ++i;
+    }
+    if (best > 0 && best_pos - beg >= min_len) orc_push(out, seq_id, 1 + beg, 1 + best_pos, best);
+  }
+}
+
+/* tr_lr_regions_r (.Call, kmer_spans.c:649-713) given the remapped tables
+ * (2-bit code order): seq_id is 1-based (i + 1). */
+int orc_tr_lr_regions(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k,
+                      int32_t min_len, const double *ks, const double *tr, orc_regions *out) {
+  if (nseq < 1) return -1;
+  if (k < 1 || k > ORC_MAX_K) return -2;
+  if (min_len < 0) return -3;
+  for (int32_t q = 0; q < nseq; ++q) orc_trlr_one(seqs[q], lens[q], q + 1, k, min_len, ks, tr, out);
+  return 0;
+}

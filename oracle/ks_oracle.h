@@ -72,6 +72,17 @@ int orc_pm1_table(const int32_t *counts, int32_t k, double *w);
  * A,C,T,G code order, written as out[i*(k+1) .. ] NUL-terminated. */
 int orc_kmer_seq(int32_t k, char *out);
 
+/* tr_lr_regions_r (kmer_spans.c:649-713, find_kmer_tr_lr_regions :329-395):
+ * orc_trlr_remap maps the user-ordered tables (kmers[i] spells entry i) to
+ * 2-bit code order; orc_tr_lr_regions scans with those tables.  Regions are
+ * 1-based (seq_id, beg, end) with the region maximum as score. */
+int orc_trlr_remap(const char *const *kmers, int32_t k, const double *ks_in, const double *tr_in,
+                   double *ks_out, double *tr_out);
+int orc_tr_lr_regions(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k,
+                      int32_t min_len, const double *ks, const double *tr, orc_regions *out);
+void orc_trlr_one(const char *s, int64_t len, int32_t seq_id, int32_t k, int32_t min_len,
+                  const double *ks, const double *tr, orc_regions *out);
+
 /* Single-sequence primitives (exposed for tests). */
 uint64_t orc_count_one(const char *s, int64_t len, int32_t k, int32_t *counts);
 void orc_scan_one(const char *s, int64_t len, int32_t seq_id, int32_t k,

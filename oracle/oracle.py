@@ -53,6 +53,8 @@ def lib():
         L.orc_pm1_table.argtypes = [P, C.c_int32, P]
         L.orc_kmer_seq.argtypes = [C.c_int32, P]
         L.orc_regions_free.argtypes = [P]
+        L.orc_trlr_remap.argtypes = [P, C.c_int32, P, P, P, P]
+        L.orc_tr_lr_regions.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P, P, P]
         _lib = L
     return _lib
 
@@ -180,3 +182,30 @@ def kmer_seq(k: int):
     _check(lib().orc_kmer_seq(k, buf), "kmer_seq")
     raw = buf.raw
     return [raw[i * (k + 1):i * (k + 1) + k].decode() for i in range(4 ** k)]
+
+
+def trlr_remap(kmers, k: int, kmer_scores, trans_scores):
+    """tr_lr_regions_r's remap of user-ordered tables to 2-bit code order:
+    returns (ks, tr, n_bad)."""
+    n = 4 ** k
+    bufs = [C.create_string_buffer(_as_bytes(x)) for x in kmers]
+    ptrs = (C.c_char_p * n)(*[C.cast(b, C.c_char_p) for b in bufs])
+    ks_in = np.ascontiguousarray(kmer_scores, dtype=np.float64)
+    tr_in = np.ascontiguousarray(trans_scores, dtype=np.float64)
+    ks = np.zeros(n, dtype=np.float64)
+    tr = np.zeros(n, dtype=np.float64)
+    bad = lib().orc_trlr_remap(ptrs, k, ks_in.ctypes.data, tr_in.ctypes.data, ks.ctypes.data, tr.ctypes.data)
+    return ks, tr, bad
+
+
+def tr_lr_regions(seqs, k: int, min_len: int, ks, tr):
+    """find_kmer_tr_lr_regions over every sequence with 2-bit-ordered tables;
+    1-based (seq_id, beg, end) and the region maximum."""
+    a = _SeqArgs(seqs)
+    ks = np.ascontiguousarray(ks, dtype=np.float64)
+    tr = np.ascontiguousarray(tr, dtype=np.float64)
+    r = _Regions()
+    _check(lib().orc_tr_lr_regions(a.ptrs, a.lens.ctypes.data, a.n, k, int(min_len), ks.ctypes.data,
+                                   tr.ctypes.data, C.byref(r)), "tr_lr_regions")
+    pos, score = _regions_to_numpy(r)
+    return {"pos": pos, "score": score}

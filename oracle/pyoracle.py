@@ -99,3 +99,87 @@ def regions(seqs, k: int, w, thr: float, min_width: int, min_score: float):
         regs.sort(key=lambda r: r[1])
         out.extend(regs)
     return out, visits.astype(np.uint32).view(np.int32)
+
+
+# ----------------------------------------------------------- tr_lr regions
+#
+# find_kmer_tr_lr_regions (kmer_spans.c:329-395) in decomposition form, the
+# form the HIP path implements.  Per N-free run [a, b) the steps are: the first
+# k-mer's kmer score at position a+k, then the transition score of the k-mer
+# ending at each position a+k .. b-1.  A clamp scan over those steps gives
+# excursions (beg, first argmax, max, end); every excursion passing
+# (pos(argmax) - pos(beg)) >= min_len is a region, and every CLOSED excursion
+# (emitted or not) spawns a fresh rescan of positions (pos(argmax), pos(end)]
+# with transition scores only; an excursion still open at the run end spawns
+# nothing.  A run whose first k-mer ends within the last two bytes of the
+# string is skipped (:341).  Finite tables only (NaN persists in the
+# reference and is exercised against the literal oracle instead).
+
+def _scan_steps(vals):
+    """Clamp scan; excursions [(beg, arg, best, end|None)] over step indices."""
+    exc = []
+    S = 0.0
+    open_ = None
+    for i, v in enumerate(vals):
+        prev = S
+        t = prev + v
+        S = t if t > 0 else 0.0
+        if prev == 0 and S > 0:
+            open_ = [i, i, S]
+        elif open_ is not None:
+            if S == 0:
+                exc.append((open_[0], open_[1], open_[2], i))
+                open_ = None
+            elif S > open_[2]:
+                open_[1], open_[2] = i, S
+    if open_ is not None:
+        exc.append((open_[0], open_[1], open_[2], None))
+    return exc
+
+
+def trlr_regions(seqs, k: int, min_len: int, ks, tr):
+    """1-based regions [(seq_id, beg, end, score)] of tr_lr_regions_r."""
+    ks = np.asarray(ks, dtype=np.float64)
+    tr = np.asarray(tr, dtype=np.float64)
+    mask = (1 << (2 * k)) - 1
+    out = []
+    for q, s in enumerate(seqs):
+        s = s.encode("latin-1") if isinstance(s, str) else bytes(s)
+        L = len(s)
+
+        def kmer_end(p):  # code of bases [p-k+1, p]
+            c = 0
+            for j in range(p - k + 1, p + 1):
+                c = (c << 2) | ((s[j] >> 1) & 3)
+            return c & mask
+
+        regs = []
+        i = 0
+        while i < L:
+            while i < L and _is_n(s[i]):
+                i += 1
+            a = i
+            while i < L and not _is_n(s[i]):
+                i += 1
+            b = i
+            if b - a < k or a + k + 1 >= L:  # :341, the string ends within a base of the k-mer
+                continue
+            pos = [a + k] + list(range(a + k, b))
+            vals = [float(ks[kmer_end(a + k - 1)])] + [float(tr[kmer_end(p)]) for p in range(a + k, b)]
+            work = [(pos, vals, True)]
+            while work:
+                ps, vs, top = work.pop()
+                for beg, arg, best, end in _scan_steps(vs):
+                    pb, pa = ps[beg], ps[arg]
+                    if pa - pb >= min_len:
+                        regs.append((q + 1, pb + 1, pa + 1, best))
+                    if end is None:
+                        assert top, "a rescan ends at 0 (coalescence)"
+                        continue
+                    pe = ps[end]
+                    if pa + 1 <= pe:
+                        rp = list(range(pa + 1, pe + 1))
+                        work.append((rp, [float(tr[kmer_end(p)]) for p in rp], False))
+        regs.sort(key=lambda r: r[1])
+        out.extend(regs)
+    return out

@@ -403,3 +403,85 @@ def test_code12_tables(K, oracle, ctx, monkeypatch, k, ndist, force):
         assert np.array_equal(vis.cpu().numpy(), o["counts"])
     ctx.set_scan_algo(-1)
     tab.close()
+
+
+# ------------------------------------------------------------------ tr_lr
+
+def _trlr_expect(oracle, seqs, k, ml, ks, tr):
+    o = oracle.tr_lr_regions(seqs, k, ml, ks, tr)
+    return o["pos"], o["score"]
+
+
+def test_trlr_random_vs_oracle(K, oracle):
+    """lr.regions through the host entry point (k-mer strings remapped on
+    the host) against the literal oracle: random sequences with N runs,
+    short runs at the string ends, integer and real scores."""
+    rng = random.Random(11)
+    for case in range(150):
+        k = rng.randint(1, 5)
+        n = 4 ** k
+        if case % 2:
+            ks = np.array([rng.randint(-3, 3) for _ in range(n)], float)
+            tr = np.array([rng.randint(-3, 2) for _ in range(n)], float)
+        else:
+            ks = np.array([rng.gauss(0, 1) for _ in range(n)])
+            tr = np.array([rng.gauss(-0.1, 1) for _ in range(n)])
+        seqs = ["".join(rng.choice("ACGTACGTACGTNacgt") for _ in range(rng.randint(0, 400)))
+                for _ in range(rng.randint(1, 4))]
+        ml = rng.choice([0, 1, 3, 10])
+        names = oracle.kmer_seq(k)
+        perm = np.random.default_rng(case).permutation(n)
+        r = K.lr_regions(seqs, (k, ml), [names[p] for p in perm], ks[perm], tr[perm])
+        pos, score = _trlr_expect(oracle, seqs, k, ml, ks, tr)
+        _assert_same_regions(r["pos"], r["score"], pos, score, ("trlr", case))
+        assert np.array_equal(r["kmer_scores"][:, 0], ks) and np.array_equal(r["kmer_scores"][:, 1], tr)
+
+
+@pytest.mark.parametrize("k", [7, 11])
+def test_trlr_device_chunked(K, oracle, ctx, k):
+    """tr_lr on a human-shaped contig through the device path, the chunked
+    scan (giant and small excursions, rescans) and the lane kernel."""
+    import torch
+    from kmer_spans_amd import device as D, genome
+    s = genome.contig(3_000_000, 40 + k, device="cuda", repeats=True)
+    ds = D.from_parts([s, s[:100_000].clone()], [s.numel(), 100_000], "cuda")
+    host = [ds.host_seq(0), ds.host_seq(1)]
+    n, oc = oracle.kmer_counts(host, k)
+    tr = np.log2(oc + 1.0) - np.log2(np.median(oc) + 1.0) - 0.4  # repeats score positive
+    ks = np.random.default_rng(k).normal(size=4 ** k)
+    D.bind_torch_stream(ctx)
+    ttr = D.DeviceTable(ctx, tr, k, 0.0, expand=True)
+    tks = D.DeviceTable(ctx, ks, k, 0.0, compress=False)
+    pos_o, score_o = _trlr_expect(oracle, host, k, 5, ks, tr)
+    assert pos_o.shape[1] >= 1
+    for algo in ALGOS:
+        ctx.set_scan_algo(algo)
+        pos, sc, st = D.tr_lr(ctx, ds, k, ttr, tks, 5)
+        _assert_same_regions(pos, sc, pos_o, score_o, ("trlr-dev", k, algo))
+        assert st["scan_algo"] == algo
+    ctx.set_scan_algo(-1)
+
+
+def test_trlr_nonfinite_tables(K, oracle, ctx):
+    """NaN / infinite scores: the reference's clamp keeps NaN, so these tables
+    take the literal kernel whatever the algorithm setting."""
+    import torch
+    from kmer_spans_amd import device as D, genome
+    k = 6
+    rng = np.random.default_rng(2)
+    tr = rng.normal(size=4 ** k) - 0.1
+    tr[rng.integers(0, 4 ** k, 20)] = np.nan
+    tr[rng.integers(0, 4 ** k, 5)] = np.inf
+    ks = rng.normal(size=4 ** k)
+    ks[:7] = -np.inf
+    s = genome.contig(200_000, 5, device="cuda", repeats=True)
+    ds = D.from_parts([s], [s.numel()], "cuda")
+    D.bind_torch_stream(ctx)
+    ttr = D.DeviceTable(ctx, tr, k, 0.0, expand=True)
+    tks = D.DeviceTable(ctx, ks, k, 0.0, compress=False)
+    pos_o, score_o = _trlr_expect(oracle, [ds.host_seq(0)], k, 0, ks, tr)
+    ctx.set_scan_algo(1)
+    pos, sc, st = D.tr_lr(ctx, ds, k, ttr, tks, 0)
+    _assert_same_regions(pos, sc, pos_o, score_o, "trlr-nan")
+    assert st["scan_algo"] == 0
+    ctx.set_scan_algo(-1)

@@ -58,6 +58,17 @@ def test_validation_errors_before_device():
         K.kmer_low_comp_regions("ACGT", 1, 0, 0.0, thr=1.0)
     with pytest.raises(K.KmerSpansError, match="should be smaller than MAX_K"):
         K.kmer_seq(0)
+    names = K.kmer_seq(1)
+    with pytest.raises(K.KmerSpansError, match="params_r should have two integers"):
+        K.lr_regions("ACGT", (1,), names, [0.0] * 4, [0.0] * 4)
+    with pytest.raises(K.KmerSpansError, match="k should be a positive value less than MAX_K"):
+        K.lr_regions("ACGT", (0, 0), names, [0.0] * 4, [0.0] * 4)
+    with pytest.raises(K.KmerSpansError, match="min_length should be a positive integer"):
+        K.lr_regions("ACGT", (1, -1), names, [0.0] * 4, [0.0] * 4)
+    with pytest.raises(K.KmerSpansError, match="should all be 4\\^k long"):
+        K.lr_regions("ACGT", (2, 0), names, [0.0] * 4, [0.0] * 4)
+    with pytest.raises(K.KmerSpansError, match="seq_r should be a character vector of of positive length"):
+        K.lr_regions([], (1, 0), names, [0.0] * 4, [0.0] * 4)
 
 
 def test_named_scores_reordered():

@@ -139,3 +139,63 @@ def test_log2_pm1_tables(oracle, k):
         assert np.allclose(w, np.log2(f / fmed), equal_nan=True)
     p = oracle.pm1_table(c, k)
     assert np.array_equal(p, np.where(f >= fmed, 1.0, -1.0))
+
+
+# ------------------------------------------------------------------ tr_lr
+
+def _trlr_case(rng):
+    k = rng.randint(1, 4)
+    n = 4 ** k
+    if rng.random() < 0.5:
+        ks = np.array([rng.randint(-3, 3) for _ in range(n)], float)
+        tr = np.array([rng.randint(-3, 2) for _ in range(n)], float)
+    else:
+        ks = np.array([rng.gauss(0, 1) for _ in range(n)])
+        tr = np.array([rng.gauss(-0.2, 1) for _ in range(n)])
+    seqs = ["".join(rng.choice("ACGTACGTACGTNacgt") for _ in range(rng.randint(0, 80)))
+            for _ in range(rng.randint(1, 3))]
+    return k, seqs, rng.choice([0, 0, 1, 2, 5]), ks, tr
+
+
+def test_trlr_known_answers(oracle):
+    """find_kmer_tr_lr_regions traced by hand (k=1, scores A,C,T,G = 1,-1,-3,2
+    for both tables): 1-based records, the first k-mer's score at the position
+    after it, a region ending at the run end without a restart, the :341 skip."""
+    ks = tr = np.array([1.0, -1.0, -3.0, 2.0])
+    def regs(s, ml=0):
+        r = oracle.tr_lr_regions([s], 1, ml, ks, tr)
+        return [tuple(int(x) for x in p) + (float(sc),) for p, sc in zip(r["pos"].T, r["score"][0])]
+    assert regs("CAAAC") == [(1, 2, 4, 3.0)]
+    assert regs("GGNGGG") == [(1, 2, 2, 4.0), (1, 5, 6, 6.0)]
+    assert regs("GGNGGG", ml=1) == [(1, 5, 6, 6.0)]
+    assert regs("GN") == []             # the first k-mer ends two bytes before the end: skipped
+    assert regs("GGN") == [(1, 2, 2, 4.0)]
+    assert regs("GG") == [] and regs("G") == []
+
+
+def test_trlr_decomposition_agrees(oracle):
+    """The decomposition the HIP path implements (every closed excursion
+    rescans its tail, open ones at the run end do not) against the literal
+    restart loop, 3,000 random cases."""
+    from oracle import pyoracle as P
+    rng = random.Random(3)
+    for _ in range(3000):
+        k, seqs, ml, ks, tr = _trlr_case(rng)
+        o = oracle.tr_lr_regions(seqs, k, ml, ks, tr)
+        got = [(int(a), int(b), int(c), float(d)) for (a, b, c), d in zip(o["pos"].T.tolist(), o["score"][0].tolist())]
+        assert got == P.trlr_regions(seqs, k, ml, ks, tr), (k, ml, seqs)
+
+
+def test_trlr_remap(oracle):
+    """tr_lr_regions_r's remap: entry i goes to the code of kmers[i]."""
+    k = 3
+    names = oracle.kmer_seq(k)
+    rng = np.random.default_rng(0)
+    perm = rng.permutation(4 ** k)
+    ks_in = np.arange(4 ** k, dtype=float)[perm]
+    tr_in = -ks_in
+    ks, tr, bad = oracle.trlr_remap([names[p] for p in perm], k, ks_in, tr_in)
+    assert bad == 0
+    assert np.array_equal(ks, np.arange(4 ** k, dtype=float)) and np.array_equal(tr, -ks)
+    _, _, bad = oracle.trlr_remap(["AN"] + names[1:], k, ks_in, tr_in)
+    assert bad == 1

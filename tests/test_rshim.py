@@ -38,7 +38,19 @@ def test_reference_error_strings(R):
          "the threshold must be a REAL vector of length 1"),
         (("kmer_seq_r", R.int_([0])), "k_r (0) should be smaller than MAX_K (16) and larger than 0"),
         (("kmer_seq_r", R.int_([1, 2])), "k_r should be an integer of length 1"),
-        (("tr_lr_regions_r", *[R.int_([0])] * 5), "not part of the MI355X span-scan build"),
+        (("tr_lr_regions_r", R.int_([0]), R.int_([1, 0]), R.str_(["A"]), R.real([0.0]), R.real([0.0])),
+         "seq_r should be a character vector of of positive length"),
+        (("tr_lr_regions_r", R.str_(["ACGT"]), R.int_([1]), R.str_(["A"]), R.real([0.0]), R.real([0.0])),
+         "params_r should have two integers (k, and min_length)"),
+        (("tr_lr_regions_r", R.str_(["ACGT"]), R.int_([1, 0]), R.int_([0]), R.real([0.0]), R.real([0.0])),
+         "kmers_r should be a character vector"),
+        (("tr_lr_regions_r", R.str_(["ACGT"]), R.int_([0, 0]), R.str_(["A"]), R.real([0.0]), R.real([0.0])),
+         "k should be a positive value less than MAX_K"),
+        (("tr_lr_regions_r", R.str_(["ACGT"]), R.int_([1, -1]), R.str_(["A"]), R.real([0.0]), R.real([0.0])),
+         "min_length should be a positive integer"),
+        (("tr_lr_regions_r", R.str_(["ACGT"]), R.int_([1, 0]), R.str_(["A"]), R.real([0.0]), R.real([0.0])),
+         "kmers_r, freq_a, freq_b should all be 4^k long"),
+        (("windowed_kmer_count_distributions_r", *[R.int_([0])] * 5), "not part of the MI355X span-scan build"),
     ]
     for args, msg in cases:
         with pytest.raises(RuntimeError, match=msg.replace("^", "\\^").replace("+", "\\+").replace("(", "\\(").replace(")", "\\)")):
@@ -67,3 +79,21 @@ def test_shim_results_vs_oracle(R, oracle):
     assert np.array_equal(got[0], lc["n"]) and np.array_equal(got[1], lc["counts"])
     assert np.array_equal(got[2], lc["w_rank"])
     assert np.array_equal(np.asarray(got[3]).reshape(3, -1), lc["pos"])
+
+
+@pytest.mark.gpu
+def test_shim_tr_lr_vs_oracle(R, oracle):
+    rng = np.random.default_rng(4)
+    k = 3
+    seqs = ["".join(rng.choice(list("ACGTN"), 2000, p=[.24, .24, .24, .24, .04])), "GGNGGG", "ACGTTTGGA"]
+    names = oracle.kmer_seq(k)
+    perm = rng.permutation(4 ** k)
+    ks = rng.normal(size=4 ** k)
+    tr = rng.normal(size=4 ** k) - 0.2
+    got = R.to_py(R.call("tr_lr_regions_r", R.str_(seqs), R.int_([k, 2]), R.str_([names[p] for p in perm]),
+                         R.real(ks[perm]), R.real(tr[perm])))
+    o = oracle.tr_lr_regions(seqs, k, 2, ks, tr)
+    spectra = np.asarray(got[0])  # 4^k x 2
+    assert np.array_equal(spectra[:, 0], ks) and np.array_equal(spectra[:, 1], tr)
+    assert np.array_equal(np.asarray(got[1]).reshape(3, -1), o["pos"])
+    assert np.array_equal(np.asarray(got[2]).reshape(2, -1)[0], o["score"][0])

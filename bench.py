@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--scale", type=float, default=1.0, help="genome scale (1.0 = 3.09 Gbp)")
     p.add_argument("--k", type=int, default=13)
     p.add_argument("--score", choices=["log2", "pm1", "rank"], default="log2")
+    p.add_argument("--trlr", action="store_true",
+                   help="scan with tr_lr_regions semantics (transition = init = the score table)")
     p.add_argument("--min-width", type=int, default=100)
     p.add_argument("--min-score", type=float, default=20.0)
     p.add_argument("--algo", type=int, default=-1, help="-1 auto, 0 lane-per-run, 1 chunked")
@@ -116,11 +118,16 @@ def main():
     else:
         w, thr = api.rank_table(hc, k, words), 0.75
     t0 = time.time()
+    if args.trlr:  # tr_lr tables carry no threshold: transition = init = w - thr
+        w, thr = np.asarray(w, dtype=np.float64) - thr, 0.0
     table = D.DeviceTable(ctx, w, k, thr, compress=True, expand=not args.no_expand, freq=counts)
+    init_table = D.DeviceTable(ctx, w, k, thr, compress=False) if args.trlr else None
     torch.cuda.synchronize()
     t_table = time.time() - t0
 
     def step():
+        if args.trlr:
+            return D.tr_lr(ctx, ds, k, table, init_table, args.min_width)
         return D.scan(ctx, ds, k, table, args.min_width, args.min_score)
 
     for _ in range(args.warmup):
@@ -164,7 +171,7 @@ def main():
     # HBM traffic per launch of the dominant kernel: rocprofv3 PMC passes of this
     # same workload (tools/gpu_pmc.sh), committed under profiles/
     pmc_path = os.path.join(ROOT, "profiles", "r1_pmc_summary.json")
-    if os.path.exists(pmc_path) and stats[-1]["scan_algo"] == 1:
+    if os.path.exists(pmc_path) and stats[-1]["scan_algo"] == 1 and not args.trlr:
         pmc = json.load(open(pmc_path))
         wl = pmc.get("workload", {})
         if (wl.get("k") == k and wl.get("score") == args.score and wl.get("scale") == args.scale
@@ -177,7 +184,7 @@ def main():
 
     # ---- PCIe-inclusive rate of the host entry point (reported, never `value`)
     host_path = None
-    if args.host_path and rank == 0:
+    if args.host_path and rank == 0 and not args.trlr:
         hs = [ds.host_seq(q) for q in range(ds.nseq)]
         t0 = time.perf_counter()
         hr = api.kmer_regions(hs, k, w, args.min_width, args.min_score, visits=False) if thr == 0.0 else None
@@ -203,16 +210,20 @@ def main():
         ids.sort()
         host = [ds.host_seq(q) for q in ids]
         t0 = time.perf_counter()
-        o = O.scan(host, k, w, thr, args.min_width, args.min_score)
+        if args.trlr:
+            o = O.tr_lr_regions(host, k, args.min_width, w, w)
+        else:
+            o = O.scan(host, k, w, thr, args.min_width, args.min_score)
         t_cpu = time.perf_counter() - t0
         cpu = {"value": round(acc / t_cpu / 1e9, 5), "unit": "Gbases/s", "cores": 1, "kind": "port",
                "sample": f"oracle/ks_oracle.c scan of {len(ids)} contigs ({acc} bp) of the same genome, same table",
                "seconds": round(t_cpu, 3), "host_cpu": cpu_model(), "host_nproc": os.cpu_count()}
         # parity of the sampled contigs: GPU records vs oracle records
-        sel = np.isin(pos[0], ids)
+        one = 1 if args.trlr else 0  # tr_lr ids are 1-based
+        sel = np.isin(pos[0] - one, ids)
         gp = pos[:, sel].copy()
         remap = {q: i for i, q in enumerate(ids)}
-        gp[0] = [remap[int(x)] for x in gp[0]]
+        gp[0] = [remap[int(x) - one] + one for x in gp[0]]
         gs = score[:, sel]
         parity = bool(np.array_equal(gp, o["pos"]) and
                       np.array_equal(gs.view(np.uint64), o["score"].view(np.uint64)))
@@ -226,6 +237,7 @@ def main():
                                f"k={k}, {args.score} score from its own counts, min_width {args.min_width}, "
                                f"min_score {args.min_score}, device-resident",
                    "k": k, "score": args.score, "genome_bp": n_bases, "parallelism": f"contig-shard x{world}",
+                   "scan": "tr_lr_regions" if args.trlr else "kmer_regions",
                    "scan_algo": int(stats[-1]["scan_algo"]), "table_compressed": table.compressed,
                    "table_distinct": table.distinct, "positions_per_read": table.positions_per_read,
                    "code_bits": table.code_bits, "escape_fraction": round(table.escape_fraction, 6)},

@@ -279,7 +279,7 @@ extern "C" ks_status ks_tr_lr_dev(ks_ctx *ctx, const ks_dev_seqs *s, int32_t k, 
   mode.trlr = 1;
   mode.ks = init->d_vals;
   mode.min_len = min_length;
-  mode.finite = trans->all_finite && init->all_finite;
+  mode.finite = trans->no_nan_posinf && init->no_nan_posinf;
   mode.maxabs = std::max(trans->max_abs, init->max_abs);
   return scan_impl(ctx, s, s->offsets_host[s->nseq], k, trans, 0, 0.0, nullptr, out, stats, mode);
 }
@@ -348,7 +348,7 @@ extern "C" ks_status ks_tr_lr_regions(ks_ctx *ctx, const char *const *seqs, cons
     mode.trlr = 1;
     mode.ks = t_ks->d_vals;
     mode.min_len = min_length;
-    mode.finite = t_tr->all_finite && t_ks->all_finite;
+    mode.finite = t_tr->no_nan_posinf && t_ks->no_nan_posinf;
     mode.maxabs = std::max(t_tr->max_abs, t_ks->max_abs);
     rc = scan_impl(ctx, &st.dev, st.total, k, t_tr, 0, 0.0, nullptr, out, nullptr, mode);
   }

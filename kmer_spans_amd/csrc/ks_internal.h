@@ -79,6 +79,7 @@ struct ks_ctx {
   void *pinned = nullptr;
   size_t pinned_bytes = 0;
   hipEvent_t ev[16] = {};
+  int64_t rescan_segcap = 0;  // grow-only rescan capacity per segment (tr_lr rescans outnumber regions)
 };
 
 struct ks_table {
@@ -97,8 +98,8 @@ struct ks_table {
   void *d_ext = nullptr;        // uint64 (J <= 4 codes) or double[4] (J <= 3 values)
   size_t ext_bytes = 0;
   double ms_ext = 0;            // build time
-  bool all_finite = true;       // every s is finite
-  double max_abs = 0.0;         // max |s|
+  bool no_nan_posinf = true;    // no s is NaN or +Inf (-Inf allowed: it clamps to 0)
+  double max_abs = 0.0;         // max |s| over the finite values
   // Narrow codes (ext_bits = 12, J = 5): the 4095 values covering most
   // positions get a 12-bit code (d_map12 -> uint16 code, d_lut12 -> value);
   // code 0xFFF escapes to the base uint16 table for that index.
@@ -172,9 +173,9 @@ ks_status launch_count(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const R
 // transition scores, ks the first-k-mer scores, regions need
 // (max_pos - begin) >= min_len, every closed excursion restarts, output is
 // 1-based.  finite / maxabs describe both tr_lr tables: the chunked path
-// needs finite scores whose partial sums cannot overflow (the reference's
-// clamp keeps NaN, the chunked path's does not); otherwise the literal lane
-// kernel runs.
+// needs scores without NaN or +Inf whose partial sums cannot overflow (the
+// reference's clamp keeps NaN, the chunked path's does not; -Inf clamps to 0
+// in both); otherwise the literal lane kernel runs.
 struct ScanMode {
   int trlr = 0;
   const double *ks = nullptr;

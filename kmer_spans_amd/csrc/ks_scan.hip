@@ -184,10 +184,15 @@ __global__ void __launch_bounds__(64) k_scan_lane_trlr(const uint8_t *__restrict
           if (last == 0 && sc > 0) { best = sc; arg = p; beg = p; }
           if (sc == 0 && last > 0) {
             if (arg - beg >= min_len) push_region(out, sid, beg, arg, best);
-            ps = arg + 1;
+            // rescans (init_step 0) skip a restart whose tail (arg, p] cannot
+            // hold a region: the scan after p is the same either way (the
+            // restarted trajectory is back at 0 at p); whole runs stay literal
+            if (init_step || p - arg - 1 >= (min_len > 1 ? min_len : 1)) {
+              ps = arg + 1;
+              restart = true;
+            }
             beg = arg;
             last = best = 0.0;
-            restart = true;
           } else {
             last = sc;
           }

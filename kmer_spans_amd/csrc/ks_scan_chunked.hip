@@ -131,7 +131,10 @@ __device__ __forceinline__ Emission decide(const EmitCfg &ec, int64_t f, int64_t
   } else {  // tr_lr: positions; every closed excursion rescans (pos(arg), pos(end)]
     const int64_t pb = pos_of(ec, beg, f), pa = pos_of(ec, arg, f), pe = pos_of(ec, end, f);
     e.reg = pa - pb >= ec.min_len;
-    e.res = closed && pe >= pa + 2;  // a one-position tail cannot hold an excursion
+    // ... but only a tail that can hold a region (>= min_len + 1 positions, and
+    // >= 2: a one-position tail cannot even hold an excursion) changes the
+    // output; the scan after the tail is the top-level one either way
+    e.res = closed && pe - pa - 1 >= (ec.min_len > 1 ? ec.min_len : 1);
     e.rbeg = pb;
     e.rend = pa;
     e.res_a = pa + 1 - ec.k;  // lane kernel (tr_lr): positions [res_a + k, res_b)
@@ -1607,12 +1610,15 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   Cand cand{reinterpret_cast<long long *>(cbuf), reinterpret_cast<long long *>(cbuf) + ccap,
             reinterpret_cast<long long *>(cbuf) + 2 * ccap, reinterpret_cast<double *>(cbuf) + 3 * ccap,
             cnts, ccap, csegcap};
-  const int64_t rcap = rb.cap;  // a rescan accompanies a region in the same segment
+  // kmer_regions: a rescan accompanies a region in the same segment; tr_lr
+  // rescans every closed excursion, so its capacity grows on its own
+  const int64_t rsegcap = std::max<int64_t>(rb.segcap, ctx->rescan_segcap);
+  const int64_t rcap = rsegcap * kSegs;
   void *rsb = nullptr;
   KS_TRY(ensure(ctx, SLOT_WORK_A, (size_t)rcap * 20 + 1024, &rsb));
   Rescan rs{reinterpret_cast<int64_t *>(rsb), reinterpret_cast<int64_t *>(rsb) + rcap,
             reinterpret_cast<int32_t *>(reinterpret_cast<int64_t *>(rsb) + 2 * rcap), cnts + kSegs, rcap,
-            rb.segcap};
+            rsegcap};
   // KS_DEBUG_CARRY=1: per-window carry statistics to stderr (diagnostics only)
   static const bool dbg_on = getenv("KS_DEBUG_CARRY") != nullptr;
   long long *dbg = nullptr;
@@ -1764,7 +1770,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     KS_TRY(ensure(ctx, SLOT_CHUNK_C, seg * kSegs * 40 + 1024, &grown));
     return KS_INTERNAL_RETRY;
   }
-  if ((int64_t)res_max > rs.segcap) return KS_INTERNAL_RETRY;  // regions overflowed too: the caller grows
+  if ((int64_t)res_max > rs.segcap) {  // grow the rescan buffer (regions may have overflowed too) and rerun
+    ctx->rescan_segcap = (int64_t)(res_max + res_max / 4 + 64);
+    return KS_INTERNAL_RETRY;
+  }
   const int64_t nres = (int64_t)hc[1];
   if (dbg_on && nres > 0) {  // rescan length histogram (log2 buckets)
     std::vector<int64_t> a(rcap), b(rcap);

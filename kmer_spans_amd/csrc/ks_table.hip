@@ -29,13 +29,14 @@ __global__ void k_sub_thr(const double *__restrict__ w, double thr, double *__re
   }
 }
 
-// max |s| (as the bits of a non-negative double) and a non-finite flag.
+// max |s| over the finite values (as the bits of a non-negative double) and
+// a flag for NaN or +Inf (-Inf only ever clamps to 0).
 __global__ void k_absmax(const double *__restrict__ s, int64_t n, unsigned long long *__restrict__ out) {
   unsigned long long m = 0, bad = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const double v = s[i];
-    if (!isfinite(v)) bad = 1;
-    else m = max(m, (unsigned long long)__double_as_longlong(fabs(v)));
+    if (isfinite(v)) m = max(m, (unsigned long long)__double_as_longlong(fabs(v)));
+    else if (!(v < 0)) bad = 1;  // NaN or +Inf
   }
   for (int d = 32; d >= 1; d >>= 1) {
     m = max(m, (unsigned long long)__shfl_down(m, d, 64));
@@ -322,7 +323,7 @@ extern "C" ks_status ks_table_create_hint(ks_ctx *ctx, const double *w_host, int
     KS_TBL_HIP(hipMemcpyAsync(h_am, d_am, 16, hipMemcpyDeviceToHost, st));
     KS_TBL_HIP(hipStreamSynchronize(st));
     KS_TBL_HIP(hipFree(d_am));
-    t->all_finite = h_am[1] == 0;
+    t->no_nan_posinf = h_am[1] == 0;
     double ma = 0;
     memcpy(&ma, &h_am[0], 8);
     t->max_abs = ma;

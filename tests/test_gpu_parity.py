@@ -462,16 +462,20 @@ def test_trlr_device_chunked(K, oracle, ctx, k):
     ctx.set_scan_algo(-1)
 
 
-def test_trlr_nonfinite_tables(K, oracle, ctx):
-    """NaN / infinite scores: the reference's clamp keeps NaN, so these tables
-    take the literal kernel whatever the algorithm setting."""
+@pytest.mark.parametrize("nan", [True, False])
+def test_trlr_nonfinite_tables(K, oracle, ctx, nan):
+    """NaN / +Inf scores: the reference's clamp keeps NaN, so these tables
+    take the literal kernel whatever the algorithm setting; -Inf alone only
+    ever clamps to 0 and stays on the chunked scan."""
     import torch
     from kmer_spans_amd import device as D, genome
     k = 6
     rng = np.random.default_rng(2)
     tr = rng.normal(size=4 ** k) - 0.1
-    tr[rng.integers(0, 4 ** k, 20)] = np.nan
-    tr[rng.integers(0, 4 ** k, 5)] = np.inf
+    if nan:
+        tr[rng.integers(0, 4 ** k, 20)] = np.nan
+        tr[rng.integers(0, 4 ** k, 5)] = np.inf
+    tr[rng.integers(0, 4 ** k, 9)] = -np.inf
     ks = rng.normal(size=4 ** k)
     ks[:7] = -np.inf
     s = genome.contig(200_000, 5, device="cuda", repeats=True)
@@ -482,6 +486,6 @@ def test_trlr_nonfinite_tables(K, oracle, ctx):
     pos_o, score_o = _trlr_expect(oracle, [ds.host_seq(0)], k, 0, ks, tr)
     ctx.set_scan_algo(1)
     pos, sc, st = D.tr_lr(ctx, ds, k, ttr, tks, 0)
-    _assert_same_regions(pos, sc, pos_o, score_o, "trlr-nan")
-    assert st["scan_algo"] == 0
+    _assert_same_regions(pos, sc, pos_o, score_o, ("trlr-nonfinite", nan))
+    assert st["scan_algo"] == (0 if nan else 1)
     ctx.set_scan_algo(-1)

@@ -223,6 +223,72 @@ ks_status ks_tr_lr_dev(ks_ctx *ctx, const ks_dev_seqs *seqs, int32_t k, const ks
 ks_status ks_count_dev(ks_ctx *ctx, const ks_dev_seqs *seqs, int32_t k, int32_t *counts_dev,
                        double *n_words);
 
+/* ---------------------------------------------------------------------
+ * Ingest: sequence files -> device-resident records,
+ * batched multi-k counting and the reference's binary count files.
+ * --------------------------------------------------------------------- */
+
+/* Records of a FASTA file resident on the device.  The reference reads
+ * sequence files with Biostrings::readDNAStringSet (kmers.to.file,
+ * kmer_spans.R:127-160); here the raw bytes go to HBM and are parsed there
+ * (description lines '>', ';' comments, one '\r' before '\n' dropped, empty
+ * lines skipped, IUPAC DNA letters of either case plus '-', '+', '.'; other
+ * bytes, or sequence before the first description line, are errors).  Kept
+ * bytes are upper-cased (as.character(DNAStringSet)).  seqs can be passed to
+ * ks_scan_dev / ks_tr_lr_dev / ks_count_dev directly. */
+typedef struct ks_fasta {
+  ks_dev_seqs seqs;   /* records with length >= min_len, device bytes + offsets */
+  char **names;       /* seqs.nseq descriptions (the line after '>')            */
+  int64_t n_records;  /* records in the file                                    */
+  int64_t bases_all;  /* bases of all records (seq.size, kmer_spans.R:139)      */
+  int64_t bases_kept; /* bases of the kept records (seq.fsize, :141)            */
+  int32_t device;
+  double ms_upload;   /* host read + H2D (overlapped)                           */
+  double ms_parse;    /* device parse + record selection                        */
+} ks_fasta;
+/* path: plain or gzip FASTA.  Keeps records with length >= min_len (:141). */
+ks_status ks_fasta_load(ks_ctx *ctx, const char *path, int64_t min_len, ks_fasta *out);
+/* The same from an in-memory FASTA text of n bytes. */
+ks_status ks_fasta_parse(ks_ctx *ctx, const char *buf, int64_t n, int64_t min_len, ks_fasta *out);
+/* Copy the kept records' bytes (offsets_host[nseq] bytes) to host memory. */
+ks_status ks_fasta_copy_seqs(const ks_fasta *f, uint8_t *dst);
+void ks_fasta_free(ks_fasta *f);
+
+/* k-mer counting for several k in one pass over device-resident sequences
+ * (kmer.counts per k, kmer_spans.R:149-151).  counts_dev[i]: device
+ * int32[4^ks[i]] accumulated (caller zeroes); n_words[i] as ks_kmer_counts. */
+ks_status ks_count_multi_dev(ks_ctx *ctx, const ks_dev_seqs *seqs, const int32_t *ks, int32_t nk,
+                             int32_t *const *counts_dev, double *n_words);
+
+/* Count file of kmers.to.file / read.kmers (kmer_spans.R:113-186): int32
+ * magic, int32 n, n x int32 4^k, then the n count vectors (int32, native
+ * order). */
+ks_status ks_count_file_write(const char *path, int32_t magic, int32_t nk, const int32_t *ks,
+                              const int32_t *const *counts);
+typedef struct ks_count_file {
+  int32_t valid;      /* 0: wrong magic or n < 1 (read.kmers returns FALSE)   */
+  int32_t nk;
+  int32_t *k;         /* as.integer(log2(4^k) / 2) (:184); -1 for length 0    */
+  int64_t *lens;      /* entries actually read (readBin stops at EOF)         */
+  int32_t **counts;
+} ks_count_file;
+ks_status ks_count_file_read(const char *path, int32_t magic, ks_count_file *out);
+void ks_count_file_free(ks_count_file *f);
+
+/* kmers.to.file(seq.f, out.prefix, k, min.l, magic) -- kmer_spans.R:127-160:
+ * load, drop records shorter than min_l, count every k (ks_count_multi_dev),
+ * write <out_prefix>counts_<k1>_<k2>...bin.  A file that cannot be read, a
+ * bad k, or no record left is the reference's NA result: KS_OK with
+ * written = 0 and the reason in message. */
+typedef struct ks_kmer_file_info {
+  int32_t written;
+  double seq_size, seq_fsize, seq_fl; /* :139-142 */
+  char out_path[4096];
+  char message[512];
+} ks_kmer_file_info;
+ks_status ks_kmers_to_file(ks_ctx *ctx, const char *seq_path, const char *out_prefix, const int32_t *ks,
+                           int32_t nk, double min_l, int32_t magic, ks_kmer_file_info *info);
+
 /* Scan algorithm selection (testing/benchmarking): -1 auto, 0 lane-per-run,
  * 1 chunked carry scan. */
 ks_status ks_ctx_set_scan_algo(ks_ctx *ctx, int32_t algo);

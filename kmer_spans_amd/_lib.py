@@ -44,6 +44,22 @@ class ScanStats(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+class Fasta(C.Structure):
+    _fields_ = [("seqs", DevSeqs), ("names", C.POINTER(C.c_char_p)), ("n_records", C.c_int64),
+                ("bases_all", C.c_int64), ("bases_kept", C.c_int64), ("device", C.c_int32),
+                ("ms_upload", C.c_double), ("ms_parse", C.c_double)]
+
+
+class CountFile(C.Structure):
+    _fields_ = [("valid", C.c_int32), ("nk", C.c_int32), ("k", C.POINTER(C.c_int32)),
+                ("lens", C.POINTER(C.c_int64)), ("counts", C.POINTER(C.POINTER(C.c_int32)))]
+
+
+class KmerFileInfo(C.Structure):
+    _fields_ = [("written", C.c_int32), ("seq_size", C.c_double), ("seq_fsize", C.c_double),
+                ("seq_fl", C.c_double), ("out_path", C.c_char * 4096), ("message", C.c_char * 512)]
+
+
 # Every symbol include/kmer_spans.h declares (tests check they are exported).
 EXPORTS = [
     "ks_last_error", "ks_version", "ks_regions_free", "ks_ctx_create", "ks_ctx_destroy",
@@ -52,6 +68,8 @@ EXPORTS = [
     "ks_table_create", "ks_table_destroy", "ks_table_is_compressed", "ks_table_distinct",
     "ks_table_positions_per_read", "ks_table_create_hint", "ks_table_code_bits", "ks_table_escape_fraction",
     "ks_scan_dev", "ks_count_dev", "ks_ctx_set_scan_algo", "ks_tr_lr_regions", "ks_tr_lr_dev",
+    "ks_fasta_load", "ks_fasta_parse", "ks_fasta_copy_seqs", "ks_fasta_free", "ks_count_multi_dev",
+    "ks_count_file_write", "ks_count_file_read", "ks_count_file_free", "ks_kmers_to_file",
 ]
 
 _lib = None
@@ -94,6 +112,15 @@ def load():
         "ks_count_dev": ([P, P, I32, P, P], I32),
         "ks_tr_lr_regions": ([P, P, P, I32, I32, I32, P, P, P, I64, P, P], I32),
         "ks_tr_lr_dev": ([P, P, I32, P, P, I32, P, P], I32),
+        "ks_fasta_load": ([P, C.c_char_p, I64, P], I32),
+        "ks_fasta_parse": ([P, C.c_char_p, I64, I64, P], I32),
+        "ks_fasta_copy_seqs": ([P, P], I32),
+        "ks_fasta_free": ([P], None),
+        "ks_count_multi_dev": ([P, P, P, I32, P, P], I32),
+        "ks_count_file_write": ([C.c_char_p, I32, I32, P, P], I32),
+        "ks_count_file_read": ([C.c_char_p, I32, P], I32),
+        "ks_count_file_free": ([P], None),
+        "ks_kmers_to_file": ([P, C.c_char_p, C.c_char_p, P, I32, D, I32, P], I32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)
@@ -130,6 +157,7 @@ class Context:
 
     def __init__(self, device: int = 0):
         self.device = device
+        self.stream = -1  # -1: the ctx's own non-blocking stream
         self._h = C.c_void_p()
         check(load().ks_ctx_create(device, C.byref(self._h)))
 
@@ -140,6 +168,7 @@ class Context:
     def set_stream(self, stream_ptr: int | None):
         """hipStream_t as an int; 0/None = HIP's default (null) stream."""
         check(load().ks_ctx_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
+        self.stream = int(stream_ptr or 0)
 
     def set_scan_algo(self, algo: int):
         check(load().ks_ctx_set_scan_algo(self._h, int(algo)))

@@ -8,6 +8,9 @@ layout and error behaviour as /root/reference/kmer_spans.R:
   kmer_low_comp_regions(seq, k, min_w, min_score, thr=0.75) :72-79
   kmer_seq(k)                                     :84-86
   lr_regions(seq, params, kmers, kmer_scores, trans_scores)  :88-99
+  kmers_to_file(seq_f, out_prefix, k, min_l=1e5, magic)      :127-160
+  read_kmers(fname, magic)                        :162-186
+  read_fasta(path, min_len=0)   (readDNAStringSet + as.character, :136-144)
 
 Sequences are a str/bytes or a list of them (R character vectors).  Results
 come from libkmerspans.so on the GPU; nothing here computes a result on the
@@ -188,3 +191,61 @@ def rank_table(counts, k: int, total: float) -> np.ndarray:
     out = np.zeros(4 ** int(k), dtype=np.float64)
     check(load().ks_rank_table(counts.ctypes.data, int(k), float(total), out.ctypes.data))
     return out
+
+
+KMER_MAGIC = 310572  # kmer.magic(), kmer_spans.R:5
+
+
+def kmer_magic() -> int:
+    return KMER_MAGIC
+
+
+def read_fasta(path, min_len: int = 0, device: int = 0):
+    """Read a (plain or gzip) FASTA file, parsed on the GPU: returns
+    (names, sequences) with the sequences upper-cased, records shorter than
+    min_len dropped."""
+    from . import device as D
+    fa = D.load_fasta(None if int(device) == 0 else _lib.context(device), path, min_len)
+    try:
+        return fa.names, [b.decode("latin-1") for b in fa.host_seqs()]
+    finally:
+        fa.close()
+
+
+def kmers_to_file(seq_f, out_prefix, k, min_l=1e5, magic: int = KMER_MAGIC, device: int = 0) -> list:
+    """kmers.to.file: count every k of seq_f's records of length >= min_l into
+    <out_prefix>counts_<k...>.bin.  Returns [seq_f, out_f or None (R's NA),
+    seq.size, seq.fsize, seq.fl] like the reference's list."""
+    ks = np.atleast_1d(np.asarray(k)).astype(np.int32)
+    info = _lib.KmerFileInfo()
+    check(load().ks_kmers_to_file(_ctx(device), str(seq_f).encode(), str(out_prefix).encode(), ks.ctypes.data,
+                                  int(ks.size), float(min_l), int(magic), C.byref(info)))
+    out_f = info.out_path.decode() if info.written else None
+    return [seq_f, out_f, info.seq_size, info.seq_fsize, info.seq_fl]
+
+
+def read_kmers(fname, magic: int = KMER_MAGIC):
+    """read.kmers: {'k': int array, 'counts': [int32 arrays]} or False."""
+    cf = _lib.CountFile()
+    check(load().ks_count_file_read(str(fname).encode(), int(magic), C.byref(cf)))
+    try:
+        if not cf.valid:
+            return False
+        nk = int(cf.nk)
+        ks = np.array([cf.k[i] for i in range(nk)], dtype=np.int32)
+        counts = [np.ctypeslib.as_array(cf.counts[i], shape=(int(cf.lens[i]),)).copy() if cf.lens[i] else
+                  np.zeros(0, dtype=np.int32) for i in range(nk)]
+        return {"k": ks, "counts": counts}
+    finally:
+        load().ks_count_file_free(C.byref(cf))
+
+
+def write_kmers(fname, ks, counts, magic: int = KMER_MAGIC) -> None:
+    """Write a count file in kmers.to.file's format from host count vectors."""
+    ks = np.atleast_1d(np.asarray(ks)).astype(np.int32)
+    arrs = [np.ascontiguousarray(c, dtype=np.int32) for c in counts]
+    for kk, a in zip(ks, arrs):
+        if a.size != 4 ** int(kk):
+            raise KmerSpansError(f"counts for k={int(kk)} must have 4^k entries")
+    ptrs = (C.c_void_p * max(len(arrs), 1))(*[a.ctypes.data for a in arrs])
+    check(load().ks_count_file_write(str(fname).encode(), int(magic), int(ks.size), ks.ctypes.data, ptrs))

@@ -188,6 +188,24 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
                     int32_t min_width, double min_score, int32_t *visits_dev, ks_regions *out,
                     ks_scan_stats *stats, const ScanMode &mode = ScanMode());
 
+// FASTA parse of raw file bytes in HBM (ks_ingest.hip).  On return either
+// err_pos >= 0 (first byte outside the DNA alphabet), first_kept <
+// first_hdr (sequence before the first description line), or out holds the
+// records' bytes (hipMalloc'd, total + 32 bytes, 'N' padded) with host
+// offsets (n_records + 1) and description-line positions.
+struct FastaParse {
+  int64_t n_records = 0, total = 0;
+  int64_t err_pos = -1, first_kept = -1, first_hdr = -1;
+  uint8_t *out = nullptr;
+  std::vector<int64_t> offsets, hdr_pos;
+};
+ks_status fasta_parse_dev(ks_ctx *ctx, const uint8_t *raw, int64_t n, FastaParse *fp);
+// Keep only the records listed (ascending); replaces out / offsets / total.
+ks_status fasta_select_dev(ks_ctx *ctx, FastaParse *fp, const std::vector<int32_t> &keep);
+// Batched k-mer counting (ks_count.hip): one pass for nk values of k.
+ks_status launch_count_multi(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const int32_t *ks, int nk,
+                             int32_t *const *counts_dev, double *n_words);
+
 // Build the expanded table of t (no-op if it exists or does not fit).
 ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t *freq_dev);
 

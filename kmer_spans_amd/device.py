@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import DevSeqs, Regions, ScanStats, check, load, regions_to_numpy
+from ._lib import DevSeqs, Fasta, Regions, ScanStats, check, load, regions_to_numpy
 
 
 @dataclass
@@ -89,6 +89,8 @@ class DeviceTable:
         self.k = k
         self._h = C.c_void_p()
         flags = (1 if compress else 0) | (2 if expand else 0)
+        if freq is not None:
+            _order(ctx)
         check(load().ks_table_create_hint(ctx.handle, w.ctypes.data, k, float(thr), flags,
                                           C.c_void_p(freq.data_ptr()) if freq is not None else None,
                                           C.byref(self._h)))
@@ -130,12 +132,23 @@ def bind_torch_stream(ctx: _lib.Context) -> None:
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
 
 
+def _order(ctx) -> None:
+    """Make torch's pending work on the buffers we are handed visible to the
+    ctx's stream: a no-op when the ctx runs on torch's current stream (see
+    bind_torch_stream), otherwise a wait for torch's stream.  Every library
+    call synchronises its own stream before returning, so results are ready
+    for torch afterwards."""
+    if ctx is None or getattr(ctx, "stream", -1) != torch.cuda.current_stream().cuda_stream:
+        torch.cuda.current_stream().synchronize()
+
+
 def scan(ctx: _lib.Context, ds: DeviceSeqs, k: int, table: DeviceTable, min_width: int, min_score: float,
          visits: torch.Tensor | None = None):
     """ks_scan_dev: returns (pos int32[3, R], score float64[2, R], stats dict)."""
     st = ScanStats()
     r = Regions()
     s = ds.struct()
+    _order(ctx)
     check(load().ks_scan_dev(ctx.handle, C.byref(s), int(k), table._h, int(min_width), float(min_score),
                              C.c_void_p(visits.data_ptr()) if visits is not None else None, C.byref(r),
                              C.byref(st)))
@@ -150,6 +163,7 @@ def tr_lr(ctx: _lib.Context, ds: DeviceSeqs, k: int, trans: DeviceTable, init: D
     st = ScanStats()
     r = Regions()
     s = ds.struct()
+    _order(ctx)
     check(load().ks_tr_lr_dev(ctx.handle, C.byref(s), int(k), trans._h, init._h, int(min_length), C.byref(r),
                               C.byref(st)))
     pos, score = regions_to_numpy(r)
@@ -160,5 +174,86 @@ def count(ctx: _lib.Context, ds: DeviceSeqs, k: int, counts: torch.Tensor) -> fl
     """ks_count_dev: accumulates into counts (int32[4^k] cuda); returns #words."""
     n = C.c_double(0)
     s = ds.struct()
+    _order(ctx)
     check(load().ks_count_dev(ctx.handle, C.byref(s), int(k), C.c_void_p(counts.data_ptr()), C.byref(n)))
     return n.value
+
+
+class FastaSeqs:
+    """Records of a FASTA file parsed on the device (ks_fasta_load /
+    ks_fasta_parse): usable wherever a DeviceSeqs is (scan, tr_lr, count).
+    The device buffers belong to the library and are freed by close()."""
+
+    def __init__(self, f: Fasta):
+        self._f = f
+        n = int(f.seqs.nseq)
+        self.offsets = (np.ctypeslib.as_array(C.cast(f.seqs.offsets_host, C.POINTER(C.c_int64)), shape=(n + 1,)).copy()
+                        if n else np.zeros(1, dtype=np.int64))
+        self.names = [f.names[q].decode("latin-1") for q in range(n)]
+        self.n_records = int(f.n_records)
+        self.bases_all = int(f.bases_all)
+        self.bases_kept = int(f.bases_kept)
+        self.ms_upload = float(f.ms_upload)
+        self.ms_parse = float(f.ms_parse)
+
+    @property
+    def nseq(self) -> int:
+        return int(self.offsets.size - 1)
+
+    @property
+    def total(self) -> int:
+        return int(self.offsets[-1])
+
+    def struct(self) -> DevSeqs:
+        if self._f is None:
+            raise ValueError("FastaSeqs is closed")
+        return self._f.seqs
+
+    def host_bytes(self) -> bytes:
+        """All kept records' bytes, concatenated (device -> host copy)."""
+        buf = np.empty(max(self.total, 1), dtype=np.uint8)
+        check(load().ks_fasta_copy_seqs(C.byref(self._f), buf.ctypes.data))
+        return buf[:self.total].tobytes()
+
+    def host_seqs(self) -> list[bytes]:
+        b = self.host_bytes()
+        return [b[int(a):int(e)] for a, e in zip(self.offsets[:-1], self.offsets[1:])]
+
+    def close(self):
+        if self._f is not None:
+            load().ks_fasta_free(C.byref(self._f))
+            self._f = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def load_fasta(ctx: _lib.Context | None, path: str, min_len: int = 0) -> FastaSeqs:
+    """ks_fasta_load: plain or gzip FASTA -> device-resident records."""
+    f = Fasta()
+    check(load().ks_fasta_load(ctx.handle if ctx is not None else None, str(path).encode(), int(min_len),
+                               C.byref(f)))
+    return FastaSeqs(f)
+
+
+def parse_fasta(ctx: _lib.Context | None, text, min_len: int = 0) -> FastaSeqs:
+    """ks_fasta_parse: FASTA text (str/bytes) -> device-resident records."""
+    b = text.encode("latin-1") if isinstance(text, str) else bytes(text)
+    f = Fasta()
+    check(load().ks_fasta_parse(ctx.handle if ctx is not None else None, b, len(b), int(min_len), C.byref(f)))
+    return FastaSeqs(f)
+
+
+def count_multi(ctx: _lib.Context, ds, ks, counts) -> list[float]:
+    """ks_count_multi_dev: one pass for several k; counts[i] int32[4^ks[i]]
+    cuda tensors (accumulated).  Returns the words counted per k."""
+    ks = np.ascontiguousarray(ks, dtype=np.int32)
+    ptrs = (C.c_void_p * max(len(ks), 1))(*[c.data_ptr() for c in counts])
+    words = np.zeros(max(len(ks), 1), dtype=np.float64)
+    s = ds.struct()
+    _order(ctx)
+    check(load().ks_count_multi_dev(ctx.handle, C.byref(s), ks.ctypes.data, len(ks), ptrs, words.ctypes.data))
+    return [float(w) for w in words[:len(ks)]]

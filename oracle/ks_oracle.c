@@ -393,3 +393,84 @@ int orc_tr_lr_regions(const char *const *seqs, const int64_t *lens, int32_t nseq
   for (int32_t q = 0; q < nseq; ++q) orc_trlr_one(seqs[q], lens[q], q + 1, k, min_len, ks, tr, out);
   return 0;
 }
+
+/* ---------------------------------------------------------------- FASTA */
+
+static int orc_dna_byte(unsigned char c) {
+  return c && strchr("ACGTMRWSYKVHDBNacgtmrwsykvhdbn-+.", c) != NULL;
+}
+
+void orc_fasta_free(orc_fasta *f) {
+  if (!f) return;
+  for (int64_t q = 0; f->names && q < f->nseq; ++q) free(f->names[q]);
+  free(f->names);
+  free(f->seq);
+  free(f->offs);
+  memset(f, 0, sizeof(*f));
+}
+
+int orc_fasta_parse(const char *buf, int64_t n, int64_t min_len, orc_fasta *out) {
+  memset(out, 0, sizeof(*out));
+  out->err_pos = -1;
+  /* pass 1: every record's bytes (kept after the filter below) */
+  int64_t cap = 16, nrec = 0;
+  int64_t *roff = malloc(sizeof(int64_t) * (cap + 1));
+  int64_t *hbeg = malloc(sizeof(int64_t) * cap), *hlen = malloc(sizeof(int64_t) * cap);
+  uint8_t *all = malloc((size_t)n + 1);
+  int64_t nall = 0;
+  roff[0] = 0;
+  int64_t i = 0;
+  while (i < n) {
+    int64_t e = i;
+    while (e < n && buf[e] != '\n') ++e;   /* line [i, e) */
+    int64_t le = e;
+    if (le > i && buf[le - 1] == '\r') --le;
+    if (le > i) {
+      if (buf[i] == '>') {
+        if (nrec == cap) {
+          cap *= 2;
+          roff = realloc(roff, sizeof(int64_t) * (cap + 1));
+          hbeg = realloc(hbeg, sizeof(int64_t) * cap);
+          hlen = realloc(hlen, sizeof(int64_t) * cap);
+        }
+        roff[nrec] = nall;
+        hbeg[nrec] = i + 1;
+        hlen[nrec] = le - i - 1;
+        ++nrec;
+      } else if (buf[i] != ';') {
+        for (int64_t j = i; j < le; ++j) {
+          const unsigned char c = (unsigned char)buf[j];
+          if (!nrec) { out->err_pos = j; goto fail2; }
+          if (!orc_dna_byte(c)) { out->err_pos = j; goto fail1; }
+          all[nall++] = (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c;
+        }
+      }
+    }
+    i = e + 1;
+  }
+  roff[nrec] = nall;
+  out->n_records = nrec;
+  out->bases_all = nall;
+  out->seq = malloc((size_t)nall + 1);
+  out->offs = malloc(sizeof(int64_t) * (nrec + 1));
+  out->names = calloc((size_t)nrec + 1, sizeof(char *));
+  out->offs[0] = 0;
+  for (int64_t r = 0; r < nrec; ++r) {
+    const int64_t len = roff[r + 1] - roff[r];
+    if (len < min_len) continue;
+    memcpy(out->seq + out->offs[out->nseq], all + roff[r], (size_t)len);
+    out->offs[out->nseq + 1] = out->offs[out->nseq] + len;
+    char *nm = malloc((size_t)hlen[r] + 1);
+    memcpy(nm, buf + hbeg[r], (size_t)hlen[r]);
+    nm[hlen[r]] = 0;
+    out->names[out->nseq++] = nm;
+  }
+  free(roff); free(hbeg); free(hlen); free(all);
+  return 0;
+fail1:
+  free(roff); free(hbeg); free(hlen); free(all);
+  return -1;
+fail2:
+  free(roff); free(hbeg); free(hlen); free(all);
+  return -2;
+}

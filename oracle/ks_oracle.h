@@ -83,6 +83,26 @@ int orc_tr_lr_regions(const char *const *seqs, const int64_t *lens, int32_t nseq
 void orc_trlr_one(const char *s, int64_t len, int32_t seq_id, int32_t k, int32_t min_len,
                   const double *ks, const double *tr, orc_regions *out);
 
+/* FASTA reading as kmers.to.file uses it (kmer_spans.R:136-148:
+ * Biostrings::readDNAStringSet, nchar filter, as.character).  Biostrings is
+ * absent here (an R/Bioconductor package, not vendored), so this restates
+ * its documented FASTA rules line by line: a line ends at '\n' with one '\r'
+ * before it dropped; empty lines are skipped; ';' lines are comments; '>'
+ * starts a record whose description is the rest of the line; other lines are
+ * sequence, each byte an IUPAC DNA letter (either case) or '-', '+', '.'.
+ * Returns 0, -1 (invalid byte at *err_pos) or -2 (sequence before the
+ * first description, *err_pos = its first byte).  Records shorter than
+ * min_len are dropped from seq/offs/names (bases_all counts them).
+ * Parity for this function is unpinned against Biostrings itself. */
+typedef struct {
+  int64_t n_records, nseq, bases_all, err_pos;
+  uint8_t *seq;      /* kept bytes, upper-cased */
+  int64_t *offs;     /* nseq + 1 */
+  char **names;      /* nseq */
+} orc_fasta;
+int orc_fasta_parse(const char *buf, int64_t n, int64_t min_len, orc_fasta *out);
+void orc_fasta_free(orc_fasta *f);
+
 /* Single-sequence primitives (exposed for tests). */
 uint64_t orc_count_one(const char *s, int64_t len, int32_t k, int32_t *counts);
 void orc_scan_one(const char *s, int64_t len, int32_t seq_id, int32_t k,

@@ -55,6 +55,8 @@ def lib():
         L.orc_regions_free.argtypes = [P]
         L.orc_trlr_remap.argtypes = [P, C.c_int32, P, P, P, P]
         L.orc_tr_lr_regions.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P, P, P]
+        L.orc_fasta_parse.argtypes = [P, C.c_int64, C.c_int64, P]
+        L.orc_fasta_free.argtypes = [P]
         _lib = L
     return _lib
 
@@ -209,3 +211,56 @@ def tr_lr_regions(seqs, k: int, min_len: int, ks, tr):
                                    tr.ctypes.data, C.byref(r)), "tr_lr_regions")
     pos, score = _regions_to_numpy(r)
     return {"pos": pos, "score": score}
+
+
+class _Fasta(C.Structure):
+    _fields_ = [("n_records", C.c_int64), ("nseq", C.c_int64), ("bases_all", C.c_int64), ("err_pos", C.c_int64),
+                ("seq", C.POINTER(C.c_uint8)), ("offs", C.POINTER(C.c_int64)), ("names", C.POINTER(C.c_char_p))]
+
+
+def fasta_parse(text, min_len: int = 0) -> dict:
+    """FASTA text -> {'names', 'seqs' (bytes, upper-cased), 'n_records',
+    'bases_all'} (orc_fasta_parse); raises OracleError with the failing byte
+    position on invalid input."""
+    b = _as_bytes(text)
+    buf = np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, dtype=np.uint8)
+    f = _Fasta()
+    rc = lib().orc_fasta_parse(buf.ctypes.data, len(b), int(min_len), C.byref(f))
+    if rc != 0:
+        pos = int(f.err_pos)
+        lib().orc_fasta_free(C.byref(f))
+        raise OracleError(("invalid byte" if rc == -1 else "sequence before description") + f" at {pos}")
+    try:
+        n = int(f.nseq)
+        offs = np.ctypeslib.as_array(f.offs, shape=(n + 1,)).copy()
+        data = np.ctypeslib.as_array(f.seq, shape=(max(int(offs[-1]), 1),))[:int(offs[-1])].tobytes()
+        return {"names": [f.names[q].decode("latin-1") for q in range(n)],
+                "seqs": [data[offs[q]:offs[q + 1]] for q in range(n)],
+                "n_records": int(f.n_records), "bases_all": int(f.bases_all)}
+    finally:
+        lib().orc_fasta_free(C.byref(f))
+
+
+def count_file_bytes(magic: int, ks, counts) -> bytes:
+    """kmers.to.file's file image (kmer_spans.R:152-159): R writeBin of
+    as.integer values, little-endian int32: magic, n, n x 4^k, counts."""
+    parts = [np.array([magic, len(ks)], dtype="<i4"), np.array([4 ** int(k) for k in ks], dtype="<i4")]
+    parts += [np.asarray(c, dtype="<i4") for c in counts]
+    return b"".join(p.tobytes() for p in parts)
+
+
+def read_count_file(data: bytes, magic: int):
+    """read.kmers (kmer_spans.R:162-186) on a file image: False on a wrong
+    magic or n < 1, else {'k', 'counts'}; readBin stops short at EOF."""
+    a = np.frombuffer(data[:len(data) // 4 * 4], dtype="<i4")
+    if a.size < 1 or a[0] != magic or a.size < 2 or a[1] < 1:
+        return False
+    kn = int(a[1])
+    lens = a[2:2 + kn]
+    pos = 2 + lens.size
+    counts = []
+    for n in lens:
+        counts.append(a[pos:pos + int(n)].astype(np.int32))
+        pos += int(n)
+    ks = np.array([int(np.log2(float(n)) / 2) if n > 0 else -1 for n in lens], dtype=np.int32)
+    return {"k": ks, "counts": counts}

@@ -289,6 +289,30 @@ typedef struct ks_kmer_file_info {
 ks_status ks_kmers_to_file(ks_ctx *ctx, const char *seq_path, const char *out_prefix, const int32_t *ks,
                            int32_t nk, double min_l, int32_t magic, ks_kmer_file_info *info);
 
+/* ---------------------------------------------------------------------
+ * Windowed k-mer count distributions.
+ * --------------------------------------------------------------------- */
+
+/* windowed_kmer_count_distributions_r(seq_r, kmers_r, k_r, window_r,
+ * ret_flag_r) -- replaces kmer_spans.c:717-793 (window.kmer.dist,
+ * kmer_spans.R:103-118).  In every N-free run of every sequence longer than
+ * window, each window of `window` bases holds window - k + 1 k-mers; for
+ * query k-mer i (kmers[i], k characters, coded by init_kmer :757-758)
+ * dist[i * (window + 1) + c] counts the windows holding it c times
+ * (column-major (window + 1) x kmer_n, overwritten).  seq_included[q] = 1 if
+ * lens[q] > window.  ret_flag & 1: scores[q] (int32 [lens[q] x kmer_n],
+ * column-major, for included q; may be NULL to skip one) receives the count
+ * at every window start, 0 elsewhere.  1 <= k <= 15, window >= 2k. */
+ks_status ks_windowed_dist(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq,
+                           const char *const *kmers, int32_t kmer_n, int32_t k, int32_t window, int32_t ret_flag,
+                           int32_t *dist, int32_t *seq_included, int32_t *const *scores);
+/* Device-resident form: kmer_codes are 2-bit codes (< 4^k); dist_dev
+ * accumulated (caller zeroes); included_dev may be NULL; scores_dev (NULL =
+ * none, zeroed by the caller) holds per sequence q the [len_q x kmer_n]
+ * matrix at element offset kmer_n * offsets[q]. */
+ks_status ks_windowed_dev(ks_ctx *ctx, const ks_dev_seqs *seqs, const uint32_t *kmer_codes, int32_t kmer_n,
+                          int32_t k, int32_t window, int32_t *dist_dev, int32_t *included_dev, int32_t *scores_dev);
+
 /* Scan algorithm selection (testing/benchmarking): -1 auto, 0 lane-per-run,
  * 1 chunked carry scan. */
 ks_status ks_ctx_set_scan_algo(ks_ctx *ctx, int32_t algo);

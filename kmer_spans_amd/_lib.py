@@ -70,6 +70,7 @@ EXPORTS = [
     "ks_scan_dev", "ks_count_dev", "ks_ctx_set_scan_algo", "ks_tr_lr_regions", "ks_tr_lr_dev",
     "ks_fasta_load", "ks_fasta_parse", "ks_fasta_copy_seqs", "ks_fasta_free", "ks_count_multi_dev",
     "ks_count_file_write", "ks_count_file_read", "ks_count_file_free", "ks_kmers_to_file",
+    "ks_windowed_dist", "ks_windowed_dev",
 ]
 
 _lib = None
@@ -121,6 +122,8 @@ def load():
         "ks_count_file_read": ([C.c_char_p, I32, P], I32),
         "ks_count_file_free": ([P], None),
         "ks_kmers_to_file": ([P, C.c_char_p, C.c_char_p, P, I32, D, I32, P], I32),
+        "ks_windowed_dist": ([P, P, P, I32, P, I32, I32, I32, I32, P, P, P], I32),
+        "ks_windowed_dev": ([P, P, P, I32, I32, I32, P, P, P], I32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -11,6 +11,7 @@ layout and error behaviour as /root/reference/kmer_spans.R:
   kmers_to_file(seq_f, out_prefix, k, min_l=1e5, magic)      :127-160
   read_kmers(fname, magic)                        :162-186
   read_fasta(path, min_len=0)   (readDNAStringSet + as.character, :136-144)
+  window_kmer_dist(seq, kmers, window, freq=True, ret_flag=0)  :103-118
 
 Sequences are a str/bytes or a list of them (R character vectors).  Results
 come from libkmerspans.so on the GPU; nothing here computes a result on the
@@ -249,3 +250,47 @@ def write_kmers(fname, ks, counts, magic: int = KMER_MAGIC) -> None:
             raise KmerSpansError(f"counts for k={int(kk)} must have 4^k entries")
     ptrs = (C.c_void_p * max(len(arrs), 1))(*[a.ctypes.data for a in arrs])
     check(load().ks_count_file_write(str(fname).encode(), int(magic), int(ks.size), ks.ctypes.data, ptrs))
+
+
+def r_recycled_freq(dist: np.ndarray) -> np.ndarray:
+    """window.kmer.dist's `dist / colSums(dist)` (kmer_spans.R:116) with R's
+    recycling: the column-major elements are divided by colSums repeated
+    along them, so element [r, c] of an (n x m) matrix is divided by
+    colSums[(r + c * n) % m] -- per-column normalisation only when n % m == 0
+    happens to align, as R computes it."""
+    dist = np.asarray(dist, dtype=np.float64)
+    flat = dist.flatten(order="F")
+    cs = dist.sum(axis=0)
+    return (flat / np.resize(cs, flat.size)).reshape(dist.shape, order="F")
+
+
+def window_kmer_dist(seq, kmers, window: int, freq: bool = True, ret_flag: int = 0, device: int = 0) -> dict:
+    """window.kmer.dist: {'dist': (window + 1) x kmer_n (counts, or R's
+    recycled ratios when freq), 'seq_i': int per sequence, 'scores': None or
+    per sequence an int32 [len x kmer_n] matrix (None where excluded)}.
+    Column j corresponds to kmers[j]."""
+    kmers = [kmers] if isinstance(kmers, (str, bytes)) else list(kmers)
+    kb = [x.encode() if isinstance(x, str) else bytes(x) for x in kmers]
+    if len(set(len(x) for x in kb)) != 1:
+        raise KmerSpansError("All kmers must be of the same size")
+    k = len(kb[0])
+    hs = _HostSeqs(seq)
+    n = len(kb)
+    window = int(window)
+    if window < 0:
+        raise KmerSpansError("The window size must be at least two times k")
+    dist = np.zeros((n, window + 1), dtype=np.int32)
+    inc = np.zeros(max(hs.n, 1), dtype=np.int32)
+    kp = (C.c_char_p * n)(*kb)
+    scores = None
+    sp = None
+    if ret_flag & 1:
+        scores = [np.zeros((n, int(L)), dtype=np.int32) if L > window else None for L in hs.lens[:hs.n]]
+        sp = (C.c_void_p * max(hs.n, 1))(*[s.ctypes.data if s is not None else None for s in scores])
+    check(load().ks_windowed_dist(_ctx(device), hs.ptrs, hs.lens.ctypes.data, hs.n, kp, n, k, window,
+                                  int(ret_flag), dist.ctypes.data, inc.ctypes.data, sp))
+    d = dist.T.copy()
+    if freq:
+        d = r_recycled_freq(d)
+    return {"dist": d, "seq_i": inc[:hs.n].copy(),
+            "scores": [s.T.copy() if s is not None else None for s in scores] if scores is not None else None}

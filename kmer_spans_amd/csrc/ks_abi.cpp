@@ -461,3 +461,86 @@ extern "C" ks_status ks_low_comp_regions(ks_ctx *ctx, const char *const *seqs, c
   if (rc != KS_OK) ks_regions_free(out);
   return rc;
 }
+
+// ----------------------------------------------------------- windowed counts
+
+static ks_status check_windowed(int32_t kmer_n, int32_t k, int32_t window) {
+  if (kmer_n < 1) return fail(KS_ERR_ARG, "kmers_r should be a character vector with at least one element");  // :722-723
+  if (k >= KS_MAX_K + 1)                                       // :729-731 (MAX_K = 16)
+    return fail(KS_ERR_ARG, "kmer sizes larger than or equal to %d not currently supported", KS_MAX_K + 1);
+  if (k < 1) return fail(KS_ERR_ARG, "k must be a positive integer");
+  if (window < 2 * k) return fail(KS_ERR_ARG, "The window size must be at least two times k");  // :738-739
+  return KS_OK;
+}
+
+extern "C" ks_status ks_windowed_dev(ks_ctx *ctx, const ks_dev_seqs *s, const uint32_t *kmer_codes, int32_t kmer_n,
+                                     int32_t k, int32_t window, int32_t *dist_dev, int32_t *included_dev,
+                                     int32_t *scores_dev) {
+  if (!ctx || !kmer_codes || !dist_dev) return fail(KS_ERR_ARG, "null argument");
+  KS_TRY(check_dev_seqs(s));
+  KS_TRY(check_windowed(kmer_n, k, window));
+  for (int32_t i = 0; i < kmer_n; ++i)
+    if (kmer_codes[i] >> (2 * k)) return fail(KS_ERR_ARG, "k-mer code %u out of range for k=%d", kmer_codes[i], k);
+  KS_TRY(activate(ctx));
+  return windowed_impl(ctx, s, s->offsets_host[s->nseq], kmer_codes, kmer_n, k, window, dist_dev, included_dev,
+                       scores_dev);
+}
+
+extern "C" ks_status ks_windowed_dist(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq,
+                                      const char *const *kmers, int32_t kmer_n, int32_t k, int32_t window,
+                                      int32_t ret_flag, int32_t *dist, int32_t *seq_included,
+                                      int32_t *const *scores) {
+  if (nseq < 1 || !seqs || !lens)                              // :720-721
+    return fail(KS_ERR_ARG, "seq_r should be a character vector with at least one element");
+  KS_TRY(check_seqs(seqs, lens, nseq));
+  if (!kmers) return fail(KS_ERR_ARG, "kmers_r should be a character vector with at least one element");
+  if (kmer_n >= 1 && k >= 1 && k <= KS_MAX_K)
+    for (int32_t i = 0; i < kmer_n; ++i)                         // :733-736
+      if (!kmers[i] || (int64_t)strlen(kmers[i]) != k) return fail(KS_ERR_ARG, "All kmers specified must be of the same length");
+  KS_TRY(check_windowed(kmer_n, k, window));
+  if (!dist || !seq_included) return fail(KS_ERR_ARG, "null output");
+  const bool want_pos = (ret_flag & 1) != 0;                   // :763-766
+  if (want_pos && !scores) return fail(KS_ERR_ARG, "null scores output");
+  std::vector<uint32_t> codes((size_t)kmer_n, 0);
+  for (int32_t i = 0; i < kmer_n; ++i) {                       // init_kmer on each query (:757-758)
+    uint64_t c = 0;
+    prime_string(kmers[i], k, &c);
+    codes[i] = (uint32_t)c;
+  }
+  if (!ctx) ctx = ks_default_ctx();
+  if (!ctx) return fail(KS_ERR_DEVICE, "no HIP device available");
+  KS_TRY(activate(ctx));
+  Staged st;
+  KS_TRY(stage(ctx, seqs, lens, nseq, &st));
+  const size_t dn = (size_t)(window + 1) * (size_t)kmer_n;
+  void *d_dist = nullptr, *d_inc = nullptr;
+  KS_TRY(ensure(ctx, SLOT_COUNTS, dn * 4, &d_dist));
+  KS_TRY(ensure(ctx, SLOT_REG_TMP, (size_t)nseq * 4 + 16, &d_inc));
+  KS_HIP(hipMemsetAsync(d_dist, 0, dn * 4, ctx->stream));
+  int32_t *d_pos = nullptr;
+  const size_t pn = want_pos ? (size_t)kmer_n * (size_t)st.total : 0;
+  if (pn) {
+    if (hipMalloc(&d_pos, pn * 4) != hipSuccess)
+      return fail(KS_ERR_NOMEM, "hipMalloc(%zu) for window scores failed", pn * 4);
+    if (hipMemsetAsync(d_pos, 0, pn * 4, ctx->stream) != hipSuccess) {
+      (void)hipFree(d_pos);
+      return fail(KS_ERR_DEVICE, "hipMemsetAsync failed");
+    }
+  }
+  ks_status rc = windowed_impl(ctx, &st.dev, st.total, codes.data(), kmer_n, k, window, (int32_t *)d_dist,
+                               (int32_t *)d_inc, d_pos);
+  hipError_t he = hipSuccess;
+  if (rc == KS_OK) he = hipMemcpyAsync(dist, d_dist, dn * 4, hipMemcpyDeviceToHost, ctx->stream);
+  if (rc == KS_OK && he == hipSuccess)
+    he = hipMemcpyAsync(seq_included, d_inc, (size_t)nseq * 4, hipMemcpyDeviceToHost, ctx->stream);
+  if (rc == KS_OK && he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+  if (rc == KS_OK && he == hipSuccess && pn) {
+    for (int32_t q = 0; q < nseq && he == hipSuccess; ++q)
+      if (seq_included[q] && scores[q])                        // :776-784 (matrix [len x kmer_n])
+        he = hipMemcpy(scores[q], d_pos + (size_t)kmer_n * st.offs[q], (size_t)kmer_n * lens[q] * 4,
+                       hipMemcpyDeviceToHost);
+  }
+  if (d_pos) (void)hipFree(d_pos);
+  if (rc == KS_OK && he != hipSuccess) rc = fail(KS_ERR_DEVICE, "window result copy failed: %s", hipGetErrorString(he));
+  return rc;
+}

@@ -10,7 +10,10 @@
 // consecutive positions, two 16-byte loads per thread covering the 15-byte
 // look-back).  k <= 7: the 4^k histogram is privatised in LDS (<= 64 KiB) and
 // flushed once per block; k >= 8: global atomics into HBM.
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
+#include <cstdlib>
 
 #include "ks_internal.h"
 
@@ -223,10 +226,510 @@ __global__ void __launch_bounds__(256) k_count_multi(const uint8_t *__restrict__
   }
 }
 
+// ------------------------------------------------------------------------
+// Partitioned counting for 4^k histograms far beyond L2 (k >= kPartMinK).
+// Global atomics execute at the memory side (one 64-B request per 4-B add,
+// MI355X_MICROARCH "Global float atomics"), so one random add per k-mer is
+// bound at ~20 G adds/s.  Instead the 2k-bit code is split into a bucket
+// (top T bits) and a bin (low L bits; 2^L counters fit LDS), and the k-mers
+// are partitioned by bucket before each bucket is histogrammed in LDS.
+// The partition is written through L2: a block appends to at most 256
+// bucket tails at a time, so the open lines of all blocks of an XCD fit its
+// L2 and leave it whole.  Hence two levels when T > 8:
+//   L1 k_part<1>   per block: LDS histogram of the top 8 bits -> mat[b][block]
+//                  (exclusive sum over mat: each block's cursor per bucket)
+//      k_part<2>   same positions, same blocks: append the code's low
+//                  2k - 8 bits (u32; u16 when single-level) to its bucket
+//   L2 k_sub<1/2>  per level-1 bucket, C chunks: the same two passes on the
+//                  next T - 8 bits, appending the bin (u16)
+//   k_bins         one block per final bucket (or a share of one): LDS
+//                  histogram of the bins, counts[bucket << L | bin] += h
+// The k-mer test (runs, Q1) is the same code as k_count.
+constexpr int kPartMinK = 11;
+constexpr int kPT = 1024;            // threads per block
+constexpr int kPTile = kPT * kPer;   // positions per tile
+constexpr int kPBlocks = 512;        // persistent blocks, level 1
+constexpr int kT1 = 8;               // level-1 bucket bits
+constexpr int kSubChunks = 8;        // level-2 blocks per level-1 bucket
+
+struct PartGeo {
+  int L, T, T1, T2;
+};
+inline PartGeo part_geo(int k) {
+  const int B = 2 * k;
+  const int L = B <= 14 ? B : (B >= 30 ? 15 : 14);
+  const int T = B - L;
+  const int T1 = T < kT1 ? T : kT1;
+  return {L, T, T1, T - T1};
+}
+
+__global__ void k_part_sum_last(const unsigned long long *__restrict__ mat, const unsigned long long *__restrict__ ex,
+                                size_t n, unsigned long long *__restrict__ last) {
+  *last = ex[n - 1] + mat[n - 1];
+}
+
+// Level 1 over the sequence.  shift = 2k - T1: bucket = code >> shift,
+// payload = code & (2^shift - 1) stored as Item.
+template <int kPass, typename Item>
+__global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, int64_t total,
+                                              const int64_t *__restrict__ offs, int32_t nseq, int k, int shift,
+                                              unsigned long long *__restrict__ mat,
+                                              const unsigned long long *__restrict__ bstart,
+                                              Item *__restrict__ part, int64_t ntiles) {
+  __shared__ uint32_t lds_b[1 << kT1];
+  __shared__ uint32_t bmask[(kPTile + kLook + 32) / 32 + 1];
+  const int nb = 1 << (2 * k - shift);
+  const int G = gridDim.x;
+  if (kPass == 1) {
+    for (int i = threadIdx.x; i < nb; i += kPT) lds_b[i] = 0;
+  } else {
+    for (int i = threadIdx.x; i < nb; i += kPT)
+      lds_b[i] = (uint32_t)(mat[(size_t)i * G + blockIdx.x] - bstart[i]);
+  }
+  const uint32_t mask = (1u << (2 * k)) - 1u;
+  const uint32_t pmask = (1u << shift) - 1u;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
+    const int64_t t0 = tile * kPTile;
+    const int64_t base = t0 - kLook;
+    __syncthreads();
+    for (int i = threadIdx.x; i < (kPTile + kLook + 32) / 32 + 1; i += kPT) bmask[i] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int lo = 0, hi = nseq + 1;
+      while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (offs[mid] < base) lo = mid + 1; else hi = mid;
+      }
+      for (int q = lo; q <= nseq && offs[q] <= t0 + kPTile; ++q) {
+        const int r = (int)(offs[q] - base);
+        bmask[r >> 5] |= 1u << (r & 31);
+      }
+    }
+    __syncthreads();
+    const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
+    if (p0 >= total) continue;
+    uint8_t b[kLook + kPer];
+    if (p0 >= kLook && p0 + kPer <= total) {
+      const uint4 v0 = *reinterpret_cast<const uint4 *>(seq + p0 - kLook);
+      const uint4 v1 = *reinterpret_cast<const uint4 *>(seq + p0);
+      const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+      for (int j = 0; j < kLook + kPer; ++j) b[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+    } else {
+#pragma unroll
+      for (int j = 0; j < kLook + kPer; ++j) {
+        const int64_t q = p0 - kLook + j;
+        b[j] = (q >= 0 && q < total) ? seq[q] : (uint8_t)'N';
+      }
+    }
+    uint32_t code = 0;
+    int len = 0;
+#pragma unroll
+    for (int j = 1; j < kLook + kPer; ++j) {
+      const int64_t q = p0 - kLook + j;
+      const int r = (int)(q - base);
+      if ((bmask[r >> 5] >> (r & 31)) & 1u) len = 0;
+      if (!is_n(b[j])) {
+        code = ((code << 2) | enc(b[j])) & mask;
+        ++len;
+      } else {
+        len = 0;
+      }
+      if (j >= kLook && q < total && len >= k) {
+        const int r1 = r + 1;
+        const bool q1 = (len == k) && ((bmask[r1 >> 5] >> (r1 & 31)) & 1u);
+        if (!q1) {
+          const uint32_t bk = code >> shift;
+          if (kPass == 1) {
+            atomicAdd(&lds_b[bk], 1u);
+          } else {
+            const uint32_t slot = atomicAdd(&lds_b[bk], 1u);
+            part[bstart[bk] + slot] = (Item)(code & pmask);
+          }
+        }
+      }
+    }
+  }
+  if (kPass == 1) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nb; i += kPT) mat[(size_t)i * G + blockIdx.x] = lds_b[i];
+  }
+}
+
+// Level-1 scatter.  Per 16K-position tile the block ranks its k-mers by
+// bucket in LDS (counting sort), then writes each bucket's run of payloads
+// contiguously at the block's cursor: consecutive lanes store consecutive
+// addresses (a lane-per-k-mer scatter issues one memory request per k-mer
+// and is request-bound at ~100 G/s).
+template <typename Item>
+__global__ void __launch_bounds__(kPT) k_part_scatter(const uint8_t *__restrict__ seq, int64_t total,
+                                                      const int64_t *__restrict__ offs, int32_t nseq, int k, int shift,
+                                                      const unsigned long long *__restrict__ ex,
+                                                      Item *__restrict__ part, int64_t ntiles) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+  Item *sorted = reinterpret_cast<Item *>(dyn);               // [kPTile]
+  uint8_t *bkt = dyn + sizeof(Item) * kPTile;                 // [kPTile]
+  __shared__ unsigned long long cur[1 << kT1];
+  __shared__ uint32_t cnt[1 << kT1], off[1 << kT1];
+  __shared__ uint32_t bmask[(kPTile + kLook + 32) / 32 + 1];
+  const int nb = 1 << (2 * k - shift);
+  const int G = gridDim.x;
+  for (int i = threadIdx.x; i < nb; i += kPT) cur[i] = ex[(size_t)i * G + blockIdx.x];
+  const uint32_t mask = (1u << (2 * k)) - 1u;
+  const uint32_t pmask = (1u << shift) - 1u;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
+    const int64_t t0 = tile * kPTile;
+    const int64_t base = t0 - kLook;
+    __syncthreads();
+    for (int i = threadIdx.x; i < (kPTile + kLook + 32) / 32 + 1; i += kPT) bmask[i] = 0;
+    for (int i = threadIdx.x; i < nb; i += kPT) cnt[i] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int lo = 0, hi = nseq + 1;
+      while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (offs[mid] < base) lo = mid + 1; else hi = mid;
+      }
+      for (int q = lo; q <= nseq && offs[q] <= t0 + kPTile; ++q) {
+        const int r = (int)(offs[q] - base);
+        bmask[r >> 5] |= 1u << (r & 31);
+      }
+    }
+    __syncthreads();
+    const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
+    uint32_t br[kPer];   // bucket << 16 | rank, or ~0u
+    uint32_t pay[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) br[j] = ~0u;
+    if (p0 < total) {
+      uint8_t b[kLook + kPer];
+      if (p0 >= kLook && p0 + kPer <= total) {
+        const uint4 v0 = *reinterpret_cast<const uint4 *>(seq + p0 - kLook);
+        const uint4 v1 = *reinterpret_cast<const uint4 *>(seq + p0);
+        const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int j = 0; j < kLook + kPer; ++j) b[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+      } else {
+#pragma unroll
+        for (int j = 0; j < kLook + kPer; ++j) {
+          const int64_t q = p0 - kLook + j;
+          b[j] = (q >= 0 && q < total) ? seq[q] : (uint8_t)'N';
+        }
+      }
+      uint32_t code = 0;
+      int len = 0;
+#pragma unroll
+      for (int j = 1; j < kLook + kPer; ++j) {
+        const int64_t q = p0 - kLook + j;
+        const int r = (int)(q - base);
+        if ((bmask[r >> 5] >> (r & 31)) & 1u) len = 0;
+        if (!is_n(b[j])) {
+          code = ((code << 2) | enc(b[j])) & mask;
+          ++len;
+        } else {
+          len = 0;
+        }
+        if (j >= kLook && q < total && len >= k) {
+          const int r1 = r + 1;
+          const bool q1 = (len == k) && ((bmask[r1 >> 5] >> (r1 & 31)) & 1u);
+          if (!q1) {
+            const uint32_t bk = code >> shift;
+            br[j - kLook] = (bk << 16) | atomicAdd(&cnt[bk], 1u);
+            pay[j - kLook] = code & pmask;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of the (<= 256) bucket counts
+      uint32_t v[4], sum = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int bi = threadIdx.x * 4 + i;
+        v[i] = bi < nb ? cnt[bi] : 0;
+        sum += v[i];
+      }
+      uint32_t inc = sum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if ((int)threadIdx.x >= d) inc += o;
+      }
+      uint32_t run = inc - sum;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int bi = threadIdx.x * 4 + i;
+        if (bi < nb) off[bi] = run;
+        run += v[i];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j)
+      if (br[j] != ~0u) {
+        const uint32_t bk = br[j] >> 16, pos = off[bk] + (br[j] & 0xffffu);
+        sorted[pos] = (Item)pay[j];
+        bkt[pos] = (uint8_t)bk;
+      }
+    __syncthreads();
+    const uint32_t n_items = off[nb - 1] + cnt[nb - 1];
+    for (uint32_t i = threadIdx.x; i < n_items; i += kPT) {
+      const uint32_t bk = bkt[i];
+      part[cur[bk] + (i - off[bk])] = sorted[i];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nb; i += kPT) cur[i] += cnt[i];
+  }
+}
+
+// Level-2 scatter: the same tile-local counting sort on the items of one
+// level-1 bucket chunk, by sub-bucket (<= 128), writing the u16 bins.
+__global__ void __launch_bounds__(kPT) k_sub_scatter(const uint32_t *__restrict__ rem,
+                                                     const unsigned long long *__restrict__ s1, int C, int L, int T2,
+                                                     const unsigned long long *__restrict__ ex2,
+                                                     uint16_t *__restrict__ out) {
+  __shared__ uint16_t sorted[kPTile];
+  __shared__ uint8_t bkt[kPTile];
+  __shared__ unsigned long long cur[128];
+  __shared__ uint32_t cnt[128], off[128];
+  const int b1 = blockIdx.x / C, c = blockIdx.x % C;
+  const int ns = 1 << T2;
+  const unsigned long long a0 = s1[b1], n = s1[b1 + 1] - a0;
+  const unsigned long long a = a0 + n * c / C, e = a0 + n * (c + 1) / C;
+  for (int i = threadIdx.x; i < ns; i += kPT) cur[i] = ex2[((((size_t)b1 << T2) | i) * C) + c];
+  const uint32_t lmask = (1u << L) - 1u;
+  for (unsigned long long t0 = a; t0 < e; t0 += kPTile) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < ns; i += kPT) cnt[i] = 0;
+    __syncthreads();
+    uint32_t br[kPer], pay[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const unsigned long long i = t0 + (unsigned long long)j * kPT + threadIdx.x;
+      br[j] = ~0u;
+      if (i < e) {
+        const uint32_t v = rem[i];
+        const uint32_t sb = v >> L;
+        br[j] = (sb << 16) | atomicAdd(&cnt[sb], 1u);
+        pay[j] = v & lmask;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      uint32_t v0 = threadIdx.x * 2 < (unsigned)ns ? cnt[threadIdx.x * 2] : 0;
+      uint32_t v1 = threadIdx.x * 2 + 1 < (unsigned)ns ? cnt[threadIdx.x * 2 + 1] : 0;
+      uint32_t inc = v0 + v1;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if ((int)threadIdx.x >= d) inc += o;
+      }
+      const uint32_t ex = inc - v0 - v1;
+      if (threadIdx.x * 2 < (unsigned)ns) off[threadIdx.x * 2] = ex;
+      if (threadIdx.x * 2 + 1 < (unsigned)ns) off[threadIdx.x * 2 + 1] = ex + v0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j)
+      if (br[j] != ~0u) {
+        const uint32_t sb = br[j] >> 16, pos = off[sb] + (br[j] & 0xffffu);
+        sorted[pos] = (uint16_t)pay[j];
+        bkt[pos] = (uint8_t)sb;
+      }
+    __syncthreads();
+    const uint32_t n_items = off[ns - 1] + cnt[ns - 1];
+    for (uint32_t i = threadIdx.x; i < n_items; i += kPT) {
+      const uint32_t sb = bkt[i];
+      out[cur[sb] + (i - off[sb])] = sorted[i];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < ns; i += kPT) cur[i] += cnt[i];
+  }
+}
+
+// Level 2 inside level-1 bucket b1 = blockIdx.x / C, chunk c of C:
+// sub-bucket = rem >> L (T2 bits), bin = rem & (2^L - 1).  mat2 index
+// ((b1 << T2) | sub) * C + c, so its exclusive sum orders the final buckets.
+template <int kPass>
+__global__ void __launch_bounds__(kPT) k_sub(const uint32_t *__restrict__ rem,
+                                             const unsigned long long *__restrict__ s1, int C, int L, int T2,
+                                             unsigned long long *__restrict__ mat2,
+                                             const unsigned long long *__restrict__ bstart2,
+                                             uint16_t *__restrict__ out) {
+  __shared__ uint32_t cur[128];
+  const int b1 = blockIdx.x / C, c = blockIdx.x % C;
+  const int ns = 1 << T2;
+  const unsigned long long a0 = s1[b1], n = s1[b1 + 1] - a0;
+  const unsigned long long a = a0 + n * c / C, e = a0 + n * (c + 1) / C;
+  if (kPass == 1) {
+    for (int i = threadIdx.x; i < ns; i += kPT) cur[i] = 0;
+  } else {
+    for (int i = threadIdx.x; i < ns; i += kPT) {
+      const size_t fb = ((size_t)b1 << T2) | i;
+      cur[i] = (uint32_t)(mat2[fb * C + c] - bstart2[fb]);
+    }
+  }
+  __syncthreads();
+  const uint32_t lmask = (1u << L) - 1u;
+  for (unsigned long long i = a + threadIdx.x; i < e; i += kPT) {
+    const uint32_t v = rem[i];
+    const uint32_t sb = v >> L;
+    if (kPass == 1) {
+      atomicAdd(&cur[sb], 1u);
+    } else {
+      const uint32_t slot = atomicAdd(&cur[sb], 1u);
+      out[bstart2[((size_t)b1 << T2) | sb] + slot] = (uint16_t)(v & lmask);
+    }
+  }
+  if (kPass == 1) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < ns; i += kPT) mat2[((((size_t)b1 << T2) | i) * C) + c] = cur[i];
+  }
+}
+
+// bstart[i] = ex[i * stride] (exclusive sums of each bucket's first
+// block); bstart[nb] = total.
+__global__ void k_part_starts(const unsigned long long *__restrict__ ex, int stride, int nb,
+                              unsigned long long *__restrict__ bstart, const unsigned long long *__restrict__ last) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nb) bstart[i] = ex[(size_t)i * stride];
+  if (i == nb) bstart[nb] = *last;
+}
+
+template <bool kOwn>
+__global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
+                                              const unsigned long long *__restrict__ bstart, int L, int split,
+                                              uint32_t *__restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [2^L]
+  const int nbin = 1 << L;
+  const int bucket = blockIdx.x / split, s = blockIdx.x % split;
+  for (int i = threadIdx.x; i < nbin; i += kPT) h[i] = 0;
+  __syncthreads();
+  const unsigned long long a0 = bstart[bucket], a1 = bstart[bucket + 1];
+  const unsigned long long n = a1 - a0;
+  const unsigned long long a = a0 + n * s / split, e = a0 + n * (s + 1) / split;
+  // aligned body: 8 bins per 16-byte load
+  unsigned long long ah = (a + 7) & ~7ull;
+  if (ah > e) ah = e;
+  const unsigned long long eb = ah + ((e - ah) & ~7ull);
+  for (unsigned long long i = a + threadIdx.x; i < ah; i += kPT) atomicAdd(&h[part[i]], 1u);
+  for (unsigned long long i = eb + threadIdx.x; i < e; i += kPT) atomicAdd(&h[part[i]], 1u);
+  const uint4 *v = reinterpret_cast<const uint4 *>(part + ah);
+  const unsigned long long nv = (eb - ah) / 8;
+  for (unsigned long long i = threadIdx.x; i < nv; i += kPT) {
+    const uint4 x = v[i];
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      atomicAdd(&h[w[j] & 0xffffu], 1u);
+      atomicAdd(&h[w[j] >> 16], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t *out = counts + ((size_t)bucket << L);
+  for (int i = threadIdx.x; i < nbin; i += kPT) {
+    const uint32_t c = h[i];
+    if (kOwn) {
+      if (c) out[i] += c;
+    } else if (c) {
+      atomicAdd(&out[i], c);
+    }
+  }
+}
+
 }  // namespace
+
+// Partitioned count of one k into counts_dev (accumulated).
+static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, int32_t *counts_dev,
+                                   double *n_words) {
+  hipStream_t st = ctx->stream;
+  const PartGeo g = part_geo(k);
+  const int nb1 = 1 << g.T1, nbf = 1 << g.T;
+  const int shift = 2 * k - g.T1;
+  const int64_t ntiles = (total + kPTile - 1) / kPTile;
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(kPBlocks, ntiles));
+  const int C = kSubChunks;
+  const size_t m1 = (size_t)nb1 * G, m2 = g.T2 ? (size_t)nbf * C : 0;
+  void *w = nullptr, *p1 = nullptr, *p2 = nullptr, *tmp = nullptr;
+  KS_TRY(ensure(ctx, SLOT_CHUNK_A, (m1 * 2 + m2 * 2 + nb1 + nbf + 8) * 8, &w));
+  unsigned long long *mat1 = static_cast<unsigned long long *>(w);
+  unsigned long long *ex1 = mat1 + m1;
+  unsigned long long *mat2 = ex1 + m1;
+  unsigned long long *ex2 = mat2 + m2;
+  unsigned long long *s1 = ex2 + m2;            // [nb1 + 1]
+  unsigned long long *sf = s1 + nb1 + 1;        // [nbf + 1]
+  unsigned long long *last = sf + nbf + 1;      // [2]
+  const size_t item1 = g.T2 ? 4 : 2;
+  KS_TRY(ensure(ctx, SLOT_CHUNK_B, (size_t)total * item1 + 64, &p1));
+  if (g.T2) KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)total * 2 + 64, &p2));
+  size_t tb = 0, tb2 = 0;
+  KS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, mat1, ex1, (int64_t)m1, st));
+  if (m2) KS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, mat2, ex2, (int64_t)m2, st));
+  tb = std::max(tb, tb2);
+  KS_TRY(ensure(ctx, SLOT_SORT_TMP, tb + 16, &tmp));
+  // level 1
+  if (g.T2) {
+    hipLaunchKernelGGL((k_part<1, uint32_t>), dim3(G), dim3(kPT), 0, st, s->seq, total, s->offsets_dev, s->nseq, k,
+                       shift, mat1, nullptr, nullptr, ntiles);
+  } else {
+    hipLaunchKernelGGL((k_part<1, uint16_t>), dim3(G), dim3(kPT), 0, st, s->seq, total, s->offsets_dev, s->nseq, k,
+                       shift, mat1, nullptr, nullptr, ntiles);
+  }
+  KS_HIP(hipGetLastError());
+  KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, mat1, ex1, (int64_t)m1, st));
+  hipLaunchKernelGGL(k_part_sum_last, dim3(1), dim3(1), 0, st, mat1, ex1, m1, last);
+  hipLaunchKernelGGL(k_part_starts, dim3((nb1 + 1 + 255) / 256), dim3(256), 0, st, ex1, G, nb1, s1, last);
+  if (g.T2) {
+    const size_t lds = (size_t)kPTile * 5;
+    KS_HIP(hipFuncSetAttribute((const void *)k_part_scatter<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
+    hipLaunchKernelGGL(k_part_scatter<uint32_t>, dim3(G), dim3(kPT), lds, st, s->seq, total, s->offsets_dev, s->nseq,
+                       k, shift, ex1, static_cast<uint32_t *>(p1), ntiles);
+  } else {
+    const size_t lds = (size_t)kPTile * 3;
+    KS_HIP(hipFuncSetAttribute((const void *)k_part_scatter<uint16_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
+    hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(G), dim3(kPT), lds, st, s->seq, total, s->offsets_dev, s->nseq,
+                       k, shift, ex1, static_cast<uint16_t *>(p1), ntiles);
+  }
+  KS_HIP(hipGetLastError());
+  const uint16_t *bins = static_cast<const uint16_t *>(p1);
+  unsigned long long *bstart = s1;
+  if (g.T2) {
+    // level 2
+    hipLaunchKernelGGL(k_sub<1>, dim3(nb1 * C), dim3(kPT), 0, st, static_cast<const uint32_t *>(p1), s1, C, g.L,
+                       g.T2, mat2, nullptr, nullptr);
+    KS_HIP(hipGetLastError());
+    KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, mat2, ex2, (int64_t)m2, st));
+    hipLaunchKernelGGL(k_part_sum_last, dim3(1), dim3(1), 0, st, mat2, ex2, m2, last + 1);
+    hipLaunchKernelGGL(k_part_starts, dim3((nbf + 1 + 255) / 256), dim3(256), 0, st, ex2, C, nbf, sf, last + 1);
+    hipLaunchKernelGGL(k_sub_scatter, dim3(nb1 * C), dim3(kPT), 0, st, static_cast<const uint32_t *>(p1), s1, C, g.L,
+                       g.T2, ex2, static_cast<uint16_t *>(p2));
+    KS_HIP(hipGetLastError());
+    bins = static_cast<const uint16_t *>(p2);
+    bstart = sf;
+  }
+  const size_t lds_h = (size_t)4 << g.L;
+  KS_HIP(hipFuncSetAttribute((const void *)k_bins<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_h));
+  KS_HIP(hipFuncSetAttribute((const void *)k_bins<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_h));
+  const int split = nbf >= 2048 ? 1 : (2048 / nbf);
+  if (split == 1)
+    hipLaunchKernelGGL(k_bins<true>, dim3(nbf), dim3(kPT), lds_h, st, bins, bstart, g.L, 1, (uint32_t *)counts_dev);
+  else
+    hipLaunchKernelGGL(k_bins<false>, dim3(nbf * split), dim3(kPT), lds_h, st, bins, bstart, g.L, split,
+                       (uint32_t *)counts_dev);
+  KS_HIP(hipGetLastError());
+  unsigned long long words = 0;
+  KS_HIP(hipMemcpyAsync(&words, last, 8, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipStreamSynchronize(st));
+  *n_words = (double)words;
+  return KS_OK;
+}
 
 ks_status launch_count(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const Runs &, int k,
                        int32_t *counts_dev, double *n_words) {
+  if (k >= kPartMinK && total > 0 && total < ((int64_t)1 << 32) && !getenv("KS_COUNT_ATOMIC"))
+    return count_partitioned(ctx, s, total, k, counts_dev, n_words);
   hipStream_t st = ctx->stream;
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
@@ -256,6 +759,28 @@ ks_status launch_count(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const R
 
 ks_status launch_count_multi(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const int32_t *ks, int nk,
                              int32_t *const *counts_dev, double *n_words) {
+  // k's whose histograms are far beyond L2 take the partitioned counter
+  // one by one; the rest share passes of k_count_multi.
+  const bool part_ok = total > 0 && total < ((int64_t)1 << 32) && !getenv("KS_COUNT_ATOMIC");
+  std::vector<int32_t> rest_k;
+  std::vector<int32_t *> rest_c;
+  std::vector<int> rest_i;
+  for (int i = 0; i < nk; ++i) {
+    if (part_ok && ks[i] >= kPartMinK) {
+      KS_TRY(count_partitioned(ctx, s, total, ks[i], counts_dev[i], &n_words[i]));
+    } else {
+      rest_k.push_back(ks[i]);
+      rest_c.push_back(counts_dev[i]);
+      rest_i.push_back(i);
+    }
+  }
+  if (rest_k.size() < (size_t)nk) {
+    std::vector<double> w(rest_k.size());
+    if (!rest_k.empty())
+      KS_TRY(launch_count_multi(ctx, s, total, rest_k.data(), (int)rest_k.size(), rest_c.data(), w.data()));
+    for (size_t j = 0; j < rest_i.size(); ++j) n_words[rest_i[j]] = w[j];
+    return KS_OK;
+  }
   hipStream_t st = ctx->stream;
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));

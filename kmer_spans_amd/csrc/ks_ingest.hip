@@ -180,9 +180,26 @@ __global__ void __launch_bounds__(kFThreads) k_fa_tile(
   const int64_t kex = block_excl_scan<int64_t>(nkeep, 0, SumOp(), lds4, &ktot);
   const int64_t hex = block_excl_scan<int64_t>(nhdr, 0, SumOp(), lds4, &htot);
   if (!kEmit) {
-    if (bad >= 0) atomicMin(&err[0], (unsigned long long)bad);
-    if (firstk >= 0) atomicMin(&err[1], (unsigned long long)firstk);
-    if (firsth >= 0) atomicMin(&err[2], (unsigned long long)firsth);
+    // block minima first; one atomic per block, and only when it can lower
+    // the current value (after the first tiles, none do)
+    unsigned long long m[3] = {(unsigned long long)bad, (unsigned long long)firstk, (unsigned long long)firsth};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      for (int d = 32; d >= 1; d >>= 1) {
+        const unsigned long long o = __shfl_xor(m[i], d, 64);
+        m[i] = o < m[i] ? o : m[i];
+      }
+    }
+    __shared__ unsigned long long wmin[3][kFThreads / 64];
+    if ((threadIdx.x & 63) == 0)
+      for (int i = 0; i < 3; ++i) wmin[i][threadIdx.x >> 6] = m[i];
+    __syncthreads();
+    if (threadIdx.x < 3) {
+      unsigned long long v = wmin[threadIdx.x][0];
+      for (int w = 1; w < kFThreads / 64; ++w) v = wmin[threadIdx.x][w] < v ? wmin[threadIdx.x][w] : v;
+      if (v != ~0ull && v < __hip_atomic_load(&err[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMin(&err[threadIdx.x], v);
+    }
     if (threadIdx.x == 0) {
       kept_tile[t] = ktot;
       hdr_tile[t] = htot;

@@ -206,6 +206,13 @@ ks_status fasta_select_dev(ks_ctx *ctx, FastaParse *fp, const std::vector<int32_
 ks_status launch_count_multi(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const int32_t *ks, int nk,
                              int32_t *const *counts_dev, double *n_words);
 
+// Windowed k-mer count distributions (ks_windowed.hip).  dist_dev: int32
+// [(window + 1) x kmer_n] accumulated; included_dev (nullable): int32[nseq];
+// pos_dev (nullable, zeroed by the caller): per sequence q an int32
+// [len_q x kmer_n] column-major matrix at kmer_n * offsets[q].
+ks_status windowed_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const uint32_t *qcodes_host, int kmer_n,
+                        int k, int window, int32_t *dist_dev, int32_t *included_dev, int32_t *pos_dev);
+
 // Build the expanded table of t (no-op if it exists or does not fit).
 ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t *freq_dev);
 

@@ -257,3 +257,24 @@ def count_multi(ctx: _lib.Context, ds, ks, counts) -> list[float]:
     _order(ctx)
     check(load().ks_count_multi_dev(ctx.handle, C.byref(s), ks.ctypes.data, len(ks), ptrs, words.ctypes.data))
     return [float(w) for w in words[:len(ks)]]
+
+
+def windowed(ctx: _lib.Context, ds, kmer_codes, k: int, window: int, dist: torch.Tensor,
+             included: torch.Tensor | None = None, scores: torch.Tensor | None = None) -> None:
+    """ks_windowed_dev: dist int32 [kmer_n, window + 1] cuda (accumulated; row
+    i = query i), included int32 [nseq] cuda or None, scores int32 cuda
+    [kmer_n * total] (zeroed; per sequence q the [kmer_n][len_q] block at
+    kmer_n * offsets[q]) or None."""
+    codes = np.ascontiguousarray(kmer_codes, dtype=np.uint32)
+    if dist.dtype != torch.int32 or dist.numel() != codes.size * (int(window) + 1) or not dist.is_cuda:
+        raise _lib.KmerSpansError("dist must be an int32 cuda tensor of kmer_n * (window + 1)")
+    if scores is not None and (scores.dtype != torch.int32 or scores.numel() < codes.size * ds.total):
+        raise _lib.KmerSpansError("scores must be an int32 cuda tensor of kmer_n * total")
+    if included is not None and (included.dtype != torch.int32 or included.numel() < ds.nseq):
+        raise _lib.KmerSpansError("included must be an int32 cuda tensor of nseq")
+    s = ds.struct()
+    _order(ctx)
+    check(load().ks_windowed_dev(ctx.handle, C.byref(s), codes.ctypes.data, int(codes.size), int(k), int(window),
+                                 C.c_void_p(dist.data_ptr()),
+                                 C.c_void_p(included.data_ptr()) if included is not None else None,
+                                 C.c_void_p(scores.data_ptr()) if scores is not None else None))

@@ -213,13 +213,82 @@ SEXP tr_lr_regions_r(SEXP seq_r, SEXP params_r, SEXP kmers_r, SEXP kmer_scores_r
   return ret;
 }
 
-/* Out of the span-scan path: not provided by this build.
- * It stays registered so that a package that registers all six names loads;
- * calling it reports that the routine lives in the reference. */
+/* windowed_kmer_count_distributions_r(seq_r, kmers_r, k_r, window_r, ret_flag_r)
+ * -- :717-793.  Returns list(dist ((window + 1) x kmer_n int), seq.i (int per
+ * sequence: 1 if longer than window), scores (ret_flag & 1: per sequence a
+ * length x kmer_n int matrix, NULL for excluded sequences; else NULL)). */
 SEXP windowed_kmer_count_distributions_r(SEXP seq_r, SEXP kmers_r, SEXP k_r, SEXP window_r, SEXP ret_flag_r) {
-  (void)seq_r; (void)kmers_r; (void)k_r; (void)window_r; (void)ret_flag_r;
-  error("windowed_kmer_count_distributions_r is not part of the MI355X span-scan build (out of scope, see DESIGN.md)");
-  return R_NilValue;
+  if (TYPEOF(seq_r) != STRSXP || length(seq_r) < 1)
+    error("seq_r should be a character vector with at least one element");
+  if (TYPEOF(kmers_r) != STRSXP || length(kmers_r) < 1)
+    error("kmers_r should be a character vector with at least one element");
+  if (TYPEOF(k_r) != INTSXP || length(k_r) != 1)
+    error("k_r should be an integer vector with one element");
+  if (TYPEOF(window_r) != INTSXP || length(window_r) != 1)
+    error("window_r should be an integer vector with one element");
+  if (TYPEOF(ret_flag_r) != INTSXP || length(ret_flag_r) != 1)
+    error("ret_flag_r should a single integer");
+  unsigned int k = (unsigned int)asInteger(k_r);
+  if (k >= MAX_K)
+    error("kmer sizes larger than or equal to %d not currently supported", MAX_K);
+  for (int i = 0; i < length(kmers_r); ++i)
+    if ((unsigned int)length(STRING_ELT(kmers_r, i)) != k)
+      error("All kmers specified must be of the same length");
+  int window = asInteger(window_r);
+  if (window < 2 * (int)k)
+    error("The window size must be at least two times k");
+  unsigned int ret_flag = (unsigned int)asInteger(ret_flag_r);
+  int kmer_n = length(kmers_r);
+  seq_view v = view_seqs(seq_r);
+  const char **kmers = (const char **)R_alloc((size_t)kmer_n, sizeof(char *));
+  for (int i = 0; i < kmer_n; ++i) kmers[i] = CHAR(STRING_ELT(kmers_r, i));
+  SEXP ret = PROTECT(allocVector(VECSXP, 3));
+  SET_VECTOR_ELT(ret, 0, allocMatrix(INTSXP, window + 1, kmer_n));
+  SET_VECTOR_ELT(ret, 1, allocVector(INTSXP, v.n));
+  int32_t **scores = NULL;
+  if (ret_flag & 1) {
+    SET_VECTOR_ELT(ret, 2, allocVector(VECSXP, v.n));
+    scores = (int32_t **)R_alloc((size_t)v.n, sizeof(int32_t *));
+    for (int i = 0; i < v.n; ++i) {
+      scores[i] = NULL;
+      if (v.lens[i] <= window) continue;
+      SET_VECTOR_ELT(VECTOR_ELT(ret, 2), i, allocMatrix(INTSXP, (int)v.lens[i], kmer_n));
+      scores[i] = INTEGER(VECTOR_ELT(VECTOR_ELT(ret, 2), i));
+    }
+  }
+  ks_status st = ks_windowed_dist(NULL, v.ptrs, v.lens, v.n, kmers, kmer_n, (int32_t)k, window, (int32_t)ret_flag,
+                                  INTEGER(VECTOR_ELT(ret, 0)), INTEGER(VECTOR_ELT(ret, 1)), scores);
+  if (st != KS_OK) { UNPROTECT(1); ks_check(st); }
+  UNPROTECT(1);
+  return ret;
+}
+
+/* kmers_to_file_r(seq_f, out_prefix, k, min_l, magic) -- the body of
+ * kmers.to.file (kmer_spans.R:127-160) as one routine over ks_kmers_to_file:
+ * list(seq.f, out.f or NA, seq.size, seq.fsize, seq.fl). */
+SEXP kmers_to_file_r(SEXP seq_f_r, SEXP out_prefix_r, SEXP k_r, SEXP min_l_r, SEXP magic_r) {
+  if (TYPEOF(seq_f_r) != STRSXP || length(seq_f_r) != 1) error("seq.f must be a single file name");
+  if (TYPEOF(out_prefix_r) != STRSXP || length(out_prefix_r) != 1) error("out.prefix must be a single string");
+  if (TYPEOF(k_r) != INTSXP) error("k must be an integer vector");
+  if (TYPEOF(min_l_r) != REALSXP || length(min_l_r) != 1) error("min.l must be a single number");
+  if (TYPEOF(magic_r) != INTSXP || length(magic_r) != 1) error("magic must be a single integer");
+  ks_kmer_file_info info;
+  ks_status st = ks_kmers_to_file(NULL, CHAR(STRING_ELT(seq_f_r, 0)), CHAR(STRING_ELT(out_prefix_r, 0)),
+                                  INTEGER(k_r), length(k_r), REAL(min_l_r)[0], INTEGER(magic_r)[0], &info);
+  ks_check(st);
+  SEXP ret = PROTECT(allocVector(VECSXP, 5));
+  SET_VECTOR_ELT(ret, 0, seq_f_r);
+  if (info.written) {
+    SET_VECTOR_ELT(ret, 1, allocVector(STRSXP, 1));
+    SET_STRING_ELT(VECTOR_ELT(ret, 1), 0, mkChar(info.out_path));
+  } else {
+    SET_VECTOR_ELT(ret, 1, ScalarLogical(NA_LOGICAL));
+  }
+  SET_VECTOR_ELT(ret, 2, ScalarReal(info.seq_size));
+  SET_VECTOR_ELT(ret, 3, ScalarReal(info.seq_fsize));
+  SET_VECTOR_ELT(ret, 4, ScalarReal(info.seq_fl));
+  UNPROTECT(1);
+  return ret;
 }
 
 static const R_CallMethodDef callMethods[] = {
@@ -229,6 +298,7 @@ static const R_CallMethodDef callMethods[] = {
     {"kmer_seq_r", (DL_FUNC)&kmer_seq_r, 1},
     {"tr_lr_regions_r", (DL_FUNC)&tr_lr_regions_r, 5},
     {"windowed_kmer_count_distributions_r", (DL_FUNC)&windowed_kmer_count_distributions_r, 5},
+    {"kmers_to_file_r", (DL_FUNC)&kmers_to_file_r, 5},
     {NULL, NULL, 0}};
 
 void R_init_kmer_spans(DllInfo *info) { R_registerRoutines(info, NULL, callMethods, NULL, NULL); }

@@ -474,3 +474,61 @@ fail2:
   free(roff); free(hbeg); free(hlen); free(all);
   return -2;
 }
+
+/* ------------------------------------------------------- windowed counts */
+
+/* windowed_kmer_count_distributions (:413-449), one sequence: per N-free
+ * run, slide a window of `window` bases; at each window start record, for
+ * every query k-mer, how many of the window's k-mers equal it. */
+static void orc_windowed_one(const unsigned char *s, int64_t len, const uint64_t *kmers, int32_t kmer_n,
+                             uint32_t *kmer_counts, int32_t k, int32_t window, int32_t *dist, int32_t *pos) {
+  const uint64_t mask = ((uint64_t)1 << (2 * k)) - 1;
+  int64_t left = 0, right = 0;
+  uint64_t right_offset = 0, left_offset = 0;
+  while (right < len) {                                          /* :420 */
+    memset(kmer_counts, 0, sizeof(uint32_t) << (2 * k));
+    right = orc_prime(s, len, right, k, &right_offset);          /* :422 */
+    if (right >= len) break;                                     /* :423-424 */
+    left = right;
+    left_offset = right_offset;
+    kmer_counts[right_offset & mask]++;                          /* :427 */
+    while (right < len && !orc_is_n(s[right])) {                 /* :428 */
+      right_offset = (right_offset << 2) | orc_code(s[right]);
+      kmer_counts[right_offset & mask]++;
+      ++right;
+      if ((uint64_t)window > (uint64_t)(right - (left - k))) continue;  /* :432-433 */
+      for (int32_t i = 0; i < kmer_n; ++i) {
+        const uint32_t c = kmer_counts[kmers[i] & mask];
+        dist[(int64_t)i * (window + 1) + c]++;
+        if (pos) pos[(int64_t)i * len + (left - k)] = (int32_t)c;
+      }
+      kmer_counts[left_offset & mask]--;                         /* :446 */
+      left_offset = (left_offset << 2) | orc_code(s[left]);
+      ++left;
+    }
+  }
+}
+
+int orc_windowed_dist(const char *const *seqs, const int64_t *lens, int32_t nseq, const char *const *kmers,
+                      int32_t kmer_n, int32_t k, int32_t window, int32_t *dist, int32_t *seq_included,
+                      int32_t *const *pos) {
+  if (k >= 16 || k < 1) return -1;                              /* :730-731 (MAX_K = 16) */
+  for (int32_t i = 0; i < kmer_n; ++i)
+    if ((int64_t)strlen(kmers[i]) != k) return -2;               /* :733-736 */
+  if (window < 2 * k) return -3;                                 /* :738-739 */
+  uint64_t *codes = calloc((size_t)(kmer_n > 0 ? kmer_n : 1), sizeof(uint64_t));
+  for (int32_t i = 0; i < kmer_n; ++i)
+    orc_prime((const unsigned char *)kmers[i], k, 0, k, codes + i);  /* :757-758 */
+  uint32_t *kc = malloc(sizeof(uint32_t) << (2 * k));
+  memset(dist, 0, sizeof(int32_t) * (size_t)(window + 1) * (size_t)kmer_n);
+  for (int32_t q = 0; q < nseq; ++q) {
+    seq_included[q] = 0;
+    if (lens[q] <= window) continue;                             /* :776-777 */
+    seq_included[q] = 1;
+    orc_windowed_one((const unsigned char *)seqs[q], lens[q], codes, kmer_n, kc, k, window, dist,
+                     pos ? pos[q] : NULL);
+  }
+  free(kc);
+  free(codes);
+  return 0;
+}

@@ -103,6 +103,19 @@ typedef struct {
 int orc_fasta_parse(const char *buf, int64_t n, int64_t min_len, orc_fasta *out);
 void orc_fasta_free(orc_fasta *f);
 
+/* windowed_kmer_count_distributions_r (.Call, kmer_spans.c:717-793) and
+ * windowed_kmer_count_distributions (:413-449).  kmers: kmer_n strings of
+ * length k (their codes via init_kmer, :757-758); dist: int32
+ * [(window + 1) x kmer_n] column-major, zeroed by the callee;
+ * seq_included[nseq]: 1 if len > window (:776-779); pos (may be NULL):
+ * per sequence an int32 [len x kmer_n] column-major matrix, zeroed by the
+ * caller, receiving the window counts at each window start (:443-444).
+ * Returns 0, -1 (k >= 16 or k < 1), -2 (a k-mer string of another length) or
+ * -3 (window < 2k), the reference's error() conditions (:729-742). */
+int orc_windowed_dist(const char *const *seqs, const int64_t *lens, int32_t nseq, const char *const *kmers,
+                      int32_t kmer_n, int32_t k, int32_t window, int32_t *dist, int32_t *seq_included,
+                      int32_t *const *pos);
+
 /* Single-sequence primitives (exposed for tests). */
 uint64_t orc_count_one(const char *s, int64_t len, int32_t k, int32_t *counts);
 void orc_scan_one(const char *s, int64_t len, int32_t seq_id, int32_t k,

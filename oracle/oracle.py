@@ -56,6 +56,7 @@ def lib():
         L.orc_trlr_remap.argtypes = [P, C.c_int32, P, P, P, P]
         L.orc_tr_lr_regions.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P, P, P]
         L.orc_fasta_parse.argtypes = [P, C.c_int64, C.c_int64, P]
+        L.orc_windowed_dist.argtypes = [P, P, C.c_int32, P, C.c_int32, C.c_int32, C.c_int32, P, P, P]
         L.orc_fasta_free.argtypes = [P]
         _lib = L
     return _lib
@@ -264,3 +265,27 @@ def read_count_file(data: bytes, magic: int):
         pos += int(n)
     ks = np.array([int(np.log2(float(n)) / 2) if n > 0 else -1 for n in lens], dtype=np.int32)
     return {"k": ks, "counts": counts}
+
+
+def windowed_dist(seqs, kmers, k: int, window: int, ret_flag: int = 0) -> dict:
+    """windowed_kmer_count_distributions_r (kmer_spans.c:717-793):
+    {'dist': int32[window + 1, kmer_n], 'seq_i': int32[nseq],
+    'scores': None or per sequence int32[len, kmer_n] (None where excluded)}."""
+    sa = _SeqArgs(seqs)
+    kb = [_as_bytes(x) for x in kmers]
+    kp = (C.c_char_p * max(len(kb), 1))(*kb)
+    n = len(kb)
+    dist = np.zeros((n, window + 1), dtype=np.int32)  # column-major [window+1, n]
+    inc = np.zeros(max(sa.n, 1), dtype=np.int32)
+    pos = None
+    pp = None
+    if ret_flag & 1:
+        pos = [np.zeros((n, int(L)), dtype=np.int32) for L in sa.lens[:sa.n]]
+        pp = (C.c_void_p * max(sa.n, 1))(*[p.ctypes.data for p in pos])
+    rc = lib().orc_windowed_dist(sa.ptrs, sa.lens.ctypes.data, sa.n, kp, n, int(k), int(window),
+                                 dist.ctypes.data, inc.ctypes.data, pp)
+    _check(rc, "windowed_dist")
+    scores = None
+    if pos is not None:
+        scores = [p.T.copy() if inc[i] else None for i, p in enumerate(pos)]
+    return {"dist": dist.T.copy(), "seq_i": inc[:sa.n].copy(), "scores": scores}

@@ -10,6 +10,7 @@ struct SEXPREC {
   void *data;
 };
 #define NILSXP 0
+#define LGLSXP 10
 #define CHARSXP 9
 #define INTSXP 13
 #define REALSXP 14
@@ -28,6 +29,10 @@ SEXP SET_VECTOR_ELT(SEXP x, R_xlen_t i, SEXP v);
 SEXP allocVector(int type, R_xlen_t n);
 SEXP allocMatrix(int type, int nrow, int ncol);
 SEXP mkChar(const char *s);
+#define NA_LOGICAL (-2147483647 - 1)
+SEXP ScalarLogical(int x);
+SEXP ScalarReal(double x);
+int asInteger(SEXP x);
 SEXP PROTECT(SEXP x);
 void UNPROTECT(int n);
 /* as in R, error() is a macro for Rf_error (glibc also exports error(3)) */

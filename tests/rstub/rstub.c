@@ -40,7 +40,7 @@ const char *rs_error(void) { return errbuf; }
 
 static size_t elt_size(int type) {
   switch (type) {
-    case INTSXP: return sizeof(int);
+    case INTSXP: case LGLSXP: return sizeof(int);
     case REALSXP: return sizeof(double);
     case STRSXP: case VECSXP: return sizeof(SEXP);
     case CHARSXP: return 1;
@@ -64,6 +64,16 @@ SEXP allocMatrix(int type, int nrow, int ncol) {
   x->ncol = ncol;
   return x;
 }
+SEXP ScalarLogical(int v) {
+  SEXP x = allocVector(LGLSXP, 1);
+  ((int *)x->data)[0] = v;
+  return x;
+}
+SEXP ScalarReal(double v) {
+  SEXP x = allocVector(REALSXP, 1);
+  ((double *)x->data)[0] = v;
+  return x;
+}
 SEXP mkChar(const char *s) {
   size_t n = strlen(s);
   SEXP x = allocVector(CHARSXP, (R_xlen_t)n);
@@ -73,6 +83,11 @@ SEXP mkChar(const char *s) {
 int TYPEOF(SEXP x) { return x->type; }
 int length(SEXP x) { return (int)x->len; }
 int *INTEGER(SEXP x) { return (int *)x->data; }
+int asInteger(SEXP x) {
+  if (x->len < 1) return NA_LOGICAL;
+  if (x->type == REALSXP) return (int)((double *)x->data)[0];
+  return ((int *)x->data)[0];
+}
 double *REAL(SEXP x) { return (double *)x->data; }
 const char *CHAR(SEXP x) { return (const char *)x->data; }
 SEXP STRING_ELT(SEXP x, R_xlen_t i) { return ((SEXP *)x->data)[i]; }

@@ -1,7 +1,8 @@
 """The R .Call shim (kmer_spans_amd/rcall/kmer_spans_call.c) through the
 tests/rstub R C-API emulation: the six registered routines of the reference
 (kmer_spans.c:795-802) with their arities, error strings, and -- on a GPU --
-results equal to the oracle."""
+results equal to the oracle; plus kmers_to_file_r, the body of kmers.to.file
+(kmer_spans.R:127-160) as one routine."""
 import numpy as np
 import pytest
 
@@ -14,7 +15,8 @@ def R():
 
 def test_registration_table(R):
     assert R.routines() == {"kmer_counts": 2, "kmer_regions_r": 5, "kmer_low_comp_regions": 5,
-                            "kmer_seq_r": 1, "tr_lr_regions_r": 5, "windowed_kmer_count_distributions_r": 5}
+                            "kmer_seq_r": 1, "tr_lr_regions_r": 5, "windowed_kmer_count_distributions_r": 5,
+                            "kmers_to_file_r": 5}
 
 
 def test_reference_error_strings(R):
@@ -50,7 +52,22 @@ def test_reference_error_strings(R):
          "min_length should be a positive integer"),
         (("tr_lr_regions_r", R.str_(["ACGT"]), R.int_([1, 0]), R.str_(["A"]), R.real([0.0]), R.real([0.0])),
          "kmers_r, freq_a, freq_b should all be 4^k long"),
-        (("windowed_kmer_count_distributions_r", *[R.int_([0])] * 5), "not part of the MI355X span-scan build"),
+        (("windowed_kmer_count_distributions_r", R.int_([0]), R.str_(["AC"]), R.int_([2]), R.int_([6]), R.int_([0])),
+         "seq_r should be a character vector with at least one element"),
+        (("windowed_kmer_count_distributions_r", R.str_(["ACGT"]), R.int_([0]), R.int_([2]), R.int_([6]), R.int_([0])),
+         "kmers_r should be a character vector with at least one element"),
+        (("windowed_kmer_count_distributions_r", R.str_(["ACGT"]), R.str_(["AC"]), R.int_([2, 3]), R.int_([6]),
+          R.int_([0])), "k_r should be an integer vector with one element"),
+        (("windowed_kmer_count_distributions_r", R.str_(["ACGT"]), R.str_(["AC"]), R.int_([2]), R.real([6.0]),
+          R.int_([0])), "window_r should be an integer vector with one element"),
+        (("windowed_kmer_count_distributions_r", R.str_(["ACGT"]), R.str_(["AC"]), R.int_([2]), R.int_([6]),
+          R.real([0.0])), "ret_flag_r should a single integer"),
+        (("windowed_kmer_count_distributions_r", R.str_(["ACGT"]), R.str_(["AC"]), R.int_([16]), R.int_([40]),
+          R.int_([0])), "kmer sizes larger than or equal to 16 not currently supported"),
+        (("windowed_kmer_count_distributions_r", R.str_(["ACGT"]), R.str_(["AC", "ACG"]), R.int_([2]), R.int_([6]),
+          R.int_([0])), "All kmers specified must be of the same length"),
+        (("windowed_kmer_count_distributions_r", R.str_(["ACGT"]), R.str_(["AC"]), R.int_([2]), R.int_([3]),
+          R.int_([0])), "The window size must be at least two times k"),
     ]
     for args, msg in cases:
         with pytest.raises(RuntimeError, match=msg.replace("^", "\\^").replace("+", "\\+").replace("(", "\\(").replace(")", "\\)")):
@@ -97,3 +114,20 @@ def test_shim_tr_lr_vs_oracle(R, oracle):
     assert np.array_equal(spectra[:, 0], ks) and np.array_equal(spectra[:, 1], tr)
     assert np.array_equal(np.asarray(got[1]).reshape(3, -1), o["pos"])
     assert np.array_equal(np.asarray(got[2]).reshape(2, -1)[0], o["score"][0])
+
+
+@pytest.mark.gpu
+def test_shim_windowed_vs_oracle(R, oracle):
+    rng = np.random.default_rng(4)
+    seqs = ["".join(rng.choice(list("ACGTN"), 5000, p=[.24, .24, .24, .24, .04])), "CGCCAATGCG", "ACGTACGTAC" * 3]
+    kmers = ["CG", "GC", "AA", "NN", "TT"]
+    o = oracle.windowed_dist(seqs, kmers, 2, 12, 1)
+    got = R.to_py(R.call("windowed_kmer_count_distributions_r", R.str_(seqs), R.str_(kmers), R.int_([2]),
+                         R.int_([12]), R.int_([1])))
+    assert np.array_equal(got[0], o["dist"])
+    assert np.array_equal(got[1], o["seq_i"])
+    for g, w in zip(got[2], o["scores"]):
+        if w is None:
+            assert g is None
+        else:
+            assert np.array_equal(g, w)

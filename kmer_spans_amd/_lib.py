@@ -13,7 +13,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkmerspans.so")
+# KS_LIB_PATH: an alternative build of the same library (kernel-variant
+# experiments, tools/p1_variants.sh); the in-tree build is the default.
+LIB_PATH = os.environ.get("KS_LIB_PATH") or os.path.join(_HERE, "libkmerspans.so")
 
 KS_OK = 0
 KS_MAX_K = 15

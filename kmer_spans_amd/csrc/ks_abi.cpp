@@ -163,6 +163,7 @@ extern "C" ks_status ks_ctx_create(int32_t device, ks_ctx **out) {
   KS_HIP(hipGetDeviceProperties(&prop, device));
   c->num_cus = prop.multiProcessorCount;
   for (auto &e : c->ev) KS_HIP(hipEventCreate(&e));
+  KS_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
   *out = c;
   return KS_OK;
 }
@@ -176,6 +177,10 @@ extern "C" void ks_ctx_destroy(ks_ctx *c) {
   if (c->pinned) (void)hipHostFree(c->pinned);
   for (auto &e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  if (c->side) {
+    (void)hipStreamSynchronize(c->side);
+    (void)hipStreamDestroy(c->side);
+  }
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

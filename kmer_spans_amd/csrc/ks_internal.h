@@ -58,6 +58,7 @@ enum Slot : int {
   SLOT_WORK_B,
   SLOT_TABLE_TMP,
   SLOT_LAYOUT,      // run layout (chunk / tile bases)
+  SLOT_PACKED,      // 2-bit base codes of the whole buffer (find_runs, want_packed)
   SLOT_COUNT
 };
 
@@ -79,6 +80,7 @@ struct ks_ctx {
   void *pinned = nullptr;
   size_t pinned_bytes = 0;
   hipEvent_t ev[16] = {};
+  hipStream_t side = nullptr;  // forked work that overlaps the main stream (joined by events)
   int64_t rescan_segcap = 0;  // grow-only rescan capacity per segment (tr_lr rescans outnumber regions)
 };
 
@@ -127,6 +129,9 @@ struct Runs {
   int64_t *b = nullptr;
   int32_t *seq = nullptr;
   int64_t n = 0;
+  // optional: enc() of every byte, 16 per word, first base most significant
+  // (word p >> 4, bits 30 - 2 * (p & 15)); total / 16 + 1 words
+  const uint32_t *packed = nullptr;
 };
 
 // Scan indices per chunk of the chunked scan, chunks per stitch tile.
@@ -165,7 +170,8 @@ struct RegionBuf {
 };
 
 // Launch wrappers (defined in the .hip files).
-ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs, float *ms);
+ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs, float *ms,
+                    bool want_packed = false);
 ks_status launch_count(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const Runs &runs, int k,
                        int32_t *counts_dev, double *n_words);
 // Which span scan a call performs.  trlr = 0: kmer_regions (kmer_spans.c:

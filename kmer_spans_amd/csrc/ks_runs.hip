@@ -27,6 +27,13 @@ __device__ __forceinline__ uint32_t n_mask4(uint32_t w) {
   return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
 }
 
+// enc() (kmer_spans.c:34-35: (c >> 1) & 3) of the 4 bytes of w as one byte,
+// first (lowest-addressed) byte in the top two bits.
+__device__ __forceinline__ uint32_t enc_pack4(uint32_t w) {
+  const uint32_t t = (w >> 1) & 0x03030303u;
+  return ((t & 3u) << 6) | (((t >> 8) & 3u) << 4) | (((t >> 16) & 3u) << 2) | ((t >> 24) & 3u);
+}
+
 // Appends the events of `cnt` set bits of starts/ends (bit i <-> p0 + i).
 __device__ __forceinline__ void append_events(uint32_t starts, uint32_t ends, int64_t p0,
                                               unsigned long long *__restrict__ ev,
@@ -60,9 +67,13 @@ __device__ __forceinline__ void append_events(uint32_t starts, uint32_t ends, in
 // N-transition events of the whole buffer read as one string with N before
 // position 0 and at position total: START at p (first non-N byte after an N),
 // END at p (first N after a non-N byte).  16 bytes per step, persistent grid.
+// packed (optional): the same pass stores the 2-bit codes of the 16 bytes as
+// one word (bytes past total encode as 'N'), which the gather pass of the
+// chunked scan reads instead of the bytes (a quarter of the lines).
 __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ seq, int64_t total,
                                                   unsigned long long *__restrict__ ev,
-                                                  unsigned long long *__restrict__ ev_count, int64_t cap) {
+                                                  unsigned long long *__restrict__ ev_count, int64_t cap,
+                                                  uint32_t *__restrict__ packed) {
   const int64_t nunits = total / 16 + 1;  // covers position total
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t u0 = (int64_t)blockIdx.x * blockDim.x; u0 < nunits; u0 += stride) {
@@ -74,9 +85,16 @@ __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ se
       if (p0 + 16 <= total) {
         const uint4 v = *reinterpret_cast<const uint4 *>(seq + p0);
         nm = n_mask4(v.x) | (n_mask4(v.y) << 4) | (n_mask4(v.z) << 8) | (n_mask4(v.w) << 12);
+        if (packed)
+          packed[u] = (enc_pack4(v.x) << 24) | (enc_pack4(v.y) << 16) | (enc_pack4(v.z) << 8) | enc_pack4(v.w);
       } else {
-        for (int j = 0; j < 16; ++j)
-          if (p0 + j < total && !is_n(seq[p0 + j])) nm &= ~(1u << j);
+        uint32_t pw = 0;
+        for (int j = 0; j < 16; ++j) {
+          const uint8_t c = p0 + j < total ? seq[p0 + j] : (uint8_t)'N';
+          if (p0 + j < total && !is_n(c)) nm &= ~(1u << j);
+          pw |= enc(c) << (30 - 2 * j);
+        }
+        if (packed) packed[u] = pw;
       }
       const uint32_t prev_n = (p0 == 0) ? 1u : (is_n(seq[p0 - 1]) ? 1u : 0u);
       const uint32_t non = ~nm & 0xffffu;
@@ -201,9 +219,16 @@ ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int t
   return KS_OK;
 }
 
-ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs, float *ms) {
+ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs, float *ms, bool want_packed) {
   hipStream_t st = ctx->stream;
   KS_HIP(hipEventRecord(ctx->ev[0], st));
+  uint32_t *packed = nullptr;
+  if (want_packed) {
+    void *pp = nullptr;
+    KS_TRY(ensure(ctx, SLOT_PACKED, (size_t)(total / 16 + 1) * 4, &pp));
+    packed = static_cast<uint32_t *>(pp);
+  }
+  runs->packed = nullptr;
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
   unsigned long long *d_count = reinterpret_cast<unsigned long long *>(scal);
@@ -217,7 +242,7 @@ ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs
     const int64_t nunits = total / 16 + 1;
     const unsigned grid = (unsigned)std::min<int64_t>((nunits + 255) / 256, (int64_t)ctx->num_cus * 16);
     hipLaunchKernelGGL(k_n_events, dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp,
-                       d_count, cap);
+                       d_count, cap, packed);
     KS_HIP(hipGetLastError());
     if (s->nseq > 1) {
       hipLaunchKernelGGL(k_seq_events, dim3((unsigned)((s->nseq + 255) / 256)), dim3(256), 0, st, s->seq, total,
@@ -232,6 +257,7 @@ ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs
   if (n_ev & 1ull) return fail(KS_ERR_INTERNAL, "run segmentation produced an odd event count");
   const int64_t nruns = (int64_t)(n_ev / 2);
   runs->n = nruns;
+  runs->packed = packed;
   if (nruns == 0) {
     KS_HIP(hipEventRecord(ctx->ev[1], st));
     KS_HIP(hipEventSynchronize(ctx->ev[1]));

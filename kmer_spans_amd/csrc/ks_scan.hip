@@ -291,7 +291,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
   KS_HIP(hipEventRecord(ctx->ev[2], st));
   Runs runs;
   float ms_runs = 0;
-  KS_TRY(find_runs(ctx, s, total, &runs, &ms_runs));
+  KS_TRY(find_runs(ctx, s, total, &runs, &ms_runs, /*want_packed=*/true));
   S->ms_runs = ms_runs;
   // chunk layout, statistics and algorithm choice (device-side, one sync)
   RunLayout lay;

@@ -170,6 +170,9 @@ __device__ __forceinline__ size_t code_slot(int64_t c, int i) {
   return ((((size_t)(c >> 6) * (CH / 4) + (size_t)(i >> 2)) * 64 + (size_t)(c & 63)) << 2) + (size_t)(i & 3);
 }
 
+// Three dwords at a 4-byte-aligned address (one global_load_dwordx3).
+typedef uint32_t u32x3a4 __attribute__((ext_vector_type(3), aligned(4)));
+
 // The 16 codes of indices b0 .. b0+15 (b0 % 4 == 0) as 8 words of 2 codes.
 __device__ __forceinline__ void load_codes16(const uint16_t *__restrict__ codes, int64_t c, int b0, uint32_t w[8]) {
 #pragma unroll
@@ -219,6 +222,10 @@ __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restri
   }
 }
 
+// Bytes a pass-1 lane may read past its chunk's last scan index: the
+// pipelined kernel reads two batches ahead (k_pass1p: < 3 * 20 + 5 + 4).
+constexpr int kP1TailMargin = 96;
+
 // ------------------------------------------------------------------- P0
 
 __global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase, int64_t nruns,
@@ -258,7 +265,8 @@ __device__ __forceinline__ bool cand_wanted(const EmitCfg &ec, bool first, int64
 template <int J, bool kCompressed, bool kLds>
 __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
                                                 int k, TableView tv, uint16_t *__restrict__ codes,
-                                                EmitCfg ec, uint32_t *__restrict__ visits, P1 o, Cand cand) {
+                                                EmitCfg ec, uint32_t *__restrict__ visits, P1 o, Cand cand,
+                                                int64_t c0, int tail_only) {
   constexpr int G = (J == 1) ? 16 : (J >= 3 ? 4 : 8);  // table reads in flight per lane and batch
   constexpr int PB = G * J;             // scan indices per batch (16, 16, 12, 16, 20)
   constexpr bool k12 = (J == 5);        // 12-bit codes with escapes (kCompressed only)
@@ -276,8 +284,10 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
     }
   }
   if (kLds || k12) __syncthreads();
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
+  // tail_only: the chunks k_pass1p leaves (reads past the buffer end)
+  if (tail_only && g.start[c] + g.n[c] + kP1TailMargin <= total) return;
   const int kx = k + J - 1;
   const GC xmask = (2 * kx >= 8 * (int)sizeof(GC)) ? ~(GC)0 : (((GC)1 << (2 * kx)) - 1);
   const uint32_t kmask = (1u << (2 * k)) - 1u;
@@ -410,14 +420,18 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
 // Software-pipelined gather pass for expanded compressed tables (J >= 2):
 // the reads of batch b+1 (and the sequence bytes of batch b+2) are issued
 // before batch b is consumed, so every wave keeps its next table reads in
-// flight while it runs the trajectory, and the escape reads of batch b (J = 5,
-// issued first) complete without waiting for them (in-order vmcnt).  All
-// loads are unconditional (dead groups read entry 0) so the wait counts stay
-// static.  Results are identical to k_pass1.
-template <int J, bool kLds>
+// flight while it runs the trajectory.  Loads are in-order on vmcnt, so the
+// loop body must never wait on a load issued after those reads: the escape
+// codes of batch b (J = 5: the first two escaped slots of the batch) are
+// issued before them, all loads are unconditional (dead groups read entry 0)
+// so the wait counts stay static, and the rare paths that do load (a third
+// escape in one batch, the candidate append) drain explicitly inside the
+// branch.  Results are identical to k_pass1.
+template <int J, bool kLds, bool kTrlr>
 __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
                                                  TableView tv, uint16_t *__restrict__ codes, EmitCfg ec,
-                                                 uint32_t *__restrict__ visits, P1 o, Cand cand) {
+                                                 uint32_t *__restrict__ visits, P1 o, Cand cand,
+                                                 const uint32_t *__restrict__ packed) {
   constexpr int G = 4;                  // table reads per batch
   constexpr int PB = G * J;             // scan indices per batch (8, 12, 16, 20)
   constexpr bool k12 = (J == 5);        // 12-bit codes with escapes
@@ -445,58 +459,86 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
   const bool first = c == 0 || g.run[c - 1] != g.run[c];  // the chunk starts its run
   GC gcode = (GC)prime_code_guarded64(seq, start - k, kx, total);  // (k+J-1)-mer of group 0
   // tr_lr: the run's first scan index scores the first k-mer's own score
-  const double first_val = (ec.trlr && first) ? ec.ks[(uint32_t)(gcode >> (2 * (J - 1))) & kmask] : 0.0;
-  uint8_t by[32];
-  // prologue: codes + reads of batch 0, bytes of batch 1
-  load16(seq, start + J - 1, total, by);
-  if (PB > 16) load16(seq, start + J - 1 + 16, total, by + 16);
+  const double first_val = (kTrlr && first) ? ec.ks[(uint32_t)(gcode >> (2 * (J - 1))) & kmask] : 0.0;
+  // tail lanes (reads could pass the end of the buffer) are left to k_pass1
+  if (start + n + kP1TailMargin > total) return;
+  // Batch m rolls the 2-bit codes of bases [q0 + m*PB, q0 + m*PB + PB) in:
+  // three packed words from word (q0 + m*PB) >> 4 (one load, 96 bits >= the
+  // 2*PB <= 40 bits at any offset), so a lane touches one or two 128-B lines
+  // of packed codes over its whole chunk.
+  const int64_t q0 = start + J - 1;
+  constexpr uint64_t fmask = (1ull << (2 * J)) - 1ull;
+  u32x3a4 win = *reinterpret_cast<const u32x3a4 *>(packed + (q0 >> 4));
   GC gc[G];
   EW e[G];
+  {
+    const uint32_t bp = 2u * (uint32_t)(q0 & 15);
+    const uint64_t x = ((((uint64_t)win.x << 32) | win.y) << bp) | (((uint64_t)win.z << bp) >> 32);
 #pragma unroll
-  for (int gi = 0; gi < G; ++gi) {
-    gc[gi] = gcode;
-#pragma unroll
-    for (int t = 0; t < J; ++t) gcode = ((gcode << 2) | enc(by[gi * J + t])) & xmask;
+    for (int gi = 0; gi < G; ++gi) {
+      gc[gi] = gcode;
+      gcode = ((gcode << (2 * J)) | (GC)((x >> (64 - 2 * J * (gi + 1))) & fmask)) & xmask;
+    }
   }
+  // prologue: reads of batch 0, window of batch 1
+  win = *reinterpret_cast<const u32x3a4 *>(packed + ((q0 + PB) >> 4));
 #pragma unroll
   for (int gi = 0; gi < G; ++gi) e[gi] = ext[(gi * J < n) ? gc[gi] : (GC)0];
-  load16(seq, start + PB + J - 1, total, by);
-  if (PB > 16) load16(seq, start + PB + J - 1 + 16, total, by + 16);
   double prev = 0.0, best = 0.0;
   int beg = -1, arg = 0;
   double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
   bool special = false;
   for (int b0 = 0; b0 < n; b0 += PB) {
-    // 1. escape reads of batch b first (one per group: its first escaped
-    //    slot; further escapes in the same group, ~1e-5 of groups, read inline)
-    uint16_t qe[k12 ? G : 1];
-    int tesc[k12 ? G : 1];
+    // 1. escape reads of batch b first: the first two escaped slots of the
+    //    batch (a third one, ~6e-5 of lane-batches, loads inline)
+    int ja = PB, jb = PB;
+    uint32_t qa = 0, qb = 0;
     if (k12) {
+      uint32_t m = 0;
 #pragma unroll
-      for (int gi = 0; gi < G; ++gi) {
-        int te = J;
+      for (int gi = 0; gi < G; ++gi)
 #pragma unroll
-        for (int t = J - 1; t >= 0; --t)
-          if (((uint32_t)(e[gi] >> (12 * t)) & 0xfffu) == 0xfffu) te = t;
-        tesc[gi] = te;
-        const uint32_t km = (uint32_t)(gc[gi] >> (2 * (J - 1 - (te < J ? te : 0)))) & kmask;
-        qe[gi] = tv.codes[te < J ? km : 0u];
-      }
+        for (int t = 0; t < J; ++t)
+          if (((uint32_t)(e[gi] >> (12 * t)) & 0xfffu) == 0xfffu) m |= 1u << (gi * J + t);
+      const uint32_t m2 = m & (m - 1u);
+      ja = m ? __builtin_ctz(m) : PB;
+      jb = m2 ? __builtin_ctz(m2) : PB;
+      uint32_t ka = 0, kb = 0;  // k-mers of slots ja, jb (index 0 when absent)
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi)
+#pragma unroll
+        for (int t = 0; t < J; ++t) {
+          const uint32_t km = (uint32_t)(gc[gi] >> (2 * (J - 1 - t))) & kmask;
+          ka = (ja == gi * J + t) ? km : ka;
+          kb = (jb == gi * J + t) ? km : kb;
+        }
+      qa = tv.codes[ka];
+      qb = tv.codes[kb];
     }
     // 2. reads of batch b+1 (entry 0 where the group is past the chunk end)
     GC gn[G];
     EW en[G];
+    {
+      const uint32_t bp = 2u * (uint32_t)((q0 + b0 + PB) & 15);
+      const uint64_t x = ((((uint64_t)win.x << 32) | win.y) << bp) | (((uint64_t)win.z << bp) >> 32);
 #pragma unroll
-    for (int gi = 0; gi < G; ++gi) {
-      gn[gi] = gcode;
-#pragma unroll
-      for (int t = 0; t < J; ++t) gcode = ((gcode << 2) | enc(by[gi * J + t])) & xmask;
+      for (int gi = 0; gi < G; ++gi) {
+        gn[gi] = gcode;
+        gcode = ((gcode << (2 * J)) | (GC)((x >> (64 - 2 * J * (gi + 1))) & fmask)) & xmask;
+      }
     }
 #pragma unroll
-    for (int gi = 0; gi < G; ++gi) en[gi] = ext[(b0 + PB + gi * J < n) ? gn[gi] : (GC)0];
-    // 3. bytes of batch b+2
-    load16(seq, start + b0 + 2 * PB + J - 1, total, by);
-    if (PB > 16) load16(seq, start + b0 + 2 * PB + J - 1 + 16, total, by + 16);
+    for (int gi = 0; gi < G; ++gi) {
+#if defined(KS_P1_NOTABLE)  // diagnostic build only: no table traffic (wrong values, no escapes)
+      en[gi] = (EW)(gn[gi] & (GC)0x7ff7ff7ff7ff7ffull);
+#elif defined(KS_P1_NT)
+      en[gi] = __builtin_nontemporal_load(ext + ((b0 + PB + gi * J < n) ? gn[gi] : (GC)0));
+#else
+      en[gi] = ext[(b0 + PB + gi * J < n) ? gn[gi] : (GC)0];
+#endif
+    }
+    // 3. window of batch b+2
+    win = *reinterpret_cast<const u32x3a4 *>(packed + ((q0 + b0 + 2 * PB) >> 4));
     // 4. batch b group by group: values, packed codes, trajectory
     uint32_t cw[PB / 2];
 #pragma unroll
@@ -512,7 +554,11 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
             qq = s_map12[c12];
             s = s_lut12[c12];
           } else {
-            qq = (t == tesc[gi]) ? qe[gi] : tv.codes[(uint32_t)(gc[gi] >> (2 * (J - 1 - t))) & kmask];
+            qq = (j == ja) ? qa : qb;
+            if (j != ja && j != jb) {  // third escape of the batch: load and drain here
+              qq = tv.codes[(uint32_t)(gc[gi] >> (2 * (J - 1 - t))) & kmask];
+              __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): never at the loop's shared waits
+            }
             s = kLds ? s_lut[qq] : tv.lut[qq];
           }
         } else {
@@ -521,7 +567,7 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
         }
         if (j & 1) cw[j >> 1] |= qq << 16;
         else cw[j >> 1] = qq;
-        if (ec.trlr && first && b0 == 0 && j == 0) s = first_val;
+        if (kTrlr && first && b0 == 0 && j == 0) s = first_val;
         const int i = b0 + j;
         if (i < n) {
           if (visits) atomicAdd(&visits[(uint32_t)(gc[gi] >> (2 * (J - 1 - t))) & kmask], 1u);
@@ -535,7 +581,10 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
           if (prev == 0 && S > 0) {
             beg = i; arg = i; best = S;
           } else if (prev > 0 && S == 0) {
-            if (cand_wanted(ec, first, start, beg, arg, i, best)) {
+            // kmer_regions: decide()'s region test on chunk-relative indices
+            const bool want = kTrlr ? cand_wanted(ec, first, start, beg, arg, i, best)
+                                    : ((uint64_t)(int64_t)(arg - beg) >= ec.mw && best >= ec.min_score);
+            if (want) {
               const int64_t slot = append_one(cand.count, cand.segcap);
               if (slot >= 0) {
                 cand.beg[slot] = start + beg;
@@ -543,6 +592,7 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
                 cand.rst[slot] = start + i;
                 cand.best[slot] = best;
               }
+              __builtin_amdgcn_s_waitcnt(0x0F70);
             }
             beg = -1;
           } else if (S > best) {
@@ -1638,18 +1688,44 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const bool lds_lut = comp && tv.nlut <= kLdsLutMax && getenv("KS_NO_LDS_LUT") == nullptr;
 #define KS_P1(J, C, L)                                                                                       \
   hipLaunchKernelGGL((k_pass1<J, C, L>), dim3(J == 1 ? gch : gch1k), dim3(J == 1 ? 256 : 1024), 0, st, g, s->seq, \
-                     total, k, tv, codes, ec, visits, p1, cand)
+                     total, k, tv, codes, ec, visits, p1, cand, (int64_t)0, 0)
+  // k_pass1p leaves the chunks whose reads could pass the end of the buffer
+  // (chunk starts increase with the chunk index, so they are among the last
+  // kP1TailMargin + CH chunks) to k_pass1
+  const int64_t ctail = nch > 512 ? nch - 512 : 0;
+#define KS_P1T(J, L)                                                                                           \
+  hipLaunchKernelGGL((k_pass1<J, true, L>), dim3((unsigned)((nch - ctail + 1023) / 1024)), dim3(1024), 0, side, g, \
+                     s->seq, total, k, tv, codes, ec, visits, p1, cand, ctail, 1)
   const int J = (tv.ext != nullptr) ? tv.ext_J : 1;
-  const bool pipelined = getenv("KS_NO_PIPELINED_P1") == nullptr;
+  const bool pipelined = getenv("KS_NO_PIPELINED_P1") == nullptr && runs.packed != nullptr;
 #define KS_P1P(J, L)                                                                                           \
-  hipLaunchKernelGGL((k_pass1p<J, L>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes, ec,       \
-                     visits, p1, cand)
+  do {                                                                                                       \
+    if (ec.trlr) hipLaunchKernelGGL((k_pass1p<J, L, true>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, \
+                                    tv, codes, ec, visits, p1, cand, runs.packed);                             \
+    else hipLaunchKernelGGL((k_pass1p<J, L, false>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv,  \
+                            codes, ec, visits, p1, cand, runs.packed);                                         \
+  } while (0)
   if (comp && J >= 2 && pipelined) {
+    // the tail chunks (a latency-bound serial walk each) run on the side
+    // stream, overlapped with the pipelined pass
+    hipStream_t side = ctx->side;
+    const bool tail = nch > ctail;
+    if (tail) {
+      KS_HIP(hipEventRecord(ctx->ev[12], st));
+      KS_HIP(hipStreamWaitEvent(side, ctx->ev[12], 0));
+      if (J == 5) KS_P1T(5, false);
+      else if (lds_lut) { if (J == 4) KS_P1T(4, true); else if (J == 3) KS_P1T(3, true); else KS_P1T(2, true); }
+      else { if (J == 4) KS_P1T(4, false); else if (J == 3) KS_P1T(3, false); else KS_P1T(2, false); }
+      KS_HIP(hipGetLastError());
+      KS_HIP(hipEventRecord(ctx->ev[13], side));
+    }
     if (lds_lut) {
       if (J == 5) KS_P1P(5, true); else if (J == 4) KS_P1P(4, true); else if (J == 3) KS_P1P(3, true); else KS_P1P(2, true);
     } else {
       if (J == 5) KS_P1P(5, false); else if (J == 4) KS_P1P(4, false); else if (J == 3) KS_P1P(3, false); else KS_P1P(2, false);
     }
+    KS_HIP(hipGetLastError());
+    if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
   } else if (comp && J == 5) {
     KS_P1(5, true, false);  // 12-bit codes: value LUT of the short codes in LDS
   } else if (comp && lds_lut) {
@@ -1660,6 +1736,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     if (J == 4) KS_P1(4, false, false); else if (J == 3) KS_P1(3, false, false); else if (J == 2) KS_P1(2, false, false); else KS_P1(1, false, false);
   }
 #undef KS_P1
+#undef KS_P1T
 #undef KS_P1P
   KS_HIP(hipGetLastError());
   KS_HIP(hipEventRecord(ctx->ev[9], st));

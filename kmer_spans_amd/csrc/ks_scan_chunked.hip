@@ -503,17 +503,17 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
       const uint32_t m2 = m & (m - 1u);
       ja = m ? __builtin_ctz(m) : PB;
       jb = m2 ? __builtin_ctz(m2) : PB;
-      uint32_t ka = 0, kb = 0;  // k-mers of slots ja, jb (index 0 when absent)
+      // k-mer of slot jj (index 0 when absent): group jj / 5, offset jj % 5
+      auto kmer_of = [&](int jj) -> uint32_t {
+        const int gi = (jj * 13) >> 6;  // jj / 5 for jj < 20
+        const int t = jj - J * gi;
+        GC gg = gc[0];
 #pragma unroll
-      for (int gi = 0; gi < G; ++gi)
-#pragma unroll
-        for (int t = 0; t < J; ++t) {
-          const uint32_t km = (uint32_t)(gc[gi] >> (2 * (J - 1 - t))) & kmask;
-          ka = (ja == gi * J + t) ? km : ka;
-          kb = (jb == gi * J + t) ? km : kb;
-        }
-      qa = tv.codes[ka];
-      qb = tv.codes[kb];
+        for (int q = 1; q < G; ++q) gg = (gi == q) ? gc[q] : gg;
+        return jj < PB ? (uint32_t)(gg >> (2 * (J - 1 - t))) & kmask : 0u;
+      };
+      qa = tv.codes[kmer_of(ja)];
+      qb = tv.codes[kmer_of(jb)];
     }
     // 2. reads of batch b+1 (entry 0 where the group is past the chunk end)
     GC gn[G];
@@ -571,33 +571,38 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
         const int i = b0 + j;
         if (i < n) {
           if (visits) atomicAdd(&visits[(uint32_t)(gc[gi] >> (2 * (J - 1 - t))) & kmask], 1u);
+          // aggregates (selects give fmin/fmax's values: asum is never a
+          // signalling NaN and a NaN asum never replaces the extreme)
           asum += s;
-          pmin = fmin(pmin, asum);
-          pmax = fmax(pmax, asum);
+          pmin = asum < pmin ? asum : pmin;
+          pmax = asum > pmax ? asum : pmax;
           sabs += fabs(s);
           special |= !isfinite(s);
+          // clean trajectory, branch-free except for the rare candidate:
+          // open (0 -> S > 0) starts an excursion, close (> 0 -> 0) ends it,
+          // the first strict maximum is kept (S > best is false at a close
+          // and while S stays 0, since best > 0 inside and >= 0 outside)
           const double tt = prev + s;
           const double S = tt > 0 ? tt : 0.0;
-          if (prev == 0 && S > 0) {
-            beg = i; arg = i; best = S;
-          } else if (prev > 0 && S == 0) {
-            // kmer_regions: decide()'s region test on chunk-relative indices
-            const bool want = kTrlr ? cand_wanted(ec, first, start, beg, arg, i, best)
-                                    : ((uint64_t)(int64_t)(arg - beg) >= ec.mw && best >= ec.min_score);
-            if (want) {
-              const int64_t slot = append_one(cand.count, cand.segcap);
-              if (slot >= 0) {
-                cand.beg[slot] = start + beg;
-                cand.arg[slot] = start + arg;
-                cand.rst[slot] = start + i;
-                cand.best[slot] = best;
-              }
-              __builtin_amdgcn_s_waitcnt(0x0F70);
+          const bool open = (prev == 0) & (S > 0);
+          const bool close = (prev > 0) & (S == 0);
+          // kmer_regions: decide()'s region test on chunk-relative indices
+          const bool want = kTrlr ? (close && cand_wanted(ec, first, start, beg, arg, i, best))
+                                  : (close & ((uint64_t)(int64_t)(arg - beg) >= ec.mw) & (best >= ec.min_score));
+          if (want) {
+            const int64_t slot = append_one(cand.count, cand.segcap);
+            if (slot >= 0) {
+              cand.beg[slot] = start + beg;
+              cand.arg[slot] = start + arg;
+              cand.rst[slot] = start + i;
+              cand.best[slot] = best;
             }
-            beg = -1;
-          } else if (S > best) {
-            best = S; arg = i;
+            __builtin_amdgcn_s_waitcnt(0x0F70);
           }
+          const bool up = open | (S > best);
+          best = up ? S : best;
+          arg = up ? i : arg;
+          beg = open ? i : (close ? -1 : beg);
           prev = S;
         }
       }

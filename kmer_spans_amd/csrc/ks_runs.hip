@@ -75,39 +75,54 @@ __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ se
                                                   unsigned long long *__restrict__ ev_count, int64_t cap,
                                                   uint32_t *__restrict__ packed) {
   const int64_t nunits = total / 16 + 1;  // covers position total
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t u0 = (int64_t)blockIdx.x * blockDim.x; u0 < nunits; u0 += stride) {
-    const int64_t u = u0 + threadIdx.x;
-    uint32_t starts = 0, ends = 0;
-    const int64_t p0 = u * 16;
-    if (u < nunits) {
-      uint32_t nm = 0xffffu;
-      if (p0 + 16 <= total) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(seq + p0);
-        nm = n_mask4(v.x) | (n_mask4(v.y) << 4) | (n_mask4(v.z) << 8) | (n_mask4(v.w) << 12);
-        if (packed)
-          packed[u] = (enc_pack4(v.x) << 24) | (enc_pack4(v.y) << 16) | (enc_pack4(v.z) << 8) | enc_pack4(v.w);
-      } else {
-        uint32_t pw = 0;
-        for (int j = 0; j < 16; ++j) {
-          const uint8_t c = p0 + j < total ? seq[p0 + j] : (uint8_t)'N';
-          if (p0 + j < total && !is_n(c)) nm &= ~(1u << j);
-          pw |= enc(c) << (30 - 2 * j);
-        }
-        if (packed) packed[u] = pw;
-      }
-      const uint32_t prev_n = (p0 == 0) ? 1u : (is_n(seq[p0 - 1]) ? 1u : 0u);
-      const uint32_t non = ~nm & 0xffffu;
-      starts = non & ((nm << 1) | prev_n);
-      ends = nm & ((non << 1) | (prev_n ^ 1u)) & 0xffffu;
-      if (p0 + 16 > total) {  // no events past position total
-        const int keep = (int)(total - p0) + 1;
-        const uint32_t km = keep >= 16 ? 0xffffu : ((1u << keep) - 1u);
-        starts &= km;
-        ends &= km;
-      }
+  constexpr int U = 4;                     // units per lane and step: U loads in flight
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
+  const int lane = threadIdx.x & 63;
+  for (int64_t ub = (int64_t)blockIdx.x * blockDim.x * U; ub < nunits; ub += stride) {
+    uint4 v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int64_t p0 = (ub + j * blockDim.x + threadIdx.x) * 16;
+      v[j] = p0 + 16 <= total ? *reinterpret_cast<const uint4 *>(seq + p0) : make_uint4(0, 0, 0, 0);
     }
-    append_events(starts, ends, p0, ev, ev_count, cap);
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int64_t u = ub + j * blockDim.x + threadIdx.x;
+      const int64_t p0 = u * 16;
+      uint32_t starts = 0, ends = 0;
+      // the byte before the unit: lane - 1's last byte (the same step's
+      // previous unit), loaded by lane 0
+      uint32_t prev_b = __shfl_up(v[j].w >> 24, 1, 64);
+      if (lane == 0 || p0 + 16 > total) prev_b = p0 == 0 ? (uint32_t)'N' : (p0 - 1 < total ? seq[p0 - 1] : 'N');
+      if (u < nunits) {
+        uint32_t nm = 0xffffu;
+        if (p0 + 16 <= total) {
+          nm = n_mask4(v[j].x) | (n_mask4(v[j].y) << 4) | (n_mask4(v[j].z) << 8) | (n_mask4(v[j].w) << 12);
+          if (packed)
+            packed[u] = (enc_pack4(v[j].x) << 24) | (enc_pack4(v[j].y) << 16) | (enc_pack4(v[j].z) << 8) |
+                        enc_pack4(v[j].w);
+        } else {
+          uint32_t pw = 0;
+          for (int q = 0; q < 16; ++q) {
+            const uint8_t c = p0 + q < total ? seq[p0 + q] : (uint8_t)'N';
+            if (p0 + q < total && !is_n(c)) nm &= ~(1u << q);
+            pw |= enc(c) << (30 - 2 * q);
+          }
+          if (packed) packed[u] = pw;
+        }
+        const uint32_t prev_n = is_n((uint8_t)prev_b) ? 1u : 0u;
+        const uint32_t non = ~nm & 0xffffu;
+        starts = non & ((nm << 1) | prev_n);
+        ends = nm & ((non << 1) | (prev_n ^ 1u)) & 0xffffu;
+        if (p0 + 16 > total) {  // no events past position total
+          const int keep = (int)(total - p0) + 1;
+          const uint32_t km = keep >= 16 ? 0xffffu : ((1u << keep) - 1u);
+          starts &= km;
+          ends &= km;
+        }
+      }
+      append_events(starts, ends, p0, ev, ev_count, cap);
+    }
   }
 }
 
@@ -240,7 +255,7 @@ ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs
     KS_TRY(ensure(ctx, SLOT_EVENTS, (size_t)cap * 8, &evp));
     KS_HIP(hipMemsetAsync(d_count, 0, 8, st));
     const int64_t nunits = total / 16 + 1;
-    const unsigned grid = (unsigned)std::min<int64_t>((nunits + 255) / 256, (int64_t)ctx->num_cus * 16);
+    const unsigned grid = (unsigned)std::min<int64_t>((nunits + 1023) / 1024, (int64_t)ctx->num_cus * 16);
     hipLaunchKernelGGL(k_n_events, dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp,
                        d_count, cap, packed);
     KS_HIP(hipGetLastError());

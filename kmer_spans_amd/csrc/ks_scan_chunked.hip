@@ -853,6 +853,14 @@ __global__ void __launch_bounds__(64) k_approx_scan(const int64_t *__restrict__ 
 // meaningful; below kLMin the trajectory crosses binades every few steps.
 constexpr double kLMin = 64.0;
 
+// Carried chunks without a usable summary are replayed wave-parallel
+// (replay_par) when its speculation verifies, else serially.
+#ifdef KS_NO_PAR_REPLAY
+constexpr bool kParReplay = false;
+#else
+constexpr bool kParReplay = true;
+#endif
+
 // Summary of each chunk for the binade of its predicted trajectory (lane per
 // chunk, full occupancy); chunks predicted to leave the binade or to approach
 // 0 get none.
@@ -938,6 +946,212 @@ __device__ __forceinline__ double rld(double v, int j) { return __longlong_as_do
 // assumed to be that chunk's clean exit, and the segments run in parallel.
 // The wave of the preceding segment checks the assumption against its exact
 // exit (bit 16 of err on mismatch; the host then redoes the carry per run).
+// Wave-parallel exact replay of one chunk (U) from its exact entry x > 0, for
+// a trajectory that stays positive (no clamp): speculate, then verify.
+//  1. approximate prefix sums y_p (wave scan) give each position the binade
+//     e_p its exact value S_p should have; every y_p must be farther than
+//     the summation error bound from a binade edge and from 0;
+//  2. inside a stretch of equal binades, fl(S + s) = S + RN(s / ulp) exactly
+//     (lemma 2 of the summaries) once S and the result are known to share
+//     binade e: integer increments d_p, an exact segmented prefix scan;
+//  3. the first position of each stretch (a binade crossing) is the
+//     reference's FP64 add on the exact previous value, walked in order
+//     (a few per chunk);
+//  4. every integer result is checked to lie strictly inside its binade
+//     (m in [2^52 + 1, 2^53 - 2]), every crossing value to have the predicted
+//     binade.  Half-ulp ties round to even, i.e. depend on the parity of m:
+//     steps are parity pairs composed associatively (as in the summaries).
+// Returns false (wave-uniform) if anything cannot be verified: the caller
+// replays serially.  On success T = exit, hmax / harg = max and first argmax.
+// Positions are lane-major: p = 4 * lane + q.
+__device__ bool replay_par(const double v[4], int n, double x, double &T, double &hmax, int &harg) {
+  const int lane = threadIdx.x & 63;
+  bool live[4];
+  double a[4];
+  double loc = 0.0, labs = 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    live[q] = 4 * lane + q < n;
+    const double vq = live[q] ? v[q] : 0.0;
+    loc += vq;
+    labs += fabs(vq);
+    a[q] = loc;
+  }
+  double incl = loc, sab = labs;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const double o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+    sab += __shfl_xor(sab, d, 64);
+  }
+  if (!(sab < 1.0e300)) return false;  // non-finite values: serial
+  const double excl = incl - loc;
+  const double err = ldexp(x + sab, -42);  // >> 2 * 256 * 2^-53 * (x + sum |s|)
+  int e[4];
+  bool ok = true;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double y = x + excl + a[q];
+    const double lo = y - err, hi = y + err;
+    e[q] = binade_of(y);
+    if (live[q]) ok &= lo > 0x1p-1000 && hi < 1.0e300 && binade_of(lo) == binade_of(hi);
+  }
+  if (!__all(ok)) return false;
+  // crossings and integer increments: a step inside binade e adds
+  // RN(s / ulp) to the mantissa m; at an exact half the even result wins, so
+  // the increment depends on the parity of m: each step is the pair
+  // (d0, d1) = increment for an even / odd m, and pairs compose
+  // associatively: (f then g)_b = f_b + g_{(b + f_b) & 1}.
+  const int ex = binade_of(x);
+  const int eprev_lane = __shfl_up(e[3], 1, 64);
+  bool cr[4];
+  long long d0[4], d1[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int ep = q ? e[q - 1] : (lane ? eprev_lane : ex);
+    cr[q] = live[q] && e[q] != ep;
+    d0[q] = 0;
+    d1[q] = 0;
+    if (live[q] && !cr[q]) {
+      const double yv = ldexp(v[q], 52 - e[q]);
+      const double fl = floor(yv), fr = yv - fl;
+      ok &= fabs(yv) < 0x1p60;
+      const long long f = (long long)fl;
+      if (fr == 0.5) {
+        d0[q] = f + (f & 1);
+        d1[q] = f + ((1 + f) & 1);
+      } else {
+        d0[q] = d1[q] = f + (fr > 0.5 ? 1 : 0);
+      }
+    }
+  }
+  if (!__all(ok)) return false;
+  auto comp = [](long long f0, long long f1, long long g0, long long g1, long long &r0, long long &r1) {
+    r0 = f0 + (((f0 & 1) == 0) ? g0 : g1);
+    r1 = f1 + ((((1 + f1) & 1) == 0) ? g0 : g1);
+  };
+  // segmented inclusive scan: (Q0, Q1)[q] = composed increments since the
+  // last crossing (a crossing position is a segment head with the identity)
+  long long Q0[4], Q1[4];
+  long long r0 = 0, r1 = 0;
+  bool lflag = false;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (cr[q]) { r0 = 0; r1 = 0; lflag = true; }
+    long long n0, n1;
+    comp(r0, r1, d0[q], d1[q], n0, n1);
+    r0 = n0; r1 = n1;
+    Q0[q] = r0;
+    Q1[q] = r1;
+  }
+  long long s0 = r0, s1 = r1;  // lane aggregate after its last crossing
+  bool fc = lflag;
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const long long o0 = __shfl_up(s0, dd, 64), o1 = __shfl_up(s1, dd, 64);
+    const int fo = __shfl_up((int)fc, dd, 64);
+    if (lane >= dd) {
+      if (!fc) {
+        long long n0, n1;
+        comp(o0, o1, s0, s1, n0, n1);
+        s0 = n0; s1 = n1;
+      }
+      fc = fc || fo;
+    }
+  }
+  long long c0 = __shfl_up(s0, 1, 64), c1 = __shfl_up(s1, 1, 64);  // exclusive carry-in
+  if (lane == 0) { c0 = 0; c1 = 0; }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (cr[q]) break;
+    long long n0, n1;
+    comp(c0, c1, Q0[q], Q1[q], n0, n1);
+    Q0[q] = n0;
+    Q1[q] = n1;
+  }
+  // walk the crossings in order: S_c = fl(S_{c-1} + v_c) on the exact previous value
+  long long Mc[4] = {0, 0, 0, 0};
+  long long Mcur = mant_of(x);
+  unsigned long long lm = __ballot(cr[0] || cr[1] || cr[2] || cr[3]);
+  bool good = true;
+  while (lm) {
+    const int L = __ffsll((long long)lm) - 1;
+    lm &= lm - 1;
+    const int crm = __builtin_amdgcn_readlane((cr[0] ? 1 : 0) | (cr[1] ? 2 : 0) | (cr[2] ? 4 : 0) | (cr[3] ? 8 : 0), L);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!(crm & (1 << q))) continue;
+      const int p = 4 * L + q;
+      double sprev;
+      if (p == 0) {
+        sprev = x;
+      } else {
+        const int pl = (p - 1) >> 2, pq = (p - 1) & 3;
+        const bool odd = Mcur & 1;
+        const long long qsel = pq == 0 ? (odd ? Q1[0] : Q0[0]) : pq == 1 ? (odd ? Q1[1] : Q0[1])
+                             : pq == 2 ? (odd ? Q1[2] : Q0[2]) : (odd ? Q1[3] : Q0[3]);
+        const int esel = pq == 0 ? e[0] : pq == 1 ? e[1] : pq == 2 ? e[2] : e[3];
+        const long long mp = Mcur + rl64(qsel, pl);
+        const int ep = rl32(esel, pl);
+        good &= mp >= (1LL << 52) + 1 && mp <= (1LL << 53) - 2;
+        sprev = from_mant(mp, ep);
+      }
+      const double vc = rld(v[q], L);
+      const double t = sprev + vc;  // the reference's add (kmer_spans.c:269)
+      const int ec = rl32(e[q], L);
+      good &= t > 0 && binade_of(t) == ec;
+      Mcur = mant_of(t);
+      if (lane == L) Mc[q] = Mcur;
+    }
+  }
+  if (!good) return false;  // wave-uniform (built from broadcast values)
+  // stretch-start mantissa per position (forward fill of the crossings) and
+  // the exact values, verified strictly inside their binades
+  long long lastm = 0;
+  bool has = false;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (cr[q]) { lastm = Mc[q]; has = true; }
+  long long fm = lastm;
+  bool ff = has;
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const long long mo = __shfl_up(fm, dd, 64);
+    const int fo = __shfl_up((int)ff, dd, 64);
+    if (lane >= dd && !ff && fo) { fm = mo; ff = true; }
+  }
+  long long start_m = __shfl_up(fm, 1, 64);
+  const int start_f = __shfl_up((int)ff, 1, 64);
+  if (lane == 0 || !start_f) start_m = mant_of(x);
+  double S[4];
+  bool inb = true;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (cr[q]) start_m = Mc[q];
+    const long long m = cr[q] ? start_m : start_m + ((start_m & 1) ? Q1[q] : Q0[q]);
+    if (live[q] && !cr[q]) inb &= m >= (1LL << 52) + 1 && m <= (1LL << 53) - 2;
+    S[q] = from_mant(m, e[q]);
+  }
+  if (!__all(inb)) return false;
+  // exit, max and first argmax
+  const int pl = (n - 1) >> 2, pq = (n - 1) & 3;
+  const double slast = pq == 0 ? S[0] : pq == 1 ? S[1] : pq == 2 ? S[2] : S[3];
+  T = rld(slast, pl);
+  double bm = -1.0;
+  int bi = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (live[q] && S[q] > bm) { bm = S[q]; bi = 4 * lane + q; }
+  double wm = bm;
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) wm = fmax(wm, __shfl_xor(wm, dd, 64));
+  const unsigned long long bl = __ballot(bm == wm && bm >= 0.0);
+  const int fl = __ffsll((long long)bl) - 1;
+  hmax = wm;
+  harg = __builtin_amdgcn_readlane(bi, fl);
+  return true;
+}
+
 template <bool kCompressed>
 __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64_t c1, const uint8_t *__restrict__ seq,
                                               int64_t total, int k, const TableView &tv,
@@ -949,7 +1163,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
   double x = (c0 > 0 && g.run[c0] == g.run[c0 - 1]) ? o.cexit[c0 - 1] : 0.0;
   unsigned long long replays = 0;
   const long long t_start = dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
-  long long n_l = 0, n_r = 0;
+  long long n_l = 0, n_r = 0, n_uq = 0, n_up = 0, n_par = 0;  // diagnostics: replays that clamp, replayed indices
   // per-lane inputs of one 64-chunk tile; the next tile's are loaded before
   // the current one is processed (all loads independent: hides their latency
   // behind the tile's scan)
@@ -1083,7 +1297,9 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
         values4(g, seq, total, k, tv, kCompressed ? codes : nullptr, cj, 4 * lane, n, v);
         double T = x, hmax = -1.0;
         int hq = -1, harg = 0;
-        for (int i = 0; i < 64 && hq < 0; ++i) {
+        const bool par = kParReplay && replay_par(v, n, x, T, hmax, harg);
+        if (par) n_par += 1;
+        for (int i = 0; i < 64 && hq < 0 && !par; ++i) {
           if (4 * i >= n) break;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -1102,6 +1318,8 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
           my_harg = harg;
         }
         x = hq >= 0 ? cj_exit : T;
+        n_uq += hq >= 0;
+        n_up += hq >= 0 ? hq + 1 : n;
       }
       if (lane == j) my_mode = mode;
       n_l += mode == kModeL;
@@ -1123,12 +1341,15 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
       __double_as_longlong(x) != __double_as_longlong(o.cexit[c1 - 1]))
     atomicOr(err, 16u);  // the next segment assumed a different entry
   if (dbg && lane == 0) {  // accumulated per block (several segments per window)
-    dbg[6 * r + 0] += (long long)__builtin_amdgcn_s_memtime() - t_start;
-    dbg[6 * r + 1] += c1 - c0;
-    dbg[6 * r + 2] += (long long)replays;
-    dbg[6 * r + 3] += 1;
-    dbg[6 * r + 4] += n_l;
-    dbg[6 * r + 5] += n_r;
+    dbg[9 * r + 0] += (long long)__builtin_amdgcn_s_memtime() - t_start;
+    dbg[9 * r + 1] += c1 - c0;
+    dbg[9 * r + 2] += (long long)replays;
+    dbg[9 * r + 3] += 1;
+    dbg[9 * r + 4] += n_l;
+    dbg[9 * r + 5] += n_r;
+    dbg[9 * r + 6] += n_uq;
+    dbg[9 * r + 7] += n_up;
+    dbg[9 * r + 8] += n_par;
   }
 }
 
@@ -1678,8 +1899,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   static const bool dbg_on = getenv("KS_DEBUG_CARRY") != nullptr;
   long long *dbg = nullptr;
   if (dbg_on) {
-    KS_HIP(hipMalloc(&dbg, nwin * 6 * sizeof(long long)));
-    KS_HIP(hipMemsetAsync(dbg, 0, nwin * 6 * sizeof(long long), st));
+    KS_HIP(hipMalloc(&dbg, nwin * 9 * sizeof(long long)));
+    KS_HIP(hipMemsetAsync(dbg, 0, nwin * 9 * sizeof(long long), st));
   }
 
   // ---- P0 chunks, P1 gather pass
@@ -1828,19 +2049,20 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   if ((errbits & 16u) && !force_fb)
     fprintf(stderr, "kmer_spans_amd: carry segment check failed; the carry was redone per run\n");
   if (dbg) {
-    std::vector<long long> h(nwin * 6);
-    KS_HIP(hipMemcpy(h.data(), dbg, nwin * 6 * sizeof(long long), hipMemcpyDeviceToHost));
+    std::vector<long long> h(nwin * 9);
+    KS_HIP(hipMemcpy(h.data(), dbg, nwin * 9 * sizeof(long long), hipMemcpyDeviceToHost));
     KS_HIP(hipFree(dbg));
     std::vector<int64_t> idx(nwin);
     for (int64_t i = 0; i < nwin; ++i) idx[i] = i;
-    std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return h[6 * a] > h[6 * b]; });
-    long long tot[6] = {0, 0, 0, 0, 0, 0};
+    std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return h[9 * a] > h[9 * b]; });
+    long long tot[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int64_t i = 0; i < nwin; ++i)
-      for (int q = 0; q < 6; ++q) tot[q] += h[6 * i + q];
-    fprintf(stderr, "[carry] windows %lld (runs %lld) chunks %lld replays %lld segments %lld L %lld R %lld\n",
-            (long long)nwin, (long long)nruns, tot[1], tot[2], tot[3], tot[4], tot[5]);
+      for (int q = 0; q < 9; ++q) tot[q] += h[9 * i + q];
+    fprintf(stderr, "[carry] windows %lld (runs %lld) chunks %lld replays %lld (wave-parallel %lld, clamping %lld, "
+            "indices %lld) segments %lld L %lld R %lld\n", (long long)nwin, (long long)nruns, tot[1], tot[2], tot[8],
+            tot[6], tot[7], tot[3], tot[4], tot[5]);
     for (int64_t i = 0; i < std::min<int64_t>(nwin, 8); ++i) {
-      const long long *d = &h[6 * idx[i]];
+      const long long *d = &h[9 * idx[i]];
       fprintf(stderr, "[carry] window %lld cycles %lld chunks %lld replays %lld segments %lld L %lld R %lld\n",
               (long long)idx[i], d[0], d[1], d[2], d[3], d[4], d[5]);
     }

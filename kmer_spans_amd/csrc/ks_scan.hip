@@ -28,9 +28,23 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
                            const unsigned long long *d_cnt = nullptr, int64_t segcap = 0,
-                           const ScanMode &mode = ScanMode(), int init_step = 1, const int64_t *offs = nullptr);
+                           const ScanMode &mode = ScanMode(), int init_step = 1, const int64_t *offs = nullptr,
+                           const uint32_t *packed = nullptr);
 
 namespace {
+
+// 64 bits of 2-bit base codes from base q0 on (first base most significant),
+// read from the packed codes of find_runs (three words); false where those
+// words are past the end of the packed array (then the bytes are rolled).
+__device__ __forceinline__ bool packed_bits(const uint32_t *__restrict__ packed, int64_t total, int64_t q0,
+                                            uint64_t &x) {
+  if (!packed || (q0 >> 4) + 2 > (total >> 4)) return false;
+  const uint32_t *w = packed + (q0 >> 4);
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+  const uint32_t bp = 2u * (uint32_t)(q0 & 15);
+  x = ((((uint64_t)w0 << 32) | w1) << bp) | (((uint64_t)w2 << bp) >> 32);
+  return true;
+}
 
 // Values of a batch of consecutive scan indices are gathered before the
 // sequential state machine consumes them, so a lane keeps several random
@@ -44,7 +58,8 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
                                                   const int32_t *__restrict__ rseq, int64_t nruns,
                                                   int k, TableView tv, uint64_t mw, double min_score,
                                                   uint32_t *__restrict__ visits, RegionBuf out,
-                                                  const unsigned long long *__restrict__ d_cnt, int64_t segcap) {
+                                                  const unsigned long long *__restrict__ d_cnt, int64_t segcap,
+                                                  const uint32_t *__restrict__ packed) {
   constexpr int G = (J == 1) ? 16 : (J >= 4 ? 4 : (J == 3 ? 6 : 8));  // reads per batch
   constexpr int PB = G * J;                                           // indices per batch (16, 16, 18, 16, 20)
   using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;  // (k+J-1)-mer code
@@ -68,15 +83,21 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
       const int n = (int)((b - p0) < PB ? (b - p0) : PB);
       double v[PB];
       GC gc[G];
+      uint64_t xb = 0;  // the batch's PB <= 20 rolled-in bases from the packed codes (2 * PB <= 64 bits)
+      const bool pk = packed_bits(packed, total, p0 + J - 1, xb);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         gc[g] = gcode;
         if (g * J < n) {
           gather_group<J, kCompressed>(tv, gcode, kmask, v + g * J);
+          if (pk) {
+            gcode = ((gcode << (2 * J)) | (GC)((xb >> (64 - 2 * J * (g + 1))) & ((1ull << (2 * J)) - 1))) & xmask;
+          } else {
 #pragma unroll
-          for (int t = 0; t < J; ++t) {
-            const int64_t q = p0 + g * J + J - 1 + t;
-            gcode = ((gcode << 2) | enc(q < total ? seq[q] : (uint8_t)'N')) & xmask;
+            for (int t = 0; t < J; ++t) {
+              const int64_t q = p0 + g * J + J - 1 + t;
+              gcode = ((gcode << 2) | enc(q < total ? seq[q] : (uint8_t)'N')) & xmask;
+            }
           }
         }
       }
@@ -252,7 +273,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
                            const unsigned long long *d_cnt, int64_t segcap, const ScanMode &mode, int init_step,
-                           const int64_t *offs) {
+                           const int64_t *offs, const uint32_t *packed) {
   if (n <= 0) return KS_OK;
   const int J = tv.ext ? tv.ext_J : 1;
   if (mode.trlr) {
@@ -270,7 +291,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
   }
 #define KS_LANE(J, C)                                                                                   \
   hipLaunchKernelGGL((k_scan_lane<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, total, \
-                     ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap)
+                     ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed)
   if (tv.compressed) {
     if (J == 5) KS_LANE(5, true); else if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
   } else {
@@ -384,7 +405,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     if (algo == 0) {
       if (runs.n)
         KS_TRY(launch_scan_lane(ctx, s->seq, total, runs.a, runs.b, runs.seq, runs.n, k, tv, mw, min_score, vis, rb,
-                                nullptr, 0, mode, 1, s->offsets_dev));
+                                nullptr, 0, mode, 1, s->offsets_dev, runs.packed));
     }
     KS_HIP(hipEventRecord(ctx->ev[4], st));
     KS_TRY(read_counts());

@@ -42,7 +42,8 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
                            const unsigned long long *d_cnt = nullptr, int64_t segcap = 0,
-                           const ScanMode &mode = ScanMode(), int init_step = 1, const int64_t *offs = nullptr);
+                           const ScanMode &mode = ScanMode(), int init_step = 1, const int64_t *offs = nullptr,
+                           const uint32_t *packed = nullptr);
 
 namespace {
 
@@ -2031,7 +2032,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   KS_HIP(hipGetLastError());
   KS_HIP(hipEventRecord(ctx->ev[10], st));
   KS_TRY(launch_scan_lane(ctx, s->seq, total, rs.a, rs.b, rs.seq, rcap, k, tv, mw, min_score, visits, rb,
-                          rs.count, rs.segcap, mode, 0));
+                          rs.count, rs.segcap, mode, 0, nullptr, runs.packed));
   KS_HIP(hipEventRecord(ctx->ev[11], st));
   std::vector<unsigned long long> hcv(2 * kSegs + 2);
   KS_HIP(hipMemcpyAsync(hcv.data(), cnts, 8 * (2 * kSegs + 2), hipMemcpyDeviceToHost, st));

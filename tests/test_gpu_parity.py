@@ -182,6 +182,30 @@ def test_human_like_device_path(K, oracle, ctx, k, score):
     D.bind_torch_stream(ctx)
 
 
+@pytest.mark.parametrize("k,expand", [(11, True), (11, False), (13, True)])
+def test_rank_carried_replays(K, oracle, ctx, k, expand):
+    """Weighted-rank scores (config 3 shape): excursions at small S cross
+    binades inside chunks, so the carry replays them (wave-parallel replay
+    with parity-pair increments, binade crossings, ties) -- bit-exact
+    regions and scores against the oracle, and the replay path was taken."""
+    import torch
+    from kmer_spans_amd import device as D, genome
+    parts, lens = genome.human_like(scale=0.004, seed=11, device="cuda")
+    ds = D.from_parts(parts, lens, "cuda")
+    D.bind_torch_stream(ctx)
+    host = [ds.host_seq(q) for q in range(ds.nseq)]
+    n, oc = oracle.kmer_counts(host, k)
+    w = K.rank_table(oc, k, n)
+    o = oracle.scan(host, k, w, 0.75, 100, 20.0)
+    tab = D.DeviceTable(ctx, w, k, 0.75, compress=True, expand=expand)
+    ctx.set_scan_algo(1)
+    pos, sc, st = D.scan(ctx, ds, k, tab, 100, 20.0)
+    ctx.set_scan_algo(-1)
+    _assert_same_regions(pos, sc, o["pos"], o["score"], ("rank", k, expand))
+    assert st["n_replay"] > 0 and pos.shape[1] > 100, (st["n_replay"], pos.shape)
+    tab.close()
+
+
 def test_edge_inputs(K, oracle):
     w = np.array([1.0, -1.0, -3.0, 2.0])
     cases = [[""], ["N" * 50], ["A"], ["ACGT" * 3, "", "NNN", "G"], ["n" * 3 + "acgt" + "N"],

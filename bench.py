@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 ALGO_BYTES_PER_BASE = 9.0      # 1 B sequence + 8 B FP64 table entry (k >= 8)
+RANDOM_WALL_GPS = 48.0         # measured random-request ceiling (profiles/r1_gather_bench2.jsonl)
 
 
 def cpu_model() -> str:
@@ -180,7 +181,31 @@ def main():
                 if name.startswith("k_pass1") and "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
                     roofline["traffic"] = round((cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1e3)  # KB -> B
                     roofline["traffic_source"] = f"profiles/r1_pmc_summary.json ({name}, FETCH+WRITE)"
+                    roofline["traffic_note"] = "PMC pass of the same workload and build (tools/gpu_pmc.sh), not this run"
                     break
+
+    # ---- the bound that applies to a gather pass: random requests.  Every
+    # table read of k_pass1p is one random request (64-B fetch) whatever its
+    # width; the chip's measured ceiling for such requests from tables of
+    # 32-128 GiB is ~48 G/s (tools/gather_bench2.hip, profiles/r1_gather_bench2.jsonl:
+    # u64 entries 47.2-49.1 G/s).  Reported beside the HBM-bytes roofline.
+    if stats[-1]["scan_algo"] == 1:
+        J = max(1, int(table.positions_per_read))
+        n_scored = int(stats[-1]["n_scored"])
+        reads = n_scored / J + (n_scored * float(table.escape_fraction) if table.code_bits == 12 else 0.0)
+        ra = {"table_reads_per_launch": int(reads), "positions_per_read": J,
+              "achieved_G_per_s": round(reads / (ms_kernel * 1e-3) / 1e9, 2), "wall_G_per_s": RANDOM_WALL_GPS,
+              "frac": round(reads / (ms_kernel * 1e-3) / 1e9 / RANDOM_WALL_GPS, 4),
+              "wall_source": "profiles/r1_gather_bench2.jsonl (random u64 reads, 32-128 GiB tables)"}
+        if roofline.get("traffic") and roofline.get("traffic_source", "").find("FETCH") >= 0:
+            pmc = json.load(open(pmc_path))
+            for name, cs in pmc.get("kernels", {}).items():
+                if name.startswith("k_pass1p") and "FETCH_SIZE" in cs:
+                    req = cs["FETCH_SIZE"] * 1e3 / 64.0  # FETCH_SIZE = TCC_EA0_RDREQ x 64 B
+                    ra["memory_read_requests_per_launch"] = int(req)
+                    ra["memory_requests_G_per_s"] = round(req / (ms_kernel * 1e-3) / 1e9, 2)
+                    break
+        roofline["random_access"] = ra
 
     # ---- PCIe-inclusive rate of the host entry point (reported, never `value`)
     host_path = None

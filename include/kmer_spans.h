@@ -54,6 +54,10 @@ const char *ks_version(void);
  * 46-58): per region (seq_id, beg, end) int32 and score double; the second
  * double the reference stores ("entropy") is always 0.0 and is not kept.
  * Regions are ordered by (seq_id, beg), the reference's emission order. */
+/* The four arrays live in one library-allocated block: seq_id, beg, end are
+ * consecutive (a column-major 3 x n int32 matrix, the reference's `pos`
+ * before kmer_spans.R:76 transposes it), score is followed by n zeros (the
+ * 2 x n `score` matrix, second row 0.0, kmer_spans.c:280). */
 typedef struct ks_regions {
   int64_t n;
   int32_t *seq_id; /* 0-based index into the input sequences (:536, :610) */

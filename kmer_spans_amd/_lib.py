@@ -141,18 +141,32 @@ def check(rc: int) -> None:
         raise KmerSpansError(msg or f"libkmerspans error {rc}")
 
 
+class _RegionBlock:
+    """Owns a ks_regions block; freed when the last numpy view of it dies."""
+
+    def __init__(self, r: Regions):
+        self.r = r
+
+    def __del__(self):
+        if _lib is not None:
+            _lib.ks_regions_free(C.byref(self.r))
+
+
 def regions_to_numpy(r: Regions):
-    """Copy a ks_regions into (pos int32[3, n], score float64[2, n]) and free it."""
+    """(pos int32[3, n], score float64[2, n]) as views of the library's output
+    block (seq_id|beg|end contiguous, score followed by zeros: include/
+    kmer_spans.h), which is freed with the last view -- no host copy."""
     n = int(r.n)
-    pos = np.empty((3, n), dtype=np.int32)
-    score = np.empty((2, n), dtype=np.float64)
-    score[1] = 0.0
-    if n:
-        pos[0] = np.ctypeslib.as_array(r.seq_id, shape=(n,))
-        pos[1] = np.ctypeslib.as_array(r.beg, shape=(n,))
-        pos[2] = np.ctypeslib.as_array(r.end, shape=(n,))
-        score[0] = np.ctypeslib.as_array(r.score, shape=(n,))
-    load().ks_regions_free(C.byref(r))
+    if n == 0:
+        load().ks_regions_free(C.byref(r))
+        return np.empty((3, 0), dtype=np.int32), np.empty((2, 0), dtype=np.float64)
+    holder = _RegionBlock(r)
+    ib = (C.c_char * (3 * n * 4)).from_address(C.cast(r.seq_id, C.c_void_p).value)
+    sb = (C.c_char * (2 * n * 8)).from_address(C.cast(r.score, C.c_void_p).value)
+    ib._holder = holder
+    sb._holder = holder
+    pos = np.frombuffer(ib, dtype=np.int32).reshape(3, n)
+    score = np.frombuffer(sb, dtype=np.float64).reshape(2, n)
     return pos, score
 
 

@@ -142,10 +142,7 @@ extern "C" const char *ks_version(void) { return "kmer_spans_amd 0.1 gfx950"; }
 
 extern "C" void ks_regions_free(ks_regions *r) {
   if (!r) return;
-  free(r->seq_id);
-  free(r->beg);
-  free(r->end);
-  free(r->score);
+  free(r->seq_id);  // one block holds all four arrays (scan_impl)
   memset(r, 0, sizeof(*r));
 }
 

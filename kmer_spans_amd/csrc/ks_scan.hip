@@ -33,19 +33,6 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
 
 namespace {
 
-// 64 bits of 2-bit base codes from base q0 on (first base most significant),
-// read from the packed codes of find_runs (three words); false where those
-// words are past the end of the packed array (then the bytes are rolled).
-__device__ __forceinline__ bool packed_bits(const uint32_t *__restrict__ packed, int64_t total, int64_t q0,
-                                            uint64_t &x) {
-  if (!packed || (q0 >> 4) + 2 > (total >> 4)) return false;
-  const uint32_t *w = packed + (q0 >> 4);
-  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-  const uint32_t bp = 2u * (uint32_t)(q0 & 15);
-  x = ((((uint64_t)w0 << 32) | w1) << bp) | (((uint64_t)w2 << bp) >> 32);
-  return true;
-}
-
 // Values of a batch of consecutive scan indices are gathered before the
 // sequential state machine consumes them, so a lane keeps several random
 // table reads in flight instead of one (the gathers do not depend on S).
@@ -431,13 +418,22 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
   pre.segcap = segcap;
   const int64_t n = pre.p[kSegs];
   out->n = n;
-  out->seq_id = (int32_t *)malloc(std::max<int64_t>(n, 1) * 4);
-  out->beg = (int32_t *)malloc(std::max<int64_t>(n, 1) * 4);
-  out->end = (int32_t *)malloc(std::max<int64_t>(n, 1) * 4);
-  out->score = (double *)malloc(std::max<int64_t>(n, 1) * 8);
-  if (!out->seq_id || !out->beg || !out->end || !out->score) {
-    ks_regions_free(out);
-    return fail(KS_ERR_NOMEM, "out of host memory for %lld regions", (long long)n);
+  // one block (ks_regions_free frees seq_id): [seq_id | beg | end] int32 (a
+  // 3 x n matrix, the layout of the reference's `pos`), then [score | 0.0]
+  // doubles (2 x n, `score`'s layout with the reference's second row, :280)
+  {
+    const size_t nn = (size_t)std::max<int64_t>(n, 1);
+    const size_t ioff = (3 * nn * 4 + 7) & ~(size_t)7;
+    char *blk = static_cast<char *>(malloc(ioff + 2 * nn * 8));
+    if (!blk) {
+      memset(out, 0, sizeof(*out));
+      return fail(KS_ERR_NOMEM, "out of host memory for %lld regions", (long long)n);
+    }
+    out->seq_id = reinterpret_cast<int32_t *>(blk);
+    out->beg = out->seq_id + nn;
+    out->end = out->beg + nn;
+    out->score = reinterpret_cast<double *>(blk + ioff);
+    if (n == 0) out->score[0] = 0.0;  // (n > 0: zero-filled while the D2H runs)
   }
   if (n > 0) {
     void *tmpb = nullptr;
@@ -471,6 +467,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     KS_TRY(ensure_pinned(ctx, blk, &hp));
     KS_HIP(hipMemcpyAsync(hp, o_seq, blk, hipMemcpyDeviceToHost, st));
     KS_HIP(hipEventRecord(ctx->ev[6], st));
+    memset(out->score + nn, 0, nn * 8);  // second row of `score` (overlaps the device work)
     KS_HIP(hipStreamSynchronize(st));
     const char *h = static_cast<const char *>(hp);
     memcpy(out->seq_id, h, nn * 4);

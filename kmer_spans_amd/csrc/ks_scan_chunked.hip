@@ -56,6 +56,7 @@ struct Chunks {
   int32_t *n;      // indices in the chunk
   int32_t *run;    // run id
   int64_t nch;
+  const uint32_t *packed;  // 2-bit base codes (Runs::packed), nullptr: roll the bytes
 };
 
 struct P1 {  // per-chunk results of the gather pass
@@ -202,7 +203,9 @@ __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restri
   }
   const int64_t p = g.start[c] + i0;
   if (tv.ext && tv.ext_J == 4) {  // FP64 expanded table: the 4 values in one 32-B entry
-    const uint64_t gcode = prime_code_guarded64(seq, p - k, k + 3, total);
+    uint64_t xp = 0;
+    const uint64_t gcode = packed_bits(g.packed, total, p - k, xp) ? (xp >> (64 - 2 * (k + 3)))
+                                                                    : prime_code_guarded64(seq, p - k, k + 3, total);
     const double2 *E = reinterpret_cast<const double2 *>(tv.ext);
     const double2 e0 = E[2 * gcode], e1 = E[2 * gcode + 1];
     const double ev[4] = {e0.x, e0.y, e1.x, e1.y};
@@ -738,7 +741,10 @@ __device__ int chunk_summary_fast(const Chunks &g, const uint8_t *__restrict__ s
   const uint32_t mask = (1u << (2 * k)) - 1u;
   const double scale = ldexp(1.0, 52 - e);
   constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
-  uint32_t code = kCompressed ? 0u : prime_code(seq, start - k, k);
+  uint64_t xp = 0;
+  uint32_t code = kCompressed ? 0u
+                  : packed_bits(g.packed, total, start - k, xp) ? (uint32_t)(xp >> (64 - 2 * k))
+                                                                : prime_code(seq, start - k, k);
   double cur = 0.0, mx = -INFINITY, mn = INFINITY;
   int arg = 0;
   bool ok = true, tie_seen = false;
@@ -754,7 +760,13 @@ __device__ int chunk_summary_fast(const Chunks &g, const uint8_t *__restrict__ s
       }
     } else if (tv.ext && tv.ext_J == 4) {  // FP64 expanded table: 4 values per 32-B read
       uint8_t by[16];
-      load16(seq, start + b0, total, by);
+      uint64_t xb = 0;
+      if (packed_bits(g.packed, total, start + b0, xb)) {  // bytes with the same enc() as the packed codes
+#pragma unroll
+        for (int j = 0; j < 16; ++j) by[j] = (uint8_t)(((xb >> (62 - 2 * j)) & 3u) << 1);
+      } else {
+        load16(seq, start + b0, total, by);
+      }
       const double2 *E = reinterpret_cast<const double2 *>(tv.ext);
 #pragma unroll
       for (int gq = 0; gq < NB / 4; ++gq) {
@@ -1422,6 +1434,7 @@ template <int J, bool kCompressed>
 __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
                                                int k, TableView tv, const uint16_t *__restrict__ codes,
                                                Carry cr, unsigned int *__restrict__ err, int gated) {
+  const uint32_t *__restrict__ packed = g.packed;
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
   if (gated && !(*(volatile unsigned int *)err & 16u)) return;  // second pass only after a fallback
@@ -1459,17 +1472,29 @@ __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restri
     constexpr int PB = G * J;
     const int kx = k + J - 1;
     const uint32_t xmask = (kx >= 16) ? 0xffffffffu : ((1u << (2 * kx)) - 1u);
-    uint32_t gcode = prime_code_guarded(seq, start - k, kx, total);
+    // prime and the first batch's bases from the packed codes: one round trip
+    uint64_t xp = 0;
+    uint32_t gcode = packed_bits(packed, total, start - k, xp) ? (uint32_t)(xp >> (64 - 2 * kx))
+                                                               : prime_code_guarded(seq, start - k, kx, total);
     for (int b0 = 0; b0 < n && hq < 0; b0 += PB) {
-      uint8_t by[32];
-      load16(seq, start + b0 + J - 1, total, by);
-      if (PB > 16) load16(seq, start + b0 + J - 1 + 16, total, by + 16);
       uint32_t gc[G];
+      uint64_t xb = 0;
+      if (2 * PB <= 64 && packed_bits(packed, total, start + b0 + J - 1, xb)) {
 #pragma unroll
-      for (int gi = 0; gi < G; ++gi) {
-        gc[gi] = gcode;
+        for (int gi = 0; gi < G; ++gi) {
+          gc[gi] = gcode;
+          gcode = ((gcode << (2 * J)) | (uint32_t)((xb >> (64 - 2 * J * (gi + 1))) & ((1u << (2 * J)) - 1u))) & xmask;
+        }
+      } else {
+        uint8_t by[32];
+        load16(seq, start + b0 + J - 1, total, by);
+        if (PB > 16) load16(seq, start + b0 + J - 1 + 16, total, by + 16);
 #pragma unroll
-        for (int t = 0; t < J; ++t) gcode = ((gcode << 2) | enc(by[gi * J + t])) & xmask;
+        for (int gi = 0; gi < G; ++gi) {
+          gc[gi] = gcode;
+#pragma unroll
+          for (int t = 0; t < J; ++t) gcode = ((gcode << 2) | enc(by[gi * J + t])) & xmask;
+        }
       }
       double v[PB];
 #pragma unroll
@@ -1844,7 +1869,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   KS_TRY(ensure(ctx, SLOT_CHUNK_A, off, &wsp));
   char *W = static_cast<char *>(wsp);
   Chunks g{reinterpret_cast<int64_t *>(W + o_start), reinterpret_cast<int32_t *>(W + o_n),
-           reinterpret_cast<int32_t *>(W + o_run), nch};
+           reinterpret_cast<int32_t *>(W + o_run), nch, runs.packed};
   double *p1d = reinterpret_cast<double *>(W + o_p1d);
   int32_t *p1i = reinterpret_cast<int32_t *>(W + o_p1i);
   P1 p1{p1d, p1d + nch, p1d + 2 * nch, p1d + 3 * nch, p1d + 4 * nch, p1d + 5 * nch, p1i, p1i + nch,

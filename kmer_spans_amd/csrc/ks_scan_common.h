@@ -110,4 +110,18 @@ __device__ __forceinline__ uint32_t prime_code(const uint8_t *__restrict__ seq, 
   return c;
 }
 
+// 64 bits of 2-bit base codes from base q0 on (first base most significant),
+// read from the packed codes of find_runs (Runs::packed, three words); false
+// where those words are past the end of the packed array (callers then roll
+// the bytes).
+__device__ __forceinline__ bool packed_bits(const uint32_t *__restrict__ packed, int64_t total, int64_t q0,
+                                            uint64_t &x) {
+  if (!packed || q0 < 0 || (q0 >> 4) + 2 > (total >> 4)) return false;
+  const uint32_t *w = packed + (q0 >> 4);
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+  const uint32_t bp = 2u * (uint32_t)(q0 & 15);
+  x = ((((uint64_t)w0 << 32) | w1) << bp) | (((uint64_t)w2 << bp) >> 32);
+  return true;
+}
+
 }  // namespace ks

@@ -591,8 +591,15 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
           const bool open = (prev == 0) & (S > 0);
           const bool close = (prev > 0) & (S == 0);
           // kmer_regions: decide()'s region test on chunk-relative indices
-          const bool want = kTrlr ? (close && cand_wanted(ec, first, start, beg, arg, i, best))
-                                  : (close & ((uint64_t)(int64_t)(arg - beg) >= ec.mw) & (best >= ec.min_score));
+          // tr_lr: decide()'s tests on chunk-relative positions (pos_of: the
+          // run's first index keeps its position, later ones report j - 1)
+          const int f0 = first ? 0 : -1;
+          const long long ml = kTrlr ? ec.min_len : 0;
+          const bool want =
+              kTrlr ? (close & (((long long)((arg != f0 ? arg - 1 : arg) - (beg != f0 ? beg - 1 : beg)) >= ml) |
+                                ((long long)((i != f0 ? i - 1 : i) - (arg != f0 ? arg - 1 : arg) - 1) >=
+                                 (ml > 1 ? ml : 1LL))))
+                    : (close & ((uint64_t)(int64_t)(arg - beg) >= ec.mw) & (best >= ec.min_score));
           if (want) {
             const int64_t slot = append_one(cand.count, cand.segcap);
             if (slot >= 0) {

@@ -641,6 +641,136 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
   }
 }
 
+// Software-pipelined gather pass for uncompressed FP64 expanded tables
+// (weighted-rank tables: every k-mer has its own value, so no codes): one
+// 16-B (J = 2) or 32-B (J = 3, 4) entry per J scan indices, the next batch's
+// entries in flight while the current batch runs the clean trajectory, bases
+// rolled from the packed codes.  Same outputs as k_pass1<J, false, false>
+// (no code store: later passes re-read the table).
+template <int J, bool kTrlr>
+__global__ void __launch_bounds__(1024) k_pass1pf(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
+                                                  TableView tv, EmitCfg ec, uint32_t *__restrict__ visits, P1 o,
+                                                  Cand cand, const uint32_t *__restrict__ packed) {
+  constexpr int G = (J == 2) ? 8 : 4;  // table reads per batch
+  constexpr int PB = G * J;            // scan indices per batch (16, 12, 16)
+  using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= g.nch) return;
+  const double2 *__restrict__ E = reinterpret_cast<const double2 *>(tv.ext);
+  const int kx = k + J - 1;
+  const GC xmask = (2 * kx >= 8 * (int)sizeof(GC)) ? ~(GC)0 : (((GC)1 << (2 * kx)) - 1);
+  const uint32_t kmask = (1u << (2 * k)) - 1u;
+  const int64_t start = g.start[c];
+  const int n = g.n[c];
+  const bool first = c == 0 || g.run[c - 1] != g.run[c];
+  // tail lanes (reads could pass the end of the buffer) are left to k_pass1
+  if (start + n + kP1TailMargin > total) return;
+  GC gcode = (GC)prime_code_guarded64(seq, start - k, kx, total);
+  const double first_val = (kTrlr && first) ? ec.ks[(uint32_t)(gcode >> (2 * (J - 1))) & kmask] : 0.0;
+  const int64_t q0 = start + J - 1;
+  constexpr uint64_t fmask = (1ull << (2 * J)) - 1ull;
+  auto roll = [&](u32x3a4 w, int64_t qb, GC gout[G]) {
+    const uint32_t bp = 2u * (uint32_t)(qb & 15);
+    const uint64_t x = ((((uint64_t)w.x << 32) | w.y) << bp) | (((uint64_t)w.z << bp) >> 32);
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+      gout[gi] = gcode;
+      gcode = ((gcode << (2 * J)) | (GC)((x >> (64 - 2 * J * (gi + 1))) & fmask)) & xmask;
+    }
+  };
+  auto fetch = [&](const GC gg[G], int b0, double2 e0[G], double2 e1[G]) {
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+      const size_t ix = (b0 + gi * J < n) ? (size_t)gg[gi] : 0;
+      if (J <= 2) {
+        e0[gi] = E[ix];
+      } else {
+        e0[gi] = E[2 * ix];
+        e1[gi] = E[2 * ix + 1];
+      }
+    }
+  };
+  GC gc[G];
+  double2 e0[G], e1[G];
+  u32x3a4 win = *reinterpret_cast<const u32x3a4 *>(packed + (q0 >> 4));
+  roll(win, q0, gc);
+  fetch(gc, 0, e0, e1);
+  win = *reinterpret_cast<const u32x3a4 *>(packed + ((q0 + PB) >> 4));
+  double prev = 0.0, best = 0.0;
+  int beg = -1, arg = 0;
+  double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
+  bool special = false;
+  for (int b0 = 0; b0 < n; b0 += PB) {
+    GC gn[G];
+    double2 n0[G], n1[G];
+    roll(win, q0 + b0 + PB, gn);
+    fetch(gn, b0 + PB, n0, n1);
+    win = *reinterpret_cast<const u32x3a4 *>(packed + ((q0 + b0 + 2 * PB) >> 4));
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+      const double ev[4] = {e0[gi].x, e0[gi].y, J > 2 ? e1[gi].x : 0.0, J > 3 ? e1[gi].y : 0.0};
+#pragma unroll
+      for (int t = 0; t < J; ++t) {
+        const int j = gi * J + t;
+        double s = ev[t];
+        if (kTrlr && first && b0 == 0 && j == 0) s = first_val;
+        const int i = b0 + j;
+        if (i < n) {
+          if (visits) atomicAdd(&visits[(uint32_t)(gc[gi] >> (2 * (J - 1 - t))) & kmask], 1u);
+          asum += s;
+          pmin = asum < pmin ? asum : pmin;
+          pmax = asum > pmax ? asum : pmax;
+          sabs += fabs(s);
+          special |= !isfinite(s);
+          const double tt = prev + s;
+          const double S = tt > 0 ? tt : 0.0;
+          const bool open = (prev == 0) & (S > 0);
+          const bool close = (prev > 0) & (S == 0);
+          const int f0 = first ? 0 : -1;
+          const long long ml = kTrlr ? ec.min_len : 0;
+          const bool want =
+              kTrlr ? (close & (((long long)((arg != f0 ? arg - 1 : arg) - (beg != f0 ? beg - 1 : beg)) >= ml) |
+                                ((long long)((i != f0 ? i - 1 : i) - (arg != f0 ? arg - 1 : arg) - 1) >=
+                                 (ml > 1 ? ml : 1LL))))
+                    : (close & ((uint64_t)(int64_t)(arg - beg) >= ec.mw) & (best >= ec.min_score));
+          if (want) {
+            const int64_t slot = append_one(cand.count, cand.segcap);
+            if (slot >= 0) {
+              cand.beg[slot] = start + beg;
+              cand.arg[slot] = start + arg;
+              cand.rst[slot] = start + i;
+              cand.best[slot] = best;
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+          }
+          const bool up = open | (S > best);
+          best = up ? S : best;
+          arg = up ? i : arg;
+          beg = open ? i : (close ? -1 : beg);
+          prev = S;
+        }
+      }
+    }
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+      gc[gi] = gn[gi];
+      e0[gi] = n0[gi];
+      e1[gi] = n1[gi];
+    }
+  }
+  o.cexit[c] = prev;
+  o.asum[c] = asum;
+  o.pmin[c] = pmin;
+  o.pmax[c] = pmax;
+  o.sabs[c] = sabs;
+  o.special[c] = special ? 1 : 0;
+  if (prev > 0) {
+    o.tbeg[c] = beg; o.tmax[c] = best; o.targ[c] = arg;
+  } else {
+    o.tbeg[c] = -1; o.tmax[c] = 0.0; o.targ[c] = 0;
+  }
+}
+
 // ------------------------------------------------------------------- P3
 
 // Bits of a positive normal double in binade e: x = m * 2^(e-52), m in [2^52, 2^53).
@@ -1952,8 +2082,9 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // (chunk starts increase with the chunk index, so they are among the last
   // kP1TailMargin + CH chunks) to k_pass1
   const int64_t ctail = nch > 512 ? nch - 512 : 0;
-#define KS_P1T(J, L)                                                                                           \
-  hipLaunchKernelGGL((k_pass1<J, true, L>), dim3((unsigned)((nch - ctail + 1023) / 1024)), dim3(1024), 0, side, g, \
+#define KS_P1T(J, L) KS_P1TC(J, true, L)
+#define KS_P1TC(J, C, L)                                                                                       \
+  hipLaunchKernelGGL((k_pass1<J, C, L>), dim3((unsigned)((nch - ctail + 1023) / 1024)), dim3(1024), 0, side, g, \
                      s->seq, total, k, tv, codes, ec, visits, p1, cand, ctail, 1)
   const int J = (tv.ext != nullptr) ? tv.ext_J : 1;
   const bool pipelined = getenv("KS_NO_PIPELINED_P1") == nullptr && runs.packed != nullptr;
@@ -1985,6 +2116,27 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     }
     KS_HIP(hipGetLastError());
     if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
+  } else if (!comp && J >= 2 && J <= 4 && pipelined) {
+    hipStream_t side = ctx->side;
+    const bool tail = nch > ctail;
+    if (tail) {
+      KS_HIP(hipEventRecord(ctx->ev[12], st));
+      KS_HIP(hipStreamWaitEvent(side, ctx->ev[12], 0));
+      if (J == 4) KS_P1TC(4, false, false); else if (J == 3) KS_P1TC(3, false, false); else KS_P1TC(2, false, false);
+      KS_HIP(hipGetLastError());
+      KS_HIP(hipEventRecord(ctx->ev[13], side));
+    }
+#define KS_P1PF(J)                                                                                             \
+    do {                                                                                                       \
+      if (ec.trlr) hipLaunchKernelGGL((k_pass1pf<J, true>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, \
+                                      tv, ec, visits, p1, cand, runs.packed);                                  \
+      else hipLaunchKernelGGL((k_pass1pf<J, false>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv,  \
+                              ec, visits, p1, cand, runs.packed);                                              \
+    } while (0)
+    if (J == 4) KS_P1PF(4); else if (J == 3) KS_P1PF(3); else KS_P1PF(2);
+#undef KS_P1PF
+    KS_HIP(hipGetLastError());
+    if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
   } else if (comp && J == 5) {
     KS_P1(5, true, false);  // 12-bit codes: value LUT of the short codes in LDS
   } else if (comp && lds_lut) {
@@ -1996,6 +2148,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   }
 #undef KS_P1
 #undef KS_P1T
+#undef KS_P1TC
 #undef KS_P1P
   KS_HIP(hipGetLastError());
   KS_HIP(hipEventRecord(ctx->ev[9], st));

@@ -174,6 +174,7 @@ __device__ __forceinline__ size_t code_slot(int64_t c, int i) {
 
 // Three dwords at a 4-byte-aligned address (one global_load_dwordx3).
 typedef uint32_t u32x3a4 __attribute__((ext_vector_type(3), aligned(4)));
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 // The 16 codes of indices b0 .. b0+15 (b0 % 4 == 0) as 8 words of 2 codes.
 __device__ __forceinline__ void load_codes16(const uint16_t *__restrict__ codes, int64_t c, int b0, uint32_t w[8]) {
@@ -228,7 +229,18 @@ __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restri
 
 // Bytes a pass-1 lane may read past its chunk's last scan index: the
 // pipelined kernel reads two batches ahead (k_pass1p: < 3 * 20 + 5 + 4).
-constexpr int kP1TailMargin = 96;
+constexpr int kP1TailMargin = 352;
+
+// Packed-code words staged in LDS per pass-1 lane: bases [q0, q0 + 320) of
+// its chunk (q0 = start + J - 1), loaded once (5 x 16 B) instead of one 12-B
+// load per batch, so the lane's two 128-B lines are fetched once even when
+// the random table reads evict them from L2 between batches.
+#ifdef KS_P1_NO_STAGE
+constexpr bool kP1Stage = false;
+#else
+constexpr bool kP1Stage = true;
+#endif
+constexpr int kP1StageWords = 20;
 
 // ------------------------------------------------------------------- P0
 
@@ -441,14 +453,19 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
   constexpr bool k12 = (J == 5);        // 12-bit codes with escapes
   using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;
   using EW = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;  // entry word
+  // LDS: the value LUT (all distinct values, kLds), the 12-bit code maps
+  // (J = 5; with kLds the 12-bit values are read through s_lut[s_map12[]] to
+  // leave room for the staged packed bases) and the staged bases.
+  constexpr bool kLut12 = k12 && !(kLds && kP1Stage);
   __shared__ double s_lut[kLds ? kLdsLutMax : 1];
-  __shared__ double s_lut12[k12 ? 4096 : 1];
+  __shared__ double s_lut12[kLut12 ? 4096 : 1];
   __shared__ uint16_t s_map12[k12 ? 4096 : 1];
+  __shared__ uint32_t s_pk[kP1Stage ? kP1StageWords * 1024 : 1];  // [word][lane]: conflict-free
   if (kLds)
     for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
   if (k12)
     for (int i = threadIdx.x; i < 4096; i += blockDim.x) {
-      s_lut12[i] = tv.lut12[i];
+      if (kLut12) s_lut12[i] = tv.lut12[i];
       s_map12[i] = tv.map12[i];
     }
   if (kLds || k12) __syncthreads();
@@ -472,7 +489,30 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
   // of packed codes over its whole chunk.
   const int64_t q0 = start + J - 1;
   constexpr uint64_t fmask = (1ull << (2 * J)) - 1ull;
-  u32x3a4 win = *reinterpret_cast<const u32x3a4 *>(packed + (q0 >> 4));
+  const int64_t w0 = q0 >> 4;
+  uint32_t *const pk = s_pk + threadIdx.x;
+  if (kP1Stage) {  // (the tail margin keeps these 20 words inside the packed array)
+#pragma unroll
+    for (int i = 0; i < kP1StageWords / 4; ++i) {
+      const u32x4a4 v4 = *reinterpret_cast<const u32x4a4 *>(packed + w0 + 4 * i);
+      pk[(4 * i + 0) * 1024] = v4.x;
+      pk[(4 * i + 1) * 1024] = v4.y;
+      pk[(4 * i + 2) * 1024] = v4.z;
+      pk[(4 * i + 3) * 1024] = v4.w;
+    }
+  }
+  // window of 3 words at packed word wq (staged: clamped to the lane's slot;
+  // only prefetches past the chunk's last batch are clamped, and unused)
+  auto window = [&](int64_t wq) -> u32x3a4 {
+    if (!kP1Stage) return *reinterpret_cast<const u32x3a4 *>(packed + wq);
+    const int i = min((int)(wq - w0), kP1StageWords - 3);
+    u32x3a4 r;
+    r.x = pk[i * 1024];
+    r.y = pk[(i + 1) * 1024];
+    r.z = pk[(i + 2) * 1024];
+    return r;
+  };
+  u32x3a4 win = window(q0 >> 4);
   GC gc[G];
   EW e[G];
   {
@@ -485,7 +525,7 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
     }
   }
   // prologue: reads of batch 0, window of batch 1
-  win = *reinterpret_cast<const u32x3a4 *>(packed + ((q0 + PB) >> 4));
+  win = window((q0 + PB) >> 4);
 #pragma unroll
   for (int gi = 0; gi < G; ++gi) e[gi] = ext[(gi * J < n) ? gc[gi] : (GC)0];
   double prev = 0.0, best = 0.0;
@@ -542,7 +582,7 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
 #endif
     }
     // 3. window of batch b+2
-    win = *reinterpret_cast<const u32x3a4 *>(packed + ((q0 + b0 + 2 * PB) >> 4));
+    win = window((q0 + b0 + 2 * PB) >> 4);
     // 4. batch b group by group: values, packed codes, trajectory
     uint32_t cw[PB / 2];
 #pragma unroll
@@ -556,7 +596,7 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
           const uint32_t c12 = (uint32_t)(e[gi] >> (12 * t)) & 0xfffu;
           if (c12 != 0xfffu) {
             qq = s_map12[c12];
-            s = s_lut12[c12];
+            s = kLut12 ? s_lut12[c12] : s_lut[qq];
           } else {
             qq = (j == ja) ? qa : qb;
             if (j != ja && j != jb) {  // third escape of the batch: load and drain here
@@ -2081,7 +2121,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // k_pass1p leaves the chunks whose reads could pass the end of the buffer
   // (chunk starts increase with the chunk index, so they are among the last
   // kP1TailMargin + CH chunks) to k_pass1
-  const int64_t ctail = nch > 512 ? nch - 512 : 0;
+  const int64_t ctail = nch > 1024 ? nch - 1024 : 0;
 #define KS_P1T(J, L) KS_P1TC(J, true, L)
 #define KS_P1TC(J, C, L)                                                                                       \
   hipLaunchKernelGGL((k_pass1<J, C, L>), dim3((unsigned)((nch - ctail + 1023) / 1024)), dim3(1024), 0, side, g, \

@@ -241,6 +241,9 @@ constexpr bool kP1Stage = false;
 constexpr bool kP1Stage = true;
 #endif
 constexpr int kP1StageWords = 20;
+#ifndef KS_P1_G
+#define KS_P1_G 4
+#endif
 
 // ------------------------------------------------------------------- P0
 
@@ -448,7 +451,8 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
                                                  TableView tv, uint16_t *__restrict__ codes, EmitCfg ec,
                                                  uint32_t *__restrict__ visits, P1 o, Cand cand,
                                                  const uint32_t *__restrict__ packed) {
-  constexpr int G = 4;                  // table reads per batch
+  constexpr int G = KS_P1_G;            // table reads per batch
+  static_assert((G * J) % 4 == 0, "the code store writes 4 codes per 8-B word");
   constexpr int PB = G * J;             // scan indices per batch (8, 12, 16, 20)
   constexpr bool k12 = (J == 5);        // 12-bit codes with escapes
   using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;
@@ -548,13 +552,17 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
       ja = m ? __builtin_ctz(m) : PB;
       jb = m2 ? __builtin_ctz(m2) : PB;
       // k-mer of slot jj (index 0 when absent): group jj / 5, offset jj % 5
+      // k-mer of slot jj (index 0 when absent), selected among per-group
+      // values (not array elements, so gc[] is never indexed dynamically)
       auto kmer_of = [&](int jj) -> uint32_t {
-        const int gi = (jj * 13) >> 6;  // jj / 5 for jj < 20
-        const int t = jj - J * gi;
-        GC gg = gc[0];
+        uint32_t km = 0;
 #pragma unroll
-        for (int q = 1; q < G; ++q) gg = (gi == q) ? gc[q] : gg;
-        return jj < PB ? (uint32_t)(gg >> (2 * (J - 1 - t))) & kmask : 0u;
+        for (int q = 0; q < G; ++q) {
+          const uint32_t t = (uint32_t)(jj - q * J);  // < J iff slot jj is in group q
+          const uint32_t kq = (uint32_t)(gc[q] >> (2 * (J - 1 - (t < J ? t : 0u)))) & kmask;
+          km = t < (uint32_t)J ? kq : km;
+        }
+        return km;
       };
       qa = tv.codes[kmer_of(ja)];
       qb = tv.codes[kmer_of(jb)];

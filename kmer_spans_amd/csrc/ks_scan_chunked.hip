@@ -240,10 +240,14 @@ constexpr bool kP1Stage = false;
 #else
 constexpr bool kP1Stage = true;
 #endif
-constexpr int kP1StageWords = 20;
 #ifndef KS_P1_G
 #define KS_P1_G 4
 #endif
+// G = 8 (40 indices per batch at J = 5): twice the table reads in flight per
+// lane, at 3 waves per SIMD (768-lane blocks, <= 168 VGPRs)
+constexpr int kP1G = KS_P1_G;
+constexpr int kP1Block = kP1G > 4 ? 768 : 1024;
+constexpr int kP1StageWords = kP1G > 4 ? 24 : 20;
 
 // ------------------------------------------------------------------- P0
 
@@ -447,11 +451,12 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
 // escape in one batch, the candidate append) drain explicitly inside the
 // branch.  Results are identical to k_pass1.
 template <int J, bool kLds, bool kTrlr>
-__global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
+__global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
                                                  TableView tv, uint16_t *__restrict__ codes, EmitCfg ec,
                                                  uint32_t *__restrict__ visits, P1 o, Cand cand,
                                                  const uint32_t *__restrict__ packed) {
-  constexpr int G = KS_P1_G;            // table reads per batch
+  constexpr int G = kP1G;               // table reads per batch
+  constexpr int BS = kP1Block;          // lanes per block (LDS staging stride)
   static_assert((G * J) % 4 == 0, "the code store writes 4 codes per 8-B word");
   constexpr int PB = G * J;             // scan indices per batch (8, 12, 16, 20)
   constexpr bool k12 = (J == 5);        // 12-bit codes with escapes
@@ -464,7 +469,7 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
   __shared__ double s_lut[kLds ? kLdsLutMax : 1];
   __shared__ double s_lut12[kLut12 ? 4096 : 1];
   __shared__ uint16_t s_map12[k12 ? 4096 : 1];
-  __shared__ uint32_t s_pk[kP1Stage ? kP1StageWords * 1024 : 1];  // [word][lane]: conflict-free
+  __shared__ uint32_t s_pk[kP1Stage ? kP1StageWords * BS : 1];  // [word][lane]: conflict-free
   if (kLds)
     for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
   if (k12)
@@ -492,40 +497,60 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
   // 2*PB <= 40 bits at any offset), so a lane touches one or two 128-B lines
   // of packed codes over its whole chunk.
   const int64_t q0 = start + J - 1;
-  constexpr uint64_t fmask = (1ull << (2 * J)) - 1ull;
   const int64_t w0 = q0 >> 4;
   uint32_t *const pk = s_pk + threadIdx.x;
   if (kP1Stage) {  // (the tail margin keeps these 20 words inside the packed array)
 #pragma unroll
     for (int i = 0; i < kP1StageWords / 4; ++i) {
       const u32x4a4 v4 = *reinterpret_cast<const u32x4a4 *>(packed + w0 + 4 * i);
-      pk[(4 * i + 0) * 1024] = v4.x;
-      pk[(4 * i + 1) * 1024] = v4.y;
-      pk[(4 * i + 2) * 1024] = v4.z;
-      pk[(4 * i + 3) * 1024] = v4.w;
+      pk[(4 * i + 0) * BS] = v4.x;
+      pk[(4 * i + 1) * BS] = v4.y;
+      pk[(4 * i + 2) * BS] = v4.z;
+      pk[(4 * i + 3) * BS] = v4.w;
     }
   }
   // window of 3 words at packed word wq (staged: clamped to the lane's slot;
   // only prefetches past the chunk's last batch are clamped, and unused)
-  auto window = [&](int64_t wq) -> u32x3a4 {
-    if (!kP1Stage) return *reinterpret_cast<const u32x3a4 *>(packed + wq);
-    const int i = min((int)(wq - w0), kP1StageWords - 3);
-    u32x3a4 r;
-    r.x = pk[i * 1024];
-    r.y = pk[(i + 1) * 1024];
-    r.z = pk[(i + 2) * 1024];
+  constexpr int WW = (2 * PB > 64) ? 5 : 3;  // window words: 2 x 64 bits of bases when PB > 32
+  struct Win { uint32_t w[WW]; };
+  auto window = [&](int64_t wq) -> Win {
+    Win r;
+    if (!kP1Stage) {
+#pragma unroll
+      for (int q = 0; q < WW; ++q) r.w[q] = packed[wq + q];
+      return r;
+    }
+    const int i = min((int)(wq - w0), kP1StageWords - WW);
+#pragma unroll
+    for (int q = 0; q < WW; ++q) r.w[q] = pk[(i + q) * BS];
     return r;
   };
-  u32x3a4 win = window(q0 >> 4);
+  // bases [qb, qb + 64) of window wn (qb & 15 = the offset in its first word)
+  auto bits = [&](const Win &wn, int64_t qb, uint64_t &lo, uint64_t &hi) {
+    const uint32_t bp = 2u * (uint32_t)(qb & 15);
+    lo = ((((uint64_t)wn.w[0] << 32) | wn.w[1]) << bp) | (((uint64_t)wn.w[2] << bp) >> 32);
+    hi = 0;
+    if (WW == 5) hi = ((((uint64_t)wn.w[2] << 32) | wn.w[3]) << bp) | (((uint64_t)wn.w[4] << bp) >> 32);
+  };
+  // the 2J bits of group gi (bases gi*J .. gi*J + J - 1 of the batch)
+  auto field = [&](uint64_t lo, uint64_t hi, int gi) -> uint64_t {
+    const int e = 2 * J * (gi + 1);  // end bit of the group in the 128-bit lo:hi
+    uint64_t f;
+    if (e <= 64) f = lo >> (64 - e);
+    else if (e - 2 * J >= 64) f = hi >> (128 - e);
+    else f = (lo << (e - 64)) | (hi >> (128 - e));
+    return f & ((1ull << (2 * J)) - 1ull);
+  };
+  Win win = window(q0 >> 4);
   GC gc[G];
   EW e[G];
   {
-    const uint32_t bp = 2u * (uint32_t)(q0 & 15);
-    const uint64_t x = ((((uint64_t)win.x << 32) | win.y) << bp) | (((uint64_t)win.z << bp) >> 32);
+    uint64_t lo, hi;
+    bits(win, q0, lo, hi);
 #pragma unroll
     for (int gi = 0; gi < G; ++gi) {
       gc[gi] = gcode;
-      gcode = ((gcode << (2 * J)) | (GC)((x >> (64 - 2 * J * (gi + 1))) & fmask)) & xmask;
+      gcode = ((gcode << (2 * J)) | (GC)field(lo, hi, gi)) & xmask;
     }
   }
   // prologue: reads of batch 0, window of batch 1
@@ -542,15 +567,15 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
     int ja = PB, jb = PB;
     uint32_t qa = 0, qb = 0;
     if (k12) {
-      uint32_t m = 0;
+      uint64_t m = 0;
 #pragma unroll
       for (int gi = 0; gi < G; ++gi)
 #pragma unroll
         for (int t = 0; t < J; ++t)
-          if (((uint32_t)(e[gi] >> (12 * t)) & 0xfffu) == 0xfffu) m |= 1u << (gi * J + t);
-      const uint32_t m2 = m & (m - 1u);
-      ja = m ? __builtin_ctz(m) : PB;
-      jb = m2 ? __builtin_ctz(m2) : PB;
+          if (((uint32_t)(e[gi] >> (12 * t)) & 0xfffu) == 0xfffu) m |= 1ull << (gi * J + t);
+      const uint64_t m2 = m & (m - 1ull);
+      ja = m ? __builtin_ctzll(m) : PB;
+      jb = m2 ? __builtin_ctzll(m2) : PB;
       // k-mer of slot jj (index 0 when absent): group jj / 5, offset jj % 5
       // k-mer of slot jj (index 0 when absent), selected among per-group
       // values (not array elements, so gc[] is never indexed dynamically)
@@ -571,12 +596,12 @@ __global__ void __launch_bounds__(1024) k_pass1p(Chunks g, const uint8_t *__rest
     GC gn[G];
     EW en[G];
     {
-      const uint32_t bp = 2u * (uint32_t)((q0 + b0 + PB) & 15);
-      const uint64_t x = ((((uint64_t)win.x << 32) | win.y) << bp) | (((uint64_t)win.z << bp) >> 32);
+      uint64_t lo, hi;
+      bits(win, q0 + b0 + PB, lo, hi);
 #pragma unroll
       for (int gi = 0; gi < G; ++gi) {
         gn[gi] = gcode;
-        gcode = ((gcode << (2 * J)) | (GC)((x >> (64 - 2 * J * (gi + 1))) & fmask)) & xmask;
+        gcode = ((gcode << (2 * J)) | (GC)field(lo, hi, gi)) & xmask;
       }
     }
 #pragma unroll
@@ -2136,11 +2161,12 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                      s->seq, total, k, tv, codes, ec, visits, p1, cand, ctail, 1)
   const int J = (tv.ext != nullptr) ? tv.ext_J : 1;
   const bool pipelined = getenv("KS_NO_PIPELINED_P1") == nullptr && runs.packed != nullptr;
+  const unsigned gp1 = (unsigned)((nch + kP1Block - 1) / kP1Block);
 #define KS_P1P(J, L)                                                                                           \
   do {                                                                                                       \
-    if (ec.trlr) hipLaunchKernelGGL((k_pass1p<J, L, true>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, \
+    if (ec.trlr) hipLaunchKernelGGL((k_pass1p<J, L, true>), dim3(gp1), dim3(kP1Block), 0, st, g, s->seq, total, k, \
                                     tv, codes, ec, visits, p1, cand, runs.packed);                             \
-    else hipLaunchKernelGGL((k_pass1p<J, L, false>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv,  \
+    else hipLaunchKernelGGL((k_pass1p<J, L, false>), dim3(gp1), dim3(kP1Block), 0, st, g, s->seq, total, k, tv,  \
                             codes, ec, visits, p1, cand, runs.packed);                                         \
   } while (0)
   if (comp && J >= 2 && pipelined) {

@@ -246,7 +246,11 @@ constexpr bool kP1Stage = true;
 // G = 8 (40 indices per batch at J = 5): twice the table reads in flight per
 // lane, at 3 waves per SIMD (768-lane blocks, <= 168 VGPRs)
 constexpr int kP1G = KS_P1_G;
-constexpr int kP1Block = kP1G > 4 ? 768 : 1024;
+#ifndef KS_P1_BLOCK
+#define KS_P1_BLOCK (KS_P1_G > 4 ? 768 : 1024)
+#endif
+constexpr int kP1Block = KS_P1_BLOCK;  // lanes per pass-1 block (build parameter for A/B runs)
+static_assert(kP1Block % 64 == 0 && kP1Block <= 1024, "pass-1 block is whole waves");
 constexpr int kP1StageWords = kP1G > 4 ? 24 : 20;
 
 // ------------------------------------------------------------------- P0

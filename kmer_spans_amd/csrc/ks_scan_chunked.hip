@@ -698,7 +698,12 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
 #pragma unroll
     for (int r4 = 0; r4 < PB / 4; ++r4)
       if (b0 + 4 * r4 < CH)
+#ifndef KS_P1_PLAIN_CODES  // nontemporal code stores: A/B 16.19-16.21 vs 16.31-16.57 ms
+        __builtin_nontemporal_store((uint64_t)cw[2 * r4] | ((uint64_t)cw[2 * r4 + 1] << 32),
+                                    reinterpret_cast<uint64_t *>(codes + code_slot(c, b0 + 4 * r4)));
+#else
         *reinterpret_cast<uint2 *>(codes + code_slot(c, b0 + 4 * r4)) = make_uint2(cw[2 * r4], cw[2 * r4 + 1]);
+#endif
 #pragma unroll
     for (int gi = 0; gi < G; ++gi) {
       gc[gi] = gn[gi];

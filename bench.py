@@ -5,22 +5,41 @@
   spans bit-exact.
 
 One *step* = one ks_scan_dev pass (run segmentation + scan + region
-ordering/D2H) over the whole device-resident genome.  The genome is
-synthetic (kmer_spans_amd.genome.human_like, GRCh38 contig lengths, repeats
-and N gaps) and generated on the GPU; the log2(f/f_med) table is built from
-the genome's own k-mer counts before timing.  With N ranks (torchrun), every
-rank scans its own genome (different seed): weak scaling, no collective on
-the data path; span records are gathered to rank 0 over RCCL after timing.
+ordering/D2H) over the device-resident sequences of a rank.  Genomes are
+synthetic (kmer_spans_amd.genome.human_like: GRCh38 contig lengths, repeats,
+N gaps), generated on the GPU from seeds; the score table is built from the
+genome's own k-mer counts before timing (the table is an input of
+kmer_regions_r), and its cost is reported beside the value as `setup_ms` and
+an end-to-end rate.
+
+Multi-GPU: `python bench.py --gpus N` starts N ranks itself
+(one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE set before any HIP call in
+the children; the parent never touches the GPU), or runs as one rank under
+torchrun.  Backend "nccl" (RCCL over xGMI) when every rank has its own GPU,
+gloo for rehearsals with more ranks than GPUs.  Modes:
+  genome  (default, weak scaling) every rank scans its own genome (config 5
+          shape: genomes stay whole per GPU); records gathered to rank 0.
+  shard   (strong scaling) ONE genome, contigs LPT-sharded over the ranks;
+          per-rank counts summed with an int32 all-reduce before the table is
+          built; records gathered to rank 0 and merged (dist.merge_shards).
+  genomes (config 5) every rank processes --genomes-per-rank genomes; each
+          timed end to end: count + table (+ expanded table) + scan.
+No collective runs on the data path: the only exchanges are the count
+all-reduce (shard) and the record gather after timing.
 
 Prints ONE JSON line on rank 0 (the driver's contract) with the roofline of
-the dominant kernel (timed with hipEvents on the library's stream inside the
-timed steps) and the CPU oracle timed on a bounded sample on rank 0.
+the dominant kernel (hipEvents on the library's stream inside the timed
+steps), and at N=1 the CPU oracle timed on a bounded sample (which always
+includes the largest contig, the longest exact-carry chain) plus the parity
+verdict of that sample.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,6 +52,8 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 ALGO_BYTES_PER_BASE = 9.0      # 1 B sequence + 8 B FP64 table entry (k >= 8)
 RANDOM_WALL_GPS = 48.0         # measured random-request ceiling (profiles/r1_gather_bench2.jsonl)
+METRIC = "Gbases/sec scanned (k=13, log-ratio score) at 1/2/4/8 MI355X; spans bit-exact"
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 
 
 def cpu_model() -> str:
@@ -45,11 +66,13 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1, help="ranks to run (one process per GPU)")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--mode", choices=["genome", "shard", "genomes"], default="genome")
+    p.add_argument("--genomes-per-rank", type=int, default=2, help="--mode genomes: genomes per rank")
     p.add_argument("--scale", type=float, default=1.0, help="genome scale (1.0 = 3.09 Gbp)")
     p.add_argument("--k", type=int, default=13)
     p.add_argument("--score", choices=["log2", "pm1", "rank"], default="log2")
@@ -59,24 +82,129 @@ def parse():
     p.add_argument("--min-score", type=float, default=20.0)
     p.add_argument("--algo", type=int, default=-1, help="-1 auto, 0 lane-per-run, 1 chunked")
     p.add_argument("--seed", type=int, default=1)
-    p.add_argument("--cpu-sample", type=float, default=2.0e8, help="bases in the CPU-baseline sample")
+    p.add_argument("--cpu-sample", type=float, default=2.0e8,
+                   help="bases of the CPU-baseline sample besides the largest contig")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-expand", action="store_true", help="do not build the expanded (k+J-1)-mer table")
     p.add_argument("--ncontigs", type=int, default=24, help="1 = the chr1-like single contig of config 2")
     p.add_argument("--host-path", action="store_true",
-                   help="also time the host-pointer entry point (ks_kmer_regions: staging + PCIe + scan)")
+                   help="also time the host-pointer entry point (ks_kmer_regions with visits: staging + PCIe + scan)")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
-    return p.parse_args()
+    return p.parse_args(argv)
 
+
+# ----------------------------------------------------------------- launcher
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn(n: int) -> int:
+    """Start n ranks of this script as child processes (the parent makes no
+    HIP call: it only sets the rank environment) and return the worst exit
+    code."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max((abs(rc) for rc in rcs), default=0)
+
+
+# ------------------------------------------------------------------ helpers
+
+def score_table(api, hc, k, words, score):
+    if score == "log2":
+        return api.log2_table(hc, k), 0.0
+    if score == "pm1":
+        return api.pm1_table(hc, k), 0.0
+    return api.rank_table(hc, k, words), 0.75
+
+
+def pmc_traffic(kernel_prefix, build_id, workload):
+    """HBM bytes per launch of the dominant kernel from the committed PMC
+    passes (tools/gpu_pmc.sh -> profiles/pmc_summary.json), used only when
+    they were taken on this very build (library build id) and workload.
+    FETCH_SIZE counts 64 B per memory-side read request; the kernel's only
+    streaming read (the packed bases, total/4 bytes, 16-B loads) is under-
+    counted by half on gfx950 (MI355X_MICROARCH.md, HBM), so that half is
+    added back; WRITE_SIZE is exact for the 8-B stores."""
+    if not os.path.exists(PMC_SUMMARY):
+        return None, "no PMC summary"
+    pmc = json.load(open(PMC_SUMMARY))
+    if pmc.get("build_id") != build_id:
+        return None, f"stale: PMC summary of build {pmc.get('build_id')}, this library is {build_id}"
+    if pmc.get("workload") != workload:
+        return None, "PMC summary is for another workload"
+    for name, cs in pmc.get("kernels", {}).items():
+        if name.startswith(kernel_prefix) and "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+            fetch = cs["FETCH_SIZE"] * 1e3
+            corr = pmc.get("streaming_read_bytes", {}).get(name, 0.0) / 2.0
+            return {"bytes": int(round(fetch + cs["WRITE_SIZE"] * 1e3 + corr)), "fetch": int(fetch),
+                    "write": int(cs["WRITE_SIZE"] * 1e3), "streaming_correction": int(corr),
+                    "read_requests": int(fetch / 64.0), "kernel": name}, "ok"
+    return None, "kernel not in the PMC summary"
+
+
+def sample_ids(offsets, budget):
+    """Contigs of the CPU sample: the largest one (longest carry chain at the
+    metric config) plus the smallest ones up to `budget` more bases."""
+    lens = np.diff(offsets)
+    big = int(np.argmax(lens))
+    ids, acc = [big], int(lens[big])
+    for q in np.argsort(lens):
+        q = int(q)
+        if q == big:
+            continue
+        if acc - int(lens[big]) >= budget:
+            break
+        ids.append(q)
+        acc += int(lens[q])
+    return sorted(ids), acc
+
+
+def parity_of(pos, score, ids, o, one):
+    """GPU records of the sampled contigs (ids, in the GPU's numbering) equal
+    the oracle's records of those contigs (numbered 0.. in ids order)."""
+    sel = np.isin(pos[0] - one, ids)
+    gp = pos[:, sel].copy()
+    remap = {q: i for i, q in enumerate(ids)}
+    gp[0] = [remap[int(x) - one] + one for x in gp[0]]
+    gs = score[:, sel]
+    return bool(np.array_equal(gp, o["pos"]) and np.array_equal(gs.view(np.uint64), o["score"].view(np.uint64)))
+
+
+class Timer:
+    """Wall time of device work: synchronize on both sides."""
+
+    def __enter__(self):
+        torch.cuda.synchronize()
+        self.t = time.perf_counter()
+        return self
+
+    def __exit__(self, *a):
+        torch.cuda.synchronize()
+        self.ms = (time.perf_counter() - self.t) * 1e3
+
+
+# --------------------------------------------------------------------- main
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
     ndev = torch.cuda.device_count()
     gpu = local % max(ndev, 1)  # ranks > GPUs only when rehearsing N>1 on a small box
+    tdist = None
     if dist:
         import torch.distributed as tdist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -96,99 +224,138 @@ def main():
     D.bind_torch_stream(ctx)
     if args.algo >= 0:
         ctx.set_scan_algo(args.algo)
+    build_id = _lib.build_id()
 
-    # ---- synthetic genome (device-resident) + score table from its counts
-    t0 = time.time()
-    parts, lens = genome.human_like(scale=args.scale, seed=args.seed + 1000 * rank, device=dev,
-                                    ncontigs=args.ncontigs)
-    ds = D.from_parts(parts, lens, dev)
-    del parts
-    torch.cuda.synchronize()
-    t_gen = time.time() - t0
-    counts = torch.zeros(4 ** k, dtype=torch.int32, device=dev)
-    t0 = time.time()
-    words = D.count(ctx, ds, k, counts)
-    torch.cuda.synchronize()
-    t_count = time.time() - t0
-    hc = counts.cpu().numpy()
-    thr = 0.0
-    if args.score == "log2":
-        w = api.log2_table(hc, k)
-    elif args.score == "pm1":
-        w = api.pm1_table(hc, k)
-    else:
-        w, thr = api.rank_table(hc, k, words), 0.75
-    t0 = time.time()
-    if args.trlr:  # tr_lr tables carry no threshold: transition = init = w - thr
-        w, thr = np.asarray(w, dtype=np.float64) - thr, 0.0
-    table = D.DeviceTable(ctx, w, k, thr, compress=True, expand=not args.no_expand, freq=counts)
-    init_table = D.DeviceTable(ctx, w, k, thr, compress=False) if args.trlr else None
-    torch.cuda.synchronize()
-    t_table = time.time() - t0
+    def barrier():
+        if dist:
+            tdist.barrier()
 
-    def step():
+    def max_over_ranks(x: float) -> float:
+        if not dist:
+            return x
+        e = torch.tensor([x], dtype=torch.float64, device=dev if tdist.get_backend() == "nccl" else "cpu")
+        tdist.all_reduce(e, op=tdist.ReduceOp.MAX)
+        return float(e.item())
+
+    def make_table(counts, words, hint=True):
+        """Host score table from the counts + device table (timed pieces)."""
+        t = {}
+        with Timer() as tm:
+            hc = counts.cpu().numpy()
+            w, thr = score_table(api, hc, k, words, args.score)
+            if args.trlr:  # tr_lr tables carry no threshold: transition = init = w - thr
+                w, thr = np.asarray(w, dtype=np.float64) - thr, 0.0
+        t["table_host"] = tm.ms
+        with Timer() as tm:
+            table = D.DeviceTable(ctx, w, k, thr, compress=True, expand=not args.no_expand,
+                                  freq=counts if hint else None)
+            init = D.DeviceTable(ctx, w, k, thr, compress=False) if args.trlr else None
+        t["table_device"] = tm.ms
+        t.update({f"table_{key}": v for key, v in table.setup_ms().items()})
+        return w, thr, table, init, t
+
+    def scan_once(ds, table, init):
         if args.trlr:
-            return D.tr_lr(ctx, ds, k, table, init_table, args.min_width)
+            return D.tr_lr(ctx, ds, k, table, init, args.min_width)
         return D.scan(ctx, ds, k, table, args.min_width, args.min_score)
 
+    setup = {}
+    extra = {}
+    # ------------------------------------------------------------ the input
+    t0 = time.time()
+    if args.mode == "shard":
+        lens_all = [max(1, int(round(L * args.scale))) for L in genome.GRCH38[:args.ncontigs]]
+        from kmer_spans_amd.dist import lpt_shards
+        shards = lpt_shards(lens_all, world)
+        mine = shards[rank]
+        parts = [genome.contig(lens_all[q], args.seed + q, dev) for q in mine]
+        ds = D.from_parts(parts, [lens_all[q] for q in mine], dev)
+        genome_bp = sum(lens_all)
+    else:
+        parts, lens = genome.human_like(scale=args.scale, seed=args.seed + 1000 * rank, device=dev,
+                                        ncontigs=args.ncontigs)
+        ds = D.from_parts(parts, lens, dev)
+    del parts
+    torch.cuda.synchronize()
+    setup["genome_s"] = round(time.time() - t0, 2)
+
+    if args.mode == "genomes":
+        return run_genomes(args, ctx, ds, dev, rank, world, dist, tdist, barrier, max_over_ranks, make_table, D,
+                           genome, build_id)
+
+    # ------------------------------------------------------ counts -> table
+    counts = torch.zeros(4 ** k, dtype=torch.int32, device=dev)
+    with Timer() as tm:
+        words = D.count(ctx, ds, k, counts)
+    setup["count_ms"] = round(tm.ms, 2)
+    if args.mode == "shard":  # the table of the whole genome: exact int32 sum of per-shard counts
+        from kmer_spans_amd.dist import allreduce_histogram
+        with Timer() as tm:
+            if tdist.get_backend() == "nccl":
+                allreduce_histogram(counts)
+                wt = torch.tensor([words], dtype=torch.float64, device=dev)
+            else:
+                c = counts.cpu()
+                allreduce_histogram(c)
+                counts.copy_(c)
+                wt = torch.tensor([words], dtype=torch.float64)
+            tdist.all_reduce(wt)
+            words = float(wt.item())
+        setup["count_allreduce_ms"] = round(tm.ms, 2)
+    w, thr, table, init_table, tt = make_table(counts, words)
+    setup.update({key: round(v, 2) for key, v in tt.items()})
+
+    # ------------------------------------------------------------- timing
     for _ in range(args.warmup):
-        step()
-    if dist:
-        tdist.barrier()
+        scan_once(ds, table, init_table)
+    barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     stats = []
     for _ in range(args.steps):
-        pos, score, st = step()
+        pos, score, st = scan_once(ds, table, init_table)
         stats.append(st)
     torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev if tdist.get_backend() == "nccl" else "cpu")
-        tdist.all_reduce(e, op=tdist.ReduceOp.MAX)
-        elapsed = float(e.item())
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
 
     n_bases = int(stats[-1]["n_bases"])
-    total_bases = n_bases * world
+    total_bases = genome_bp if args.mode == "shard" else n_bases * world
     ms_step = elapsed / args.steps * 1e3
     value = total_bases / (elapsed / args.steps) / 1e9
 
     # ---- span records to rank 0 (RCCL gather; not on the timed path)
     n_regions_all = int(pos.shape[1])
     if dist:
-        from kmer_spans_amd.dist import gather_regions
-        allpos, _ = gather_regions(pos, score, dev)
-        n_regions_all = sum(int(p.shape[1]) for p in allpos) if rank == 0 else n_regions_all
+        from kmer_spans_amd.dist import gather_regions, merge_shards
+        allpos, allscore = gather_regions(pos, score, dev)
+        if rank == 0:
+            n_regions_all = sum(int(p.shape[1]) for p in allpos)
+            if args.mode == "shard":
+                mpos, _ = merge_shards(shards, allpos, allscore, one_based=args.trlr)
+                extra["merged_regions"] = int(mpos.shape[1])
+                extra["merged_order_ok"] = bool(np.all(np.diff(mpos[0].astype(np.int64) * (1 << 32) + mpos[1]) > 0))
 
     # ---- dominant kernel roofline (hipEvents on the library stream)
     ms_kernel = float(np.mean([s["ms_scan"] for s in stats]))
     achieved = ALGO_BYTES_PER_BASE * n_bases / (ms_kernel * 1e-3) / 1e9
+    kernel = "k_scan_lane" if stats[-1]["scan_algo"] == 0 else "k_pass1p"
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": "k_scan_lane" if stats[-1]["scan_algo"] == 0 else "k_pass1p",
-                "kernel_ms": round(ms_kernel, 3), "algo_bytes_per_base": ALGO_BYTES_PER_BASE}
-    # HBM traffic per launch of the dominant kernel: rocprofv3 PMC passes of this
-    # same workload (tools/gpu_pmc.sh), committed under profiles/
-    pmc_path = os.path.join(ROOT, "profiles", "r1_pmc_summary.json")
-    if os.path.exists(pmc_path) and stats[-1]["scan_algo"] == 1 and not args.trlr:
-        pmc = json.load(open(pmc_path))
-        wl = pmc.get("workload", {})
-        if (wl.get("k") == k and wl.get("score") == args.score and wl.get("scale") == args.scale
-                and wl.get("ncontigs") == args.ncontigs and not args.no_expand):
-            for name, cs in pmc.get("kernels", {}).items():
-                if name.startswith("k_pass1") and "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
-                    roofline["traffic"] = round((cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1e3)  # KB -> B
-                    roofline["traffic_source"] = f"profiles/r1_pmc_summary.json ({name}, FETCH+WRITE)"
-                    roofline["traffic_note"] = "PMC pass of the same workload and build (tools/gpu_pmc.sh), not this run"
-                    break
-
-    # ---- the bound that applies to a gather pass: random requests.  Every
-    # table read of k_pass1p is one random request (64-B fetch) whatever its
-    # width; the chip's measured ceiling for such requests from tables of
-    # 32-128 GiB is ~48 G/s (tools/gather_bench2.hip, profiles/r1_gather_bench2.jsonl:
-    # u64 entries 47.2-49.1 G/s).  Reported beside the HBM-bytes roofline.
+                "kernel": kernel, "kernel_ms": round(ms_kernel, 3), "algo_bytes_per_base": ALGO_BYTES_PER_BASE,
+                "algo_bytes_per_launch": int(ALGO_BYTES_PER_BASE * n_bases)}
+    workload = {"k": k, "score": args.score, "scale": args.scale, "ncontigs": args.ncontigs,
+                "expand": not args.no_expand, "trlr": args.trlr, "mode": args.mode, "world": world}
+    traffic, why = pmc_traffic(kernel, build_id, workload)
+    if traffic:
+        roofline["traffic"] = traffic["bytes"]
+        roofline["traffic_detail"] = traffic
+        roofline["traffic_source"] = "profiles/pmc_summary.json (rocprofv3 --pmc passes of this build and workload)"
+    else:
+        roofline["traffic_note"] = why
+    # the bound that applies to a gather pass: random requests (every table
+    # read is one 64-B request whatever its width; the chip's measured ceiling
+    # for such requests from 32-128 GiB tables is ~48 G/s, tools/gather_bench2.hip)
     if stats[-1]["scan_algo"] == 1:
         J = max(1, int(table.positions_per_read))
         n_scored = int(stats[-1]["n_scored"])
@@ -197,42 +364,33 @@ def main():
               "achieved_G_per_s": round(reads / (ms_kernel * 1e-3) / 1e9, 2), "wall_G_per_s": RANDOM_WALL_GPS,
               "frac": round(reads / (ms_kernel * 1e-3) / 1e9 / RANDOM_WALL_GPS, 4),
               "wall_source": "profiles/r1_gather_bench2.jsonl (random u64 reads, 32-128 GiB tables)"}
-        if roofline.get("traffic") and roofline.get("traffic_source", "").find("FETCH") >= 0:
-            pmc = json.load(open(pmc_path))
-            for name, cs in pmc.get("kernels", {}).items():
-                if name.startswith("k_pass1p") and "FETCH_SIZE" in cs:
-                    req = cs["FETCH_SIZE"] * 1e3 / 64.0  # FETCH_SIZE = TCC_EA0_RDREQ x 64 B
-                    ra["memory_read_requests_per_launch"] = int(req)
-                    ra["memory_requests_G_per_s"] = round(req / (ms_kernel * 1e-3) / 1e9, 2)
-                    break
+        if traffic:
+            ra["memory_read_requests_per_launch"] = traffic["read_requests"]
+            ra["memory_requests_G_per_s"] = round(traffic["read_requests"] / (ms_kernel * 1e-3) / 1e9, 2)
         roofline["random_access"] = ra
 
-    # ---- PCIe-inclusive rate of the host entry point (reported, never `value`)
+    # ---- PCIe-inclusive rate of the drop-in host entry point (never `value`)
     host_path = None
-    if args.host_path and rank == 0 and not args.trlr:
+    if args.host_path and rank == 0 and not args.trlr and thr == 0.0:
         hs = [ds.host_seq(q) for q in range(ds.nseq)]
+        api.kmer_regions(hs, k, w, args.min_width, args.min_score)  # warm (pinned staging, workspace)
         t0 = time.perf_counter()
-        hr = api.kmer_regions(hs, k, w, args.min_width, args.min_score, visits=False) if thr == 0.0 else None
+        hr = api.kmer_regions(hs, k, w, args.min_width, args.min_score)
         t_host = time.perf_counter() - t0
-        if hr is not None:
-            host_path = {"seconds": round(t_host, 4), "Gbases_per_s": round(n_bases / t_host / 1e9, 3),
-                         "regions_equal": bool(np.array_equal(hr["pos"], pos)),
-                         "note": "ks_kmer_regions from host memory: pinned staging + H2D + table upload/compress + scan"}
+        host_path = {"seconds": round(t_host, 4), "Gbases_per_s": round(n_bases / t_host / 1e9, 3),
+                     "regions_equal": bool(np.array_equal(hr["pos"], pos)),
+                     "scores_equal": bool(np.array_equal(hr["score"].view(np.uint64), score.view(np.uint64))),
+                     "visits": True, "timing": hr.get("timing"),
+                     "note": "ks_kmer_regions from host memory with the visit histogram: pinned staging + H2D + "
+                             "table upload/compress/expand + count-derived visits + scan + D2H"}
         del hs
 
-    # ---- CPU baseline: the oracle (single thread) on a bounded sample
+    # ---- CPU baseline (N=1 only): the oracle, single thread, bounded sample
     cpu = None
     parity = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:
         from oracle import oracle as O
-        order = np.argsort(np.diff(ds.offsets))
-        ids, acc = [], 0
-        for q in order:  # smallest contigs first until the sample size is reached
-            ids.append(int(q))
-            acc += int(ds.offsets[q + 1] - ds.offsets[q])
-            if acc >= args.cpu_sample:
-                break
-        ids.sort()
+        ids, acc = sample_ids(ds.offsets, args.cpu_sample)
         host = [ds.host_seq(q) for q in ids]
         t0 = time.perf_counter()
         if args.trlr:
@@ -240,42 +398,113 @@ def main():
         else:
             o = O.scan(host, k, w, thr, args.min_width, args.min_score)
         t_cpu = time.perf_counter() - t0
+        lens = np.diff(ds.offsets)
         cpu = {"value": round(acc / t_cpu / 1e9, 5), "unit": "Gbases/s", "cores": 1, "kind": "port",
-               "sample": f"oracle/ks_oracle.c scan of {len(ids)} contigs ({acc} bp) of the same genome, same table",
+               "sample": f"oracle/ks_oracle.c scan of {len(ids)} contigs ({acc} bp: the largest, "
+                         f"{int(lens.max())} bp, plus the smallest) of the same genome, same table",
                "seconds": round(t_cpu, 3), "host_cpu": cpu_model(), "host_nproc": os.cpu_count()}
-        # parity of the sampled contigs: GPU records vs oracle records
-        one = 1 if args.trlr else 0  # tr_lr ids are 1-based
-        sel = np.isin(pos[0] - one, ids)
-        gp = pos[:, sel].copy()
-        remap = {q: i for i, q in enumerate(ids)}
-        gp[0] = [remap[int(x) - one] + one for x in gp[0]]
-        gs = score[:, sel]
-        parity = bool(np.array_equal(gp, o["pos"]) and
-                      np.array_equal(gs.view(np.uint64), o["score"].view(np.uint64)))
+        parity = parity_of(pos, score, ids, o, 1 if args.trlr else 0)
+        extra["parity_contigs"] = ids
+        extra["parity_bp"] = acc
 
+    step_ms = ms_step
+    e2e_ms = setup["count_ms"] + setup["table_host"] + setup["table_device"] + step_ms
     line = {
-        "metric": "Gbases/sec scanned (k=13, log-ratio score) at 1/2/4/8 MI355X; spans bit-exact",
+        "metric": METRIC,
         "value": round(value, 4), "unit": "Gbases/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": f"human-shaped synthetic genome ({n_bases} bp, {ds.nseq} contigs, scale {args.scale}), "
-                               f"k={k}, {args.score} score from its own counts, min_width {args.min_width}, "
-                               f"min_score {args.min_score}, device-resident",
-                   "k": k, "score": args.score, "genome_bp": n_bases, "parallelism": f"contig-shard x{world}",
-                   "scan": "tr_lr_regions" if args.trlr else "kmer_regions",
+        "scaling": "strong" if args.mode == "shard" else "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": f"human-shaped synthetic genome ({total_bases if args.mode == 'shard' else n_bases} bp, "
+                               f"{args.ncontigs} contigs, scale {args.scale}), k={k}, {args.score} score from its "
+                               f"own counts, min_width {args.min_width}, min_score {args.min_score}, device-resident"
+                               + (", contigs LPT-sharded over the ranks" if args.mode == "shard" else
+                                  ", one genome per rank"),
+                   "k": k, "score": args.score, "genome_bp": total_bases if args.mode == "shard" else n_bases,
+                   "parallelism": f"{'contig-shard' if args.mode == 'shard' else 'genome-per-rank'} x{world}",
+                   "mode": args.mode, "scan": "tr_lr_regions" if args.trlr else "kmer_regions",
                    "scan_algo": int(stats[-1]["scan_algo"]), "table_compressed": table.compressed,
                    "table_distinct": table.distinct, "positions_per_read": table.positions_per_read,
-                   "code_bits": table.code_bits, "escape_fraction": round(table.escape_fraction, 6)},
+                   "code_bits": table.code_bits, "escape_fraction": round(table.escape_fraction, 6),
+                   "build_id": build_id},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "parity_sample": parity,
         "regions": n_regions_all,
         "replayed_chunks": int(stats[-1]["n_replay"]),
         "host_path": host_path,
-        "phase_ms": {key: round(float(np.mean([s[key] for s in stats])), 3)
-                     for key in ("ms_runs", "ms_scan", "ms_rescan", "ms_finish", "ms_total")},
-        "setup_s": {"genome": round(t_gen, 2), "count": round(t_count, 3), "table": round(t_table, 3)},
+        "phase_ms": {key[3:]: round(float(np.mean([s[key] for s in stats])), 3)
+                     for key in stats[-1] if key.startswith("ms_")},
+        "setup_ms": setup,
+        "end_to_end": {"ms": round(e2e_ms, 2), "Gbases_per_s": round(n_bases / (e2e_ms * 1e-3) / 1e9, 3),
+                       "what": "count + host score table + device table (compress, 12-bit codes, expanded "
+                               "table) + one scan step, per rank"},
     }
+    line.update(extra)
+    if rank == 0:
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(s + "\n")
+    if dist:
+        tdist.destroy_process_group()
+
+
+def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over_ranks, make_table, D, genome,
+                build_id):
+    """Config 5: G genomes per rank, each end to end (count -> table ->
+    scan) inside the timed region; genome generation is not timed (it stands
+    in for reading the genome).  Records gathered to rank 0 after timing."""
+    k = args.k
+    G = max(1, args.genomes_per_rank)
+    seeds = [args.seed + 1000 * (rank * G + g) for g in range(G)]
+    dss = [ds0]
+    for s_ in seeds[1:]:
+        parts, lens = genome.human_like(scale=args.scale, seed=s_, device=dev, ncontigs=args.ncontigs)
+        dss.append(D.from_parts(parts, lens, dev))
+        del parts
+    counts = torch.zeros(4 ** k, dtype=torch.int32, device=dev)
+
+    def one(ds):
+        counts.zero_()
+        words = D.count(ctx, ds, k, counts)
+        _, _, table, init, _ = make_table(counts, words)
+        if args.trlr:
+            out = D.tr_lr(ctx, ds, k, table, init, args.min_width)
+        else:
+            out = D.scan(ctx, ds, k, table, args.min_width, args.min_score)
+        table.close()
+        if init is not None:
+            init.close()
+        return out
+
+    one(dss[0])  # warm-up (workspace, pinned staging)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    results = [one(ds) for ds in dss]
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    bases = sum(int(r[2]["n_bases"]) for r in results) * world
+    n_regions = sum(int(r[0].shape[1]) for r in results)
+    if dist:
+        from kmer_spans_amd.dist import gather_regions
+        pos = np.concatenate([r[0] for r in results], axis=1)
+        sc = np.concatenate([r[1] for r in results], axis=1)
+        allpos, _ = gather_regions(pos, sc, dev)
+        if rank == 0:
+            n_regions = sum(int(p.shape[1]) for p in allpos)
+    line = {"metric": METRIC + " [config 5: genomes per rank, end to end]",
+            "value": round(bases / elapsed / 1e9, 4), "unit": "Gbases/s", "n_gpus": world, "steps": G,
+            "warmup": 1, "ms_per_step": round(elapsed / G * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"{G * world} human-shaped genomes (scale {args.scale}), {G} per rank, k={k}, "
+                                   f"{args.score}, each: count + table + expanded table + scan",
+                       "k": k, "score": args.score, "genomes": G * world, "mode": "genomes",
+                       "parallelism": f"genome-per-rank x{world}", "build_id": build_id},
+            "regions": n_regions}
     if rank == 0:
         s = json.dumps(line)
         print(s, flush=True)

@@ -47,7 +47,8 @@ typedef int32_t ks_status;
 
 /* Thread-local message of the last failing call. */
 const char *ks_last_error(void);
-/* Library version string, e.g. "kmer_spans_amd 0.1 gfx950". */
+/* Library version string, e.g. "kmer_spans_amd 0.2 gfx950 build 1a2b3c4d5e6f"
+ * (the build id is a hash of the library's sources, see csrc/Makefile). */
 const char *ks_version(void);
 
 /* Region list in the reference's record layout (seq_regions, kmer_spans.c:
@@ -189,6 +190,21 @@ int32_t ks_table_code_bits(const ks_table *t);
 /* Share of positions (by the hint, else by k-mer multiplicity) whose value
  * escapes the 12-bit codes; 0 unless code bits are 12. */
 double ks_table_escape_fraction(const ks_table *t);
+
+/* Shape and setup cost of a device table (host wall clock around the
+ * synchronised device work of ks_table_create*, milliseconds). */
+typedef struct ks_table_info {
+  int32_t k, compressed, positions_per_read, code_bits;
+  int64_t distinct, ext_bytes;
+  double escape_fraction;
+  double ms_upload;    /* w to the device, s = w - thr, finiteness scan          */
+  double ms_compress;  /* distinct values (radix sort + unique), uint16 codes    */
+  double ms_codes12;   /* 12-bit code choice: position-weight histogram, renumber */
+  double ms_ext_alloc; /* hipMalloc of the expanded table                        */
+  double ms_ext_build; /* expanded-table build kernel                            */
+  double ms_total;
+} ks_table_info;
+ks_status ks_table_get_info(const ks_table *t, ks_table_info *out);
 
 /* Scan statistics of the last ks_scan_dev call (device time of each phase,
  * measured with hipEvents on the ctx stream). */

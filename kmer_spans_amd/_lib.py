@@ -46,6 +46,17 @@ class ScanStats(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+class TableInfo(C.Structure):
+    _fields_ = [("k", C.c_int32), ("compressed", C.c_int32), ("positions_per_read", C.c_int32),
+                ("code_bits", C.c_int32), ("distinct", C.c_int64), ("ext_bytes", C.c_int64),
+                ("escape_fraction", C.c_double), ("ms_upload", C.c_double), ("ms_compress", C.c_double),
+                ("ms_codes12", C.c_double), ("ms_ext_alloc", C.c_double), ("ms_ext_build", C.c_double),
+                ("ms_total", C.c_double)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
 class Fasta(C.Structure):
     _fields_ = [("seqs", DevSeqs), ("names", C.POINTER(C.c_char_p)), ("n_records", C.c_int64),
                 ("bases_all", C.c_int64), ("bases_kept", C.c_int64), ("device", C.c_int32),
@@ -69,6 +80,7 @@ EXPORTS = [
     "ks_low_comp_regions", "ks_kmer_seq", "ks_rank_table", "ks_log2_table", "ks_pm1_table",
     "ks_table_create", "ks_table_destroy", "ks_table_is_compressed", "ks_table_distinct",
     "ks_table_positions_per_read", "ks_table_create_hint", "ks_table_code_bits", "ks_table_escape_fraction",
+    "ks_table_get_info",
     "ks_scan_dev", "ks_count_dev", "ks_ctx_set_scan_algo", "ks_tr_lr_regions", "ks_tr_lr_dev",
     "ks_fasta_load", "ks_fasta_parse", "ks_fasta_copy_seqs", "ks_fasta_free", "ks_count_multi_dev",
     "ks_count_file_write", "ks_count_file_read", "ks_count_file_free", "ks_kmers_to_file",
@@ -111,6 +123,7 @@ def load():
         "ks_table_create_hint": ([P, P, I32, D, I32, P, P], I32),
         "ks_table_code_bits": ([P], I32),
         "ks_table_escape_fraction": ([P], D),
+        "ks_table_get_info": ([P, P], I32),
         "ks_scan_dev": ([P, P, I32, P, I32, D, P, P, P], I32),
         "ks_count_dev": ([P, P, I32, P, P], I32),
         "ks_tr_lr_regions": ([P, P, P, I32, I32, I32, P, P, P, I64, P, P], I32),
@@ -133,6 +146,16 @@ def load():
         f.restype = res
     _lib = L
     return L
+
+
+def version() -> str:
+    return load().ks_version().decode()
+
+
+def build_id() -> str:
+    """Hash of the library's sources and build flags (csrc/Makefile)."""
+    v = version()
+    return v.rsplit("build ", 1)[1] if "build " in v else "unknown"
 
 
 def check(rc: int) -> None:

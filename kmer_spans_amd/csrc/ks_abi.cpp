@@ -10,6 +10,8 @@
 #include <vector>
 #include <mutex>
 
+#include <unistd.h>
+
 #include "ks_internal.h"
 
 namespace ks {
@@ -31,7 +33,26 @@ ks_status fail(ks_status st, const char *fmt, ...) {
   return st;
 }
 
+// The process that first touched HIP through this library.  HIP state does
+// not survive fork(): a child (R's mclapply, test.R:550-567) that inherits a
+// context must not use it -- a HIP call there can hang -- so every entry
+// point refuses it with a clear status instead.
+static pid_t g_hip_pid = 0;
+
+static ks_status fork_check(const ks_ctx *ctx) {
+  const pid_t me = getpid();
+  if ((ctx && ctx->pid != me) || (g_hip_pid != 0 && g_hip_pid != me))
+    return fail(KS_ERR_DEVICE,
+                "HIP was initialised in process %d before fork(); this child (%d) cannot use the GPU: "
+                "make the first kmer_spans call inside each worker (see INTEGRATION.md, fork safety)",
+                (int)(ctx ? ctx->pid : g_hip_pid), (int)me);
+  return KS_OK;
+}
+
+bool hip_usable_here() { return g_hip_pid == 0 || g_hip_pid == getpid(); }
+
 ks_status activate(ks_ctx *ctx) {
+  KS_TRY(fork_check(ctx));
   KS_HIP(hipSetDevice(ctx->device));
   return KS_OK;
 }
@@ -138,7 +159,6 @@ ks_ctx *g_default = nullptr;
 using namespace ks;
 
 extern "C" const char *ks_last_error(void) { return g_err; }
-extern "C" const char *ks_version(void) { return "kmer_spans_amd 0.1 gfx950"; }
 
 extern "C" void ks_regions_free(ks_regions *r) {
   if (!r) return;
@@ -148,11 +168,14 @@ extern "C" void ks_regions_free(ks_regions *r) {
 
 extern "C" ks_status ks_ctx_create(int32_t device, ks_ctx **out) {
   if (!out) return fail(KS_ERR_ARG, "null output");
+  KS_TRY(fork_check(nullptr));
+  if (g_hip_pid == 0) g_hip_pid = getpid();
   int ndev = 0;
   KS_HIP(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail(KS_ERR_ARG, "device %d out of range (%d devices)", device, ndev);
   ks_ctx *c = new ks_ctx();
   c->device = device;
+  c->pid = getpid();
   KS_HIP(hipSetDevice(device));
   KS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   c->own_stream = true;
@@ -167,6 +190,7 @@ extern "C" ks_status ks_ctx_create(int32_t device, ks_ctx **out) {
 
 extern "C" void ks_ctx_destroy(ks_ctx *c) {
   if (!c) return;
+  if (c->pid != getpid()) return;  // inherited across fork(): its HIP handles are not ours
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (auto &b : c->slots)
@@ -202,11 +226,27 @@ extern "C" ks_status ks_ctx_set_scan_algo(ks_ctx *c, int32_t algo) {
 
 extern "C" ks_ctx *ks_default_ctx(void) {
   std::lock_guard<std::mutex> g(g_default_mu);
+  if (g_default && fork_check(g_default) != KS_OK) return nullptr;
   if (!g_default) {
     if (ks_ctx_create(0, &g_default) != KS_OK) g_default = nullptr;
   }
   return g_default;
 }
+
+namespace ks {
+// *ctx, or the process default context; the error of a failed creation (no
+// device, inherited across fork) is kept for ks_last_error().
+ks_status default_ctx(ks_ctx **ctx) {
+  if (*ctx) return fork_check(*ctx);
+  g_err[0] = 0;
+  *ctx = ks_default_ctx();
+  if (!*ctx) {
+    if (g_err[0] == 0) return fail(KS_ERR_DEVICE, "no HIP device available");
+    return KS_ERR_DEVICE;
+  }
+  return KS_OK;
+}
+}  // namespace ks
 
 // ------------------------------------------------------------ host entries
 
@@ -337,8 +377,7 @@ extern "C" ks_status ks_tr_lr_regions(ks_ctx *ctx, const char *const *seqs, cons
     memcpy(spectra, ks.data(), (size_t)nk * 8);
     memcpy(spectra + nk, tr.data(), (size_t)nk * 8);
   }
-  if (!ctx) ctx = ks_default_ctx();
-  if (!ctx) return fail(KS_ERR_DEVICE, "no HIP device available");
+  KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
   Staged st;
   KS_TRY(stage(ctx, seqs, lens, nseq, &st));
@@ -366,8 +405,7 @@ extern "C" ks_status ks_kmer_counts(ks_ctx *ctx, const char *const *seqs, const 
   if (k < 1 || k > KS_MAX_K)                                  // :461-462 (and Q2)
     return fail(KS_ERR_ARG, "k must be a positive integer less than 1+MAX_K");
   if (!counts || !n_words) return fail(KS_ERR_ARG, "null output");
-  if (!ctx) ctx = ks_default_ctx();
-  if (!ctx) return fail(KS_ERR_DEVICE, "no HIP device available");
+  KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
   Staged st;
   KS_TRY(stage(ctx, seqs, lens, nseq, &st));
@@ -397,8 +435,7 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
                 (long long)want);
   if (!out || !n_bases) return fail(KS_ERR_ARG, "null output");
   memset(out, 0, sizeof(*out));
-  if (!ctx) ctx = ks_default_ctx();
-  if (!ctx) return fail(KS_ERR_DEVICE, "no HIP device available");
+  KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
   double n = 0;
   for (int32_t q = 0; q < nseq; ++q)
@@ -439,8 +476,7 @@ extern "C" ks_status ks_low_comp_regions(ks_ctx *ctx, const char *const *seqs, c
     return fail(KS_ERR_ARG, "k must be a positive integer less than 1+MAX_K");
   if (!counts || !ranks || !n || !out) return fail(KS_ERR_ARG, "null output");
   memset(out, 0, sizeof(*out));
-  if (!ctx) ctx = ks_default_ctx();
-  if (!ctx) return fail(KS_ERR_DEVICE, "no HIP device available");
+  KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
   Staged st;
   KS_TRY(stage(ctx, seqs, lens, nseq, &st));
@@ -509,8 +545,7 @@ extern "C" ks_status ks_windowed_dist(ks_ctx *ctx, const char *const *seqs, cons
     prime_string(kmers[i], k, &c);
     codes[i] = (uint32_t)c;
   }
-  if (!ctx) ctx = ks_default_ctx();
-  if (!ctx) return fail(KS_ERR_DEVICE, "no HIP device available");
+  KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
   Staged st;
   KS_TRY(stage(ctx, seqs, lens, nseq, &st));

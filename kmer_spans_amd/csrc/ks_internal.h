@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -71,6 +72,7 @@ struct DevBuf {
 
 struct ks_ctx {
   int device = 0;
+  int pid = 0;  // creating process (fork check)
   hipStream_t stream = nullptr;
   bool own_stream = false;
   int scan_algo = -1;
@@ -99,24 +101,37 @@ struct ks_table {
   int ext_J = 1;
   void *d_ext = nullptr;        // uint64 (J <= 4 codes) or double[4] (J <= 3 values)
   size_t ext_bytes = 0;
-  double ms_ext = 0;            // build time
+  // setup time (ms, host wall clock around synchronised device work)
+  double ms_upload = 0;         // w -> device, s = w - thr, finiteness scan
+  double ms_compress = 0;       // distinct values: radix sort + unique + code assignment
+  double ms_codes12 = 0;        // 12-bit code choice: weight histogram + renumbering
+  double ms_ext_alloc = 0;      // hipMalloc of the expanded table
+  double ms_ext = 0;            // expanded-table build kernel (hipEvents)
+  double ms_total = 0;
   bool no_nan_posinf = true;    // no s is NaN or +Inf (-Inf allowed: it clamps to 0)
   double max_abs = 0.0;         // max |s| over the finite values
-  // Narrow codes (ext_bits = 12, J = 5): the 4095 values covering most
-  // positions get a 12-bit code (d_map12 -> uint16 code, d_lut12 -> value);
-  // code 0xFFF escapes to the base uint16 table for that index.
+  // Narrow codes (ext_bits = 12, J = 5): the uint16 codes are numbered by
+  // position weight, so the 4095 values covering most positions have codes
+  // 0..4094, which are also their 12-bit codes (d_map12 is the identity,
+  // d_lut12 = d_lut[0..4096)); 0xFFF escapes to the base uint16 table.
   int ext_bits = 16;
   uint16_t *d_map12 = nullptr;  // [4096]
   double *d_lut12 = nullptr;    // [4096]
   double escape_frac = 0.0;     // estimated share of positions that escape
-  uint16_t *d_rank12_tmp = nullptr;  // build-time uint16 -> 12-bit map
 };
 
 namespace ks {
 
+// Host wall clock in milliseconds (setup timings).
+inline double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out);
 ks_status ensure_pinned(ks_ctx *ctx, size_t bytes, void **out);
-ks_status activate(ks_ctx *ctx);  // hipSetDevice
+ks_status activate(ks_ctx *ctx);  // fork check + hipSetDevice
+ks_status default_ctx(ks_ctx **ctx);  // *ctx or the process default context (fork-checked)
+bool hip_usable_here();  // false in a child forked after HIP was initialised
 
 // -------------------------------------------------------------- encoding
 __host__ __device__ __forceinline__ bool is_n(uint8_t c) { return (c | 0x20) == 'n'; }

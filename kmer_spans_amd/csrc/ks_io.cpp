@@ -30,10 +30,6 @@
 namespace ks {
 namespace {
 
-double now_ms() {
-  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
 // The bytes of a sequence file: mapped, inflated, or borrowed.
 struct HostView {
   const uint8_t *p = nullptr;
@@ -243,9 +239,11 @@ using namespace ks;
 
 extern "C" void ks_fasta_free(ks_fasta *f) {
   if (!f) return;
-  if (f->seqs.seq || f->seqs.offsets_dev) (void)hipSetDevice(f->device);
-  if (f->seqs.seq) (void)hipFree((void *)f->seqs.seq);
-  if (f->seqs.offsets_dev) (void)hipFree((void *)f->seqs.offsets_dev);
+  if (hip_usable_here()) {  // (a child forked after HIP init leaves the parent's device memory alone)
+    if (f->seqs.seq || f->seqs.offsets_dev) (void)hipSetDevice(f->device);
+    if (f->seqs.seq) (void)hipFree((void *)f->seqs.seq);
+    if (f->seqs.offsets_dev) (void)hipFree((void *)f->seqs.offsets_dev);
+  }
   if (f->names)
     for (int32_t q = 0; q < f->seqs.nseq; ++q) free(f->names[q]);
   free(f->names);
@@ -256,8 +254,7 @@ extern "C" void ks_fasta_free(ks_fasta *f) {
 extern "C" ks_status ks_fasta_load(ks_ctx *ctx, const char *path, int64_t min_len, ks_fasta *out) {
   if (!path || !out) return fail(KS_ERR_ARG, "null argument");
   fasta_reset(out);
-  if (!ctx) ctx = ks_default_ctx();
-  if (!ctx) return fail(KS_ERR_DEVICE, "no HIP device available");
+  KS_TRY(default_ctx(&ctx));
   HostView v;
   KS_TRY(open_view(path, &v));
   KS_TRY(activate(ctx));
@@ -267,8 +264,7 @@ extern "C" ks_status ks_fasta_load(ks_ctx *ctx, const char *path, int64_t min_le
 extern "C" ks_status ks_fasta_parse(ks_ctx *ctx, const char *buf, int64_t n, int64_t min_len, ks_fasta *out) {
   if (!out || n < 0 || (n > 0 && !buf)) return fail(KS_ERR_ARG, "null argument");
   fasta_reset(out);
-  if (!ctx) ctx = ks_default_ctx();
-  if (!ctx) return fail(KS_ERR_DEVICE, "no HIP device available");
+  KS_TRY(default_ctx(&ctx));
   HostView v;
   v.p = reinterpret_cast<const uint8_t *>(buf);
   v.n = (size_t)n;
@@ -382,8 +378,7 @@ extern "C" ks_status ks_kmers_to_file(ks_ctx *ctx, const char *seq_path, const c
   of += ".bin";
   if (of.size() >= sizeof(info->out_path)) return fail(KS_ERR_ARG, "output path too long");
   memcpy(info->out_path, of.c_str(), of.size() + 1);
-  if (!ctx) ctx = ks_default_ctx();
-  if (!ctx) return fail(KS_ERR_DEVICE, "no HIP device available");
+  KS_TRY(default_ctx(&ctx));
   // read.count() inside try(): any failure there is the NA result (:145-148)
   auto na = [&](const char *why) {
     info->written = 0;

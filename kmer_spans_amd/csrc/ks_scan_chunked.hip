@@ -227,10 +227,6 @@ __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restri
   }
 }
 
-// Bytes a pass-1 lane may read past its chunk's last scan index: the
-// pipelined kernel reads two batches ahead (k_pass1p: < 3 * 20 + 5 + 4).
-constexpr int kP1TailMargin = 352;
-
 // Packed-code words staged in LDS per pass-1 lane: bases [q0, q0 + 320) of
 // its chunk (q0 = start + J - 1), loaded once (5 x 16 B) instead of one 12-B
 // load per batch, so the lane's two 128-B lines are fetched once even when
@@ -252,6 +248,18 @@ constexpr int kP1G = KS_P1_G;
 constexpr int kP1Block = KS_P1_BLOCK;  // lanes per pass-1 block (build parameter for A/B runs)
 static_assert(kP1Block % 64 == 0 && kP1Block <= 1024, "pass-1 block is whole waves");
 constexpr int kP1StageWords = kP1G > 4 ? 24 : 20;
+// Bases past its chunk's first scan index a pass-1 lane may read: the
+// pipelined kernel's windows reach two batches ahead (< 256 + 2 * 40 + 3 * 16)
+// and the LDS staging reads kP1StageWords words from word (start + J - 1) / 16.
+// Lanes closer than this to the buffer end are left to k_pass1 (tail_only),
+// so every packed word they stage exists (the packed array has total / 16 + 1
+// words, ks_runs.hip).
+constexpr int kP1WinReach = 4 + 255 + 2 * 5 * kP1G + 16 * (kP1G > 4 ? 5 : 3);  // J - 1 + last b0 + 2 PB + window
+constexpr int kP1StageReach = 16 * kP1StageWords + 21;
+constexpr int kP1TailMargin = kP1WinReach > kP1StageReach ? (kP1WinReach > 352 ? kP1WinReach : 352)
+                                                          : (kP1StageReach > 352 ? kP1StageReach : 352);
+static_assert(16 * kP1StageWords + 4 <= kP1TailMargin + 16 + 1, "staged packed words stay inside the buffer");
+static_assert(kP1WinReach <= kP1TailMargin + 1, "pipelined windows stay inside the buffer");
 
 // ------------------------------------------------------------------- P0
 

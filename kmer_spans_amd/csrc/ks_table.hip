@@ -77,29 +77,94 @@ __global__ void k_build_ext_u16(const uint16_t *__restrict__ codes, int k, uint6
   }
 }
 
-// Position weight of every uint16 code: number of k-mers with that code, or
-// (with a frequency hint) the number of positions scoring them.
-__global__ void k_code_hist(const uint16_t *__restrict__ codes, const int32_t *__restrict__ freq, int64_t n,
-                            unsigned long long *__restrict__ hist) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const unsigned long long wgt = freq ? (unsigned long long)(uint32_t)freq[i] : 1ull;
-    if (wgt) atomicAdd(&hist[codes[i]], wgt);
+// Position weight of every uint16 code in [lo, lo + kHistBins): number of
+// k-mers with that code, or (with a frequency hint) the number of positions
+// scoring them.  LDS-privatised 64-bit histogram (one 1024-lane block per CU:
+// 128 KiB of bins), flushed with one global atomic per non-zero bin and
+// block: the codes of log2/+-1 tables are heavily skewed (most k-mers have a
+// count near the median), which serialised the former global atomics
+// (77 ms at k = 13, profiles/r1_v24) on a few hot bins.
+constexpr int kHistBins = 16384;
+__global__ void __launch_bounds__(1024) k_code_hist(const uint16_t *__restrict__ codes,
+                                                    const int32_t *__restrict__ freq, int64_t n, int lo,
+                                                    unsigned long long *__restrict__ hist) {
+  __shared__ unsigned long long h[kHistBins];
+  for (int i = threadIdx.x; i < kHistBins; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n8 = n >> 3;  // 8 codes (16 B) and 8 weights (2 x 16 B) per lane and step
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n8; v += stride) {
+    const uint4 c = reinterpret_cast<const uint4 *>(codes)[v];
+    uint4 f0 = make_uint4(1, 1, 1, 1), f1 = f0;
+    if (freq) {
+      f0 = reinterpret_cast<const uint4 *>(freq)[2 * v];
+      f1 = reinterpret_cast<const uint4 *>(freq)[2 * v + 1];
+    }
+    const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+    const uint32_t fw[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint32_t b = ((cw[q >> 1] >> (16 * (q & 1))) & 0xffffu) - (uint32_t)lo;
+      if (b < (uint32_t)kHistBins && fw[q]) atomicAdd(&h[b], (unsigned long long)fw[q]);
+    }
   }
+  for (int64_t i = (n8 << 3) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t b = (uint32_t)codes[i] - (uint32_t)lo;
+    const unsigned long long w = freq ? (unsigned long long)(uint32_t)freq[i] : 1ull;
+    if (b < (uint32_t)kHistBins && w) atomicAdd(&h[b], w);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHistBins; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[lo + i], h[i]);
 }
 
-// Expanded table, 12-bit codes: J = 5 codes per uint64 entry (rank12 maps a
-// uint16 code to its 12-bit code or the escape 0xFFF).
-__global__ void k_build_ext_c12(const uint16_t *__restrict__ codes, const uint16_t *__restrict__ rank12, int k,
-                                uint64_t nent, uint64_t *__restrict__ ext) {
-  constexpr int J = 5;
-  const uint64_t mk = ((uint64_t)1 << (2 * k)) - 1;
-  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nent;
-       e += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t v = 0;
+// codes[i] = perm[codes[i]]: the uint16 codes renumbered by position weight
+// (perm staged in LDS, 128 KiB for 65536 codes).
+__global__ void __launch_bounds__(1024) k_remap_codes(uint16_t *__restrict__ codes,
+                                                      const uint16_t *__restrict__ perm, int nperm, int64_t n) {
+  __shared__ uint16_t p[65536];
+  for (int i = threadIdx.x; i < nperm; i += blockDim.x) p[i] = perm[i];
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n8 = n >> 3;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n8; v += stride) {
+    uint4 c = reinterpret_cast<uint4 *>(codes)[v];
+    uint32_t *w = reinterpret_cast<uint32_t *>(&c);
 #pragma unroll
-    for (int t = 0; t < J; ++t) v |= (uint64_t)rank12[codes[(e >> (2 * (J - 1 - t))) & mk]] << (12 * t);
-    ext[e] = v;
+    for (int q = 0; q < 4; ++q) w[q] = (uint32_t)p[w[q] & 0xffffu] | ((uint32_t)p[w[q] >> 16] << 16);
+    reinterpret_cast<uint4 *>(codes)[v] = c;
+  }
+  for (int64_t i = (n8 << 3) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    codes[i] = p[codes[i]];
+}
+
+// Expanded table, 12-bit codes: J = 5 codes per uint64 entry, first k-mer
+// in the low 12 bits.  The uint16 codes are numbered by position weight
+// (choose_code12), so a code below 4095 is its own 12-bit code and every
+// other code escapes (0xFFF).  Lane m builds entries 4m .. 4m+3: their first
+// four k-mers are shared ((4m + d) >> 2(4 - t) does not depend on d for
+// t <= 3), their fifth k-mers are the 4 consecutive k-mers 4m .. 4m+3 (one
+// 8-B load), and the 32 B of output go out as two 16-B stores.
+__device__ __forceinline__ uint64_t c12_of(uint32_t code) { return code < 0xFFFu ? code : 0xFFFu; }
+__global__ void k_build_ext_c12(const uint16_t *__restrict__ codes, int k, uint64_t nent,
+                                uint64_t *__restrict__ ext) {
+  const uint64_t mk = ((uint64_t)1 << (2 * k)) - 1;
+  const uint64_t nq = nent >> 2;
+  for (uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; m < nq;
+       m += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t e0 = m << 2;
+    uint64_t base = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) base |= c12_of(codes[(e0 >> (2 * (4 - t))) & mk]) << (12 * t);
+    const uint2 w = *reinterpret_cast<const uint2 *>(codes + (e0 & mk));
+    const uint32_t c4[4] = {w.x & 0xffffu, w.x >> 16, w.y & 0xffffu, w.y >> 16};
+    ulonglong2 o0, o1;
+    o0.x = base | (c12_of(c4[0]) << 48);
+    o0.y = base | (c12_of(c4[1]) << 48);
+    o1.x = base | (c12_of(c4[2]) << 48);
+    o1.y = base | (c12_of(c4[3]) << 48);
+    reinterpret_cast<ulonglong2 *>(ext)[2 * m] = o0;
+    reinterpret_cast<ulonglong2 *>(ext)[2 * m + 1] = o1;
   }
 }
 
@@ -130,10 +195,12 @@ static size_t ext_entry_bytes(bool u16, int J) {
   return J <= 2 ? 16 : 32;
 }
 
-// 12-bit code assignment for J = 5: the 4095 heaviest uint16 codes (by
-// position weight) get codes 0..4094, the rest escape.  Returns false if the
+// 12-bit code assignment for J = 5: the uint16 codes are renumbered by
+// position weight (heaviest first, ties by code), the LUT permuted to match,
+// so that the 4095 heaviest codes are their own 12-bit codes (0..4094) and
+// every other code escapes.  Sets *use = false (and changes nothing) if the
 // escape share is above max_escape.
-static ks_status assign_code12(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev, double max_escape, bool *use) {
+static ks_status choose_code12(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev, double max_escape, bool *use) {
   *use = false;
   hipStream_t st = ctx->stream;
   const int64_t n = (int64_t)1 << (2 * t->k);
@@ -141,8 +208,11 @@ static ks_status assign_code12(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev
   unsigned long long *d_hist = nullptr;
   KS_HIP(hipMalloc(&d_hist, 65536 * 8));
   KS_HIP(hipMemsetAsync(d_hist, 0, 65536 * 8, st));
-  const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ctx->num_cus * 16);
-  hipLaunchKernelGGL(k_code_hist, dim3(grid), dim3(256), 0, st, t->d_codes, freq_dev, n, d_hist);
+  const unsigned grid = (unsigned)std::min<int64_t>((n / 8 + 1023) / 1024, (int64_t)ctx->num_cus);
+  for (int64_t lo = 0; lo < nu; lo += kHistBins)
+    hipLaunchKernelGGL(k_code_hist, dim3(std::max(grid, 1u)), dim3(1024), 0, st, t->d_codes, freq_dev, n, (int)lo,
+                       d_hist);
+  KS_HIP(hipGetLastError());
   std::vector<unsigned long long> h(65536);
   std::vector<double> lut(nu);
   KS_HIP(hipMemcpyAsync(h.data(), d_hist, 65536 * 8, hipMemcpyDeviceToHost, st));
@@ -158,22 +228,28 @@ static ks_status assign_code12(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev
   for (int64_t i = 0; i < ndirect; ++i) cov += h[order[i]];
   t->escape_frac = tot > 0 ? (double)(1.0L - cov / tot) : 0.0;
   if (t->escape_frac > max_escape) return KS_OK;
-  std::vector<uint16_t> rank12(65536, 0xFFF), map12(4096, 0);
-  std::vector<double> lut12(4096, 0.0);
-  for (int64_t i = 0; i < ndirect; ++i) {
-    rank12[order[i]] = (uint16_t)i;
-    map12[i] = (uint16_t)order[i];
-    lut12[i] = lut[order[i]];
+  std::vector<uint16_t> perm(nu), map12(4096, 0);
+  std::vector<double> nlut(nu), lut12(4096, 0.0);
+  for (int64_t i = 0; i < nu; ++i) {
+    perm[order[i]] = (uint16_t)i;
+    nlut[i] = lut[order[i]];
   }
+  for (int64_t i = 0; i < 4096; ++i) {  // identity: a short code is the uint16 code
+    map12[i] = (uint16_t)i;
+    lut12[i] = i < nu ? nlut[i] : 0.0;
+  }
+  uint16_t *d_perm = nullptr;
+  KS_HIP(hipMalloc(&d_perm, nu * 2));
+  KS_HIP(hipMemcpyAsync(d_perm, perm.data(), nu * 2, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_remap_codes, dim3(std::max(grid, 1u)), dim3(1024), 0, st, t->d_codes, d_perm, (int)nu, n);
+  KS_HIP(hipGetLastError());
+  KS_HIP(hipMemcpyAsync(t->d_lut, nlut.data(), nu * 8, hipMemcpyHostToDevice, st));
   KS_HIP(hipMalloc(&t->d_map12, 4096 * 2));
   KS_HIP(hipMalloc(&t->d_lut12, 4096 * 8));
   KS_HIP(hipMemcpyAsync(t->d_map12, map12.data(), 4096 * 2, hipMemcpyHostToDevice, st));
   KS_HIP(hipMemcpyAsync(t->d_lut12, lut12.data(), 4096 * 8, hipMemcpyHostToDevice, st));
-  uint16_t *d_rank = nullptr;
-  KS_HIP(hipMalloc(&d_rank, 65536 * 2));
-  KS_HIP(hipMemcpyAsync(d_rank, rank12.data(), 65536 * 2, hipMemcpyHostToDevice, st));
   KS_HIP(hipStreamSynchronize(st));
-  t->d_rank12_tmp = d_rank;
+  KS_HIP(hipFree(d_perm));
   *use = true;
   return KS_OK;
 }
@@ -208,7 +284,9 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
     if (c.bits == 12) {
       if (getenv("KS_NO_CODE12")) continue;
       bool use = false;
-      KS_TRY(assign_code12(ctx, t, freq_dev, max_escape, &use));
+      const double t0 = now_ms();
+      KS_TRY(choose_code12(ctx, t, freq_dev, max_escape, &use));
+      t->ms_codes12 = now_ms() - t0;
       if (!use) continue;
     }
     J = c.J;
@@ -221,18 +299,19 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   const size_t bytes = nent * ext_entry_bytes(u16, J);
   hipStream_t st = ctx->stream;
   void *ext = nullptr;
+  const double ta = now_ms();
   if (hipMalloc(&ext, bytes) != hipSuccess) {
     (void)hipGetLastError();
     return KS_OK;
   }
+  t->ms_ext_alloc = now_ms() - ta;
   hipEvent_t a, b;
   KS_HIP(hipEventCreate(&a));
   KS_HIP(hipEventCreate(&b));
   KS_HIP(hipEventRecord(a, st));
   const unsigned grid = (unsigned)std::min<uint64_t>((nent + 255) / 256, (uint64_t)ctx->num_cus * 32);
   if (u16 && bits == 12) {
-    hipLaunchKernelGGL(k_build_ext_c12, dim3(grid), dim3(256), 0, st, t->d_codes, t->d_rank12_tmp, t->k, nent,
-                       (uint64_t *)ext);
+    hipLaunchKernelGGL(k_build_ext_c12, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
   } else if (u16) {
     if (J == 4) hipLaunchKernelGGL((k_build_ext_u16<4, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
     else if (J == 3) hipLaunchKernelGGL((k_build_ext_u16<3, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
@@ -249,10 +328,6 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   KS_HIP(hipEventElapsedTime(&ms, a, b));
   KS_HIP(hipEventDestroy(a));
   KS_HIP(hipEventDestroy(b));
-  if (t->d_rank12_tmp) {
-    KS_HIP(hipFree(t->d_rank12_tmp));
-    t->d_rank12_tmp = nullptr;
-  }
   if (bits != 12) {  // a 12-bit assignment that was not used
     if (t->d_map12) (void)hipFree(t->d_map12);
     if (t->d_lut12) (void)hipFree(t->d_lut12);
@@ -282,6 +357,7 @@ extern "C" ks_status ks_table_create_hint(ks_ctx *ctx, const double *w_host, int
   if (!ctx || !w_host || !out) return fail(KS_ERR_ARG, "ks_table_create: null argument");
   if (k < 1 || k > KS_MAX_K) return fail(KS_ERR_ARG, "k must be between 1 and %d", KS_MAX_K);
   KS_TRY(activate(ctx));
+  const double t_start = now_ms();
   const int64_t n = (int64_t)1 << (2 * k);
   hipStream_t st = ctx->stream;
   ks_table *t = new ks_table();
@@ -328,6 +404,7 @@ extern "C" ks_status ks_table_create_hint(ks_ctx *ctx, const double *w_host, int
     memcpy(&ma, &h_am[0], 8);
     t->max_abs = ma;
   }
+  t->ms_upload = now_ms() - t_start;
   t->distinct = -1;
   if (allow_compress) {
     KS_TBL_HIP(hipMalloc(&d_sorted, n * sizeof(unsigned long long)));
@@ -358,23 +435,28 @@ extern "C" ks_status ks_table_create_hint(ks_ctx *ctx, const double *w_host, int
   KS_TBL_HIP(hipStreamSynchronize(st));
 #undef KS_TBL_HIP
   cleanup();
+  t->ms_compress = now_ms() - t_start - t->ms_upload;
   if (flags & KS_TABLE_EXPAND) {
     const ks_status rc = table_expand(ctx, t, (size_t)160 << 30, freq_dev);
     if (rc != KS_OK) { ks_table_destroy(t); return rc; }
   }
+  t->ms_total = now_ms() - t_start;
   *out = t;
   return KS_OK;
 }
 
 extern "C" void ks_table_destroy(ks_table *t) {
   if (!t) return;
+  if (!hip_usable_here()) {  // inherited across fork(): leave the parent's device memory alone
+    delete t;
+    return;
+  }
   if (t->d_vals) (void)hipFree(t->d_vals);
   if (t->d_codes) (void)hipFree(t->d_codes);
   if (t->d_lut) (void)hipFree(t->d_lut);
   if (t->d_ext) (void)hipFree(t->d_ext);
   if (t->d_map12) (void)hipFree(t->d_map12);
   if (t->d_lut12) (void)hipFree(t->d_lut12);
-  if (t->d_rank12_tmp) (void)hipFree(t->d_rank12_tmp);
   delete t;
 }
 
@@ -386,6 +468,25 @@ extern "C" int32_t ks_table_code_bits(const ks_table *t) {
   if (t->ext_J > 1 && t->compressed) return t->ext_bits;
   return t->compressed ? 16 : 64;
 }
+extern "C" ks_status ks_table_get_info(const ks_table *t, ks_table_info *out) {
+  if (!t || !out) return fail(KS_ERR_ARG, "null argument");
+  memset(out, 0, sizeof(*out));
+  out->k = t->k;
+  out->compressed = t->compressed ? 1 : 0;
+  out->positions_per_read = t->ext_J;
+  out->code_bits = ks_table_code_bits(t);
+  out->distinct = t->distinct;
+  out->ext_bytes = (int64_t)t->ext_bytes;
+  out->escape_fraction = ks_table_escape_fraction(t);
+  out->ms_upload = t->ms_upload;
+  out->ms_compress = t->ms_compress;
+  out->ms_codes12 = t->ms_codes12;
+  out->ms_ext_alloc = t->ms_ext_alloc;
+  out->ms_ext_build = t->ms_ext;
+  out->ms_total = t->ms_total;
+  return KS_OK;
+}
+
 extern "C" double ks_table_escape_fraction(const ks_table *t) {
   return (t && t->ext_bits == 12) ? t->escape_frac : 0.0;
 }

@@ -95,6 +95,18 @@ class DeviceTable:
                                           C.c_void_p(freq.data_ptr()) if freq is not None else None,
                                           C.byref(self._h)))
 
+    def info(self) -> dict:
+        """ks_table_get_info: shape and setup cost (ms) of the table."""
+        inf = _lib.TableInfo()
+        check(load().ks_table_get_info(self._h, C.byref(inf)))
+        return inf.as_dict()
+
+    def setup_ms(self) -> dict:
+        """Setup time of this table by phase (ms; host wall clock around the
+        synchronised device work)."""
+        inf = self.info()
+        return {key[3:]: round(v, 3) for key, v in inf.items() if key.startswith("ms_")}
+
     @property
     def code_bits(self) -> int:
         return int(load().ks_table_code_bits(self._h))

@@ -3,9 +3,9 @@
 N-free runs (hence contigs) are independent (restarts never leave a run,
 kmer_spans.c:281,303), so the scan shards with no exchange on the data path.
 The only collectives are after the scan:
-  * span-record gather to rank 0 (all_gather of per-rank counts, then
-    all_gather of the padded records; payload = 32 B/region) -- RCCL over
-    xGMI with the "nccl" backend, gloo in the CPU tests;
+  * span-record gather to rank 0 (all_gather of the per-rank record counts,
+    then a gather of the padded records to rank 0; payload = 32 B/region) --
+    RCCL over xGMI with the "nccl" backend, gloo in the CPU tests;
   * an int32 sum of per-rank histograms when one genome's counts or visits
     are split across ranks (exact, order-independent).
 Contigs are assigned by LPT (longest processing time first) on length.
@@ -62,8 +62,8 @@ def gather_regions(pos: np.ndarray, score: np.ndarray, device=None):
     rec = np.zeros((m, 4), dtype=np.int64)
     rec[:pos.shape[1]] = _pack(pos, score)
     t = torch.from_numpy(rec).to(dev)
-    outs = [torch.zeros_like(t) for _ in range(world)]
-    tdist.all_gather(outs, t)
+    outs = [torch.zeros_like(t) for _ in range(world)] if rank == 0 else None
+    tdist.gather(t, outs, dst=0)
     if rank != 0:
         return [], []
     P, S = [], []
@@ -74,16 +74,18 @@ def gather_regions(pos: np.ndarray, score: np.ndarray, device=None):
     return P, S
 
 
-def merge_shards(shard_ids, pos_list, score_list):
+def merge_shards(shard_ids, pos_list, score_list, one_based: bool = False):
     """Map shard-local seq ids back to global contig ids and order the union
-    by (seq_id, beg) -- the reference's emission order."""
+    by (seq_id, beg) -- the reference's emission order.  one_based: the
+    records carry 1-based seq ids (tr_lr_regions_r, kmer_spans.c:699)."""
     if not pos_list:
         return np.zeros((3, 0), np.int32), np.zeros((2, 0), np.float64)
+    one = 1 if one_based else 0
     ps, ss = [], []
     for ids, p, s in zip(shard_ids, pos_list, score_list):
         p = p.copy()
         if p.shape[1]:
-            p[0] = np.asarray(ids, dtype=np.int32)[p[0]]
+            p[0] = np.asarray(ids, dtype=np.int32)[p[0] - one] + one
         ps.append(p)
         ss.append(s)
     pos = np.concatenate(ps, axis=1)

@@ -63,3 +63,80 @@ def test_gather_regions_gloo_world2():
     # bitwise score round trip
     allsc = np.concatenate([s[0] for s in S])
     assert sorted(allsc.view(np.uint64)) == sorted(score[0].view(np.uint64))
+
+
+def _genome(seed=7):
+    """A multi-contig genome with N gaps (host bytes) and its log2 table."""
+    rng = np.random.default_rng(seed)
+    lens = [40000, 9000, 26000, 3000, 17000, 5, 31000]
+    seqs = []
+    for L in lens:
+        b = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=L, p=[0.3, 0.2, 0.2, 0.3])
+        for _ in range(L // 8000):
+            a = int(rng.integers(0, max(L - 300, 1)))
+            b[a:a + int(rng.integers(1, 300))] = ord("N")
+        if L > 2000:  # a low-complexity stretch so that regions exist
+            a = int(rng.integers(0, L - 1500))
+            b[a:a + 1200] = np.frombuffer((b"CA" * 600), np.uint8)
+        seqs.append(b.tobytes())
+    return seqs, lens
+
+
+def _shard_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as tdist
+    from kmer_spans_amd import dist
+    from oracle import oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    k = 6
+    seqs, lens = _genome()
+    shards = dist.lpt_shards(lens, world)
+    mine = [seqs[i] for i in shards[rank]]
+    # per-shard counts, summed exactly across ranks (the shard-mode table)
+    _, c = O.kmer_counts(mine, k)
+    h = torch.from_numpy(c.astype(np.int32))
+    dist.allreduce_histogram(h)
+    w = O.log2_table(h.numpy(), k)
+    r = O.scan(mine, k, w, 0.0, 20, 3.0)
+    P, S = dist.gather_regions(r["pos"], r["score"])
+    t = O.tr_lr_regions(mine, k, 15, w, w)
+    PT, ST = dist.gather_regions(t["pos"], t["score"])
+    if rank == 0:
+        q.put((shards, h.numpy(), P, S, PT, ST))
+    tdist.destroy_process_group()
+
+
+def test_sharded_equals_unsharded_gloo_world2(oracle):
+    """Contigs LPT-sharded over two ranks, scanned per shard, gathered to rank
+    0 and merged == the unsharded scan, bit for bit (regions, order, scores),
+    for kmer_regions (0-based seq ids) and tr_lr (1-based, kmer_spans.c:699);
+    the all-reduced shard counts == the unsharded counts."""
+    from kmer_spans_amd import dist
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() + 17) % 1000
+    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    shards, h, P, S, PT, ST = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    O = oracle
+    k = 6
+    seqs, _ = _genome()
+    _, c = O.kmer_counts(seqs, k)
+    assert np.array_equal(h, c)
+    w = O.log2_table(c, k)
+    full = O.scan(seqs, k, w, 0.0, 20, 3.0)
+    pos, score = dist.merge_shards(shards, P, S)
+    assert full["pos"].shape[1] > 5
+    assert np.array_equal(pos, full["pos"])
+    assert np.array_equal(score.view(np.uint64), full["score"].view(np.uint64))
+    tfull = O.tr_lr_regions(seqs, k, 15, w, w)
+    tpos, tscore = dist.merge_shards(shards, PT, ST, one_based=True)
+    assert tfull["pos"].shape[1] > 5
+    assert np.array_equal(tpos, tfull["pos"])
+    assert np.array_equal(tscore.view(np.uint64), tfull["score"].view(np.uint64))

@@ -91,11 +91,41 @@ def test_shim_results_vs_oracle(R, oracle):
     got = R.to_py(R.call("kmer_regions_r", R.str_(seqs), R.int_([4]), R.real(w), R.int_([3]), R.real([1.0])))
     assert got[0][0] == o["n"] and np.array_equal(got[1], o["counts"])
     assert np.array_equal(np.asarray(got[2]).reshape(3, -1), o["pos"])
+    # scores bitwise, with the reference's zero second row (kmer_spans.c:280)
+    sc = np.ascontiguousarray(np.asarray(got[3], dtype=np.float64).reshape(2, -1))
+    assert np.array_equal(sc.view(np.uint64), o["score"].view(np.uint64))
     lc = oracle.low_comp_regions(seqs, 3, 5, 2.0, 0.6)
     got = R.to_py(R.call("kmer_low_comp_regions", R.str_(seqs), R.int_([3]), R.int_([5]), R.real([2.0]), R.real([0.6])))
     assert np.array_equal(got[0], lc["n"]) and np.array_equal(got[1], lc["counts"])
-    assert np.array_equal(got[2], lc["w_rank"])
+    assert np.array_equal(np.asarray(got[2]).view(np.uint64), lc["w_rank"].view(np.uint64))
     assert np.array_equal(np.asarray(got[3]).reshape(3, -1), lc["pos"])
+    sc = np.ascontiguousarray(np.asarray(got[4], dtype=np.float64).reshape(2, -1))
+    assert np.array_equal(sc.view(np.uint64), lc["score"].view(np.uint64))
+
+
+@pytest.mark.gpu
+def test_config1_through_call_shim(R, oracle):
+    """BASELINE config 1 through the .Call entry points: 1 Mbp i.i.d. ACGT
+    (xorshift64, seed 1), k = 7, +-1 table from its own counts
+    (README.md:37-42: f >= f_med -> 1 else -1), min_width 100, min_score 20.
+    kmer_counts and kmer_regions_r results (counts, visit histogram, regions,
+    scores) equal the oracle's bit for bit; SURVEY 8(d) expects one region."""
+    from kmer_spans_amd import api, genome
+    seq = genome.uniform_xorshift(1_000_000, 1).decode()
+    got = R.to_py(R.call("kmer_counts", R.str_([seq]), R.int_([7])))
+    n, c = oracle.kmer_counts([seq], 7)
+    assert got[0][0] == n and np.array_equal(got[1], c)
+    w = api.pm1_table(np.asarray(got[1], dtype=np.int32), 7)
+    assert np.array_equal(np.asarray(w).view(np.uint64), oracle.pm1_table(c, 7).view(np.uint64))
+    got = R.to_py(R.call("kmer_regions_r", R.str_([seq]), R.int_([7]), R.real(w), R.int_([100]), R.real([20.0])))
+    o = oracle.kmer_regions([seq], 7, w, 100, 20.0)
+    pos = np.asarray(got[2]).reshape(3, -1)
+    assert got[0][0] == o["n"] == 1_000_000
+    assert np.array_equal(got[1], o["counts"])
+    assert np.array_equal(pos, o["pos"])
+    sc = np.ascontiguousarray(np.asarray(got[3], dtype=np.float64).reshape(2, -1))
+    assert np.array_equal(sc.view(np.uint64), o["score"].view(np.uint64))
+    assert pos.shape[1] >= 1
 
 
 @pytest.mark.gpu

@@ -86,6 +86,9 @@ def parse(argv=None):
                    help="bases of the CPU-baseline sample besides the largest contig")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-expand", action="store_true", help="do not build the expanded (k+J-1)-mer table")
+    p.add_argument("--ext-max-gib", type=float, default=None,
+                   help="cap on the expanded table (GiB); default: no cap beyond HBM (J = 5, 128 GiB at k = 13) "
+                        "for the scan modes, 32 GiB (J = 4) for --mode genomes, where it is built per genome")
     p.add_argument("--ncontigs", type=int, default=24, help="1 = the chr1-like single contig of config 2")
     p.add_argument("--host-path", action="store_true",
                    help="also time the host-pointer entry point (ks_kmer_regions with visits: staging + PCIe + scan)")
@@ -237,22 +240,30 @@ def main():
         tdist.all_reduce(e, op=tdist.ReduceOp.MAX)
         return float(e.item())
 
-    def make_table(counts, words, hint=True):
-        """Host score table from the counts + device table (timed pieces)."""
+    def make_table(counts, words, ext_gib=None, warm=True):
+        """Score table built on the device from the device counts
+        (ks_table_from_counts: no 4^k host round trip), timed; w (the
+        reference's weight vector) stays on the device for the parity leg."""
         t = {}
+        thr = 0.75 if args.score == "rank" else 0.0
+        cap = int((ext_gib if ext_gib is not None else (args.ext_max_gib or 0.0)) * (1 << 30))
+        w_dev = torch.empty(4 ** k, dtype=torch.float64, device=dev)
+
+        def build():
+            return D.DeviceTable.from_counts(ctx, counts, k, args.score, total=words, thr=thr,
+                                             expand=not args.no_expand, max_ext_bytes=cap, w_out=w_dev)
+        if warm:  # first build: grows the workspace and allocates the expanded table (fresh VRAM is
+            with Timer() as tm:  # cleared by the driver: seconds for 128 GiB), reported apart
+                build().close()
+            t["table_first_call"] = tm.ms
         with Timer() as tm:
-            hc = counts.cpu().numpy()
-            w, thr = score_table(api, hc, k, words, args.score)
-            if args.trlr:  # tr_lr tables carry no threshold: transition = init = w - thr
-                w, thr = np.asarray(w, dtype=np.float64) - thr, 0.0
-        t["table_host"] = tm.ms
-        with Timer() as tm:
-            table = D.DeviceTable(ctx, w, k, thr, compress=True, expand=not args.no_expand,
-                                  freq=counts if hint else None)
-            init = D.DeviceTable(ctx, w, k, thr, compress=False) if args.trlr else None
+            table = build()
         t["table_device"] = tm.ms
         t.update({f"table_{key}": v for key, v in table.setup_ms().items()})
-        return w, thr, table, init, t
+        init = None
+        if args.trlr:  # tr_lr tables carry no threshold: transition = init = w - thr
+            init = D.DeviceTable(ctx, w_dev.cpu().numpy() - thr, k, 0.0, compress=False)
+        return w_dev, thr, table, init, t
 
     def scan_once(ds, table, init):
         if args.trlr:
@@ -302,8 +313,9 @@ def main():
             tdist.all_reduce(wt)
             words = float(wt.item())
         setup["count_allreduce_ms"] = round(tm.ms, 2)
-    w, thr, table, init_table, tt = make_table(counts, words)
+    w_dev, thr, table, init_table, tt = make_table(counts, words)
     setup.update({key: round(v, 2) for key, v in tt.items()})
+    w = None  # host copy of w, fetched after timing for the oracle legs
 
     # ------------------------------------------------------------- timing
     for _ in range(args.warmup):
@@ -371,6 +383,17 @@ def main():
 
     # ---- PCIe-inclusive rate of the drop-in host entry point (never `value`)
     host_path = None
+    need_w = (args.host_path or not args.no_cpu) and rank == 0
+    table_equal_host = None
+    if need_w:
+        w = w_dev.cpu().numpy()
+        if world == 1 and not args.no_cpu:  # the device-built table against the host builder (bitwise)
+            hc = counts.cpu().numpy()
+            wh = np.asarray(score_table(api, hc, k, words, args.score)[0], dtype=np.float64)
+            table_equal_host = bool(np.array_equal(w.view(np.uint64), wh.view(np.uint64)))
+            del hc, wh
+    if args.trlr and w is not None:
+        w = w - thr
     if args.host_path and rank == 0 and not args.trlr and thr == 0.0:
         hs = [ds.host_seq(q) for q in range(ds.nseq)]
         api.kmer_regions(hs, k, w, args.min_width, args.min_score)  # warm (pinned staging, workspace)
@@ -408,7 +431,7 @@ def main():
         extra["parity_bp"] = acc
 
     step_ms = ms_step
-    e2e_ms = setup["count_ms"] + setup["table_host"] + setup["table_device"] + step_ms
+    e2e_ms = setup["count_ms"] + setup["table_device"] + step_ms
     line = {
         "metric": METRIC,
         "value": round(value, 4), "unit": "Gbases/s", "n_gpus": world, "steps": args.steps,
@@ -430,6 +453,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "parity_sample": parity,
+        "table_equal_host": table_equal_host,
         "regions": n_regions_all,
         "replayed_chunks": int(stats[-1]["n_replay"]),
         "host_path": host_path,
@@ -437,8 +461,8 @@ def main():
                      for key in stats[-1] if key.startswith("ms_")},
         "setup_ms": setup,
         "end_to_end": {"ms": round(e2e_ms, 2), "Gbases_per_s": round(n_bases / (e2e_ms * 1e-3) / 1e9, 3),
-                       "what": "count + host score table + device table (compress, 12-bit codes, expanded "
-                               "table) + one scan step, per rank"},
+                       "what": "count + device score table from the counts (values, codes, 12-bit codes, "
+                               "expanded table) + one scan step, per rank"},
     }
     line.update(extra)
     if rank == 0:
@@ -469,7 +493,8 @@ def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over
     def one(ds):
         counts.zero_()
         words = D.count(ctx, ds, k, counts)
-        _, _, table, init, _ = make_table(counts, words)
+        _, _, table, init, _ = make_table(counts, words, ext_gib=args.ext_max_gib if args.ext_max_gib else 32.0,
+                                          warm=False)
         if args.trlr:
             out = D.tr_lr(ctx, ds, k, table, init, args.min_width)
         else:

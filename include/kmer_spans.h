@@ -177,7 +177,35 @@ ks_status ks_table_create(ks_ctx *ctx, const double *w_host, int32_t k, double t
  * never the results. */
 ks_status ks_table_create_hint(ks_ctx *ctx, const double *w_host, int32_t k, double thr,
                                int32_t flags, const int32_t *freq_dev, ks_table **out);
+/* Score table built on the device from device-resident k-mer counts
+ * (counts_dev: int32[4^k], e.g. ks_count_dev's), with no 4^k-sized host
+ * round trip.  score:
+ *   KS_SCORE_LOG2  w = log2(f / f_med), f = counts / sum(counts), f_med = R
+ *                  median(f) (README.md:27-42, kmer.counts()$f kmer_spans.R:25)
+ *   KS_SCORE_PM1   w = f >= f_med ? 1 : -1 (README.md:37-42)
+ *   KS_SCORE_RANK  w = rank_kmers_w(counts, total) (kmer_spans.c:189-202;
+ *                  total = the word count, as kmer_low_comp_regions :600-602)
+ * total is ignored for LOG2 / PM1.  The table holds s = w - thr; it is
+ * bitwise the table ks_table_create_hint(ks_log2_table / ks_pm1_table /
+ * ks_rank_table(...), thr, flags, counts_dev) builds: log2 and +-1 are
+ * evaluated once per distinct count on the host (glibc log2), the ranks by
+ * a closed-form exact evaluation of the sequential FP64 prefix.  counts_dev
+ * also serves as the position-frequency hint.  max_ext_bytes caps the
+ * expanded table (<= 0: the default cap).  w_dev: optional device
+ * double[4^k] receiving w.  In ks_table_info, ms_upload is the sort + value
+ * phase and ms_compress the code/value mapping. */
+#define KS_SCORE_LOG2 1
+#define KS_SCORE_PM1 2
+#define KS_SCORE_RANK 3
+ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev, int32_t k, int32_t score,
+                               double total, double thr, int32_t flags, int64_t max_ext_bytes,
+                               double *w_dev, ks_table **out);
 void ks_table_destroy(ks_table *t);
+/* The library keeps the buffer of the last destroyed expanded table (one
+ * per device) for the next table that fits in it: a fresh 32-128 GiB
+ * hipMalloc can take seconds (the driver clears new VRAM).  This returns it
+ * to the driver (also: environment KS_EXT_POOL=0 disables the pool). */
+void ks_release_cache(void);
 /* 1 if the table is stored compressed (uint16 codes + LUT), else 0. */
 int32_t ks_table_is_compressed(const ks_table *t);
 int64_t ks_table_distinct(const ks_table *t);
@@ -221,6 +249,11 @@ typedef struct ks_scan_stats {
   int64_t n_rescan;     /* rescan ranges processed */
   int32_t scan_algo;    /* 0 = lane per run, 1 = chunked carry scan */
   int64_t n_replay;     /* chunks whose carry needed an exact replay */
+  /* chunked scan (scan_algo 1) phases inside the step; ms_scan is P1 */
+  double ms_layout;     /* chunk table (k_make_chunks) */
+  double ms_predict;    /* P2: approximate carry scan, segment marks, binade summaries */
+  double ms_carry;      /* P3/P4: exact carry, heads */
+  double ms_stitch;     /* P5: excursion stitch, candidates */
 } ks_scan_stats;
 
 /* Span scan of device-resident sequences (the hot path).  visits_dev: device

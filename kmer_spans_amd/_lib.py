@@ -40,7 +40,8 @@ class ScanStats(C.Structure):
                 ("ms_rescan", C.c_double), ("ms_finish", C.c_double), ("n_bases", C.c_int64),
                 ("n_scored", C.c_int64), ("n_runs", C.c_int64), ("n_regions", C.c_int64),
                 ("n_rescan", C.c_int64), ("scan_algo", C.c_int32),
-                ("n_replay", C.c_int64)]
+                ("n_replay", C.c_int64), ("ms_layout", C.c_double), ("ms_predict", C.c_double),
+                ("ms_carry", C.c_double), ("ms_stitch", C.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -84,8 +85,11 @@ EXPORTS = [
     "ks_scan_dev", "ks_count_dev", "ks_ctx_set_scan_algo", "ks_tr_lr_regions", "ks_tr_lr_dev",
     "ks_fasta_load", "ks_fasta_parse", "ks_fasta_copy_seqs", "ks_fasta_free", "ks_count_multi_dev",
     "ks_count_file_write", "ks_count_file_read", "ks_count_file_free", "ks_kmers_to_file",
-    "ks_windowed_dist", "ks_windowed_dev",
+    "ks_windowed_dist", "ks_windowed_dev", "ks_table_from_counts",
+    "ks_release_cache",
 ]
+
+SCORES = {"log2": 1, "pm1": 2, "rank": 3}  # KS_SCORE_* of ks_table_from_counts
 
 _lib = None
 
@@ -139,6 +143,8 @@ def load():
         "ks_kmers_to_file": ([P, C.c_char_p, C.c_char_p, P, I32, D, I32, P], I32),
         "ks_windowed_dist": ([P, P, P, I32, P, I32, I32, I32, I32, P, P, P], I32),
         "ks_windowed_dev": ([P, P, P, I32, I32, I32, P, P, P], I32),
+        "ks_table_from_counts": ([P, P, I32, I32, D, D, I32, I64, P, P], I32),
+        "ks_release_cache": ([], None),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

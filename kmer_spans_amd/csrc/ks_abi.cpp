@@ -444,7 +444,8 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
   Staged st;
   KS_TRY(stage(ctx, seqs, lens, nseq, &st));
   ks_table *t = nullptr;
-  KS_TRY(ks_table_create(ctx, w, k, 0.0, k >= 9 ? 1 : 0, &t));
+  KS_TRY(table_create(ctx, w, k, 0.0, (k >= 9 ? KS_TABLE_COMPRESS : 0) | KS_TABLE_EXPAND, nullptr,
+                      host_ext_cap(st.total), &t));
   const size_t nb = (size_t)4 << (2 * k);
   void *d_vis = nullptr;
   ks_status rc = KS_OK;
@@ -487,14 +488,22 @@ extern "C" ks_status ks_low_comp_regions(ks_ctx *ctx, const char *const *seqs, c
   double words = 0;
   Runs none;
   KS_TRY(launch_count(ctx, &st.dev, st.total, none, k, (int32_t *)d_counts, &words));  // :592-601
-  KS_HIP(hipMemcpyAsync(counts, d_counts, nb, hipMemcpyDeviceToHost, ctx->stream));
-  KS_HIP(hipStreamSynchronize(ctx->stream));
   n[0] = words;
-  KS_TRY(rank_table_host(counts, k, words, ranks));           // :602
+  // weighted ranks on the device (rank_kmers_w :602, closed-form exact prefix),
+  // straight into the expanded FP64 table of the scan
+  double *d_ranks = nullptr;
+  if (hipMalloc(&d_ranks, (size_t)8 << (2 * k)) != hipSuccess)
+    return fail(KS_ERR_NOMEM, "hipMalloc of the rank table (k = %d) failed", k);
   ks_table *t = nullptr;
-  KS_TRY(ks_table_create(ctx, ranks, k, thr, 0, &t));         // ranks are ~unique: no LUT
-  ks_status rc = scan_impl(ctx, &st.dev, st.total, k, t, min_width, min_score, nullptr, out, nullptr);
+  ks_status rc = ks_table_from_counts(ctx, (const int32_t *)d_counts, k, KS_SCORE_RANK, words, thr, KS_TABLE_EXPAND,
+                                      host_ext_cap(st.total), d_ranks, &t);
+  if (rc == KS_OK && (hipMemcpyAsync(counts, d_counts, nb, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+                      hipMemcpyAsync(ranks, d_ranks, (size_t)8 << (2 * k), hipMemcpyDeviceToHost, ctx->stream) !=
+                          hipSuccess))
+    rc = fail(KS_ERR_DEVICE, "count / rank copy failed");
+  if (rc == KS_OK) rc = scan_impl(ctx, &st.dev, st.total, k, t, min_width, min_score, nullptr, out, nullptr);
   ks_table_destroy(t);
+  (void)hipFree(d_ranks);
   n[1] = 0;                                                   // Q8 (:613)
   if (rc != KS_OK) ks_regions_free(out);
   return rc;

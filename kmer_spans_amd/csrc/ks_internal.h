@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdarg>
 #include <cstdint>
@@ -101,6 +102,8 @@ struct ks_table {
   int ext_J = 1;
   void *d_ext = nullptr;        // uint64 (J <= 4 codes) or double[4] (J <= 3 values)
   size_t ext_bytes = 0;
+  size_t ext_cap = 0;           // bytes of the allocation (a pooled buffer may be larger)
+  int device = 0;
   // setup time (ms, host wall clock around synchronised device work)
   double ms_upload = 0;         // w -> device, s = w - thr, finiteness scan
   double ms_compress = 0;       // distinct values: radix sort + unique + code assignment
@@ -234,6 +237,14 @@ ks_status launch_count_multi(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, c
 ks_status windowed_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const uint32_t *qcodes_host, int kmer_n,
                         int k, int window, int32_t *dist_dev, int32_t *included_dev, int32_t *pos_dev);
 
+// ks_table_create_hint with a cap on the expanded table (<= 0: default).
+ks_status table_create(ks_ctx *ctx, const double *w_host, int32_t k, double thr, int32_t flags,
+                       const int32_t *freq_dev, int64_t max_ext_bytes, ks_table **out);
+// Expanded-table cap of the host entry points, whose table is built per
+// call: 16 B per input base (3.1 Gbp at k = 13: J = 4 (32 GiB, ~7 ms to
+// build) rather than J = 5 (128 GiB)), so the build stays a fraction of the
+// scan it speeds up.
+inline int64_t host_ext_cap(int64_t total_bases) { return std::max<int64_t>(16 * total_bases, (int64_t)1 << 20); }
 // Build the expanded table of t (no-op if it exists or does not fit).
 ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t *freq_dev);
 
@@ -241,5 +252,40 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
 ks_status rank_table_host(const int32_t *counts, int k, double total, double *ranks);
 ks_status log2_table_host(const int32_t *counts, int k, double *w);
 ks_status pm1_table_host(const int32_t *counts, int k, double *w);
+
+// The weighted-rank prefix of rank_kmers_w (kmer_spans.c:196-200) in closed
+// form.  In the stable (count, index) order, position j holds
+// R_j = fl(R_{j-1} + c_{j-1} / total), R_0 = 0.  Equal counts are adjacent, so
+// over a run of equal counts the same d is added again and again; while R
+// stays in one binade [2^e, 2^(e+1)), R = m * 2^(e-52) and fl(R + d) adds
+// RN(d * 2^(52-e)) to the integer m (an exact half rounds to the even
+// result: after one such step m is even and the increment is constant).  So a
+// run is a few arithmetic progressions of m, cut where R leaves the binade;
+// those crossing steps are FP64 additions done here exactly as the reference
+// does them.  A piece covers sorted positions [j0, next j0):
+//   kind 0: R = r0 throughout;
+//   kind 1: R = r0 at j0, then m(r0) + inc1 + (j - j0 - 1) * inc in binade e.
+struct RankPiece {
+  int64_t j0;
+  double r0;
+  int64_t inc1, inc;
+  int32_t e, kind;
+};
+__host__ __device__ __forceinline__ double rank_piece_value(const RankPiece &p, int64_t j) {
+  if (p.kind == 0 || j == p.j0) return p.r0;
+  union { double d; int64_t i; } u;
+  u.d = p.r0;
+  const int64_t m = (u.i & ((1LL << 52) - 1)) | (1LL << 52);
+  const int64_t mt = m + p.inc1 + (j - p.j0 - 1) * p.inc;
+  u.i = ((int64_t)(p.e + 1023) << 52) | (mt - (1LL << 52));
+  return u.d;
+}
+// Pieces of the whole prefix from the distinct counts (ascending) and their
+// multiplicities.  Empty if a count is negative (wrapped int32 counts: the
+// caller then runs the sequential prefix).
+std::vector<RankPiece> rank_pieces(const int32_t *vals, const int64_t *mult, int64_t nu, double total);
+// log2(f / f_med) (score 1) or +-1 (score 2) of each distinct count, with f
+// and f_med as log2_table_host / pm1_table_host compute them (bit-identical).
+void score_of_counts(int score, const int32_t *vals, const int64_t *mult, int64_t nu, double *w);
 
 }  // namespace ks

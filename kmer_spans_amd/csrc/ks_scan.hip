@@ -22,8 +22,8 @@
 namespace ks {
 
 ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, const RunLayout &lay, int k,
-                       const TableView &tv, uint64_t mw, double min_score, uint32_t *visits, const RegionBuf &rb,
-                       ks_scan_stats *stats, const ScanMode &mode);
+                       const TableView &tv, uint64_t mw, double min_score, uint32_t *visits,
+                       uint32_t *visits_rescan, const RegionBuf &rb, ks_scan_stats *stats, const ScanMode &mode);
 ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const int64_t *ra, const int64_t *rb,
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
@@ -249,6 +249,21 @@ __global__ void k_region_gather(RegionBuf rb, const int32_t *__restrict__ perm, 
   o_score[j] = rb.score[i];
 }
 
+// Top-level visits from the k-mer counts (kmer_spans.c:266-267): a run's
+// top-level scan scores every k-mer of the run except its last one (quirk Q5),
+// so visits = sequence_kmer_count's counts minus the last k-mer of every
+// counted run: runs of length >= k, except a run of exactly k bases at the
+// end of its sequence, which the count already skips (quirk Q1, :142-144).
+__global__ void k_visit_correct(const int64_t *__restrict__ ra, const int64_t *__restrict__ rb,
+                                const int32_t *__restrict__ rs, int64_t n, const int64_t *__restrict__ offs,
+                                const uint8_t *__restrict__ seq, int k, uint32_t *__restrict__ vis) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const int64_t a = ra[r], b = rb[r];
+  if (b - a < k || (b - a == k && b == offs[rs[r] + 1])) return;
+  atomicSub(&vis[prime_code(seq, b - k, k)], 1u);
+}
+
 __global__ void k_add_hist(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     dst[i] += src[i];
@@ -366,7 +381,12 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
         vscr = static_cast<uint32_t *>(vp);
         KS_HIP(hipMemsetAsync(vscr, 0, nb, st));
       }
-      ks_status rc = scan_chunked(ctx, s, runs, lay, k, tv, mw, min_score, vscr, rb, S, mode);
+      // top-level visits: from the k-mer counts (one partitioned count pass)
+      // unless KS_VISITS_ATOMIC is set (one random atomic per scanned index in
+      // pass 1, the former path, kept for A/B runs and tests)
+      static const bool vis_atomic = getenv("KS_VISITS_ATOMIC") != nullptr;
+      ks_status rc = scan_chunked(ctx, s, runs, lay, k, tv, mw, min_score, vis_atomic ? vscr : nullptr, vscr, rb, S,
+                                  mode);
       if (rc == KS_INTERNAL_RETRY) {  // a buffer did not fit: grow, rerun, visits untouched
         KS_TRY(read_counts());
         const int64_t m = max_count();
@@ -376,6 +396,15 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
       if (rc == KS_OK) {
         if (vis) {
           const int64_t n = (int64_t)1 << (2 * k);
+          if (!vis_atomic) {
+            double words = 0;
+            KS_TRY(launch_count(ctx, s, total, runs, k, visits_dev, &words));
+            if (runs.n > 0) {
+              hipLaunchKernelGGL(k_visit_correct, dim3((unsigned)((runs.n + 255) / 256)), dim3(256), 0, st, runs.a,
+                                 runs.b, runs.seq, runs.n, s->offsets_dev, s->seq, k, vis);
+              KS_HIP(hipGetLastError());
+            }
+          }
           hipLaunchKernelGGL(k_add_hist, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, st,
                              vis, vscr, n);
           KS_HIP(hipGetLastError());

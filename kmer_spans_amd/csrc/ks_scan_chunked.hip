@@ -186,6 +186,27 @@ __device__ __forceinline__ void load_codes16(const uint16_t *__restrict__ codes,
   }
 }
 
+// Values of scan indices b0 .. b0+15 of chunk c (0 past n) of a compressed
+// table whose per-index codes were not stored (small-k pass 1): the 16
+// k-mers from one 64-bit window of packed bases (bytes near the buffer end),
+// each looked up in the base code table (L2-resident for small k) and the LUT.
+__device__ __forceinline__ void values16_nostore(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total,
+                                                 int k, const TableView &tv, int64_t c, int b0, int n, double v[16],
+                                                 const double *s_lut) {
+  const int64_t p = g.start[c] + b0 - k;  // first base of index b0's k-mer
+  const uint32_t kmask = (1u << (2 * k)) - 1u;
+  uint64_t x = 0;
+  const bool pk = packed_bits(g.packed, total, p, x);
+  uint32_t code = pk ? 0u : prime_code(seq, p, k);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (pk) code = (uint32_t)(x >> (64 - 2 * (j + k))) & kmask;
+    else if (j > 0 && b0 + j < n) code = ((code << 2) | enc(seq[p + k - 1 + j])) & kmask;
+    const uint32_t q = b0 + j < n ? tv.codes[code] : 0u;
+    v[j] = b0 + j < n ? (s_lut ? s_lut[q] : tv.lut[q]) : 0.0;
+  }
+}
+
 // Values of scan indices i0 .. i0+3 of chunk c (0 past n): one 8-byte code
 // load (compressed) or one k-mer prime plus three rolls.
 __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
@@ -246,6 +267,11 @@ constexpr int kP1G = KS_P1_G;
 #define KS_P1_BLOCK (KS_P1_G > 4 ? 768 : 1024)
 #endif
 constexpr int kP1Block = KS_P1_BLOCK;  // lanes per pass-1 block (build parameter for A/B runs)
+#ifdef KS_P1_NOSTORE  // diagnostic build: no code store in k_pass1p, later passes gather (slow, exact)
+constexpr bool kP1NoStore = true;
+#else
+constexpr bool kP1NoStore = false;
+#endif
 static_assert(kP1Block % 64 == 0 && kP1Block <= 1024, "pass-1 block is whole waves");
 constexpr int kP1StageWords = kP1G > 4 ? 24 : 20;
 // Bases past its chunk's first scan index a pass-1 lane may read: the
@@ -705,7 +731,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
     }
 #pragma unroll
     for (int r4 = 0; r4 < PB / 4; ++r4)
-      if (b0 + 4 * r4 < CH)
+      if (b0 + 4 * r4 < CH && !kP1NoStore)
 #ifndef KS_P1_PLAIN_CODES  // nontemporal code stores: A/B 16.19-16.21 vs 16.31-16.57 ms
         __builtin_nontemporal_store((uint64_t)cw[2 * r4] | ((uint64_t)cw[2 * r4 + 1] << 32),
                                     reinterpret_cast<uint64_t *>(codes + code_slot(c, b0 + 4 * r4)));
@@ -728,6 +754,93 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
     o.tbeg[c] = beg; o.tmax[c] = best; o.targ[c] = arg;
   } else {
     o.tbeg[c] = -1; o.tmax[c] = 0.0; o.targ[c] = 0;
+  }
+}
+
+// Pass 1 for small k (north_star: "the frequency table LDS-staged for small
+// k"): the 4^k FP64 values s[code] (k <= 7: <= 128 KiB) are staged in LDS
+// once per persistent block, so every scanned index costs one LDS read and no
+// random HBM request; bases are rolled from the packed 2-bit codes (one
+// 4-B word per 16 bases).  No code store: later passes re-derive values from
+// the packed bases and the base table (values16_nostore / values4).  Same
+// outputs as k_pass1.
+constexpr int kLdsTableK = 7;
+template <bool kTrlr>
+__global__ void __launch_bounds__(1024) k_pass1_lds(Chunks g, int k, TableView tv, EmitCfg ec,
+                                                    uint32_t *__restrict__ visits, P1 o, Cand cand) {
+  __shared__ double s_val[1 << (2 * kLdsTableK)];
+  const int nk = 1 << (2 * k);
+  for (int i = threadIdx.x; i < nk; i += blockDim.x) s_val[i] = tv_get(tv, (uint32_t)i);
+  __syncthreads();
+  const uint32_t kmask = (uint32_t)nk - 1u;
+  const uint32_t *__restrict__ packed = g.packed;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < g.nch;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t start = g.start[c];
+    const int n = g.n[c];
+    const bool first = c == 0 || g.run[c - 1] != g.run[c];
+    int64_t wi = (start - k) >> 4;
+    uint32_t w = packed[wi];
+    auto base = [&](int64_t q) -> uint32_t {
+      if ((q >> 4) != wi) {
+        wi = q >> 4;
+        w = packed[wi];
+      }
+      return (w >> (30 - 2 * (int)(q & 15))) & 3u;
+    };
+    uint32_t code = 0;  // k-mer ending at start - 1 (scan index 0)
+    for (int j = 0; j < k; ++j) code = (code << 2) | base(start - k + j);
+    double prev = 0.0, best = 0.0;
+    int beg = -1, arg = 0;
+    double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
+    bool special = false;
+    for (int i = 0; i < n; ++i) {
+      double s = s_val[code];
+      if (kTrlr && first && i == 0) s = ec.ks[code];  // tr_lr: the run's first k-mer's own score
+      if (visits) atomicAdd(&visits[code], 1u);
+      asum += s;
+      pmin = asum < pmin ? asum : pmin;
+      pmax = asum > pmax ? asum : pmax;
+      sabs += fabs(s);
+      special |= !isfinite(s);
+      const double tt = prev + s;
+      const double S = tt > 0 ? tt : 0.0;
+      const bool open = (prev == 0) & (S > 0);
+      const bool close = (prev > 0) & (S == 0);
+      const int f0 = first ? 0 : -1;
+      const long long ml = kTrlr ? ec.min_len : 0;
+      const bool want =
+          kTrlr ? (close & (((long long)((arg != f0 ? arg - 1 : arg) - (beg != f0 ? beg - 1 : beg)) >= ml) |
+                            ((long long)((i != f0 ? i - 1 : i) - (arg != f0 ? arg - 1 : arg) - 1) >=
+                             (ml > 1 ? ml : 1LL))))
+                : (close & ((uint64_t)(int64_t)(arg - beg) >= ec.mw) & (best >= ec.min_score));
+      if (want) {
+        const int64_t slot = append_one(cand.count, cand.segcap);
+        if (slot >= 0) {
+          cand.beg[slot] = start + beg;
+          cand.arg[slot] = start + arg;
+          cand.rst[slot] = start + i;
+          cand.best[slot] = best;
+        }
+      }
+      const bool up = open | (S > best);
+      best = up ? S : best;
+      arg = up ? i : arg;
+      beg = open ? i : (close ? -1 : beg);
+      prev = S;
+      if (i + 1 < n) code = ((code << 2) | base(start + i)) & kmask;  // k-mer ending at start + i
+    }
+    o.cexit[c] = prev;
+    o.asum[c] = asum;
+    o.pmin[c] = pmin;
+    o.pmax[c] = pmax;
+    o.sabs[c] = sabs;
+    o.special[c] = special ? 1 : 0;
+    if (prev > 0) {
+      o.tbeg[c] = beg; o.tmax[c] = best; o.targ[c] = arg;
+    } else {
+      o.tbeg[c] = -1; o.tmax[c] = 0.0; o.targ[c] = 0;
+    }
   }
 }
 
@@ -896,7 +1009,9 @@ __device__ int chunk_summary_impl(const Chunks &g, const uint8_t *__restrict__ s
   bool ok = true, tie_seen = false;
   for (int b0 = 0; b0 < n; b0 += NB) {
     double v[NB];
-    if (kCompressed) {
+    if (kCompressed && !codes) {
+      values16_nostore(g, seq, total, k, tv, c, b0, n, v, nullptr);
+    } else if (kCompressed) {
       uint32_t w[8];
       load_codes16(codes, c, b0, w);
 #pragma unroll
@@ -977,7 +1092,9 @@ __device__ int chunk_summary_fast(const Chunks &g, const uint8_t *__restrict__ s
   bool ok = true, tie_seen = false;
   for (int b0 = 0; b0 < n; b0 += NB) {
     double v[NB];
-    if (kCompressed) {
+    if (kCompressed && !codes) {
+      values16_nostore(g, seq, total, k, tv, c, b0, n, v, kLds ? s_lut : nullptr);
+    } else if (kCompressed) {
       uint32_t w[8];
       load_codes16(codes, c, b0, w);
 #pragma unroll
@@ -1679,10 +1796,14 @@ __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restri
   if (kCompressed) {
     for (int b0 = 0; b0 < n && hq < 0; b0 += NB) {
       double v[NB];
-      uint32_t w[8];
-      load_codes16(codes, c, b0, w);
+      if (!codes) {
+        values16_nostore(g, seq, total, k, tv, c, b0, n, v, nullptr);
+      } else {
+        uint32_t w[8];
+        load_codes16(codes, c, b0, w);
 #pragma unroll
-      for (int j = 0; j < NB; ++j) v[j] = tv.lut[(w[j >> 1] >> (16 * (j & 1))) & 0xffffu];
+        for (int j = 0; j < NB; ++j) v[j] = tv.lut[(w[j >> 1] >> (16 * (j & 1))) & 0xffffu];
+      }
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int i = b0 + j;
@@ -2060,8 +2181,8 @@ __global__ void k_candidates(Chunks g, const int64_t *__restrict__ ra, const int
 }  // namespace
 
 ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, const RunLayout &lay, int k,
-                       const TableView &tv, uint64_t mw, double min_score, uint32_t *visits, const RegionBuf &rb,
-                       ks_scan_stats *stats, const ScanMode &mode) {
+                       const TableView &tv, uint64_t mw, double min_score, uint32_t *visits,
+                       uint32_t *visits_rescan, const RegionBuf &rb, ks_scan_stats *stats, const ScanMode &mode) {
   const EmitCfg ec{mode.trlr, mw, min_score, mode.min_len, mode.ks, k};
   hipStream_t st = ctx->stream;
   const int64_t total = s->offsets_host[s->nseq];
@@ -2186,7 +2307,14 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     else hipLaunchKernelGGL((k_pass1p<J, L, false>), dim3(gp1), dim3(kP1Block), 0, st, g, s->seq, total, k, tv,  \
                             codes, ec, visits, p1, cand, runs.packed);                                         \
   } while (0)
-  if (comp && J >= 2 && pipelined) {
+  const bool lds_table = k <= kLdsTableK && runs.packed != nullptr && getenv("KS_NO_LDS_TABLE") == nullptr;
+  if (lds_table) {
+    // small k: the whole table in LDS, persistent blocks (one per CU), no code store
+    const unsigned gl = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nch + 1023) / 1024, ctx->num_cus));
+    if (ec.trlr) hipLaunchKernelGGL(k_pass1_lds<true>, dim3(gl), dim3(1024), 0, st, g, k, tv, ec, visits, p1, cand);
+    else hipLaunchKernelGGL(k_pass1_lds<false>, dim3(gl), dim3(1024), 0, st, g, k, tv, ec, visits, p1, cand);
+    codes = nullptr;
+  } else if (comp && J >= 2 && pipelined) {
     // the tail chunks (a latency-bound serial walk each) run on the side
     // stream, overlapped with the pipelined pass
     hipStream_t side = ctx->side;
@@ -2207,6 +2335,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     }
     KS_HIP(hipGetLastError());
     if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
+    if (kP1NoStore) codes = nullptr;  // diagnostic build: later passes gather their values
   } else if (!comp && J >= 2 && J <= 4 && pipelined) {
     hipStream_t side = ctx->side;
     const bool tail = nch > ctail;
@@ -2259,6 +2388,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     hipLaunchKernelGGL((k_summaries<false, false>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes,
                        p1, xt, sm);
   KS_HIP(hipGetLastError());
+  KS_HIP(hipEventRecord(ctx->ev[14], st));
 
   // ---- P3 carry by segments + P4 heads; then the gated per-run fallback
   if (comp)
@@ -2292,6 +2422,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                        k, tv, codes, p1, sm, cr, d_replays, d_err, nullptr);
   heads(1);
   KS_HIP(hipGetLastError());
+  KS_HIP(hipEventRecord(ctx->ev[15], st));
 
   // ---- P5 stitch, candidates (count read on the device), rescans
   hipLaunchKernelGGL(k_stitch_tiles, dim3((unsigned)ntiles), dim3(64), 0, st, g, d_tbase, d_cbase, nruns, p1, cr,
@@ -2307,7 +2438,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                      nruns, runs.seq, ec, cand, cr, rb, rs);
   KS_HIP(hipGetLastError());
   KS_HIP(hipEventRecord(ctx->ev[10], st));
-  KS_TRY(launch_scan_lane(ctx, s->seq, total, rs.a, rs.b, rs.seq, rcap, k, tv, mw, min_score, visits, rb,
+  KS_TRY(launch_scan_lane(ctx, s->seq, total, rs.a, rs.b, rs.seq, rcap, k, tv, mw, min_score, visits_rescan, rb,
                           rs.count, rs.segcap, mode, 0, nullptr, runs.packed));
   KS_HIP(hipEventRecord(ctx->ev[11], st));
   std::vector<unsigned long long> hcv(2 * kSegs + 2);
@@ -2376,13 +2507,19 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     fprintf(stderr, "\n");
   }
   if (stats) {
-    float ms_p1 = 0, ms_all = 0, ms_res = 0;
+    float ms_lay = 0, ms_p1 = 0, ms_p2 = 0, ms_p34 = 0, ms_p5 = 0, ms_res = 0;
+    KS_HIP(hipEventElapsedTime(&ms_lay, ctx->ev[7], ctx->ev[8]));
     KS_HIP(hipEventElapsedTime(&ms_p1, ctx->ev[8], ctx->ev[9]));
-    KS_HIP(hipEventElapsedTime(&ms_all, ctx->ev[7], ctx->ev[10]));
+    KS_HIP(hipEventElapsedTime(&ms_p2, ctx->ev[9], ctx->ev[14]));
+    KS_HIP(hipEventElapsedTime(&ms_p34, ctx->ev[14], ctx->ev[15]));
+    KS_HIP(hipEventElapsedTime(&ms_p5, ctx->ev[15], ctx->ev[10]));
     KS_HIP(hipEventElapsedTime(&ms_res, ctx->ev[10], ctx->ev[11]));
+    stats->ms_layout = ms_lay;
     stats->ms_scan = ms_p1;
+    stats->ms_predict = ms_p2;
+    stats->ms_carry = ms_p34;
+    stats->ms_stitch = ms_p5;
     stats->ms_rescan = ms_res;
-    stats->ms_finish += ms_all - ms_p1;
     stats->n_rescan = nres;
     stats->n_replay = (int64_t)hc[2];
   }

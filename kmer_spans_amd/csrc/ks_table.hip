@@ -10,8 +10,10 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <cstdlib>
+#include <mutex>
 #include <vector>
 
 #include "ks_internal.h"
@@ -63,17 +65,36 @@ __global__ void k_assign_codes(const double *__restrict__ s, const unsigned long
 }
 
 // Expanded table, uint16 codes: entry for the (k+J-1)-mer x packs the codes of
-// its J k-mers (first k-mer in the low 16 bits).  Consecutive entries share
-// their k-mers, so the base-table reads are cached and the build is a stream.
+// its J k-mers (first k-mer in the low 16 bits).  Lane p builds the entry
+// pair 2p, 2p+1: their first J-1 k-mers coincide ((2p + d) >> 2(J-1-t) does
+// not depend on d for t < J-1), their last k-mers are two consecutive codes
+// (one 4-B load).  Consecutive lanes write consecutive pairs, so one store
+// instruction covers a contiguous span; the table is far larger than every
+// cache, so the stores are nontemporal.  The code reads repeat across the
+// wave and stay cached: the build is a write stream.
+typedef unsigned long long ks_u64x2 __attribute__((ext_vector_type(2)));
 template <int J, typename E>
 __global__ void k_build_ext_u16(const uint16_t *__restrict__ codes, int k, uint64_t nent, E *__restrict__ ext) {
   const uint64_t mk = ((uint64_t)1 << (2 * k)) - 1;
-  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nent;
-       e += (uint64_t)gridDim.x * blockDim.x) {
+  const uint64_t npair = nent >> 1;
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npair;
+       p += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t e0 = p << 1;
     uint64_t v = 0;
 #pragma unroll
-    for (int t = 0; t < J; ++t) v |= (uint64_t)codes[(e >> (2 * (J - 1 - t))) & mk] << (16 * t);
-    ext[e] = (E)v;
+    for (int t = 0; t < J - 1; ++t) v |= (uint64_t)codes[(e0 >> (2 * (J - 1 - t))) & mk] << (16 * t);
+    const uint32_t w = *reinterpret_cast<const uint32_t *>(codes + (e0 & mk));
+    const uint64_t v0 = v | ((uint64_t)(w & 0xffffu) << (16 * (J - 1)));
+    const uint64_t v1 = v | ((uint64_t)(w >> 16) << (16 * (J - 1)));
+    if (sizeof(E) == 8) {
+      ks_u64x2 o;
+      o.x = v0;
+      o.y = v1;
+      __builtin_nontemporal_store(o, reinterpret_cast<ks_u64x2 *>(ext) + p);
+    } else {
+      __builtin_nontemporal_store((uint64_t)(uint32_t)v0 | ((uint64_t)(uint32_t)v1 << 32),
+                                  reinterpret_cast<uint64_t *>(ext) + p);
+    }
   }
 }
 
@@ -141,30 +162,25 @@ __global__ void __launch_bounds__(1024) k_remap_codes(uint16_t *__restrict__ cod
 // Expanded table, 12-bit codes: J = 5 codes per uint64 entry, first k-mer
 // in the low 12 bits.  The uint16 codes are numbered by position weight
 // (choose_code12), so a code below 4095 is its own 12-bit code and every
-// other code escapes (0xFFF).  Lane m builds entries 4m .. 4m+3: their first
-// four k-mers are shared ((4m + d) >> 2(4 - t) does not depend on d for
-// t <= 3), their fifth k-mers are the 4 consecutive k-mers 4m .. 4m+3 (one
-// 8-B load), and the 32 B of output go out as two 16-B stores.
+// other code escapes (0xFFF).  Same pair-per-lane layout and nontemporal
+// stores as k_build_ext_u16 (was four entries per lane as two 16-B stores
+// at a 32-B stride: 42-56 ms for the 128 GiB table at k = 13).
 __device__ __forceinline__ uint64_t c12_of(uint32_t code) { return code < 0xFFFu ? code : 0xFFFu; }
 __global__ void k_build_ext_c12(const uint16_t *__restrict__ codes, int k, uint64_t nent,
                                 uint64_t *__restrict__ ext) {
   const uint64_t mk = ((uint64_t)1 << (2 * k)) - 1;
-  const uint64_t nq = nent >> 2;
-  for (uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; m < nq;
-       m += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t e0 = m << 2;
+  const uint64_t npair = nent >> 1;
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npair;
+       p += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t e0 = p << 1;
     uint64_t base = 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) base |= c12_of(codes[(e0 >> (2 * (4 - t))) & mk]) << (12 * t);
-    const uint2 w = *reinterpret_cast<const uint2 *>(codes + (e0 & mk));
-    const uint32_t c4[4] = {w.x & 0xffffu, w.x >> 16, w.y & 0xffffu, w.y >> 16};
-    ulonglong2 o0, o1;
-    o0.x = base | (c12_of(c4[0]) << 48);
-    o0.y = base | (c12_of(c4[1]) << 48);
-    o1.x = base | (c12_of(c4[2]) << 48);
-    o1.y = base | (c12_of(c4[3]) << 48);
-    reinterpret_cast<ulonglong2 *>(ext)[2 * m] = o0;
-    reinterpret_cast<ulonglong2 *>(ext)[2 * m + 1] = o1;
+    const uint32_t w = *reinterpret_cast<const uint32_t *>(codes + (e0 & mk));
+    ks_u64x2 o;
+    o.x = base | (c12_of(w & 0xffffu) << 48);
+    o.y = base | (c12_of(w >> 16) << 48);
+    __builtin_nontemporal_store(o, reinterpret_cast<ks_u64x2 *>(ext) + p);
   }
 }
 
@@ -187,6 +203,102 @@ __global__ void k_build_ext_f64(const double *__restrict__ vals, int k, uint64_t
   }
 }
 
+// out[i] = lut[index of counts[i] in dv]: dv = the sorted distinct counts
+// (every count occurs in it), staged in LDS with the LUT when they fit.
+constexpr int kMapLds = 8192;
+template <typename V>
+__global__ void __launch_bounds__(1024) k_map_counts(const int32_t *__restrict__ counts, int64_t n,
+                                                     const int32_t *__restrict__ dv, int64_t nu,
+                                                     const V *__restrict__ lut, V *__restrict__ out) {
+  __shared__ int32_t s_dv[kMapLds];
+  __shared__ V s_lut[kMapLds];
+  const bool lds = nu <= kMapLds;
+  if (lds) {
+    for (int i = threadIdx.x; i < nu; i += blockDim.x) {
+      s_dv[i] = dv[i];
+      s_lut[i] = lut[i];
+    }
+    __syncthreads();
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t c = counts[i];
+    int64_t lo = 0, hi = nu - 1;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((lds ? s_dv[mid] : dv[mid]) < c) lo = mid + 1; else hi = mid;
+    }
+    out[i] = lds ? s_lut[lo] : lut[lo];
+  }
+}
+
+// Weighted ranks from the closed-form prefix (RankPiece, ks_internal.h):
+// sorted position j (stable (count, index) order, idx = the sorted indices)
+// takes its piece's value; 16 consecutive positions per lane, one binary
+// search per lane.
+__global__ void k_rank_fill(const uint32_t *__restrict__ idx, int64_t n, const RankPiece *__restrict__ P, int64_t np,
+                            double *__restrict__ ranks) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g * 16 < n; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j0 = g * 16;
+    int64_t lo = 0, hi = np - 1;  // last piece starting at or before j0
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (P[mid].j0 <= j0) lo = mid; else hi = mid - 1;
+    }
+    const int64_t j1 = min(n, j0 + 16);
+    for (int64_t j = j0; j < j1; ++j) {
+      while (lo + 1 < np && P[lo + 1].j0 <= j) ++lo;
+      ranks[idx[j]] = rank_piece_value(P[lo], j);
+    }
+  }
+}
+
+__global__ void k_iota(uint32_t *__restrict__ x, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = (uint32_t)i;
+}
+
+}  // namespace
+
+// Process-wide pool of ONE expanded-table buffer per device.  A fresh
+// hipMalloc of 32-128 GiB takes 0.3 ms to 6 s on the box (the driver clears
+// new VRAM; tools/alloc_probe.py), while a buffer freed by this process is
+// handed back at once; tables built per call (host entry points, one table
+// per genome) would pay that on every table.  A destroyed table's buffer is
+// kept here and reused by the next expansion that fits in it;
+// ks_release_cache() returns it to the driver; KS_EXT_POOL=0 disables it.
+namespace {
+std::mutex g_pool_mu;
+struct PoolBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+};
+PoolBuf g_pool[64];
+bool pool_on() {
+  static const bool on = !(getenv("KS_EXT_POOL") && atoi(getenv("KS_EXT_POOL")) == 0);
+  return on;
+}
+void *pool_take(int dev, size_t bytes, size_t *cap) {
+  if (!pool_on() || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  PoolBuf &b = g_pool[dev];
+  if (!b.p || b.bytes < bytes) return nullptr;
+  void *p = b.p;
+  *cap = b.bytes;
+  b = PoolBuf();
+  return p;
+}
+void pool_give(int dev, void *p, size_t bytes) {
+  if (!p) return;
+  if (pool_on() && dev >= 0 && dev < 64) {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    PoolBuf &b = g_pool[dev];
+    if (!b.p || b.bytes < bytes) {
+      std::swap(b.p, p);
+      std::swap(b.bytes, bytes);
+    }
+  }
+  if (p) (void)hipFree(p);
+}
 }  // namespace
 
 // Entry bytes of an expanded table with J values per entry.
@@ -259,6 +371,10 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   const bool u16 = t->compressed;
   size_t free_b = 0, total_b = 0;
   KS_HIP(hipMemGetInfo(&free_b, &total_b));
+  {  // the pooled buffer of a destroyed table is free memory for this purpose
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    if (ctx->device >= 0 && ctx->device < 64) free_b += g_pool[ctx->device].bytes;
+  }
   // leave room for the sequences and the scan workspace
   const size_t reserve = std::max<size_t>((size_t)32 << 30, total_b / 4);
   const size_t budget = std::min(max_bytes, free_b > reserve ? free_b - reserve : (size_t)0);
@@ -300,11 +416,27 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   hipStream_t st = ctx->stream;
   void *ext = nullptr;
   const double ta = now_ms();
-  if (hipMalloc(&ext, bytes) != hipSuccess) {
-    (void)hipGetLastError();
-    return KS_OK;
+  size_t cap = bytes;
+  ext = pool_take(ctx->device, bytes, &cap);
+  if (!ext) {
+    cap = bytes;
+    if (hipMalloc(&ext, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      {  // a pooled buffer too small for this table may be what is in the way
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        if (ctx->device >= 0 && ctx->device < 64 && g_pool[ctx->device].p) {
+          (void)hipFree(g_pool[ctx->device].p);
+          g_pool[ctx->device] = PoolBuf();
+        }
+      }
+      if (hipMalloc(&ext, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return KS_OK;
+      }
+    }
   }
   t->ms_ext_alloc = now_ms() - ta;
+  t->ext_cap = cap;
   hipEvent_t a, b;
   KS_HIP(hipEventCreate(&a));
   KS_HIP(hipEventCreate(&b));
@@ -353,6 +485,11 @@ extern "C" ks_status ks_table_create(ks_ctx *ctx, const double *w_host, int32_t 
 
 extern "C" ks_status ks_table_create_hint(ks_ctx *ctx, const double *w_host, int32_t k, double thr,
                                           int32_t flags, const int32_t *freq_dev, ks_table **out) {
+  return table_create(ctx, w_host, k, thr, flags, freq_dev, 0, out);
+}
+
+ks_status ks::table_create(ks_ctx *ctx, const double *w_host, int32_t k, double thr, int32_t flags,
+                           const int32_t *freq_dev, int64_t max_ext_bytes, ks_table **out) {
   const int32_t allow_compress = flags & KS_TABLE_COMPRESS;
   if (!ctx || !w_host || !out) return fail(KS_ERR_ARG, "ks_table_create: null argument");
   if (k < 1 || k > KS_MAX_K) return fail(KS_ERR_ARG, "k must be between 1 and %d", KS_MAX_K);
@@ -362,6 +499,7 @@ extern "C" ks_status ks_table_create_hint(ks_ctx *ctx, const double *w_host, int
   hipStream_t st = ctx->stream;
   ks_table *t = new ks_table();
   t->ctx = ctx;
+  t->device = ctx->device;
   t->k = k;
   t->thr = thr;
   double *d_w = nullptr;
@@ -437,8 +575,229 @@ extern "C" ks_status ks_table_create_hint(ks_ctx *ctx, const double *w_host, int
   cleanup();
   t->ms_compress = now_ms() - t_start - t->ms_upload;
   if (flags & KS_TABLE_EXPAND) {
-    const ks_status rc = table_expand(ctx, t, (size_t)160 << 30, freq_dev);
+    const ks_status rc = table_expand(ctx, t, max_ext_bytes > 0 ? (size_t)max_ext_bytes : (size_t)160 << 30, freq_dev);
     if (rc != KS_OK) { ks_table_destroy(t); return rc; }
+  }
+  t->ms_total = now_ms() - t_start;
+  *out = t;
+  return KS_OK;
+}
+
+
+extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev, int32_t k, int32_t score,
+                                          double total, double thr, int32_t flags, int64_t max_ext_bytes,
+                                          double *w_dev, ks_table **out) {
+  if (!ctx || !counts_dev || !out) return fail(KS_ERR_ARG, "ks_table_from_counts: null argument");
+  if (k < 1 || k > KS_MAX_K) return fail(KS_ERR_ARG, "k must be between 1 and %d", KS_MAX_K);
+  if (score != KS_SCORE_LOG2 && score != KS_SCORE_PM1 && score != KS_SCORE_RANK)
+    return fail(KS_ERR_ARG, "ks_table_from_counts: unknown score %d", score);
+  KS_TRY(activate(ctx));
+  const double t_start = now_ms();
+  const int64_t n = (int64_t)1 << (2 * k);
+  hipStream_t st = ctx->stream;
+  const bool rank = score == KS_SCORE_RANK;
+  ks_table *t = new ks_table();
+  t->ctx = ctx;
+  t->device = ctx->device;
+  t->k = k;
+  t->thr = thr;
+  std::vector<void *> tmp;
+  auto cleanup = [&]() {
+    for (void *p : tmp) (void)hipFree(p);
+    tmp.clear();
+  };
+#define KS_TFC(call)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      cleanup();                                                                       \
+      ks_table_destroy(t);                                                             \
+      return fail(KS_ERR_DEVICE, "%s failed: %s", #call, hipGetErrorString(e_));      \
+    }                                                                                  \
+  } while (0)
+  auto dalloc = [&](size_t bytes) -> void * {
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    tmp.push_back(p);
+    return p;
+  };
+  // 1. the counts in stable (count, index) order, their distinct values and
+  // multiplicities; scratch in the ctx's grow-only table slot (no per-call
+  // hipMalloc of 4^k-sized buffers)
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  size_t b1 = 0, b2 = 0;
+  KS_TFC(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, counts_dev, (int32_t *)nullptr, (uint32_t *)nullptr,
+                                            (uint32_t *)nullptr, (int)n, 0, 32, st));
+  KS_TFC(hipcub::DeviceRunLengthEncode::Encode(nullptr, b2, (int32_t *)nullptr, (int32_t *)nullptr, (int *)nullptr,
+                                               (int *)nullptr, (int)n, st));
+  {
+    size_t bk = 0;
+    KS_TFC(hipcub::DeviceRadixSort::SortKeys(nullptr, bk, counts_dev, (int32_t *)nullptr, (int)n, 0, 32, st));
+    b1 = std::max(b1, bk);
+  }
+  const size_t sn = ((size_t)n * 4 + 255) & ~(size_t)255, tmpb = (std::max(b1, b2) + 255) & ~(size_t)255;
+  void *ws = nullptr;
+  {
+    const ks_status rc = ensure(ctx, SLOT_TABLE_TMP, 5 * sn + 256 + tmpb, &ws);
+    if (rc != KS_OK) {
+      ks_table_destroy(t);
+      return rc;
+    }
+  }
+  char *W = static_cast<char *>(ws);
+  int32_t *d_keys = reinterpret_cast<int32_t *>(W);
+  uint32_t *d_idx_in = reinterpret_cast<uint32_t *>(W + sn);
+  uint32_t *d_idx = reinterpret_cast<uint32_t *>(W + 2 * sn);
+  int32_t *d_uniq = reinterpret_cast<int32_t *>(W + 3 * sn);
+  int *d_mult = reinterpret_cast<int *>(W + 4 * sn);
+  int *d_nu = reinterpret_cast<int *>(W + 5 * sn);
+  void *d_tmp = W + 5 * sn + 256;
+  if (rank) {
+    hipLaunchKernelGGL(k_iota, dim3(grid), dim3(256), 0, st, d_idx_in, n);
+    KS_TFC(hipGetLastError());
+  }
+  if (rank)
+    KS_TFC(hipcub::DeviceRadixSort::SortPairs(d_tmp, b1, counts_dev, d_keys, d_idx_in, d_idx, (int)n, 0, 32, st));
+  else
+    KS_TFC(hipcub::DeviceRadixSort::SortKeys(d_tmp, b1, counts_dev, d_keys, (int)n, 0, 32, st));
+  KS_TFC(hipcub::DeviceRunLengthEncode::Encode(d_tmp, b2, d_keys, d_uniq, d_mult, d_nu, (int)n, st));
+  int nu = 0;
+  KS_TFC(hipMemcpyAsync(&nu, d_nu, sizeof(int), hipMemcpyDeviceToHost, st));
+  KS_TFC(hipStreamSynchronize(st));
+  std::vector<int32_t> dv(nu);
+  std::vector<int> dm32(nu);
+  KS_TFC(hipMemcpyAsync(dv.data(), d_uniq, (size_t)nu * 4, hipMemcpyDeviceToHost, st));
+  KS_TFC(hipMemcpyAsync(dm32.data(), d_mult, (size_t)nu * 4, hipMemcpyDeviceToHost, st));
+  KS_TFC(hipStreamSynchronize(st));
+  std::vector<int64_t> dm(dm32.begin(), dm32.end());
+  t->distinct = -1;
+  if (rank) {
+    // 2r. ranks: closed-form prefix pieces filled on the device, then s = w - thr
+    double *d_w = w_dev ? w_dev : static_cast<double *>(dalloc(n * 8));
+    if (!d_w) {
+      cleanup();
+      ks_table_destroy(t);
+      return fail(KS_ERR_NOMEM, "ks_table_from_counts: device allocation failed (ranks)");
+    }
+    const std::vector<RankPiece> P = rank_pieces(dv.data(), dm.data(), nu, total);
+    if (!P.empty()) {
+      RankPiece *d_p = static_cast<RankPiece *>(dalloc(P.size() * sizeof(RankPiece)));
+      if (!d_p) {
+        cleanup();
+        ks_table_destroy(t);
+        return fail(KS_ERR_NOMEM, "ks_table_from_counts: device allocation failed (pieces)");
+      }
+      KS_TFC(hipMemcpyAsync(d_p, P.data(), P.size() * sizeof(RankPiece), hipMemcpyHostToDevice, st));
+      const unsigned g = (unsigned)std::min<int64_t>(((n + 15) / 16 + 255) / 256, 8192);
+      hipLaunchKernelGGL(k_rank_fill, dim3(g), dim3(256), 0, st, d_idx, n, d_p, (int64_t)P.size(), d_w);
+      KS_TFC(hipGetLastError());
+    } else {  // wrapped (negative) counts: the host's sequential prefix
+      std::vector<int32_t> hc(n);
+      std::vector<double> hr(n);
+      KS_TFC(hipMemcpyAsync(hc.data(), counts_dev, n * 4, hipMemcpyDeviceToHost, st));
+      KS_TFC(hipStreamSynchronize(st));
+      const ks_status rc = rank_table_host(hc.data(), k, total, hr.data());
+      if (rc != KS_OK) {
+        cleanup();
+        ks_table_destroy(t);
+        return rc;
+      }
+      KS_TFC(hipMemcpyAsync(d_w, hr.data(), n * 8, hipMemcpyHostToDevice, st));
+      KS_TFC(hipStreamSynchronize(st));
+    }
+    KS_TFC(hipMalloc(&t->d_vals, n * sizeof(double)));
+    hipLaunchKernelGGL(k_sub_thr, dim3(grid), dim3(256), 0, st, d_w, thr, t->d_vals, nullptr, n);
+    KS_TFC(hipGetLastError());
+    unsigned long long *d_am = static_cast<unsigned long long *>(dalloc(16)), h_am[2] = {0, 0};
+    if (!d_am) {
+      cleanup();
+      ks_table_destroy(t);
+      return fail(KS_ERR_NOMEM, "ks_table_from_counts: device allocation failed");
+    }
+    KS_TFC(hipMemsetAsync(d_am, 0, 16, st));
+    hipLaunchKernelGGL(k_absmax, dim3(grid), dim3(256), 0, st, t->d_vals, n, d_am);
+    KS_TFC(hipMemcpyAsync(h_am, d_am, 16, hipMemcpyDeviceToHost, st));
+    KS_TFC(hipStreamSynchronize(st));
+    t->no_nan_posinf = h_am[1] == 0;
+    memcpy(&t->max_abs, &h_am[0], 8);
+    t->ms_upload = now_ms() - t_start;
+  } else {
+    // 2s. log2 / +-1 of each distinct count on the host (glibc log2, exactly as
+    // ks_log2_table / ks_pm1_table), s = w - thr, distinct s values by bits
+    std::vector<double> wv(nu), sv(nu);
+    score_of_counts(score == KS_SCORE_LOG2 ? 1 : 2, dv.data(), dm.data(), nu, wv.data());
+    std::vector<uint64_t> sb(nu);
+    double ma = 0.0;
+    bool bad = false;
+    for (int i = 0; i < nu; ++i) {
+      sv[i] = wv[i] - thr;
+      memcpy(&sb[i], &sv[i], 8);
+      if (std::isfinite(sv[i])) ma = std::max(ma, std::fabs(sv[i]));
+      else if (!(sv[i] < 0)) bad = true;
+    }
+    t->no_nan_posinf = !bad;
+    t->max_abs = ma;
+    std::vector<uint64_t> ub(sb);
+    std::sort(ub.begin(), ub.end());
+    ub.erase(std::unique(ub.begin(), ub.end()), ub.end());
+    const int64_t nv = (int64_t)ub.size();
+    t->distinct = nv;
+    t->ms_upload = now_ms() - t_start;
+    const int gm = (int)std::min<int64_t>((n + 1023) / 1024, (int64_t)ctx->num_cus * 8);
+    if ((flags & KS_TABLE_COMPRESS) && nv <= 65536) {
+      std::vector<uint16_t> cmap(nu);
+      for (int i = 0; i < nu; ++i) cmap[i] = (uint16_t)(std::lower_bound(ub.begin(), ub.end(), sb[i]) - ub.begin());
+      uint16_t *d_cmap = static_cast<uint16_t *>(dalloc((size_t)nu * 2 + 16));
+      if (!d_cmap) {
+        cleanup();
+        ks_table_destroy(t);
+        return fail(KS_ERR_NOMEM, "ks_table_from_counts: device allocation failed");
+      }
+      KS_TFC(hipMalloc(&t->d_codes, n * sizeof(uint16_t)));
+      KS_TFC(hipMalloc(&t->d_lut, nv * sizeof(double)));
+      KS_TFC(hipMemcpyAsync(t->d_lut, ub.data(), nv * 8, hipMemcpyHostToDevice, st));
+      KS_TFC(hipMemcpyAsync(d_cmap, cmap.data(), (size_t)nu * 2, hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(k_map_counts<uint16_t>, dim3(gm), dim3(1024), 0, st, counts_dev, n, d_uniq, (int64_t)nu, d_cmap,
+                         t->d_codes);
+      KS_TFC(hipGetLastError());
+      t->compressed = true;
+    } else {
+      double *d_sv = static_cast<double *>(dalloc((size_t)nu * 8 + 16));
+      if (!d_sv) {
+        cleanup();
+        ks_table_destroy(t);
+        return fail(KS_ERR_NOMEM, "ks_table_from_counts: device allocation failed");
+      }
+      KS_TFC(hipMalloc(&t->d_vals, n * sizeof(double)));
+      KS_TFC(hipMemcpyAsync(d_sv, sv.data(), (size_t)nu * 8, hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(k_map_counts<double>, dim3(gm), dim3(1024), 0, st, counts_dev, n, d_uniq, (int64_t)nu, d_sv,
+                         t->d_vals);
+      KS_TFC(hipGetLastError());
+    }
+    if (w_dev) {
+      double *d_wv = static_cast<double *>(dalloc((size_t)nu * 8 + 16));
+      if (!d_wv) {
+        cleanup();
+        ks_table_destroy(t);
+        return fail(KS_ERR_NOMEM, "ks_table_from_counts: device allocation failed");
+      }
+      KS_TFC(hipMemcpyAsync(d_wv, wv.data(), (size_t)nu * 8, hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(k_map_counts<double>, dim3(gm), dim3(1024), 0, st, counts_dev, n, d_uniq, (int64_t)nu, d_wv,
+                         w_dev);
+      KS_TFC(hipGetLastError());
+    }
+  }
+  KS_TFC(hipStreamSynchronize(st));
+#undef KS_TFC
+  cleanup();
+  t->ms_compress = now_ms() - t_start - t->ms_upload;
+  if (flags & KS_TABLE_EXPAND) {
+    const size_t cap = max_ext_bytes > 0 ? (size_t)max_ext_bytes : (size_t)160 << 30;
+    const ks_status rc = table_expand(ctx, t, cap, counts_dev);
+    if (rc != KS_OK) {
+      ks_table_destroy(t);
+      return rc;
+    }
   }
   t->ms_total = now_ms() - t_start;
   *out = t;
@@ -454,10 +813,19 @@ extern "C" void ks_table_destroy(ks_table *t) {
   if (t->d_vals) (void)hipFree(t->d_vals);
   if (t->d_codes) (void)hipFree(t->d_codes);
   if (t->d_lut) (void)hipFree(t->d_lut);
-  if (t->d_ext) (void)hipFree(t->d_ext);
+  if (t->d_ext) pool_give(t->device, t->d_ext, t->ext_cap);
   if (t->d_map12) (void)hipFree(t->d_map12);
   if (t->d_lut12) (void)hipFree(t->d_lut12);
   delete t;
+}
+
+extern "C" void ks_release_cache(void) {
+  if (!hip_usable_here()) return;
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  for (PoolBuf &b : g_pool) {
+    if (b.p) (void)hipFree(b.p);
+    b = PoolBuf();
+  }
 }
 
 extern "C" int32_t ks_table_is_compressed(const ks_table *t) { return t && t->compressed ? 1 : 0; }

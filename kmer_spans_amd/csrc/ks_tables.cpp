@@ -76,20 +76,40 @@ ks_status rank_table_host(const int32_t *counts, int k, double total, double *ra
     });
     std::vector<double> rs(n);
     std::vector<uint64_t> start(span);
+    std::vector<int32_t> dv;
+    std::vector<int64_t> dm;
     uint64_t pos = 0;
-    double r = 0.0, d_prev = 0.0;
-    bool first = true;
     for (uint64_t v = 0; v < span; ++v) {
       uint64_t hv = 0;
       for (int t = 0; t < nt; ++t) hv += th[t][v];
       start[v] = pos;
       if (!hv) continue;
-      const double d = (double)((int64_t)cmin + (int64_t)v) / total;
-      for (uint64_t j = 0; j < hv; ++j) {
-        if (first) { r = 0.0; first = false; }  // r[idx[0]] = 0 (quirk Q3)
-        else r = r + d_prev;
-        rs[pos++] = r;
-        d_prev = d;
+      dv.push_back((int32_t)((int64_t)cmin + (int64_t)v));
+      dm.push_back((int64_t)hv);
+      pos += hv;
+    }
+    const std::vector<RankPiece> pcs = rank_pieces(dv.data(), dm.data(), (int64_t)dv.size(), total);
+    if (!pcs.empty()) {  // closed-form pieces, positions filled in parallel
+      parallel_for(n, [&](size_t a, size_t b) {
+        size_t q = (size_t)(std::upper_bound(pcs.begin(), pcs.end(), (int64_t)a,
+                                             [](int64_t j, const RankPiece &p) { return j < p.j0; }) -
+                            pcs.begin()) - 1;
+        for (size_t j = a; j < b; ++j) {
+          while (q + 1 < pcs.size() && pcs[q + 1].j0 <= (int64_t)j) ++q;
+          rs[j] = rank_piece_value(pcs[q], (int64_t)j);
+        }
+      });
+    } else {  // negative (wrapped) counts: the sequential prefix
+      double r = 0.0, d_prev = 0.0;
+      size_t j = 0;
+      for (size_t v = 0; v < dv.size(); ++v) {
+        const double d = (double)dv[v] / total;
+        for (int64_t t = 0; t < dm[v]; ++t) {
+          if (j == 0) r = 0.0;  // r[idx[0]] = 0 (quirk Q3)
+          else r = r + d_prev;
+          rs[j++] = r;
+          d_prev = d;
+        }
       }
     }
     // per-thread cursors: start[v] + elements with count v in earlier threads
@@ -129,6 +149,73 @@ ks_status rank_table_host(const int32_t *counts, int k, double total, double *ra
   ranks[idx[0]] = 0.0;
   for (size_t i = 1; i < n; ++i) ranks[idx[i]] = ranks[idx[i - 1]] + ((double)counts[idx[i - 1]] / total);
   return KS_OK;
+}
+
+std::vector<RankPiece> rank_pieces(const int32_t *vals, const int64_t *mult, int64_t nu, double total) {
+  std::vector<RankPiece> P;
+  for (int64_t v = 0; v < nu; ++v)
+    if (vals[v] < 0) return P;
+  auto bits = [](double x) { int64_t i; memcpy(&i, &x, 8); return i; };
+  const int64_t M52 = (int64_t)1 << 52, M53 = (int64_t)1 << 53;
+  int64_t j = 0;
+  double R = 0.0;  // R_0 = 0: r[idx[0]] of the zeroed allocation (quirk Q3)
+  for (int64_t v = 0; v < nu; ++v) {
+    const double d = (double)vals[v] / total;
+    int64_t rem = mult[v];
+    while (rem > 0) {
+      const double R1 = R + d;
+      if (bits(R1) == bits(R)) {  // R absorbs d (d = 0, NaN R, ...): constant to the end of the run
+        P.push_back({j, R, 0, 0, 0, 0});
+        j += rem;
+        break;
+      }
+      bool closed = false;
+      if (std::isnormal(R) && R > 0 && std::isfinite(d) && d > 0) {
+        const int e = std::ilogb(R);
+        const int64_t m = (bits(R) & (M52 - 1)) | M52;
+        const double y = std::ldexp(d, 52 - e);  // exact
+        if (y < 2251799813685248.0) {            // 2^51
+          const double q = std::floor(y), f = y - q;
+          const int64_t qi = (int64_t)q;
+          int64_t inc1, inc;
+          if (f > 0.5) inc1 = inc = qi + 1;
+          else if (f < 0.5) inc1 = inc = qi;
+          else {  // exact half: the first step rounds to an even m, every later step adds the even increment
+            inc1 = ((m + qi) & 1) ? qi + 1 : qi;
+            inc = (qi & 1) ? qi + 1 : qi;
+          }
+          const int64_t m1 = m + inc1;
+          if (m1 <= M53 - 1) {
+            const int64_t T = inc > 0 ? 1 + (M53 - 1 - m1) / inc : INT64_MAX;  // steps inside the binade
+            P.push_back({j, R, inc1, inc, e, 1});
+            if (T >= rem) {
+              const int64_t mt = m + inc1 + (rem - 1) * inc;
+              int64_t b = ((int64_t)(e + 1023) << 52) | (mt - M52);
+              memcpy(&R, &b, 8);
+              j += rem;
+              rem = 0;
+            } else {  // T + 1 positions in this binade, then the crossing step in FP64
+              const int64_t mt = m + inc1 + (T - 1) * inc;
+              int64_t b = ((int64_t)(e + 1023) << 52) | (mt - M52);
+              double Rt;
+              memcpy(&Rt, &b, 8);
+              R = Rt + d;
+              j += T + 1;
+              rem -= T + 1;
+            }
+            closed = true;
+          }
+        }
+      }
+      if (!closed) {  // one position, one FP64 step
+        P.push_back({j, R, 0, 0, 0, 0});
+        R = R1;
+        j += 1;
+        rem -= 1;
+      }
+    }
+  }
+  return P;
 }
 
 namespace {
@@ -209,11 +296,18 @@ void map_counts(const int32_t *counts, size_t n, double *w, G g) {
 
 }  // namespace
 
+// The per-count scores of README.md:27-42 (f = c / total, f_med = R median).
+static double log2_score(int32_t c, double total, double fmed) { return std::log2(((double)c / total) / fmed); }
+static double pm1_score(int32_t c, double total, double fmed) {
+  const double f = (double)c / total;
+  return (std::isnan(f) || std::isnan(fmed)) ? std::nan("") : (f >= fmed ? 1.0 : -1.0);
+}
+
 ks_status log2_table_host(const int32_t *counts, int k, double *w) {
   const size_t n = (size_t)1 << (2 * k);
   double total = 0;
   const double fmed = median_freq(counts, n, &total);
-  map_counts(counts, n, w, [&](int32_t c) { return std::log2(((double)c / total) / fmed); });
+  map_counts(counts, n, w, [&](int32_t c) { return log2_score(c, total, fmed); });
   return KS_OK;
 }
 
@@ -221,11 +315,31 @@ ks_status pm1_table_host(const int32_t *counts, int k, double *w) {
   const size_t n = (size_t)1 << (2 * k);
   double total = 0;
   const double fmed = median_freq(counts, n, &total);
-  map_counts(counts, n, w, [&](int32_t c) {
-    const double f = (double)c / total;
-    return (std::isnan(f) || std::isnan(fmed)) ? std::nan("") : (f >= fmed ? 1.0 : -1.0);
-  });
+  map_counts(counts, n, w, [&](int32_t c) { return pm1_score(c, total, fmed); });
   return KS_OK;
+}
+
+void score_of_counts(int score, const int32_t *vals, const int64_t *mult, int64_t nu, double *w) {
+  int64_t sum = 0, n = 0;
+  for (int64_t v = 0; v < nu; ++v) {
+    sum += (int64_t)vals[v] * mult[v];
+    n += mult[v];
+  }
+  const double total = (double)sum;
+  double fmed = std::nan("");  // f all NaN -> median NA
+  if (sum != 0 && n >= 2) {
+    auto kth = [&](int64_t r) {  // order statistic r (0-based) of the counts
+      int64_t acc = 0;
+      for (int64_t v = 0; v < nu; ++v) {
+        acc += mult[v];
+        if (acc > r) return vals[v];
+      }
+      return vals[nu - 1];
+    };
+    fmed = r_mean2((double)kth(n / 2 - 1) / total, (double)kth(n / 2) / total);
+  }
+  for (int64_t v = 0; v < nu; ++v)
+    w[v] = score == 1 ? log2_score(vals[v], total, fmed) : pm1_score(vals[v], total, fmed);
 }
 
 }  // namespace ks

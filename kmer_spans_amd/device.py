@@ -95,6 +95,28 @@ class DeviceTable:
                                           C.c_void_p(freq.data_ptr()) if freq is not None else None,
                                           C.byref(self._h)))
 
+    @classmethod
+    def from_counts(cls, ctx: _lib.Context, counts: torch.Tensor, k: int, score: str, total: float = 0.0,
+                    thr: float = 0.0, compress: bool = True, expand: bool = False, max_ext_bytes: int = 0,
+                    w_out: torch.Tensor | None = None) -> "DeviceTable":
+        """ks_table_from_counts: the log2 / pm1 / rank table of device counts
+        (int32[4^k] cuda) built on the device; w_out (float64[4^k] cuda, optional)
+        receives w.  total: the word count (rank only)."""
+        if counts.dtype != torch.int32 or counts.numel() != 4 ** k or not counts.is_cuda:
+            raise _lib.KmerSpansError("counts must be an int32 cuda tensor of 4^k counts")
+        if w_out is not None and (w_out.dtype != torch.float64 or w_out.numel() != 4 ** k or not w_out.is_cuda):
+            raise _lib.KmerSpansError("w_out must be a float64 cuda tensor of 4^k values")
+        self = cls.__new__(cls)
+        self.k = k
+        self._h = C.c_void_p()
+        flags = (1 if compress else 0) | (2 if expand else 0)
+        _order(ctx)
+        check(load().ks_table_from_counts(ctx.handle, C.c_void_p(counts.data_ptr()), int(k), _lib.SCORES[score],
+                                          float(total), float(thr), flags, int(max_ext_bytes),
+                                          C.c_void_p(w_out.data_ptr()) if w_out is not None else None,
+                                          C.byref(self._h)))
+        return self
+
     def info(self) -> dict:
         """ks_table_get_info: shape and setup cost (ms) of the table."""
         inf = _lib.TableInfo()

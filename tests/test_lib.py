@@ -104,3 +104,28 @@ def test_kmer_seq_matches_oracle(oracle):
     import kmer_spans_amd as K
     for k in (1, 2, 5):
         assert K.kmer_seq(k) == oracle.kmer_seq(k)
+
+
+@pytest.mark.parametrize("case", ["huge_sum_ties", "dyadic", "skewed"])
+def test_rank_table_closed_form(oracle, case):
+    """The closed-form weighted-rank prefix (ks_internal.h RankPiece: runs of
+    equal counts as integer progressions inside a binade, FP64 steps at the
+    binade crossings) equals the sequential prefix bit for bit, including
+    exact-half ties (odd counts added to a sum beyond 2^53) and long runs."""
+    import kmer_spans_amd as K
+    rng = np.random.default_rng({"huge_sum_ties": 1, "dyadic": 2, "skewed": 3}[case])
+    if case == "huge_sum_ties":
+        k = 12
+        c = ((1 << 30) + 2 * rng.integers(0, 1000, 4 ** k) + 1).astype(np.int32)  # odd, sum > 2^53
+        total = 1.0
+    elif case == "dyadic":
+        k = 10
+        c = rng.integers(0, 40, 4 ** k).astype(np.int32)
+        total = 2.0 ** -3  # d = 8c: exact steps, sums far past 2^53 ulp boundaries of small R
+    else:
+        k = 11
+        c = np.minimum(rng.geometric(0.02, 4 ** k), 1 << 20).astype(np.int32)
+        c[rng.integers(0, 4 ** k, 4 ** k // 4)] = 0
+        total = float(c.astype(np.int64).sum())
+    got, want = K.rank_table(c, k, total), oracle.rank_table(c, k, total)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))

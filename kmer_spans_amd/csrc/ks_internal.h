@@ -121,6 +121,11 @@ struct ks_table {
   uint16_t *d_map12 = nullptr;  // [4096]
   double *d_lut12 = nullptr;    // [4096]
   double escape_frac = 0.0;     // estimated share of positions that escape
+  // Approximate value per (approx_k)-base prefix of the k-mer (fp16 bits):
+  // the position-weighted mean of s over the k-mers sharing the prefix.  Only
+  // predicts which binade the exact carry will be in (k_predict); never a result.
+  uint16_t *d_approx = nullptr;
+  int approx_k = 0;
 };
 
 namespace ks {

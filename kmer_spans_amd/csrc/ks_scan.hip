@@ -328,7 +328,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
   }
 
   TableView tv{t->d_vals,  t->d_codes,   t->d_lut,     t->compressed ? 1 : 0, t->d_ext,
-               t->ext_J, (int)t->distinct, t->ext_bits, t->d_lut12, t->d_map12};
+               t->ext_J, (int)t->distinct, t->ext_bits, t->d_lut12, t->d_map12, t->d_approx, t->approx_k};
   const uint64_t mw = (uint64_t)(int64_t)min_width;
   int algo = ctx->scan_algo;
   if (algo < 0) algo = (longest > (1 << 15)) ? 1 : 0;

@@ -28,6 +28,7 @@
 //     excursion before its first clamp (replay, or the summary).
 //  P5 stitch per run: excursions from heads, tails and candidates; emit
 //     regions + rescan ranges; rescans run on the lane kernel.
+#include <hip/hip_fp16.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -70,6 +71,12 @@ struct Summ {  // binade-integer summaries for the predicted binade (P2)
   long long *D, *M, *N;   // [2 * nch] by entry parity
   int32_t *A;             // [2 * nch]
 };
+
+struct SummP1 {  // binade summaries computed by pass 1 for the predicted binade (single trajectory)
+  int32_t *e;             // [2 * nch] binade, INT32_MIN: none (no prediction, a tie, out of range)
+  long long *D, *M, *N;   // [2 * nch] total, max, lower bound of the min (units 2^(e-52))
+  int32_t *A;             // [2 * nch] first argmax
+};                        // slot 2c: the predicted binade, 2c + 1: its neighbour near an edge
 
 struct Carry {  // P3/P4
   double *x;      // exact entry value
@@ -146,6 +153,17 @@ __device__ __forceinline__ Emission decide(const EmitCfg &ec, int64_t f, int64_t
   return e;
 }
 
+// Bits of a positive normal double in binade e: x = m * 2^(e-52), m in [2^52, 2^53).
+__device__ __forceinline__ int binade_of(double x) {
+  return (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
+}
+__device__ __forceinline__ long long mant_of(double x) {
+  return (__double_as_longlong(x) & ((1LL << 52) - 1)) | (1LL << 52);
+}
+__device__ __forceinline__ double from_mant(long long m, int e) {
+  return __longlong_as_double(((long long)(e + 1023) << 52) | (m - (1LL << 52)));
+}
+
 __device__ __forceinline__ uint32_t roll(uint32_t c, uint8_t b, uint32_t mask) {
   return ((c << 2) | enc(b)) & mask;
 }
@@ -197,6 +215,40 @@ __device__ __forceinline__ void values16_nostore(const Chunks &g, const uint8_t 
   const uint32_t kmask = (1u << (2 * k)) - 1u;
   uint64_t x = 0;
   const bool pk = packed_bits(g.packed, total, p, x);
+  if (pk && tv.ext && tv.ext_J >= 2 && k + tv.ext_J - 1 + 15 <= 32) {
+    // one expanded-table read per J indices (the gathers of k_summ_fix and
+    // the heads: 4 random requests per 16 indices at J = 5 instead of 32)
+    const int J = tv.ext_J, kx = k + J - 1;
+    const uint64_t xmask = (kx >= 32) ? ~0ull : ((1ull << (2 * kx)) - 1ull);
+    const bool c12 = tv.ext_bits == 12;
+    for (int o = 0; o < 16; o += J) {
+      if (b0 + o >= n) {
+        for (int t = o; t < 16; ++t) v[t] = 0.0;
+        break;
+      }
+      const uint64_t gx = (x >> (64 - 2 * (o + kx))) & xmask;
+      uint64_t e;
+      if (J <= 2) e = reinterpret_cast<const uint32_t *>(tv.ext)[gx];
+      else e = reinterpret_cast<const uint64_t *>(tv.ext)[gx];
+      for (int t = 0; t < J && o + t < 16; ++t) {
+        const int j = o + t;
+        double val = 0.0;
+        if (b0 + j < n) {
+          uint32_t q;
+          if (c12) {
+            const uint32_t q12 = (uint32_t)(e >> (12 * t)) & 0xfffu;
+            q = q12 != 0xfffu ? (uint32_t)tv.map12[q12]
+                              : (uint32_t)tv.codes[(uint32_t)(x >> (64 - 2 * (j + k))) & kmask];
+          } else {
+            q = (uint32_t)(e >> (16 * t)) & 0xffffu;
+          }
+          val = s_lut ? s_lut[q] : tv.lut[q];
+        }
+        v[j] = val;
+      }
+    }
+    return;
+  }
   uint32_t code = pk ? 0u : prime_code(seq, p, k);
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
@@ -224,7 +276,7 @@ __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restri
     return;
   }
   const int64_t p = g.start[c] + i0;
-  if (tv.ext && tv.ext_J == 4) {  // FP64 expanded table: the 4 values in one 32-B entry
+  if (!tv.compressed && tv.ext && tv.ext_J == 4) {  // FP64 expanded table: the 4 values in one 32-B entry
     uint64_t xp = 0;
     const uint64_t gcode = packed_bits(g.packed, total, p - k, xp) ? (xp >> (64 - 2 * (k + 3)))
                                                                     : prime_code_guarded64(seq, p - k, k + 3, total);
@@ -267,6 +319,18 @@ constexpr int kP1G = KS_P1_G;
 #define KS_P1_BLOCK (KS_P1_G > 4 ? 768 : 1024)
 #endif
 constexpr int kP1Block = KS_P1_BLOCK;  // lanes per pass-1 block (build parameter for A/B runs)
+// Pass-1 summaries start at predicted entries of 1024 (below, exact halves
+// make most chunks' single-trajectory summaries void; k_summ_fix does those).
+constexpr double kP1SumMin = 1024.0;
+// Table reads per batch of the summarising pass 1 (no code store, so no
+// 4-codes-per-word constraint): 3 leaves registers for two summaries.
+#ifndef KS_P1_GSUMM
+#define KS_P1_GSUMM 3
+#endif
+constexpr int kP1GSumm = KS_P1_GSUMM;
+// A predicted entry within this relative distance of a binade edge is
+// summarised in the neighbouring binade too.
+constexpr double kP1Margin = 0.125;
 #ifdef KS_P1_NOSTORE  // diagnostic build: no code store in k_pass1p, later passes gather (slow, exact)
 constexpr bool kP1NoStore = true;
 #else
@@ -303,6 +367,54 @@ __global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__r
   g.start[c] = first;
   g.n[c] = (int32_t)min((int64_t)CH, last - first + 1);
   g.run[c] = (int32_t)lo;
+}
+
+// P0 binade predictor (pass-1 summaries): the approximate sum and clean
+// exit of every chunk from the fp16 prefix means of the table (ks_table::
+// d_approx, <= 128 KiB in LDS, one block per CU), rolled from the packed
+// bases; a max-plus scan of them (k_approx_scan) predicts each chunk's entry,
+// i.e. the binade pass 1 summarises in.  Only a prediction: a wrong binade
+// costs one gathered summary (k_summ_fix), never a result.
+__global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k, const uint16_t *__restrict__ approx, int kp,
+                                                  double *__restrict__ pa, double *__restrict__ pb) {
+  __shared__ __half s_ap[1 << 16];
+  const int np = 1 << (2 * kp);
+  for (int i = threadIdx.x; i < np; i += blockDim.x) s_ap[i] = __ushort_as_half(approx[i]);
+  __syncthreads();
+  const uint32_t pmask = (uint32_t)np - 1u;
+  const uint32_t *__restrict__ packed = g.packed;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < g.nch;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t start = g.start[c];
+    const int n = g.n[c];
+    const int64_t q0 = start - k;  // index i's k-mer prefix: bases [q0 + i, q0 + i + kp)
+    // 16 indices per batch: their kp-base prefixes from one 64-bit window of
+    // packed bases (three words, loaded one batch ahead); every lane loads at
+    // the same iterations, so no wave waits on another lane's word
+    const int64_t last = total >> 4;
+    auto load3 = [&](int64_t q) {
+      const int64_t w = q >> 4;
+      return make_uint3(packed[min(w, last)], packed[min(w + 1, last)], packed[min(w + 2, last)]);
+    };
+    uint3 cur = load3(q0);
+    float tsum = 0.f, tex = 0.f;
+    for (int b0 = 0; b0 < n; b0 += 16) {
+      const uint3 nxt = load3(q0 + b0 + 16);
+      const uint32_t bp = 2u * (uint32_t)((q0 + b0) & 15);
+      const uint64_t x = ((((uint64_t)cur.x << 32) | cur.y) << bp) | (((uint64_t)cur.z << bp) >> 32);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (b0 + j < n) {
+          const float a = __half2float(s_ap[(uint32_t)(x >> (64 - 2 * (j + kp))) & pmask]);
+          tsum += a;
+          tex = fmaxf(tex + a, 0.f);
+        }
+      }
+      cur = nxt;
+    }
+    pa[c] = tsum;
+    pb[c] = tex;
+  }
 }
 
 // ------------------------------------------------------------------- P1
@@ -423,7 +535,7 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
         if (!k12) v[j] = kLds ? s_lut[q[j]] : tv.lut[q[j]];
 #pragma unroll
       for (int r4 = 0; r4 < PB / 4; ++r4) {
-        if (b0 + 4 * r4 < CH) {
+        if (codes && b0 + 4 * r4 < CH) {
           uint2 w;
           w.x = q[4 * r4 + 0] | ((uint32_t)q[4 * r4 + 1] << 16);
           w.y = q[4 * r4 + 2] | ((uint32_t)q[4 * r4 + 3] << 16);
@@ -488,14 +600,15 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
 // so the wait counts stay static, and the rare paths that do load (a third
 // escape in one batch, the candidate append) drain explicitly inside the
 // branch.  Results are identical to k_pass1.
-template <int J, bool kLds, bool kTrlr>
+template <int J, bool kLds, bool kTrlr, bool kSumm>
 __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
                                                  TableView tv, uint16_t *__restrict__ codes, EmitCfg ec,
                                                  uint32_t *__restrict__ visits, P1 o, Cand cand,
-                                                 const uint32_t *__restrict__ packed) {
-  constexpr int G = kP1G;               // table reads per batch
+                                                 const uint32_t *__restrict__ packed, const double *__restrict__ xh,
+                                                 SummP1 sp) {
+  constexpr int G = kSumm ? kP1GSumm : kP1G;  // table reads per batch
   constexpr int BS = kP1Block;          // lanes per block (LDS staging stride)
-  static_assert((G * J) % 4 == 0, "the code store writes 4 codes per 8-B word");
+  static_assert(kSumm || (G * J) % 4 == 0, "the code store writes 4 codes per 8-B word");
   constexpr int PB = G * J;             // scan indices per batch (8, 12, 16, 20)
   constexpr bool k12 = (J == 5);        // 12-bit codes with escapes
   using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;
@@ -529,7 +642,10 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
   // tr_lr: the run's first scan index scores the first k-mer's own score
   const double first_val = (kTrlr && first) ? ec.ks[(uint32_t)(gcode >> (2 * (J - 1))) & kmask] : 0.0;
   // tail lanes (reads could pass the end of the buffer) are left to k_pass1
-  if (start + n + kP1TailMargin > total) return;
+  if (start + n + kP1TailMargin > total) {
+    if (kSumm) sp.e[2 * c] = sp.e[2 * c + 1] = INT32_MIN;  // no pass-1 summary (the workspace is reused)
+    return;
+  }
   // Batch m rolls the 2-bit codes of bases [q0 + m*PB, q0 + m*PB + PB) in:
   // three packed words from word (q0 + m*PB) >> 4 (one load, 96 bits >= the
   // 2*PB <= 40 bits at any offset), so a lane touches one or two 128-B lines
@@ -599,6 +715,35 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
   int beg = -1, arg = 0;
   double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
   bool special = false;
+  // kSumm: the binade-integer summary of this chunk for the binade of its
+  // predicted entry xh (k_predict), single trajectory: s rounded to the binade's
+  // ulp u = 2^(e-52) as (s + C) - C with C = 1.5 * 2^e, exact partial sums while
+  // they stay within (-2^e, 2^e); an exact half (tie: the increment would depend
+  // on the parity of the entry) or |s| >= 2^(e-1) voids it (k_summ_fix then
+  // recomputes it).  Replaces the per-position code store and k_summaries.
+  // (|s| < 2^(e-1) is checked once through sabs, and the minimum through the
+  // FP64 prefix minimum: N is stored as a lower bound, which keeps the carry's
+  // validity test conservative; both save registers in this 128-VGPR kernel.)
+  int se = INT32_MIN, se2 = INT32_MIN;
+  double sC = 0.0, sH = 0.0, scur = 0.0, smx = -INFINITY;
+  double sC2 = 0.0, sH2 = 0.0, scur2 = 0.0, smx2 = -INFINITY;
+  int sarg = 0, sarg2 = 0;
+  bool sbad = false, sbad2 = false;
+  if (kSumm) {
+    const double x = xh[c];
+    if (x >= kP1SumMin && x < 1.0e15) {
+      se = binade_of(x);
+      sC = 1.5 * ldexp(1.0, se);
+      sH = ldexp(1.0, se - 53);
+      const double lo = ldexp(1.0, se);
+      if (x < lo * (1.0 + kP1Margin)) se2 = se - 1;
+      else if (x > 2.0 * lo * (1.0 - kP1Margin)) se2 = se + 1;
+      if (se2 != INT32_MIN) {
+        sC2 = 1.5 * ldexp(1.0, se2);
+        sH2 = ldexp(1.0, se2 - 53);
+      }
+    }
+  }
   for (int b0 = 0; b0 < n; b0 += PB) {
     // 1. escape reads of batch b first: the first two escaped slots of the
     //    batch (a third one, ~6e-5 of lane-batches, loads inline)
@@ -680,8 +825,10 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
           qq = (uint32_t)(e[gi] >> (16 * t)) & 0xffffu;
           s = kLds ? s_lut[qq] : tv.lut[qq];
         }
-        if (j & 1) cw[j >> 1] |= qq << 16;
-        else cw[j >> 1] = qq;
+        if (!kSumm) {
+          if (j & 1) cw[j >> 1] |= qq << 16;
+          else cw[j >> 1] = qq;
+        }
         if (kTrlr && first && b0 == 0 && j == 0) s = first_val;
         const int i = b0 + j;
         if (i < n) {
@@ -693,6 +840,22 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
           pmax = asum > pmax ? asum : pmax;
           sabs += fabs(s);
           special |= !isfinite(s);
+          if (kSumm && se != INT32_MIN) {
+            const double r = (s + sC) - sC;
+            sbad |= fabs(r - s) == sH;
+            scur += r;
+            const bool su = scur > smx;
+            smx = su ? scur : smx;
+            sarg = su ? i : sarg;
+            if (se2 != INT32_MIN) {
+              const double r2 = (s + sC2) - sC2;
+              sbad2 |= fabs(r2 - s) == sH2;
+              scur2 += r2;
+              const bool su2 = scur2 > smx2;
+              smx2 = su2 ? scur2 : smx2;
+              sarg2 = su2 ? i : sarg2;
+            }
+          }
           // clean trajectory, branch-free except for the rare candidate:
           // open (0 -> S > 0) starts an excursion, close (> 0 -> 0) ends it,
           // the first strict maximum is kept (S > best is false at a close
@@ -731,7 +894,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
     }
 #pragma unroll
     for (int r4 = 0; r4 < PB / 4; ++r4)
-      if (b0 + 4 * r4 < CH && !kP1NoStore)
+      if (b0 + 4 * r4 < CH && !kP1NoStore && !kSumm)
 #ifndef KS_P1_PLAIN_CODES  // nontemporal code stores: A/B 16.19-16.21 vs 16.31-16.57 ms
         __builtin_nontemporal_store((uint64_t)cw[2 * r4] | ((uint64_t)cw[2 * r4 + 1] << 32),
                                     reinterpret_cast<uint64_t *>(codes + code_slot(c, b0 + 4 * r4)));
@@ -743,6 +906,27 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
       gc[gi] = gn[gi];
       e[gi] = en[gi];
     }
+  }
+  if (kSumm) {
+    // valid if no tie, every |s| < 2^(e-1) (so (s + C) - C rounds s to the ulp
+    // 2^(e-52)) and every partial sum inside (-2^e, 2^e) (all exact).  N is a
+    // lower bound of the integer trajectory's minimum: each rounded step is
+    // within u/2 of s (<= 128 u over the chunk), the FP64 prefix sums within
+    // 256 * 2^-53 * sabs of the exact ones.
+    auto put = [&](int t, int e, bool bad, double cur, double mx, int a) {
+      const double lim = ldexp(1.0, e);
+      const bool ok = e != INT32_MIN && !bad && sabs < 0.5 * lim && mx < 0.5 * lim && pmin > -0.5 * lim;
+      sp.e[2 * c + t] = ok ? e : INT32_MIN;
+      if (ok) {
+        const double sc = ldexp(1.0, 52 - e);
+        sp.D[2 * c + t] = (long long)(cur * sc);
+        sp.M[2 * c + t] = (long long)(mx * sc);
+        sp.N[2 * c + t] = (long long)floor((pmin - sabs * 0x1p-44) * sc) - 130;
+        sp.A[2 * c + t] = a;
+      }
+    };
+    put(0, se, sbad, scur, smx, sarg);
+    put(1, se2, sbad2, scur2, smx2, sarg2);
   }
   o.cexit[c] = prev;
   o.asum[c] = asum;
@@ -766,7 +950,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
 // outputs as k_pass1.
 constexpr int kLdsTableK = 7;
 template <bool kTrlr>
-__global__ void __launch_bounds__(1024) k_pass1_lds(Chunks g, int k, TableView tv, EmitCfg ec,
+__global__ void __launch_bounds__(1024) k_pass1_lds(Chunks g, int64_t total, int k, TableView tv, EmitCfg ec,
                                                     uint32_t *__restrict__ visits, P1 o, Cand cand) {
   __shared__ double s_val[1 << (2 * kLdsTableK)];
   const int nk = 1 << (2 * k);
@@ -779,56 +963,61 @@ __global__ void __launch_bounds__(1024) k_pass1_lds(Chunks g, int k, TableView t
     const int64_t start = g.start[c];
     const int n = g.n[c];
     const bool first = c == 0 || g.run[c - 1] != g.run[c];
-    int64_t wi = (start - k) >> 4;
-    uint32_t w = packed[wi];
-    auto base = [&](int64_t q) -> uint32_t {
-      if ((q >> 4) != wi) {
-        wi = q >> 4;
-        w = packed[wi];
-      }
-      return (w >> (30 - 2 * (int)(q & 15))) & 3u;
+    // 16 indices per batch: their k-mers from one 64-bit window of packed
+    // bases (three words, loaded one batch ahead, uniform across the wave)
+    const int64_t q0 = start - k, last = total >> 4;
+    auto load3 = [&](int64_t q) {
+      const int64_t w = q >> 4;
+      return make_uint3(packed[min(w, last)], packed[min(w + 1, last)], packed[min(w + 2, last)]);
     };
-    uint32_t code = 0;  // k-mer ending at start - 1 (scan index 0)
-    for (int j = 0; j < k; ++j) code = (code << 2) | base(start - k + j);
+    uint3 cur = load3(q0);
     double prev = 0.0, best = 0.0;
     int beg = -1, arg = 0;
     double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
     bool special = false;
-    for (int i = 0; i < n; ++i) {
-      double s = s_val[code];
-      if (kTrlr && first && i == 0) s = ec.ks[code];  // tr_lr: the run's first k-mer's own score
-      if (visits) atomicAdd(&visits[code], 1u);
-      asum += s;
-      pmin = asum < pmin ? asum : pmin;
-      pmax = asum > pmax ? asum : pmax;
-      sabs += fabs(s);
-      special |= !isfinite(s);
-      const double tt = prev + s;
-      const double S = tt > 0 ? tt : 0.0;
-      const bool open = (prev == 0) & (S > 0);
-      const bool close = (prev > 0) & (S == 0);
-      const int f0 = first ? 0 : -1;
-      const long long ml = kTrlr ? ec.min_len : 0;
-      const bool want =
-          kTrlr ? (close & (((long long)((arg != f0 ? arg - 1 : arg) - (beg != f0 ? beg - 1 : beg)) >= ml) |
-                            ((long long)((i != f0 ? i - 1 : i) - (arg != f0 ? arg - 1 : arg) - 1) >=
-                             (ml > 1 ? ml : 1LL))))
-                : (close & ((uint64_t)(int64_t)(arg - beg) >= ec.mw) & (best >= ec.min_score));
-      if (want) {
-        const int64_t slot = append_one(cand.count, cand.segcap);
-        if (slot >= 0) {
-          cand.beg[slot] = start + beg;
-          cand.arg[slot] = start + arg;
-          cand.rst[slot] = start + i;
-          cand.best[slot] = best;
+    for (int b0 = 0; b0 < n; b0 += 16) {
+      const uint3 nxt = load3(q0 + b0 + 16);
+      const uint32_t bp = 2u * (uint32_t)((q0 + b0) & 15);
+      const uint64_t x = ((((uint64_t)cur.x << 32) | cur.y) << bp) | (((uint64_t)cur.z << bp) >> 32);
+      for (int j = 0; j < 16; ++j) {
+        const int i = b0 + j;
+        if (i >= n) break;
+        const uint32_t code = (uint32_t)(x >> (64 - 2 * (j + k))) & kmask;  // k-mer ending at start + i - 1
+        double s = s_val[code];
+        if (kTrlr && first && i == 0) s = ec.ks[code];  // tr_lr: the run's first k-mer's own score
+        if (visits) atomicAdd(&visits[code], 1u);
+        asum += s;
+        pmin = asum < pmin ? asum : pmin;
+        pmax = asum > pmax ? asum : pmax;
+        sabs += fabs(s);
+        special |= !isfinite(s);
+        const double tt = prev + s;
+        const double S = tt > 0 ? tt : 0.0;
+        const bool open = (prev == 0) & (S > 0);
+        const bool close = (prev > 0) & (S == 0);
+        const int f0 = first ? 0 : -1;
+        const long long ml = kTrlr ? ec.min_len : 0;
+        const bool want =
+            kTrlr ? (close & (((long long)((arg != f0 ? arg - 1 : arg) - (beg != f0 ? beg - 1 : beg)) >= ml) |
+                              ((long long)((i != f0 ? i - 1 : i) - (arg != f0 ? arg - 1 : arg) - 1) >=
+                               (ml > 1 ? ml : 1LL))))
+                  : (close & ((uint64_t)(int64_t)(arg - beg) >= ec.mw) & (best >= ec.min_score));
+        if (want) {
+          const int64_t slot = append_one(cand.count, cand.segcap);
+          if (slot >= 0) {
+            cand.beg[slot] = start + beg;
+            cand.arg[slot] = start + arg;
+            cand.rst[slot] = start + i;
+            cand.best[slot] = best;
+          }
         }
+        const bool up = open | (S > best);
+        best = up ? S : best;
+        arg = up ? i : arg;
+        beg = open ? i : (close ? -1 : beg);
+        prev = S;
       }
-      const bool up = open | (S > best);
-      best = up ? S : best;
-      arg = up ? i : arg;
-      beg = open ? i : (close ? -1 : beg);
-      prev = S;
-      if (i + 1 < n) code = ((code << 2) | base(start + i)) & kmask;  // k-mer ending at start + i
+      cur = nxt;
     }
     o.cexit[c] = prev;
     o.asum[c] = asum;
@@ -975,17 +1164,6 @@ __global__ void __launch_bounds__(1024) k_pass1pf(Chunks g, const uint8_t *__res
 }
 
 // ------------------------------------------------------------------- P3
-
-// Bits of a positive normal double in binade e: x = m * 2^(e-52), m in [2^52, 2^53).
-__device__ __forceinline__ int binade_of(double x) {
-  return (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
-}
-__device__ __forceinline__ long long mant_of(double x) {
-  return (__double_as_longlong(x) & ((1LL << 52) - 1)) | (1LL << 52);
-}
-__device__ __forceinline__ double from_mant(long long m, int e) {
-  return __longlong_as_double(((long long)(e + 1023) << 52) | (m - (1LL << 52)));
-}
 
 // Binade-integer summary of chunk c for binade e: with S = m * 2^(e-52) and
 // the whole trajectory inside [2^e, 2^(e+1)), fl(S + s) = S + RN(s * 2^(52-e))
@@ -1250,6 +1428,87 @@ __global__ void __launch_bounds__(1024) k_summaries(Chunks g, const uint8_t *__r
     sm.M[2 * c + t] = M[t];
     sm.N[2 * c + t] = N[t];
     sm.A[2 * c + t] = A[t];
+  }
+}
+
+// Pass-1 summaries (kSumm): the summary of every chunk whose exact carry will
+// want one (same test as k_summaries) is the pass-1 one when pass 1 predicted
+// this binade; the others (no or another prediction, a tie, the tail chunks)
+// are listed for k_summ_fix.
+__global__ void __launch_bounds__(256) k_summ_select(Chunks g, P1 o, const double *__restrict__ xt, SummP1 sp,
+                                                     Summ sm, int64_t *__restrict__ fix,
+                                                     unsigned long long *__restrict__ nfix,
+                                                     const double *__restrict__ xh,
+                                                     unsigned long long *__restrict__ why) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool want = false;
+  if (c < g.nch) {
+    sm.e[c] = INT32_MIN;
+    const double x = xt[c];
+    if (!o.special[c] && x >= kLMin && x < 1.0e18) {
+      const int e = (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
+      const double lo = fmin(x, x + o.pmin[c]), hi = fmax(x, x + o.pmax[c]);
+      const double slack = ldexp(1.0, e - 24) + o.sabs[c] * 1e-9;
+      if (lo - slack >= ldexp(1.0, e) && hi + slack < ldexp(1.0, e + 1)) {
+        const int t = sp.e[2 * c] == e ? 0 : (sp.e[2 * c + 1] == e ? 1 : -1);
+        if (t >= 0) {
+          sm.e[c] = e;
+          const long long D = sp.D[2 * c + t], M = sp.M[2 * c + t], N = sp.N[2 * c + t];
+          const int A = sp.A[2 * c + t];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            sm.D[2 * c + q] = D;
+            sm.M[2 * c + q] = M;
+            sm.N[2 * c + q] = N;
+            sm.A[2 * c + q] = A;
+          }
+        } else {
+          want = true;
+          // diagnostics (KS_DEBUG_CARRY): no prediction / void summary / other binade
+          if (why) atomicAdd(&why[sp.e[2 * c] != INT32_MIN ? 2 : (xh[c] >= kP1SumMin ? 1 : 0)], 1ull);
+        }
+      }
+    }
+  }
+  // wave-aggregated append to the fix list
+  const unsigned long long b = __ballot(want);
+  if (!b) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)b) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(nfix, (unsigned long long)__popcll(b));
+  base = __shfl(base, leader, 64);
+  if (want) fix[base + __popcll(b & ((1ull << lane) - 1ull))] = c;
+}
+
+// Summaries of the listed chunks from gathered values (their codes were not
+// stored): lane per listed chunk, persistent grid, count read on the device.
+template <bool kLds>
+__global__ void __launch_bounds__(256) k_summ_fix(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
+                                                  TableView tv, const double *__restrict__ xt,
+                                                  const int64_t *__restrict__ fix,
+                                                  const unsigned long long *__restrict__ nfix, Summ sm) {
+  __shared__ double s_lut[kLds ? kLdsLutMax : 1];
+  if (kLds) {
+    for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
+    __syncthreads();
+  }
+  const int64_t nf = (int64_t)*nfix;
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < nf; f += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = fix[f];
+    const double x = xt[c];
+    const int e = (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
+    long long D[2], M[2], N[2];
+    int A[2];
+    if (!chunk_summary<true, kLds>(g, seq, total, k, tv, nullptr, c, e, D, M, A, N, s_lut)) continue;
+    sm.e[c] = e;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      sm.D[2 * c + t] = D[t];
+      sm.M[2 * c + t] = M[t];
+      sm.N[2 * c + t] = N[t];
+      sm.A[2 * c + t] = A[t];
+    }
   }
 }
 
@@ -2213,6 +2472,16 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const size_t o_cnt = off; off += al(8 * (2 * kSegs + 8));
   const size_t o_flag = off; off += al(nch + 64);
   const size_t o_xagg = off; off += al(ntiles * 32) * 2;
+  // pass-1 summaries: predictor sums / exits / zero flags, predicted entries,
+  // the summaries, the fix list
+  const size_t o_pa = off; off += al(nch * 8);
+  const size_t o_pb = off; off += al(nch * 8);
+  const size_t o_pz = off; off += al(nch);
+  const size_t o_xh = off; off += al(nch * 8);
+  const size_t o_spe = off; off += al(nch * 4 * 2);
+  const size_t o_spd = off; off += al(nch * 8 * 6);
+  const size_t o_spa = off; off += al(nch * 4 * 2);
+  const size_t o_fix = off; off += al(nch * 8 + 8);
   void *wsp = nullptr;
   KS_TRY(ensure(ctx, SLOT_CHUNK_A, off, &wsp));
   char *W = static_cast<char *>(wsp);
@@ -2237,6 +2506,12 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                   reinterpret_cast<double *>(p + ntiles * 24)};
   };
   const XTiles xagg = xtiles(W + o_xagg), xtin = xtiles(W + o_xagg + al(ntiles * 32));
+  double *d_xh = reinterpret_cast<double *>(W + o_xh);
+  long long *spd = reinterpret_cast<long long *>(W + o_spd);
+  const SummP1 sp1{reinterpret_cast<int32_t *>(W + o_spe), spd, spd + 2 * nch, spd + 4 * nch,
+                   reinterpret_cast<int32_t *>(W + o_spa)};
+  unsigned long long *d_nfix = reinterpret_cast<unsigned long long *>(W + o_fix);
+  int64_t *d_fix = reinterpret_cast<int64_t *>(W + o_fix + 8);
   // cnts: [0, kSegs) candidate counters, [kSegs, 2 kSegs) rescan counters,
   // [2 kSegs] replays, [2 kSegs + 1] error bits (u32)
   KS_HIP(hipMemsetAsync(cnts, 0, 8 * (2 * kSegs + 8), st));
@@ -2273,8 +2548,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   static const bool dbg_on = getenv("KS_DEBUG_CARRY") != nullptr;
   long long *dbg = nullptr;
   if (dbg_on) {
-    KS_HIP(hipMalloc(&dbg, nwin * 9 * sizeof(long long)));
-    KS_HIP(hipMemsetAsync(dbg, 0, nwin * 9 * sizeof(long long), st));
+    KS_HIP(hipMalloc(&dbg, (nwin * 9 + 4) * sizeof(long long)));
+    KS_HIP(hipMemsetAsync(dbg, 0, (nwin * 9 + 4) * sizeof(long long), st));
   }
 
   // ---- P0 chunks, P1 gather pass
@@ -2284,6 +2559,26 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   KS_HIP(hipGetLastError());
   const unsigned gch = (unsigned)((nch + 255) / 256);
   const unsigned gch1k = (unsigned)((nch + 1023) / 1024);
+  const int Jt = (tv.ext != nullptr) ? tv.ext_J : 1;
+  const bool lds_table = k <= kLdsTableK && runs.packed != nullptr && getenv("KS_NO_LDS_TABLE") == nullptr;
+  // pass-1 summaries (no per-position code store): compressed tables on the
+  // pipelined pass with a binade predictor; KS_NO_P1_SUMMARY: the code store
+  const bool p1summ = comp && Jt >= 2 && !lds_table && runs.packed != nullptr && tv.approx != nullptr &&
+                      !kP1NoStore && getenv("KS_NO_P1_SUMMARY") == nullptr &&
+                      getenv("KS_NO_PIPELINED_P1") == nullptr;
+  if (p1summ) {  // P0: predicted entries
+    KS_HIP(hipMemsetAsync(W + o_pz, 0, nch, st));
+    const unsigned gl = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nch + 1023) / 1024, ctx->num_cus));
+    hipLaunchKernelGGL(k_predict, dim3(gl), dim3(1024), 0, st, g, total, k, tv.approx, tv.approx_k,
+                       reinterpret_cast<double *>(W + o_pa), reinterpret_cast<double *>(W + o_pb));
+    KS_HIP(hipGetLastError());
+    P1 pp = p1;
+    pp.asum = reinterpret_cast<double *>(W + o_pa);
+    pp.cexit = reinterpret_cast<double *>(W + o_pb);
+    pp.special = reinterpret_cast<uint8_t *>(W + o_pz);
+    hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)nruns), dim3(64), 0, st, d_cbase, nruns, pp, d_xh);
+    KS_HIP(hipGetLastError());
+  }
   KS_HIP(hipEventRecord(ctx->ev[8], st));
   const bool lds_lut = comp && tv.nlut <= kLdsLutMax && getenv("KS_NO_LDS_LUT") == nullptr;
 #define KS_P1(J, C, L)                                                                                       \
@@ -2296,23 +2591,30 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
 #define KS_P1T(J, L) KS_P1TC(J, true, L)
 #define KS_P1TC(J, C, L)                                                                                       \
   hipLaunchKernelGGL((k_pass1<J, C, L>), dim3((unsigned)((nch - ctail + 1023) / 1024)), dim3(1024), 0, side, g, \
-                     s->seq, total, k, tv, codes, ec, visits, p1, cand, ctail, 1)
+                     s->seq, total, k, tv, p1summ ? nullptr : codes, ec, visits, p1, cand, ctail, 1)
   const int J = (tv.ext != nullptr) ? tv.ext_J : 1;
   const bool pipelined = getenv("KS_NO_PIPELINED_P1") == nullptr && runs.packed != nullptr;
   const unsigned gp1 = (unsigned)((nch + kP1Block - 1) / kP1Block);
 #define KS_P1P(J, L)                                                                                           \
   do {                                                                                                       \
-    if (ec.trlr) hipLaunchKernelGGL((k_pass1p<J, L, true>), dim3(gp1), dim3(kP1Block), 0, st, g, s->seq, total, k, \
-                                    tv, codes, ec, visits, p1, cand, runs.packed);                             \
-    else hipLaunchKernelGGL((k_pass1p<J, L, false>), dim3(gp1), dim3(kP1Block), 0, st, g, s->seq, total, k, tv,  \
-                            codes, ec, visits, p1, cand, runs.packed);                                         \
+    if (ec.trlr && p1summ)                                                                                   \
+      hipLaunchKernelGGL((k_pass1p<J, L, true, true>), dim3(gp1), dim3(kP1Block), 0, st, g, s->seq, total, k, \
+                         tv, codes, ec, visits, p1, cand, runs.packed, d_xh, sp1);                           \
+    else if (ec.trlr)                                                                                        \
+      hipLaunchKernelGGL((k_pass1p<J, L, true, false>), dim3(gp1), dim3(kP1Block), 0, st, g, s->seq, total, k, \
+                         tv, codes, ec, visits, p1, cand, runs.packed, d_xh, sp1);                           \
+    else if (p1summ)                                                                                         \
+      hipLaunchKernelGGL((k_pass1p<J, L, false, true>), dim3(gp1), dim3(kP1Block), 0, st, g, s->seq, total, k, \
+                         tv, codes, ec, visits, p1, cand, runs.packed, d_xh, sp1);                           \
+    else                                                                                                     \
+      hipLaunchKernelGGL((k_pass1p<J, L, false, false>), dim3(gp1), dim3(kP1Block), 0, st, g, s->seq, total, k, \
+                         tv, codes, ec, visits, p1, cand, runs.packed, d_xh, sp1);                           \
   } while (0)
-  const bool lds_table = k <= kLdsTableK && runs.packed != nullptr && getenv("KS_NO_LDS_TABLE") == nullptr;
   if (lds_table) {
     // small k: the whole table in LDS, persistent blocks (one per CU), no code store
     const unsigned gl = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nch + 1023) / 1024, ctx->num_cus));
-    if (ec.trlr) hipLaunchKernelGGL(k_pass1_lds<true>, dim3(gl), dim3(1024), 0, st, g, k, tv, ec, visits, p1, cand);
-    else hipLaunchKernelGGL(k_pass1_lds<false>, dim3(gl), dim3(1024), 0, st, g, k, tv, ec, visits, p1, cand);
+    if (ec.trlr) hipLaunchKernelGGL(k_pass1_lds<true>, dim3(gl), dim3(1024), 0, st, g, total, k, tv, ec, visits, p1, cand);
+    else hipLaunchKernelGGL(k_pass1_lds<false>, dim3(gl), dim3(1024), 0, st, g, total, k, tv, ec, visits, p1, cand);
     codes = nullptr;
   } else if (comp && J >= 2 && pipelined) {
     // the tail chunks (a latency-bound serial walk each) run on the side
@@ -2335,7 +2637,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     }
     KS_HIP(hipGetLastError());
     if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
-    if (kP1NoStore) codes = nullptr;  // diagnostic build: later passes gather their values
+    if (kP1NoStore || p1summ) codes = nullptr;  // no code store: later passes gather their values
   } else if (!comp && J >= 2 && J <= 4 && pipelined) {
     hipStream_t side = ctx->side;
     const bool tail = nch > ctail;
@@ -2378,7 +2680,17 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   KS_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_seg_marks, dim3((unsigned)nwin), dim3(64), 0, st, g, p1, xt, d_flag);
   KS_HIP(hipGetLastError());
-  if (lds_lut)
+  if (p1summ) {
+    KS_HIP(hipMemsetAsync(d_nfix, 0, 8, st));
+    hipLaunchKernelGGL(k_summ_select, dim3(gch), dim3(256), 0, st, g, p1, xt, sp1, sm, d_fix, d_nfix, d_xh,
+                       dbg ? reinterpret_cast<unsigned long long *>(dbg + nwin * 9) : nullptr);
+    KS_HIP(hipGetLastError());
+    const unsigned gf = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nch + 255) / 256, (int64_t)ctx->num_cus * 8));
+    if (lds_lut)
+      hipLaunchKernelGGL(k_summ_fix<true>, dim3(gf), dim3(256), 0, st, g, s->seq, total, k, tv, xt, d_fix, d_nfix, sm);
+    else
+      hipLaunchKernelGGL(k_summ_fix<false>, dim3(gf), dim3(256), 0, st, g, s->seq, total, k, tv, xt, d_fix, d_nfix, sm);
+  } else if (lds_lut)
     hipLaunchKernelGGL((k_summaries<true, true>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes, p1,
                        xt, sm);
   else if (comp)
@@ -2456,6 +2768,14 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const unsigned int errbits = (unsigned int)(hc[3] & 0xffffffffu);
   if ((errbits & 16u) && !force_fb)
     fprintf(stderr, "kmer_spans_amd: carry segment check failed; the carry was redone per run\n");
+  if (dbg_on && p1summ) {
+    unsigned long long nf = 0;
+    KS_HIP(hipMemcpy(&nf, d_nfix, 8, hipMemcpyDeviceToHost));
+    unsigned long long why[3] = {0, 0, 0};
+    KS_HIP(hipMemcpy(why, dbg + nwin * 9, 24, hipMemcpyDeviceToHost));
+    fprintf(stderr, "[p1summ] chunks %lld gathered summaries %llu (no prediction %llu, void %llu, other binade %llu)\n",
+            (long long)nch, nf, why[0], why[1], why[2]);
+  }
   if (dbg) {
     std::vector<long long> h(nwin * 9);
     KS_HIP(hipMemcpy(h.data(), dbg, nwin * 9 * sizeof(long long), hipMemcpyDeviceToHost));

@@ -18,6 +18,8 @@ struct TableView {
   int ext_bits;     // 12: J = 5 narrow codes (lut12 / map12, 0xFFF escapes)
   const double *lut12;
   const uint16_t *map12;
+  const uint16_t *approx;  // fp16 prefix means (ks_table::d_approx), nullptr if absent
+  int approx_k;
 };
 
 // LUT entries that fit the LDS copy used by the streaming passes (64 KiB).

@@ -7,6 +7,7 @@
 // log2(f/f_med) and +-1 tables depend only on the k-mer count, so at k=13 the
 // 512 MiB FP64 table becomes a 128 MiB code table that stays resident in the
 // 256 MiB Infinity Cache while the sequence streams past.
+#include <hip/hip_fp16.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -257,6 +258,30 @@ __global__ void k_iota(uint32_t *__restrict__ x, int64_t n) {
     x[i] = (uint32_t)i;
 }
 
+// Approximate prefix table (the binade predictor of the chunked scan): for
+// each kp-base prefix p, the mean of s over the 4^(k-kp) k-mers extending it,
+// weighted by their position frequency (the counts hint; 1 without one).
+// Non-finite values and zero weights are left out.
+__global__ void k_build_approx(const uint16_t *__restrict__ codes, const double *__restrict__ lut,
+                               const double *__restrict__ vals, const int32_t *__restrict__ freq, int k, int kp,
+                               uint16_t *__restrict__ out) {
+  const int64_t np = (int64_t)1 << (2 * kp);
+  const int sub = 2 * (k - kp);
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np; p += (int64_t)gridDim.x * blockDim.x) {
+    double num = 0.0, den = 0.0;
+    const int64_t b = p << sub, e = (p + 1) << sub;
+    for (int64_t i = b; i < e; ++i) {
+      const double v = codes ? lut[codes[i]] : vals[i];
+      const double wt = freq ? (double)(uint32_t)freq[i] : 1.0;
+      if (wt > 0 && isfinite(v)) {
+        num += wt * v;
+        den += wt;
+      }
+    }
+    out[p] = __half_as_ushort(__float2half(den > 0 ? (float)(num / den) : 0.0f));
+  }
+}
+
 }  // namespace
 
 // Process-wide pool of ONE expanded-table buffer per device.  A fresh
@@ -300,6 +325,10 @@ void pool_give(int dev, void *p, size_t bytes) {
   if (p) (void)hipFree(p);
 }
 }  // namespace
+
+// Tables whose chunked scan predicts carry binades before pass 1: compressed
+// tables scanned by the pipelined pass (k > 7: small k stages the table in LDS).
+static bool k_approx_ok(const ks_table *t) { return t->compressed && t->k > 7; }
 
 // Entry bytes of an expanded table with J values per entry.
 static size_t ext_entry_bytes(bool u16, int J) {
@@ -465,6 +494,18 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
     if (t->d_lut12) (void)hipFree(t->d_lut12);
     t->d_map12 = nullptr;
     t->d_lut12 = nullptr;
+  }
+  if (k_approx_ok(t)) {  // binade predictor of the pass-1 summaries (k_predict)
+    const int kp = std::min(t->k, 8);
+    if (hipMalloc(&t->d_approx, ((size_t)2 << (2 * kp)) + 16) == hipSuccess) {
+      t->approx_k = kp;
+      hipLaunchKernelGGL(k_build_approx, dim3((unsigned)std::min<int64_t>(((int64_t)1 << (2 * kp)) / 256 + 1, 4096)),
+                         dim3(256), 0, st, t->d_codes, t->d_lut, t->d_vals, freq_dev, t->k, kp, t->d_approx);
+      KS_HIP(hipGetLastError());
+    } else {
+      (void)hipGetLastError();
+      t->d_approx = nullptr;
+    }
   }
   t->d_ext = ext;
   t->ext_J = J;
@@ -816,6 +857,7 @@ extern "C" void ks_table_destroy(ks_table *t) {
   if (t->d_ext) pool_give(t->device, t->d_ext, t->ext_cap);
   if (t->d_map12) (void)hipFree(t->d_map12);
   if (t->d_lut12) (void)hipFree(t->d_lut12);
+  if (t->d_approx) (void)hipFree(t->d_approx);
   delete t;
 }
 

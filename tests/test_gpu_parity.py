@@ -407,6 +407,7 @@ def test_code12_tables(K, oracle, ctx, monkeypatch, k, ndist, force):
     from kmer_spans_amd import device as D, genome
     if force:
         monkeypatch.setenv("KS_EXT_ESCAPE_MAX", "1.0")
+    torch.cuda.empty_cache()  # the 128 GiB J = 5 table at k = 13 must fit beside torch's cache
     rng = np.random.default_rng(k + ndist)
     vals = np.round(rng.normal(size=ndist) * 64) / 64 + rng.normal(size=ndist) * 1e-3
     w = vals[rng.integers(0, ndist, size=4 ** k)]
@@ -424,7 +425,9 @@ def test_code12_tables(K, oracle, ctx, monkeypatch, k, ndist, force):
         vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
         pos, sc, st = D.scan(ctx, ds, k, tab, 30, 3.0, vis)
         _assert_same_regions(pos, sc, o["pos"], o["score"], ("c12", k, algo))
-        assert np.array_equal(vis.cpu().numpy(), o["counts"])
+        hv = vis.cpu().numpy()
+        bad = np.nonzero(hv != o["counts"])[0]
+        assert bad.size == 0, ("c12 visits", k, algo, bad.size, bad[:5], hv[bad[:5]], o["counts"][bad[:5]])
     ctx.set_scan_algo(-1)
     tab.close()
 

@@ -170,6 +170,10 @@ struct RunLayout {
   int64_t scored = 0;   // scan indices (sum over runs of len - k)
   int64_t nscan = 0;    // runs longer than k
   int64_t longest = 0;  // longest run (bases)
+  // split of the runs into two halves of about nch / 2 chunks (the chunked
+  // scan overlaps the second half's pass 1 with the first half's later
+  // passes): runs [0, split_r), chunks [0, split_c), tiles [0, split_t)
+  int64_t split_r = 0, split_c = 0, split_t = 0;
 };
 // trlr: one more scan index per run (the first k-mer's own step) and the
 // :341 skip of runs whose first k-mer ends within two bytes of the string end.

@@ -194,6 +194,21 @@ __global__ void k_run_counts(const int64_t *__restrict__ ra, const int64_t *__re
   }
 }
 
+// The run where the first half of the chunks ends: first r with
+// cbase[r] >= cbase[n] / 2 (out: r, cbase[r], tbase[r]).
+__global__ void k_split(const int64_t *__restrict__ cbase, const int64_t *__restrict__ tbase, int64_t n,
+                        unsigned long long *__restrict__ out) {
+  const int64_t half = cbase[n] / 2;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (cbase[mid] < half) lo = mid + 1; else hi = mid;
+  }
+  out[0] = (unsigned long long)lo;
+  out[1] = (unsigned long long)cbase[lo];
+  out[2] = (unsigned long long)tbase[lo];
+}
+
 }  // namespace
 
 ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int trlr, const int64_t *offs_dev) {
@@ -220,17 +235,22 @@ ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int t
   KS_TRY(ensure(ctx, SLOT_SORT_TMP, tb, &tmp));
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt_c, lay->cbase, (int)(n + 1), st));
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt_t, lay->tbase, (int)(n + 1), st));
+  hipLaunchKernelGGL(k_split, dim3(1), dim3(1), 0, st, lay->cbase, lay->tbase, n, agg + 3);
+  KS_HIP(hipGetLastError());
   int64_t h[2] = {0, 0};
-  unsigned long long ha[3] = {0, 0, 0};
+  unsigned long long ha[6] = {0, 0, 0, 0, 0, 0};
   KS_HIP(hipMemcpyAsync(&h[0], lay->cbase + n, 8, hipMemcpyDeviceToHost, st));
   KS_HIP(hipMemcpyAsync(&h[1], lay->tbase + n, 8, hipMemcpyDeviceToHost, st));
-  KS_HIP(hipMemcpyAsync(ha, agg, 24, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipMemcpyAsync(ha, agg, 48, hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
   lay->nch = h[0];
   lay->ntiles = h[1];
   lay->scored = (int64_t)ha[0];
   lay->nscan = (int64_t)ha[1];
   lay->longest = (int64_t)ha[2];
+  lay->split_r = (int64_t)ha[3];
+  lay->split_c = (int64_t)ha[4];
+  lay->split_t = (int64_t)ha[5];
   return KS_OK;
 }
 

@@ -56,8 +56,9 @@ struct Chunks {
   int64_t *start;  // first scan index (global position)
   int32_t *n;      // indices in the chunk
   int32_t *run;    // run id
-  int64_t nch;
+  int64_t nch;     // chunks [c0, nch) are this launch's (a half of the runs, see scan_chunked)
   const uint32_t *packed;  // 2-bit base codes (Runs::packed), nullptr: roll the bytes
+  int64_t c0 = 0;
 };
 
 struct P1 {  // per-chunk results of the gather pass
@@ -637,7 +638,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
       s_map12[i] = tv.map12[i];
     }
   if (kLds || k12) __syncthreads();
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
   const EW *__restrict__ ext = reinterpret_cast<const EW *>(tv.ext);
   const int kx = k + J - 1;
@@ -1362,8 +1363,8 @@ __device__ bool chunk_summary(const Chunks &g, const uint8_t *__restrict__ seq, 
 // (a = sum, b = clean exit); x~_j = composite of chunks < j applied to 0.  Only
 // a prediction (which binade the exact carry will be in); never trusted.
 __global__ void __launch_bounds__(64) k_approx_scan(const int64_t *__restrict__ cbase, int64_t nruns, P1 o,
-                                                    double *__restrict__ xt) {
-  const int64_t r = blockIdx.x;
+                                                    double *__restrict__ xt, int64_t r_lo) {
+  const int64_t r = r_lo + blockIdx.x;
   if (r >= nruns) return;
   const int lane = threadIdx.x;
   const int64_t c0 = cbase[r], c1 = cbase[r + 1];
@@ -1448,7 +1449,7 @@ __global__ void __launch_bounds__(256) k_summ_select(Chunks g, P1 o, const doubl
                                                      unsigned long long *__restrict__ nfix,
                                                      const double *__restrict__ xh,
                                                      unsigned long long *__restrict__ why) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool want = false;
   if (c < g.nch) {
     sm.e[c] = INT32_MIN;
@@ -1525,19 +1526,21 @@ __global__ void __launch_bounds__(256) k_summ_fix(Chunks g, const uint8_t *__res
 // exact entry, which differs from x~ by rounding only, clamps too).
 __global__ void __launch_bounds__(64) k_seg_marks(Chunks g, P1 o, const double *__restrict__ xt,
                                                   uint8_t *__restrict__ flag) {
-  const int64_t e = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  // windows of 64 chunks from the one holding c0 - 1; only this launch's
+  // chunks [c0, nch) are read and marked
+  const int64_t e = ((g.c0 > 0 ? g.c0 - 1 : 0) / 64 + (int64_t)blockIdx.x) * 64 + threadIdx.x;
   bool elig = false, next_run = false;
-  if (e + 1 < g.nch) {
+  if (e + 1 < g.nch && e + 1 >= g.c0) {
     next_run = g.run[e + 1] != g.run[e];
-    if (!next_run && !o.special[e]) {
+    if (!next_run && e >= g.c0 && !o.special[e]) {
       const double x = xt[e];
       elig = x + o.pmin[e] < -ldexp(fabs(x) + o.sabs[e], -20);  // false for NaN
     }
   }
   const unsigned long long b = __ballot(elig);
   const int f = b ? __ffsll((long long)b) - 1 : 64;
-  if (e + 1 < g.nch) flag[e + 1] = (next_run || (int)threadIdx.x == f) ? 1 : 0;
-  if (e == 0) flag[0] = 1;
+  if (e + 1 < g.nch && e + 1 >= g.c0) flag[e + 1] = (next_run || (int)threadIdx.x == f) ? 1 : 0;
+  if (e == 0 && g.c0 == 0) flag[0] = 1;
 }
 
 
@@ -1986,10 +1989,10 @@ __global__ void __launch_bounds__(64) k_carry_win(Chunks g, const uint8_t *__res
                                                   const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
                                                   unsigned long long *__restrict__ nreplay,
                                                   unsigned int *__restrict__ err, long long *__restrict__ dbg) {
-  const int64_t w = blockIdx.x;
+  const int64_t w = g.c0 / 64 + blockIdx.x;  // segment starts in [c0, nch); segments end by nch
   const int lane = threadIdx.x;
   const int64_t base = w * 64;
-  unsigned long long m = __ballot(base + lane < g.nch && flag[base + lane]);
+  unsigned long long m = __ballot(base + lane >= g.c0 && base + lane < g.nch && flag[base + lane]);
   while (m) {
     const int b = __ffsll((long long)m) - 1;
     m &= m - 1;
@@ -2017,8 +2020,9 @@ __global__ void __launch_bounds__(64) k_carry_run(Chunks g, const int64_t *__res
                                                   const uint8_t *__restrict__ seq, int64_t total, int k, TableView tv,
                                                   const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
                                                   unsigned long long *__restrict__ nreplay,
-                                                  unsigned int *__restrict__ err, long long *__restrict__ dbg) {
-  const int64_t r = blockIdx.x;
+                                                  unsigned int *__restrict__ err, long long *__restrict__ dbg,
+                                                  int64_t r_lo) {
+  const int64_t r = r_lo + blockIdx.x;
   if (r >= nruns || !(*(volatile unsigned int *)err & 16u)) return;
   const int64_t c0 = cbase[r], c1 = cbase[r + 1];
   if (c0 < c1) carry_segment<kCompressed>(g, c0, c1, seq, total, k, tv, codes, o, sm, cr, nreplay, err, nullptr, r);
@@ -2046,7 +2050,7 @@ __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restri
                                                int k, TableView tv, const uint16_t *__restrict__ codes,
                                                Carry cr, unsigned int *__restrict__ err, int gated) {
   const uint32_t *__restrict__ packed = g.packed;
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
   if (gated && !(*(volatile unsigned int *)err & 16u)) return;  // second pass only after a fallback
   const int mode = cr.mode[c];
@@ -2338,8 +2342,8 @@ __device__ __forceinline__ XState xt_load(const XTiles &a, int64_t t) {
 
 __global__ void __launch_bounds__(64) k_stitch_tiles(Chunks g, const int64_t *__restrict__ tbase,
                                                      const int64_t *__restrict__ cbase, int64_t nruns, P1 o,
-                                                     Carry cr, XTiles agg) {
-  const int64_t t = blockIdx.x;
+                                                     Carry cr, XTiles agg, int64_t t_lo) {
+  const int64_t t = t_lo + blockIdx.x;
   const int lane = threadIdx.x;
   int64_t r, c0, c1;
   tile_of(tbase, cbase, nruns, t, r, c0, c1);
@@ -2356,8 +2360,8 @@ __global__ void __launch_bounds__(64) k_stitch_tiles(Chunks g, const int64_t *__
 __global__ void __launch_bounds__(64) k_stitch_runs(const int64_t *__restrict__ tbase, int64_t nruns,
                                                     const int64_t *__restrict__ ra, const int64_t *__restrict__ rb_end,
                                                     const int32_t *__restrict__ rseq, EmitCfg ec, XTiles agg,
-                                                    XTiles tin, RegionBuf out, Rescan rs) {
-  const int64_t r = blockIdx.x;
+                                                    XTiles tin, RegionBuf out, Rescan rs, int64_t r_lo) {
+  const int64_t r = r_lo + blockIdx.x;  // runs [r_lo, nruns)
   if (r >= nruns) return;
   const int lane = threadIdx.x;
   const int64_t t0 = tbase[r], t1 = tbase[r + 1];
@@ -2383,8 +2387,8 @@ __global__ void __launch_bounds__(64) k_stitch_emit(Chunks g, const int64_t *__r
                                                     const int64_t *__restrict__ cbase, int64_t nruns,
                                                     const int64_t *__restrict__ ra, const int32_t *__restrict__ rseq,
                                                     P1 o, Carry cr, EmitCfg ec, XTiles tin, RegionBuf out,
-                                                    Rescan rs, unsigned int *__restrict__ err) {
-  const int64_t t = blockIdx.x;
+                                                    Rescan rs, unsigned int *__restrict__ err, int64_t t_lo) {
+  const int64_t t = t_lo + blockIdx.x;
   const int lane = threadIdx.x;
   int64_t r, c0, c1;
   tile_of(tbase, cbase, nruns, t, r, c0, c1);
@@ -2489,7 +2493,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const size_t o_spe = off; off += al(nch * 4 * 2);
   const size_t o_spd = off; off += al(nch * 8 * 6);
   const size_t o_spa = off; off += al(nch * 4 * 2);
-  const size_t o_fix = off; off += al(nch * 8 + 8);
+  const size_t o_fix = off; off += al(nch * 8 + 16);
   void *wsp = nullptr;
   KS_TRY(ensure(ctx, SLOT_CHUNK_A, off, &wsp));
   char *W = static_cast<char *>(wsp);
@@ -2518,10 +2522,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   long long *spd = reinterpret_cast<long long *>(W + o_spd);
   const SummP1 sp1{reinterpret_cast<int32_t *>(W + o_spe), spd, spd + 2 * nch, spd + 4 * nch,
                    reinterpret_cast<int32_t *>(W + o_spa)};
-  unsigned long long *d_nfix = reinterpret_cast<unsigned long long *>(W + o_fix);
-  int64_t *d_fix = reinterpret_cast<int64_t *>(W + o_fix + 8);
+  unsigned long long *d_nfix = reinterpret_cast<unsigned long long *>(W + o_fix);  // [2]: one per half
+  int64_t *d_fix = reinterpret_cast<int64_t *>(W + o_fix + 16);
   // cnts: [0, kSegs) candidate counters, [kSegs, 2 kSegs) rescan counters,
-  // [2 kSegs] replays, [2 kSegs + 1] error bits (u32)
+  // [2 kSegs + 2h] replays, [2 kSegs + 2h + 1] error bits (u32) of half h
   KS_HIP(hipMemsetAsync(cnts, 0, 8 * (2 * kSegs + 8), st));
   unsigned long long *d_replays = cnts + 2 * kSegs;
   unsigned int *d_err = reinterpret_cast<unsigned int *>(cnts + 2 * kSegs + 1);
@@ -2584,11 +2588,35 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     pp.asum = reinterpret_cast<double *>(W + o_pa);
     pp.cexit = reinterpret_cast<double *>(W + o_pb);
     pp.special = reinterpret_cast<uint8_t *>(W + o_pz);
-    hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)nruns), dim3(64), 0, st, d_cbase, nruns, pp, d_xh);
+    hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)nruns), dim3(64), 0, st, d_cbase, nruns, pp, d_xh, (int64_t)0);
     KS_HIP(hipGetLastError());
   }
   KS_HIP(hipEventRecord(ctx->ev[8], st));
   const bool lds_lut = comp && tv.nlut <= kLdsLutMax && getenv("KS_NO_LDS_LUT") == nullptr;
+  // Two halves of the runs (pass-1-summary path): the second half's pass 1
+  // (side stream) runs while the first half's latency-bound later passes
+  // (carry, stitch) run on the main stream; halves split at a run boundary,
+  // so no carry or stitch crosses it.  KS_NO_SPLIT: one half.
+  struct Half {
+    int64_t c0, c1, r0, r1, t0, t1;
+  };
+  const int64_t ctail_all = nch > 1024 ? nch - 1024 : 0;
+  const bool split = p1summ && lay.split_r > 0 && lay.split_r < nruns && lay.split_c >= 1024 &&
+                     lay.split_c + 1024 <= ctail_all && getenv("KS_NO_SPLIT") == nullptr;
+  Half halves[2];
+  int nhalf = 1;
+  halves[0] = Half{0, nch, 0, nruns, 0, ntiles};
+  if (split) {
+    nhalf = 2;
+    halves[0] = Half{0, lay.split_c, 0, lay.split_r, 0, lay.split_t};
+    halves[1] = Half{lay.split_c, nch, lay.split_r, nruns, lay.split_t, ntiles};
+  }
+  auto view = [&](const Half &h) {
+    Chunks v = g;
+    v.c0 = h.c0;
+    v.nch = h.c1;
+    return v;
+  };
 #define KS_P1(J, C, L)                                                                                       \
   hipLaunchKernelGGL((k_pass1<J, C, L>), dim3(J == 1 ? gch : gch1k), dim3(J == 1 ? 256 : 1024), 0, st, g, s->seq, \
                      total, k, tv, codes, ec, visits, p1, cand, (int64_t)0, 0)
@@ -2603,19 +2631,19 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const int J = (tv.ext != nullptr) ? tv.ext_J : 1;
   const bool pipelined = getenv("KS_NO_PIPELINED_P1") == nullptr && runs.packed != nullptr;
   const unsigned gp1 = (unsigned)((nch + kP1Block - 1) / kP1Block);
-#define KS_P1P(J, L)                                                                                           \
+#define KS_P1P(J, L, GV, GRID, STRM)                                                                           \
   do {                                                                                                       \
     if (ec.trlr && p1summ)                                                                                   \
-      hipLaunchKernelGGL((k_pass1p<J, L, true, true>), dim3(gp1), dim3(kP1Block), 0, st, g, s->seq, total, k, \
+      hipLaunchKernelGGL((k_pass1p<J, L, true, true>), dim3(GRID), dim3(kP1Block), 0, STRM, GV, s->seq, total, k, \
                          tv, codes, ec, visits, p1, cand, runs.packed, d_xh, sp1);                           \
     else if (ec.trlr)                                                                                        \
-      hipLaunchKernelGGL((k_pass1p<J, L, true, false>), dim3(gp1), dim3(kP1Block), 0, st, g, s->seq, total, k, \
+      hipLaunchKernelGGL((k_pass1p<J, L, true, false>), dim3(GRID), dim3(kP1Block), 0, STRM, GV, s->seq, total, k, \
                          tv, codes, ec, visits, p1, cand, runs.packed, d_xh, sp1);                           \
     else if (p1summ)                                                                                         \
-      hipLaunchKernelGGL((k_pass1p<J, L, false, true>), dim3(gp1), dim3(kP1Block), 0, st, g, s->seq, total, k, \
+      hipLaunchKernelGGL((k_pass1p<J, L, false, true>), dim3(GRID), dim3(kP1Block), 0, STRM, GV, s->seq, total, k, \
                          tv, codes, ec, visits, p1, cand, runs.packed, d_xh, sp1);                           \
     else                                                                                                     \
-      hipLaunchKernelGGL((k_pass1p<J, L, false, false>), dim3(gp1), dim3(kP1Block), 0, st, g, s->seq, total, k, \
+      hipLaunchKernelGGL((k_pass1p<J, L, false, false>), dim3(GRID), dim3(kP1Block), 0, STRM, GV, s->seq, total, k, \
                          tv, codes, ec, visits, p1, cand, runs.packed, d_xh, sp1);                           \
   } while (0)
   if (lds_table) {
@@ -2626,25 +2654,49 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     codes = nullptr;
   } else if (comp && J >= 2 && pipelined) {
     // the tail chunks (a latency-bound serial walk each) run on the side
-    // stream, overlapped with the pipelined pass
+    // stream, overlapped with the pipelined pass (of the last half)
     hipStream_t side = ctx->side;
     const bool tail = nch > ctail;
-    if (tail) {
+    auto p1p = [&](const Half &h, hipStream_t strm) {
+      const Chunks gv = view(h);
+      const unsigned grid = (unsigned)((h.c1 - h.c0 + kP1Block - 1) / kP1Block);
+      if (lds_lut) {
+        if (J == 5) KS_P1P(5, true, gv, grid, strm); else if (J == 4) KS_P1P(4, true, gv, grid, strm);
+        else if (J == 3) KS_P1P(3, true, gv, grid, strm); else KS_P1P(2, true, gv, grid, strm);
+      } else {
+        if (J == 5) KS_P1P(5, false, gv, grid, strm); else if (J == 4) KS_P1P(4, false, gv, grid, strm);
+        else if (J == 3) KS_P1P(3, false, gv, grid, strm); else KS_P1P(2, false, gv, grid, strm);
+      }
+    };
+    if (split) {
+      // first half on the main stream; the side stream waits for it, then
+      // runs the tail chunks and the second half (pass 1 end = ev[9] on side)
+      p1p(halves[0], st);
+      KS_HIP(hipGetLastError());
       KS_HIP(hipEventRecord(ctx->ev[12], st));
       KS_HIP(hipStreamWaitEvent(side, ctx->ev[12], 0));
-      if (J == 5) KS_P1T(5, false);
-      else if (lds_lut) { if (J == 4) KS_P1T(4, true); else if (J == 3) KS_P1T(3, true); else KS_P1T(2, true); }
-      else { if (J == 4) KS_P1T(4, false); else if (J == 3) KS_P1T(3, false); else KS_P1T(2, false); }
+      if (tail) {
+        if (J == 5) KS_P1T(5, false);
+        else if (lds_lut) { if (J == 4) KS_P1T(4, true); else if (J == 3) KS_P1T(3, true); else KS_P1T(2, true); }
+        else { if (J == 4) KS_P1T(4, false); else if (J == 3) KS_P1T(3, false); else KS_P1T(2, false); }
+        KS_HIP(hipGetLastError());
+      }
+      p1p(halves[1], side);
       KS_HIP(hipGetLastError());
-      KS_HIP(hipEventRecord(ctx->ev[13], side));
-    }
-    if (lds_lut) {
-      if (J == 5) KS_P1P(5, true); else if (J == 4) KS_P1P(4, true); else if (J == 3) KS_P1P(3, true); else KS_P1P(2, true);
     } else {
-      if (J == 5) KS_P1P(5, false); else if (J == 4) KS_P1P(4, false); else if (J == 3) KS_P1P(3, false); else KS_P1P(2, false);
+      if (tail) {
+        KS_HIP(hipEventRecord(ctx->ev[12], st));
+        KS_HIP(hipStreamWaitEvent(side, ctx->ev[12], 0));
+        if (J == 5) KS_P1T(5, false);
+        else if (lds_lut) { if (J == 4) KS_P1T(4, true); else if (J == 3) KS_P1T(3, true); else KS_P1T(2, true); }
+        else { if (J == 4) KS_P1T(4, false); else if (J == 3) KS_P1T(3, false); else KS_P1T(2, false); }
+        KS_HIP(hipGetLastError());
+        KS_HIP(hipEventRecord(ctx->ev[13], side));
+      }
+      p1p(halves[0], st);
+      KS_HIP(hipGetLastError());
+      if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
     }
-    KS_HIP(hipGetLastError());
-    if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
     if (kP1NoStore || p1summ) codes = nullptr;  // no code store: later passes gather their values
   } else if (!comp && J >= 2 && J <= 4 && pipelined) {
     hipStream_t side = ctx->side;
@@ -2681,79 +2733,116 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
 #undef KS_P1TC
 #undef KS_P1P
   KS_HIP(hipGetLastError());
-  KS_HIP(hipEventRecord(ctx->ev[9], st));
+  KS_HIP(hipEventRecord(ctx->ev[9], split ? ctx->side : st));  // end of pass 1 (the last half's stream)
 
-  // ---- P2 prediction, segment starts, summaries
-  hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)nruns), dim3(64), 0, st, d_cbase, nruns, p1, xt);
-  KS_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_seg_marks, dim3((unsigned)nwin), dim3(64), 0, st, g, p1, xt, d_flag);
-  KS_HIP(hipGetLastError());
-  if (p1summ) {
-    KS_HIP(hipMemsetAsync(d_nfix, 0, 8, st));
-    hipLaunchKernelGGL(k_summ_select, dim3(gch), dim3(256), 0, st, g, p1, xt, sp1, sm, d_fix, d_nfix, d_xh,
-                       dbg ? reinterpret_cast<unsigned long long *>(dbg + nwin * 9) : nullptr);
+  // P2-P5 (without the candidates) of one half on stream strm, with its own
+  // replay counter, error bits and fix list; ev[14] / ev[15] mark the last
+  // half's phases
+  const int force_fb = getenv("KS_TEST_SEG_FALLBACK") != nullptr ? 1 : 0;  // tests: force the fallback path
+  auto post = [&](int hi, const Half &h, hipStream_t strm) -> ks_status {
+    const bool last = hi == nhalf - 1;
+    const Chunks gv = view(h);
+    const int64_t nh = h.c1 - h.c0, nr = h.r1 - h.r0, nt = h.t1 - h.t0;
+    if (nh <= 0) return KS_OK;
+    unsigned long long *rep_h = d_replays + 2 * hi;
+    unsigned int *err_h = reinterpret_cast<unsigned int *>(d_replays + 2 * hi + 1);
+    const unsigned gch_h = (unsigned)((nh + 255) / 256);
+    // ---- P2 prediction, segment starts, summaries
+    if (nr > 0) {
+      hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)nr), dim3(64), 0, strm, d_cbase, h.r1, p1, xt, h.r0);
+      KS_HIP(hipGetLastError());
+    }
+    const int64_t wl = (h.c0 > 0 ? h.c0 - 1 : 0) / 64;
+    hipLaunchKernelGGL(k_seg_marks, dim3((unsigned)((h.c1 + 63) / 64 - wl)), dim3(64), 0, strm, gv, p1, xt, d_flag);
     KS_HIP(hipGetLastError());
-    const unsigned gf = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nch + 255) / 256, (int64_t)ctx->num_cus * 8));
-    if (lds_lut)
-      hipLaunchKernelGGL(k_summ_fix<true>, dim3(gf), dim3(256), 0, st, g, s->seq, total, k, tv, xt, d_fix, d_nfix, sm);
+    if (p1summ) {
+      KS_HIP(hipMemsetAsync(d_nfix + hi, 0, 8, strm));
+      hipLaunchKernelGGL(k_summ_select, dim3(gch_h), dim3(256), 0, strm, gv, p1, xt, sp1, sm, d_fix + h.c0,
+                         d_nfix + hi, d_xh, dbg ? reinterpret_cast<unsigned long long *>(dbg + nwin * 9) : nullptr);
+      KS_HIP(hipGetLastError());
+      const unsigned gf = (unsigned)std::max<int64_t>(1, std::min<int64_t>(gch_h, (int64_t)ctx->num_cus * 8));
+      if (lds_lut)
+        hipLaunchKernelGGL(k_summ_fix<true>, dim3(gf), dim3(256), 0, strm, g, s->seq, total, k, tv, xt, d_fix + h.c0,
+                           d_nfix + hi, sm);
+      else
+        hipLaunchKernelGGL(k_summ_fix<false>, dim3(gf), dim3(256), 0, strm, g, s->seq, total, k, tv, xt, d_fix + h.c0,
+                           d_nfix + hi, sm);
+    } else if (lds_lut)
+      hipLaunchKernelGGL((k_summaries<true, true>), dim3(gch1k), dim3(1024), 0, strm, g, s->seq, total, k, tv, codes,
+                         p1, xt, sm);
+    else if (comp)
+      hipLaunchKernelGGL((k_summaries<true, false>), dim3(gch1k), dim3(1024), 0, strm, g, s->seq, total, k, tv, codes,
+                         p1, xt, sm);
     else
-      hipLaunchKernelGGL(k_summ_fix<false>, dim3(gf), dim3(256), 0, st, g, s->seq, total, k, tv, xt, d_fix, d_nfix, sm);
-  } else if (lds_lut)
-    hipLaunchKernelGGL((k_summaries<true, true>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes, p1,
-                       xt, sm);
-  else if (comp)
-    hipLaunchKernelGGL((k_summaries<true, false>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes, p1,
-                       xt, sm);
-  else
-    hipLaunchKernelGGL((k_summaries<false, false>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv, codes,
-                       p1, xt, sm);
-  KS_HIP(hipGetLastError());
-  KS_HIP(hipEventRecord(ctx->ev[14], st));
+      hipLaunchKernelGGL((k_summaries<false, false>), dim3(gch1k), dim3(1024), 0, strm, g, s->seq, total, k, tv,
+                         codes, p1, xt, sm);
+    KS_HIP(hipGetLastError());
+    if (last) KS_HIP(hipEventRecord(ctx->ev[14], strm));
 
-  // ---- P3 carry by segments + P4 heads; then the gated per-run fallback
-  if (comp)
-    hipLaunchKernelGGL(k_carry_win<true>, dim3((unsigned)nwin), dim3(64), 0, st, g, d_flag, s->seq, total, k, tv,
-                       codes, p1, sm, cr, d_replays, d_err, dbg);
-  else
-    hipLaunchKernelGGL(k_carry_win<false>, dim3((unsigned)nwin), dim3(64), 0, st, g, d_flag, s->seq, total, k, tv,
-                       codes, p1, sm, cr, d_replays, d_err, dbg);
-  KS_HIP(hipGetLastError());
-#define KS_HEADS(J, C, GATED)                                                                                 \
-  hipLaunchKernelGGL((k_heads<J, C>), dim3(gch), dim3(256), 0, st, g, s->seq, total, k, tv, codes, cr, d_err, \
-                     GATED)
-  auto heads = [&](int gated) {
-    if (comp) KS_HEADS(1, true, gated);
-    else if (J == 4) KS_HEADS(4, false, gated);
-    else if (J == 3) KS_HEADS(3, false, gated);
-    else if (J == 2) KS_HEADS(2, false, gated);
-    else KS_HEADS(1, false, gated);
-  };
+    // ---- P3 carry by segments + P4 heads; then the gated per-run fallback
+    const int64_t wc = h.c0 / 64;
+    const unsigned nwc = (unsigned)((h.c1 - 1) / 64 - wc + 1);
+    if (comp)
+      hipLaunchKernelGGL(k_carry_win<true>, dim3(nwc), dim3(64), 0, strm, gv, d_flag, s->seq, total, k, tv, codes, p1,
+                         sm, cr, rep_h, err_h, dbg);
+    else
+      hipLaunchKernelGGL(k_carry_win<false>, dim3(nwc), dim3(64), 0, strm, gv, d_flag, s->seq, total, k, tv, codes,
+                         p1, sm, cr, rep_h, err_h, dbg);
+    KS_HIP(hipGetLastError());
+    auto heads = [&](int gated) {
+#define KS_HEADS(J, C)                                                                                           \
+  hipLaunchKernelGGL((k_heads<J, C>), dim3(gch_h), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes, cr, err_h, \
+                     gated)
+      if (comp) KS_HEADS(1, true);
+      else if (J == 4) KS_HEADS(4, false);
+      else if (J == 3) KS_HEADS(3, false);
+      else if (J == 2) KS_HEADS(2, false);
+      else KS_HEADS(1, false);
 #undef KS_HEADS
-  heads(0);
-  KS_HIP(hipGetLastError());
-  // KS_TEST_SEG_FALLBACK=1 forces the fallback path (tests)
-  const int force_fb = getenv("KS_TEST_SEG_FALLBACK") != nullptr ? 1 : 0;
-  hipLaunchKernelGGL(k_fallback_prep, dim3(1), dim3(1), 0, st, d_err, d_replays, force_fb);
-  if (comp)
-    hipLaunchKernelGGL(k_carry_run<true>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, total,
-                       k, tv, codes, p1, sm, cr, d_replays, d_err, nullptr);
-  else
-    hipLaunchKernelGGL(k_carry_run<false>, dim3((unsigned)nruns), dim3(64), 0, st, g, d_cbase, nruns, s->seq, total,
-                       k, tv, codes, p1, sm, cr, d_replays, d_err, nullptr);
-  heads(1);
-  KS_HIP(hipGetLastError());
-  KS_HIP(hipEventRecord(ctx->ev[15], st));
+    };
+    heads(0);
+    KS_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_fallback_prep, dim3(1), dim3(1), 0, strm, err_h, rep_h, force_fb);
+    if (nr > 0) {
+      if (comp)
+        hipLaunchKernelGGL(k_carry_run<true>, dim3((unsigned)nr), dim3(64), 0, strm, gv, d_cbase, h.r1, s->seq, total,
+                           k, tv, codes, p1, sm, cr, rep_h, err_h, nullptr, h.r0);
+      else
+        hipLaunchKernelGGL(k_carry_run<false>, dim3((unsigned)nr), dim3(64), 0, strm, gv, d_cbase, h.r1, s->seq,
+                           total, k, tv, codes, p1, sm, cr, rep_h, err_h, nullptr, h.r0);
+    }
+    heads(1);
+    KS_HIP(hipGetLastError());
+    if (last) KS_HIP(hipEventRecord(ctx->ev[15], strm));
 
-  // ---- P5 stitch, candidates (count read on the device), rescans
-  hipLaunchKernelGGL(k_stitch_tiles, dim3((unsigned)ntiles), dim3(64), 0, st, g, d_tbase, d_cbase, nruns, p1, cr,
-                     xagg);
-  KS_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_stitch_runs, dim3((unsigned)nruns), dim3(64), 0, st, d_tbase, nruns, runs.a, runs.b,
-                     runs.seq, ec, xagg, xtin, rb, rs);
-  KS_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_stitch_emit, dim3((unsigned)ntiles), dim3(64), 0, st, g, d_tbase, d_cbase, nruns, runs.a,
-                     runs.seq, p1, cr, ec, xtin, rb, rs, d_err);
-  KS_HIP(hipGetLastError());
+    // ---- P5 stitch
+    if (nt > 0) {
+      hipLaunchKernelGGL(k_stitch_tiles, dim3((unsigned)nt), dim3(64), 0, strm, g, d_tbase, d_cbase, nruns, p1, cr,
+                         xagg, h.t0);
+      KS_HIP(hipGetLastError());
+    }
+    if (nr > 0) {
+      hipLaunchKernelGGL(k_stitch_runs, dim3((unsigned)nr), dim3(64), 0, strm, d_tbase, h.r1, runs.a, runs.b, runs.seq,
+                         ec, xagg, xtin, rb, rs, h.r0);
+      KS_HIP(hipGetLastError());
+    }
+    if (nt > 0) {
+      hipLaunchKernelGGL(k_stitch_emit, dim3((unsigned)nt), dim3(64), 0, strm, g, d_tbase, d_cbase, nruns, runs.a,
+                         runs.seq, p1, cr, ec, xtin, rb, rs, err_h, h.t0);
+      KS_HIP(hipGetLastError());
+    }
+    return KS_OK;
+  };
+  if (split) {
+    KS_TRY(post(0, halves[0], st));         // under the second half's pass 1
+    KS_TRY(post(1, halves[1], ctx->side));
+    KS_HIP(hipEventRecord(ctx->ev[13], ctx->side));
+    KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
+  } else {
+    KS_TRY(post(0, halves[0], st));
+  }
+
+  // ---- candidates (count read on the device), rescans
   hipLaunchKernelGGL(k_candidates, dim3((unsigned)((ccap + 255) / 256)), dim3(256), 0, st, g, runs.a, d_cbase,
                      nruns, runs.seq, ec, cand, cr, rb, rs);
   KS_HIP(hipGetLastError());
@@ -2761,8 +2850,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   KS_TRY(launch_scan_lane(ctx, s->seq, total, rs.a, rs.b, rs.seq, rcap, k, tv, mw, min_score, visits_rescan, rb,
                           rs.count, rs.segcap, mode, 0, nullptr, runs.packed));
   KS_HIP(hipEventRecord(ctx->ev[11], st));
-  std::vector<unsigned long long> hcv(2 * kSegs + 2);
-  KS_HIP(hipMemcpyAsync(hcv.data(), cnts, 8 * (2 * kSegs + 2), hipMemcpyDeviceToHost, st));
+  std::vector<unsigned long long> hcv(2 * kSegs + 4);
+  KS_HIP(hipMemcpyAsync(hcv.data(), cnts, 8 * (2 * kSegs + 4), hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
   unsigned long long cand_max = 0, res_max = 0, res_tot = 0;
   for (int q = 0; q < kSegs; ++q) {
@@ -2771,14 +2860,17 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     res_tot += std::min<unsigned long long>(hcv[kSegs + q], (unsigned long long)rs.segcap);
   }
   // hc: [0] largest candidate segment, [1] rescans, [2] replays, [3] error bits
-  const unsigned long long hc[4] = {cand_max, res_tot, hcv[2 * kSegs], hcv[2 * kSegs + 1]};
+  const unsigned long long hc[4] = {cand_max, res_tot, hcv[2 * kSegs] + hcv[2 * kSegs + 2],
+                                     (hcv[2 * kSegs + 1] | hcv[2 * kSegs + 3]) & 0xffffffffull};
 
   const unsigned int errbits = (unsigned int)(hc[3] & 0xffffffffu);
   if ((errbits & 16u) && !force_fb)
     fprintf(stderr, "kmer_spans_amd: carry segment check failed; the carry was redone per run\n");
   if (dbg_on && p1summ) {
     unsigned long long nf = 0;
-    KS_HIP(hipMemcpy(&nf, d_nfix, 8, hipMemcpyDeviceToHost));
+    unsigned long long nf2[2] = {0, 0};
+    KS_HIP(hipMemcpy(nf2, d_nfix, 16, hipMemcpyDeviceToHost));
+    nf = nf2[0] + nf2[1];
     unsigned long long why[3] = {0, 0, 0};
     KS_HIP(hipMemcpy(why, dbg + nwin * 9, 24, hipMemcpyDeviceToHost));
     fprintf(stderr, "[p1summ] chunks %lld gathered summaries %llu (no prediction %llu, void %llu, other binade %llu)\n",

@@ -209,8 +209,9 @@ __device__ __forceinline__ void load_codes16(const uint16_t *__restrict__ codes,
 // table whose per-index codes were not stored (small-k pass 1): the 16
 // k-mers from one 64-bit window of packed bases (bytes near the buffer end),
 // each looked up in the base code table (L2-resident for small k) and the LUT.
+template <int NV = 16>
 __device__ __forceinline__ void values16_nostore(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total,
-                                                 int k, const TableView &tv, int64_t c, int b0, int n, double v[16],
+                                                 int k, const TableView &tv, int64_t c, int b0, int n, double v[NV],
                                                  const double *s_lut) {
   const int64_t p = g.start[c] + b0 - k;  // first base of index b0's k-mer
   const uint32_t kmask = (1u << (2 * k)) - 1u;
@@ -222,16 +223,16 @@ __device__ __forceinline__ void values16_nostore(const Chunks &g, const uint8_t 
     const int J = tv.ext_J, kx = k + J - 1;
     const uint64_t xmask = (kx >= 32) ? ~0ull : ((1ull << (2 * kx)) - 1ull);
     const bool c12 = tv.ext_bits == 12;
-    for (int o = 0; o < 16; o += J) {
+    for (int o = 0; o < NV; o += J) {
       if (b0 + o >= n) {
-        for (int t = o; t < 16; ++t) v[t] = 0.0;
+        for (int t = o; t < NV; ++t) v[t] = 0.0;
         break;
       }
       const uint64_t gx = (x >> (64 - 2 * (o + kx))) & xmask;
       uint64_t e;
       if (J <= 2) e = reinterpret_cast<const uint32_t *>(tv.ext)[gx];
       else e = reinterpret_cast<const uint64_t *>(tv.ext)[gx];
-      for (int t = 0; t < J && o + t < 16; ++t) {
+      for (int t = 0; t < J && o + t < NV; ++t) {
         const int j = o + t;
         double val = 0.0;
         if (b0 + j < n) {
@@ -252,7 +253,7 @@ __device__ __forceinline__ void values16_nostore(const Chunks &g, const uint8_t 
   }
   uint32_t code = pk ? 0u : prime_code(seq, p, k);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
+  for (int j = 0; j < NV; ++j) {
     if (pk) code = (uint32_t)(x >> (64 - 2 * (j + k))) & kmask;
     else if (j > 0 && b0 + j < n) code = ((code << 2) | enc(seq[p + k - 1 + j])) & kmask;
     const uint32_t q = b0 + j < n ? tv.codes[code] : 0u;
@@ -1393,6 +1394,95 @@ __global__ void __launch_bounds__(64) k_approx_scan(const int64_t *__restrict__ 
   }
 }
 
+__device__ __forceinline__ void tile_of(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
+                                        int64_t nruns, int64_t t, int64_t &r, int64_t &c0, int64_t &c1) {
+  int64_t lo = 0, hi = nruns - 1;  // last run with tbase[r] <= t
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (tbase[mid] <= t) lo = mid; else hi = mid - 1;
+  }
+  r = lo;
+  c0 = cbase[lo] + (t - tbase[lo]) * 64;
+  c1 = min(c0 + 64, cbase[lo + 1]);
+}
+
+// The same prediction as k_approx_scan in three parallel steps over the
+// 64-chunk tiles of the runs (the stitch tiles): (A) every tile's composite
+// map, (B) per run a wave scan of its tiles' maps (64 tiles per step instead
+// of 64 chunks), (C) every tile applies its entry to its chunks.  The
+// composition order differs from k_approx_scan, so the FP64 results may
+// differ in the last bits: only a prediction, never a result.
+__device__ __forceinline__ void ascan_pair(double &a, double &b, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {  // (a1,b1) then (a2,b2) = (a1+a2, max(b1+a2, b2))
+    const double pa = __shfl_up(a, d, 64), pb = __shfl_up(b, d, 64);
+    if (lane >= d) {
+      b = fmax(pb + a, b);
+      a = pa + a;
+    }
+  }
+}
+__global__ void __launch_bounds__(64) k_ascan_tiles(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
+                                                    int64_t nruns, P1 o, double2 *__restrict__ tagg, int64_t t_lo) {
+  const int64_t t = t_lo + blockIdx.x;
+  const int lane = threadIdx.x;
+  int64_t r, c0, c1;
+  tile_of(tbase, cbase, nruns, t, r, c0, c1);
+  const int64_t c = c0 + lane;
+  double a = 0.0, b = -INFINITY;
+  if (c < c1) {
+    a = o.special[c] ? -INFINITY : o.asum[c];
+    b = o.cexit[c];
+  }
+  ascan_pair(a, b, lane);
+  if (lane == 63) tagg[t] = make_double2(a, b);
+}
+__global__ void __launch_bounds__(64) k_ascan_runs(const int64_t *__restrict__ tbase, int64_t nruns,
+                                                   const double2 *__restrict__ tagg, double *__restrict__ tin,
+                                                   int64_t r_lo) {
+  const int64_t r = r_lo + blockIdx.x;
+  if (r >= nruns) return;
+  const int lane = threadIdx.x;
+  const int64_t t0 = tbase[r], t1 = tbase[r + 1];
+  double carry = 0.0;
+  for (int64_t tb = t0; tb < t1; tb += 64) {
+    const int64_t t = tb + lane;
+    double a = 0.0, b = -INFINITY;
+    if (t < t1) {
+      const double2 v = tagg[t];
+      a = v.x;
+      b = v.y;
+    }
+    ascan_pair(a, b, lane);
+    double ea = __shfl_up(a, 1, 64), eb = __shfl_up(b, 1, 64);
+    if (lane == 0) { ea = 0.0; eb = -INFINITY; }
+    double xin = fmax(carry + ea, eb);
+    if (!(xin == xin)) xin = 0.0;
+    if (t < t1) tin[t] = xin;
+    const double la = __shfl(a, 63, 64), lb = __shfl(b, 63, 64);
+    carry = fmax(carry + la, lb);
+    if (!(carry == carry)) carry = 0.0;
+  }
+}
+__global__ void __launch_bounds__(64) k_ascan_apply(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
+                                                    int64_t nruns, P1 o, const double *__restrict__ tin,
+                                                    double *__restrict__ xt, int64_t t_lo) {
+  const int64_t t = t_lo + blockIdx.x;
+  const int lane = threadIdx.x;
+  int64_t r, c0, c1;
+  tile_of(tbase, cbase, nruns, t, r, c0, c1);
+  const int64_t c = c0 + lane;
+  double a = 0.0, b = -INFINITY;
+  if (c < c1) {
+    a = o.special[c] ? -INFINITY : o.asum[c];
+    b = o.cexit[c];
+  }
+  ascan_pair(a, b, lane);
+  double ea = __shfl_up(a, 1, 64), eb = __shfl_up(b, 1, 64);
+  if (lane == 0) { ea = 0.0; eb = -INFINITY; }
+  if (c < c1) xt[c] = fmax(tin[t] + ea, eb);
+}
+
 // Largest value of the predicted trajectory that keeps a binade summary
 // meaningful; below kLMin the trajectory crosses binades every few steps.
 constexpr double kLMin = 64.0;
@@ -1517,6 +1607,109 @@ __global__ void __launch_bounds__(256) k_summ_fix(Chunks g, const uint8_t *__res
       sm.M[2 * c + t] = M[t];
       sm.N[2 * c + t] = N[t];
       sm.A[2 * c + t] = A[t];
+    }
+  }
+}
+
+// Parity map of a run of steps: entry parity p -> the increment d_p of the
+// integer trajectory (exact halves round to even, so a step's increment
+// depends on the accumulator's parity).  Composition is associative.
+struct PMap {
+  long long d0, d1;
+};
+__device__ __forceinline__ PMap pm_compose(const PMap &a, const PMap &b) {  // a then b
+  return PMap{a.d0 + ((a.d0 & 1) ? b.d1 : b.d0), a.d1 + (((1 + a.d1) & 1) ? b.d1 : b.d0)};
+}
+
+// k_summ_fix with one wave per listed chunk (4 indices per lane): the values
+// through the expanded table in one or two round trips, the binade-integer
+// increments as parity maps, a wave scan of the maps, and wave reductions
+// for the total, first maximum and minimum of both entry parities -- the
+// same summary chunk_summary_impl computes serially.
+template <bool kLds>
+__global__ void __launch_bounds__(256) k_summ_fixw(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
+                                                   TableView tv, const double *__restrict__ xt,
+                                                   const int64_t *__restrict__ fix,
+                                                   const unsigned long long *__restrict__ nfix, Summ sm) {
+  __shared__ double s_lut[kLds ? kLdsLutMax : 1];
+  if (kLds) {
+    for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t nf = (int64_t)*nfix;
+  for (int64_t f = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); f < nf; f += nw) {
+    const int64_t c = fix[f];
+    const int e = binade_of(xt[c]);
+    const double scale = ldexp(1.0, 52 - e);
+    const int n = g.n[c];
+    double v[4];
+    values16_nostore<4>(g, seq, total, k, tv, c, 4 * lane, n, v, kLds ? s_lut : nullptr);
+    bool ok = true;
+    PMap lm{0, 0}, pre[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (4 * lane + q < n) {
+        const double y = v[q] * scale;  // exact: power-of-two scaling
+        ok &= fabs(y) < 2251799813685248.0;  // 2^51; false for NaN / Inf
+        const double fq = floor(y), fr = y - fq;
+        const long long qi = ok ? (long long)fq : 0;
+        const bool up = fr > 0.5, tie = fr == 0.5;
+        const PMap el{qi + ((up || (tie && (qi & 1))) ? 1 : 0), qi + ((up || (tie && ((1 + qi) & 1))) ? 1 : 0)};
+        lm = pm_compose(lm, el);
+      }
+      pre[q] = lm;
+    }
+    PMap inc = lm;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const PMap o{__shfl_up(inc.d0, d, 64), __shfl_up(inc.d1, d, 64)};
+      if (lane >= d) inc = pm_compose(o, inc);
+    }
+    PMap exc{__shfl_up(inc.d0, 1, 64), __shfl_up(inc.d1, 1, 64)};
+    if (lane == 0) exc = PMap{0, 0};
+    const PMap tot{__shfl(inc.d0, 63, 64), __shfl(inc.d1, 63, 64)};
+    ok = __all(ok);
+    long long M[2], N[2];
+    int A[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const long long et = t ? exc.d1 : exc.d0;
+      const int pt = (int)((t + et) & 1);  // parity entering this lane's first step
+      long long best = LLONG_MIN, mn = LLONG_MAX;
+      int barg = 0x7fffffff;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (4 * lane + q < n) {
+          const long long val = et + (pt ? pre[q].d1 : pre[q].d0);
+          if (val > best) { best = val; barg = 4 * lane + q; }
+          mn = min(mn, val);
+        }
+      }
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {  // max with the first index, min
+        const long long ob = __shfl_xor(best, d, 64);
+        const int oa = __shfl_xor(barg, d, 64);
+        if (ob > best || (ob == best && oa < barg)) { best = ob; barg = oa; }
+        mn = min(mn, (long long)__shfl_xor(mn, d, 64));
+      }
+      M[t] = best;
+      N[t] = mn;
+      A[t] = barg;
+    }
+    const long long lim = 4503599627370496LL;  // 2^52: partial sums exact and far from overflow
+    ok = ok && M[0] < lim && M[1] < lim && N[0] > -lim && N[1] > -lim;
+    if (lane == 0 && ok) {
+      sm.e[c] = e;
+      sm.D[2 * c] = tot.d0;
+      sm.D[2 * c + 1] = tot.d1;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        sm.M[2 * c + t] = M[t];
+        sm.N[2 * c + t] = N[t];
+        sm.A[2 * c + t] = A[t];
+      }
     }
   }
 }
@@ -2307,17 +2500,6 @@ __device__ __forceinline__ XState wave_inclusive(XState inc, int lane) {
 
 // Tile t (64 chunks of one run, aligned to the run's first chunk) -> run id
 // and first chunk.
-__device__ __forceinline__ void tile_of(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
-                                        int64_t nruns, int64_t t, int64_t &r, int64_t &c0, int64_t &c1) {
-  int64_t lo = 0, hi = nruns - 1;  // last run with tbase[r] <= t
-  while (lo < hi) {
-    const int64_t mid = (lo + hi + 1) >> 1;
-    if (tbase[mid] <= t) lo = mid; else hi = mid - 1;
-  }
-  r = lo;
-  c0 = cbase[lo] + (t - tbase[lo]) * 64;
-  c1 = min(c0 + 64, cbase[lo + 1]);
-}
 
 // Stitch as a three-phase segmented scan (tile aggregates in parallel, a
 // short per-run scan of the aggregates, then every tile again with its
@@ -2494,6 +2676,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const size_t o_spd = off; off += al(nch * 8 * 6);
   const size_t o_spa = off; off += al(nch * 4 * 2);
   const size_t o_fix = off; off += al(nch * 8 + 16);
+  const size_t o_tagg = off; off += al(ntiles * 16);  // parallel approximate scan: tile maps, tile entries
+  const size_t o_tin = off; off += al(ntiles * 8);
   void *wsp = nullptr;
   KS_TRY(ensure(ctx, SLOT_CHUNK_A, off, &wsp));
   char *W = static_cast<char *>(wsp);
@@ -2518,6 +2702,28 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                   reinterpret_cast<double *>(p + ntiles * 24)};
   };
   const XTiles xagg = xtiles(W + o_xagg), xtin = xtiles(W + o_xagg + al(ntiles * 32));
+  double2 *d_tagg = reinterpret_cast<double2 *>(W + o_tagg);
+  double *d_tin = reinterpret_cast<double *>(W + o_tin);
+  // approximate max-plus scan of (sum, clean exit) over runs [r0, r1) (tiles
+  // [t0, t1)): three parallel kernels, or the one-wave-per-run k_approx_scan
+  // with KS_SERIAL_ASCAN
+  static const bool serial_ascan = getenv("KS_SERIAL_ASCAN") != nullptr;
+  auto ascan = [&](const P1 &o, double *out, int64_t r0, int64_t r1, int64_t t0, int64_t t1,
+                   hipStream_t strm) -> ks_status {
+    if (r1 <= r0) return KS_OK;
+    if (serial_ascan || t1 <= t0) {
+      hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)(r1 - r0)), dim3(64), 0, strm, d_cbase, r1, o, out, r0);
+      KS_HIP(hipGetLastError());
+      return KS_OK;
+    }
+    hipLaunchKernelGGL(k_ascan_tiles, dim3((unsigned)(t1 - t0)), dim3(64), 0, strm, d_tbase, d_cbase, nruns, o,
+                       d_tagg, t0);
+    hipLaunchKernelGGL(k_ascan_runs, dim3((unsigned)(r1 - r0)), dim3(64), 0, strm, d_tbase, r1, d_tagg, d_tin, r0);
+    hipLaunchKernelGGL(k_ascan_apply, dim3((unsigned)(t1 - t0)), dim3(64), 0, strm, d_tbase, d_cbase, nruns, o, d_tin,
+                       out, t0);
+    KS_HIP(hipGetLastError());
+    return KS_OK;
+  };
   double *d_xh = reinterpret_cast<double *>(W + o_xh);
   long long *spd = reinterpret_cast<long long *>(W + o_spd);
   const SummP1 sp1{reinterpret_cast<int32_t *>(W + o_spe), spd, spd + 2 * nch, spd + 4 * nch,
@@ -2588,8 +2794,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     pp.asum = reinterpret_cast<double *>(W + o_pa);
     pp.cexit = reinterpret_cast<double *>(W + o_pb);
     pp.special = reinterpret_cast<uint8_t *>(W + o_pz);
-    hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)nruns), dim3(64), 0, st, d_cbase, nruns, pp, d_xh, (int64_t)0);
-    KS_HIP(hipGetLastError());
+    KS_TRY(ascan(pp, d_xh, 0, nruns, 0, ntiles, st));
   }
   KS_HIP(hipEventRecord(ctx->ev[8], st));
   const bool lds_lut = comp && tv.nlut <= kLdsLutMax && getenv("KS_NO_LDS_LUT") == nullptr;
@@ -2748,10 +2953,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     unsigned int *err_h = reinterpret_cast<unsigned int *>(d_replays + 2 * hi + 1);
     const unsigned gch_h = (unsigned)((nh + 255) / 256);
     // ---- P2 prediction, segment starts, summaries
-    if (nr > 0) {
-      hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)nr), dim3(64), 0, strm, d_cbase, h.r1, p1, xt, h.r0);
-      KS_HIP(hipGetLastError());
-    }
+    KS_TRY(ascan(p1, xt, h.r0, h.r1, h.t0, h.t1, strm));
     const int64_t wl = (h.c0 > 0 ? h.c0 - 1 : 0) / 64;
     hipLaunchKernelGGL(k_seg_marks, dim3((unsigned)((h.c1 + 63) / 64 - wl)), dim3(64), 0, strm, gv, p1, xt, d_flag);
     KS_HIP(hipGetLastError());
@@ -2761,12 +2963,23 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                          d_nfix + hi, d_xh, dbg ? reinterpret_cast<unsigned long long *>(dbg + nwin * 9) : nullptr);
       KS_HIP(hipGetLastError());
       const unsigned gf = (unsigned)std::max<int64_t>(1, std::min<int64_t>(gch_h, (int64_t)ctx->num_cus * 8));
-      if (lds_lut)
-        hipLaunchKernelGGL(k_summ_fix<true>, dim3(gf), dim3(256), 0, strm, g, s->seq, total, k, tv, xt, d_fix + h.c0,
-                           d_nfix + hi, sm);
-      else
-        hipLaunchKernelGGL(k_summ_fix<false>, dim3(gf), dim3(256), 0, strm, g, s->seq, total, k, tv, xt, d_fix + h.c0,
-                           d_nfix + hi, sm);
+      static const bool fix_serial = getenv("KS_FIX_SERIAL") != nullptr;  // A/B: lane-serial summaries
+      if (fix_serial) {
+        if (lds_lut)
+          hipLaunchKernelGGL(k_summ_fix<true>, dim3(gf), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
+                             d_fix + h.c0, d_nfix + hi, sm);
+        else
+          hipLaunchKernelGGL(k_summ_fix<false>, dim3(gf), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
+                             d_fix + h.c0, d_nfix + hi, sm);
+      } else {
+        const unsigned gw = (unsigned)std::max<int64_t>(1, (int64_t)ctx->num_cus * 8);
+        if (lds_lut)
+          hipLaunchKernelGGL(k_summ_fixw<true>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
+                             d_fix + h.c0, d_nfix + hi, sm);
+        else
+          hipLaunchKernelGGL(k_summ_fixw<false>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
+                             d_fix + h.c0, d_nfix + hi, sm);
+      }
     } else if (lds_lut)
       hipLaunchKernelGGL((k_summaries<true, true>), dim3(gch1k), dim3(1024), 0, strm, g, s->seq, total, k, tv, codes,
                          p1, xt, sm);

@@ -2014,7 +2014,9 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
   };
   TileIn cur;
   load_tile(c0, cur);
+  long long t_fast = 0, t_rep = 0;  // diagnostics: cycles in fast tiles, in replays
   for (int64_t cb = c0; cb < c1; cb += 64) {
+    const long long tt0 = dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
     TileIn nxt = cur;
     if (cb + 64 < c1) load_tile(cb + 64, nxt);
     const int64_t c = cb + lane;
@@ -2108,6 +2110,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
         x = cj_exit;
         done = true;
       }
+      const long long tr0 = dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
       if (!done) {  // exact replay of chunk cb + j from x; also yields its head
         mode = kModeU;
         ++replays;
@@ -2140,6 +2143,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
         x = hq >= 0 ? cj_exit : T;
         n_uq += hq >= 0;
         n_up += hq >= 0 ? hq + 1 : n;
+        if (dbg) t_rep += (long long)__builtin_amdgcn_s_memtime() - tr0;
       }
       if (lane == j) my_mode = mode;
       n_l += mode == kModeL;
@@ -2154,6 +2158,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
         cr.harg[c] = my_harg;
       }
     }
+    if (dbg && tile_done) t_fast += (long long)__builtin_amdgcn_s_memtime() - tt0;
     cur = nxt;
   }
   if (lane == 0 && replays) atomicAdd(nreplay, replays);
@@ -2167,8 +2172,8 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
     dbg[9 * r + 3] += 1;
     dbg[9 * r + 4] += n_l;
     dbg[9 * r + 5] += n_r;
-    dbg[9 * r + 6] += n_uq;
-    dbg[9 * r + 7] += n_up;
+    dbg[9 * r + 6] += t_fast;
+    dbg[9 * r + 7] += t_rep;
     dbg[9 * r + 8] += n_par;
   }
 }
@@ -3099,13 +3104,13 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     long long tot[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int64_t i = 0; i < nwin; ++i)
       for (int q = 0; q < 9; ++q) tot[q] += h[9 * i + q];
-    fprintf(stderr, "[carry] windows %lld (runs %lld) chunks %lld replays %lld (wave-parallel %lld, clamping %lld, "
-            "indices %lld) segments %lld L %lld R %lld\n", (long long)nwin, (long long)nruns, tot[1], tot[2], tot[8],
-            tot[6], tot[7], tot[3], tot[4], tot[5]);
+    fprintf(stderr, "[carry] windows %lld (runs %lld) chunks %lld replays %lld (wave-parallel %lld; cycles in fast tiles "
+            "%lld, in replays %lld) segments %lld L %lld R %lld\n", (long long)nwin, (long long)nruns, tot[1], tot[2],
+            tot[8], tot[6], tot[7], tot[3], tot[4], tot[5]);
     for (int64_t i = 0; i < std::min<int64_t>(nwin, 8); ++i) {
       const long long *d = &h[9 * idx[i]];
-      fprintf(stderr, "[carry] window %lld cycles %lld chunks %lld replays %lld segments %lld L %lld R %lld\n",
-              (long long)idx[i], d[0], d[1], d[2], d[3], d[4], d[5]);
+      fprintf(stderr, "[carry] window %lld cycles %lld (fast tiles %lld, replays %lld) chunks %lld replays %lld "
+              "segments %lld L %lld R %lld\n", (long long)idx[i], d[0], d[6], d[7], d[1], d[2], d[3], d[4], d[5]);
     }
   }
   if (errbits & ~16u) return fail(KS_ERR_INTERNAL, "chunked scan consistency check failed (bits %u)", errbits);

@@ -233,15 +233,16 @@ __global__ void __launch_bounds__(256) k_count_multi(const uint8_t *__restrict__
 // bound at ~20 G adds/s.  Instead the 2k-bit code is split into a bucket
 // (top T bits) and a bin (low L bits; 2^L counters fit LDS), and the k-mers
 // are partitioned by bucket before each bucket is histogrammed in LDS.
-// The partition is written through L2: a block appends to at most 256
-// bucket tails at a time, so the open lines of all blocks of an XCD fit its
-// L2 and leave it whole.  Hence two levels when T > 8:
-//   L1 k_part<1>   per block: LDS histogram of the top 8 bits -> mat[b][block]
+// Each tile of 16K positions is counting-sorted by bucket in LDS before it
+// is written, so a block appends runs (not single items) to at most 2048
+// bucket tails.  One level up to k = 13 (2k - 15 <= 11 bucket bits), two
+// levels beyond:
+//   L1 k_part<1>   per block: LDS histogram of the top 11 bits -> mat[b][block]
 //                  (exclusive sum over mat: each block's cursor per bucket)
-//      k_part<2>   same positions, same blocks: append the code's low
-//                  2k - 8 bits (u32; u16 when single-level) to its bucket
+//      k_part_scatter  same positions, same blocks: append the code's low
+//                  2k - 11 bits (u32; u16 when single-level) to its bucket
 //   L2 k_sub<1/2>  per level-1 bucket, C chunks: the same two passes on the
-//                  next T - 8 bits, appending the bin (u16)
+//                  next T - 11 bits, appending the bin (u16)
 //   k_bins         one block per final bucket (or a share of one): LDS
 //                  histogram of the bins, counts[bucket << L | bin] += h
 // The k-mer test (runs, Q1) is the same code as k_count.
@@ -249,7 +250,7 @@ constexpr int kPartMinK = 11;
 constexpr int kPT = 1024;            // threads per block
 constexpr int kPTile = kPT * kPer;   // positions per tile
 constexpr int kPBlocks = 512;        // persistent blocks, level 1
-constexpr int kT1 = 8;               // level-1 bucket bits
+constexpr int kT1 = 11;              // level-1 bucket bits (2048 buckets: one level up to k = 13)
 constexpr int kSubChunks = 8;        // level-2 blocks per level-1 bucket
 
 struct PartGeo {
@@ -257,7 +258,7 @@ struct PartGeo {
 };
 inline PartGeo part_geo(int k) {
   const int B = 2 * k;
-  const int L = B <= 14 ? B : (B >= 30 ? 15 : 14);
+  const int L = B <= 15 ? B : 15;  // 2^15 u32 bins = 128 KiB of LDS per k_bins block
   const int T = B - L;
   const int T1 = T < kT1 ? T : kT1;
   return {L, T, T1, T - T1};
@@ -368,9 +369,10 @@ __global__ void __launch_bounds__(kPT) k_part_scatter(const uint8_t *__restrict_
                                                       Item *__restrict__ part, int64_t ntiles) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
   Item *sorted = reinterpret_cast<Item *>(dyn);               // [kPTile]
-  uint8_t *bkt = dyn + sizeof(Item) * kPTile;                 // [kPTile]
+  uint16_t *bkt = reinterpret_cast<uint16_t *>(dyn + sizeof(Item) * kPTile);  // [kPTile]
   __shared__ unsigned long long cur[1 << kT1];
   __shared__ uint32_t cnt[1 << kT1], off[1 << kT1];
+  __shared__ uint32_t wtot[kPT / 64];
   __shared__ uint32_t bmask[(kPTile + kLook + 32) / 32 + 1];
   const int nb = 1 << (2 * k - shift);
   const int G = gridDim.x;
@@ -441,24 +443,40 @@ __global__ void __launch_bounds__(kPT) k_part_scatter(const uint8_t *__restrict_
       }
     }
     __syncthreads();
-    if (threadIdx.x < 64) {  // exclusive scan of the (<= 256) bucket counts
-      uint32_t v[4], sum = 0;
+    {  // exclusive scan of the (<= 2048) bucket counts: two per thread, wave
+       // scans, then the 16 wave totals
+      constexpr int kPerT = (1 << kT1) / kPT;
+      static_assert(kPerT * kPT == (1 << kT1), "buckets per thread");
+      uint32_t v[kPerT], sum = 0;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int bi = threadIdx.x * 4 + i;
+      for (int i = 0; i < kPerT; ++i) {
+        const int bi = threadIdx.x * kPerT + i;
         v[i] = bi < nb ? cnt[bi] : 0;
         sum += v[i];
       }
+      const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
       uint32_t inc = sum;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
         const uint32_t o = __shfl_up(inc, d, 64);
-        if ((int)threadIdx.x >= d) inc += o;
+        if (lane >= d) inc += o;
       }
-      uint32_t run = inc - sum;
+      if (lane == 63) wtot[wv] = inc;
+      __syncthreads();
+      if (threadIdx.x < 64) {
+        uint32_t t = threadIdx.x < kPT / 64 ? wtot[threadIdx.x] : 0, ti = t;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int bi = threadIdx.x * 4 + i;
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t o = __shfl_up(ti, d, 64);
+          if ((int)threadIdx.x >= d) ti += o;
+        }
+        if (threadIdx.x < kPT / 64) wtot[threadIdx.x] = ti - t;  // exclusive
+      }
+      __syncthreads();
+      uint32_t run = wtot[wv] + inc - sum;
+#pragma unroll
+      for (int i = 0; i < kPerT; ++i) {
+        const int bi = threadIdx.x * kPerT + i;
         if (bi < nb) off[bi] = run;
         run += v[i];
       }
@@ -469,7 +487,7 @@ __global__ void __launch_bounds__(kPT) k_part_scatter(const uint8_t *__restrict_
       if (br[j] != ~0u) {
         const uint32_t bk = br[j] >> 16, pos = off[bk] + (br[j] & 0xffffu);
         sorted[pos] = (Item)pay[j];
-        bkt[pos] = (uint8_t)bk;
+        bkt[pos] = (uint16_t)bk;
       }
     __syncthreads();
     const uint32_t n_items = off[nb - 1] + cnt[nb - 1];
@@ -680,13 +698,13 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   hipLaunchKernelGGL(k_part_sum_last, dim3(1), dim3(1), 0, st, mat1, ex1, m1, last);
   hipLaunchKernelGGL(k_part_starts, dim3((nb1 + 1 + 255) / 256), dim3(256), 0, st, ex1, G, nb1, s1, last);
   if (g.T2) {
-    const size_t lds = (size_t)kPTile * 5;
+    const size_t lds = (size_t)kPTile * (4 + 2);  // items + u16 bucket tags
     KS_HIP(hipFuncSetAttribute((const void *)k_part_scatter<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
     hipLaunchKernelGGL(k_part_scatter<uint32_t>, dim3(G), dim3(kPT), lds, st, s->seq, total, s->offsets_dev, s->nseq,
                        k, shift, ex1, static_cast<uint32_t *>(p1), ntiles);
   } else {
-    const size_t lds = (size_t)kPTile * 3;
+    const size_t lds = (size_t)kPTile * (2 + 2);
     KS_HIP(hipFuncSetAttribute((const void *)k_part_scatter<uint16_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
     hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(G), dim3(kPT), lds, st, s->seq, total, s->offsets_dev, s->nseq,

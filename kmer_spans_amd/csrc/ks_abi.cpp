@@ -183,7 +183,10 @@ extern "C" ks_status ks_ctx_create(int32_t device, ks_ctx **out) {
   KS_HIP(hipGetDeviceProperties(&prop, device));
   c->num_cus = prop.multiProcessorCount;
   for (auto &e : c->ev) KS_HIP(hipEventCreate(&e));
-  KS_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  int least = 0, greatest = 0;
+  KS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  KS_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, least));
+  KS_HIP(hipStreamCreateWithPriority(&c->hi, hipStreamNonBlocking, greatest));
   *out = c;
   return KS_OK;
 }
@@ -198,10 +201,11 @@ extern "C" void ks_ctx_destroy(ks_ctx *c) {
   if (c->pinned) (void)hipHostFree(c->pinned);
   for (auto &e : c->ev)
     if (e) (void)hipEventDestroy(e);
-  if (c->side) {
-    (void)hipStreamSynchronize(c->side);
-    (void)hipStreamDestroy(c->side);
-  }
+  for (hipStream_t x : {c->side, c->hi})
+    if (x) {
+      (void)hipStreamSynchronize(x);
+      (void)hipStreamDestroy(x);
+    }
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

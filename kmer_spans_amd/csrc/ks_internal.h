@@ -82,8 +82,9 @@ struct ks_ctx {
   // pinned host staging
   void *pinned = nullptr;
   size_t pinned_bytes = 0;
-  hipEvent_t ev[16] = {};
-  hipStream_t side = nullptr;  // forked work that overlaps the main stream (joined by events)
+  hipEvent_t ev[20] = {};
+  hipStream_t side = nullptr;  // forked work that overlaps the main stream (joined by events; lowest priority)
+  hipStream_t hi = nullptr;    // highest-priority stream: the first half's pass 1 (ks_scan_chunked.hip)
   int64_t rescan_segcap = 0;  // grow-only rescan capacity per segment (tr_lr rescans outnumber regions)
 };
 

@@ -194,11 +194,11 @@ __global__ void k_run_counts(const int64_t *__restrict__ ra, const int64_t *__re
   }
 }
 
-// The run where the first half of the chunks ends: first r with
-// cbase[r] >= cbase[n] / 2 (out: r, cbase[r], tbase[r]).
+// The run where the first part of the chunks ends: first r with
+// cbase[r] >= frac * cbase[n] (out: r, cbase[r], tbase[r]).
 __global__ void k_split(const int64_t *__restrict__ cbase, const int64_t *__restrict__ tbase, int64_t n,
-                        unsigned long long *__restrict__ out) {
-  const int64_t half = cbase[n] / 2;
+                        double frac, unsigned long long *__restrict__ out) {
+  const int64_t half = (int64_t)((double)cbase[n] * frac);
   int64_t lo = 0, hi = n;
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
@@ -235,7 +235,10 @@ ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int t
   KS_TRY(ensure(ctx, SLOT_SORT_TMP, tb, &tmp));
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt_c, lay->cbase, (int)(n + 1), st));
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt_t, lay->tbase, (int)(n + 1), st));
-  hipLaunchKernelGGL(k_split, dim3(1), dim3(1), 0, st, lay->cbase, lay->tbase, n, agg + 3);
+  // the first half (highest priority) ends first; its carry and stitch run
+  // under the rest of the second half (KS_SPLIT_FRAC: A/B, tools/ab_inproc.py)
+  const double frac = getenv("KS_SPLIT_FRAC") ? atof(getenv("KS_SPLIT_FRAC")) : 0.7;
+  hipLaunchKernelGGL(k_split, dim3(1), dim3(1), 0, st, lay->cbase, lay->tbase, n, frac, agg + 3);
   KS_HIP(hipGetLastError());
   int64_t h[2] = {0, 0};
   unsigned long long ha[6] = {0, 0, 0, 0, 0, 0};

@@ -385,7 +385,7 @@ __global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k
   __syncthreads();
   const uint32_t pmask = (uint32_t)np - 1u;
   const uint32_t *__restrict__ packed = g.packed;
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < g.nch;
+  for (int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < g.nch;
        c += (int64_t)gridDim.x * blockDim.x) {
     const int64_t start = g.start[c];
     const int n = g.n[c];
@@ -2789,20 +2789,6 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const bool p1summ = comp && Jt >= 2 && !lds_table && runs.packed != nullptr && tv.approx != nullptr &&
                       !kP1NoStore && getenv("KS_NO_P1_SUMMARY") == nullptr &&
                       getenv("KS_NO_PIPELINED_P1") == nullptr;
-  if (p1summ) {  // P0: predicted entries
-    KS_HIP(hipMemsetAsync(W + o_pz, 0, nch, st));
-    const unsigned gl = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nch + 1023) / 1024, ctx->num_cus));
-    hipLaunchKernelGGL(k_predict, dim3(gl), dim3(1024), 0, st, g, total, k, tv.approx, tv.approx_k,
-                       reinterpret_cast<double *>(W + o_pa), reinterpret_cast<double *>(W + o_pb));
-    KS_HIP(hipGetLastError());
-    P1 pp = p1;
-    pp.asum = reinterpret_cast<double *>(W + o_pa);
-    pp.cexit = reinterpret_cast<double *>(W + o_pb);
-    pp.special = reinterpret_cast<uint8_t *>(W + o_pz);
-    KS_TRY(ascan(pp, d_xh, 0, nruns, 0, ntiles, st));
-  }
-  KS_HIP(hipEventRecord(ctx->ev[8], st));
-  const bool lds_lut = comp && tv.nlut <= kLdsLutMax && getenv("KS_NO_LDS_LUT") == nullptr;
   // Two halves of the runs (pass-1-summary path): the second half's pass 1
   // (side stream) runs while the first half's latency-bound later passes
   // (carry, stitch) run on the main stream; halves split at a run boundary,
@@ -2827,6 +2813,35 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     v.nch = h.c1;
     return v;
   };
+  bool side_forked = false;  // the side stream already waits for the chunks (P0 overlap)
+  if (p1summ) {  // P0: predicted entries of each half (the second half's on the side stream, under
+                 // the first half's predictor and pass 1)
+    P1 pp = p1;
+    pp.asum = reinterpret_cast<double *>(W + o_pa);
+    pp.cexit = reinterpret_cast<double *>(W + o_pb);
+    pp.special = reinterpret_cast<uint8_t *>(W + o_pz);
+    auto predict = [&](const Half &h, hipStream_t strm) -> ks_status {
+      KS_HIP(hipMemsetAsync(W + o_pz + h.c0, 0, (size_t)(h.c1 - h.c0), strm));
+      const unsigned gl =
+          (unsigned)std::max<int64_t>(1, std::min<int64_t>((h.c1 - h.c0 + 1023) / 1024, ctx->num_cus));
+      hipLaunchKernelGGL(k_predict, dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx, tv.approx_k,
+                         pp.asum, pp.cexit);
+      KS_HIP(hipGetLastError());
+      return ascan(pp, d_xh, h.r0, h.r1, h.t0, h.t1, strm);
+    };
+    if (split) {  // KS_NO_P0_OVERLAP (A/B): both halves' predictors on the main stream
+      const bool ov = getenv("KS_NO_P0_OVERLAP") == nullptr;
+      side_forked = ov;
+      if (ov) {
+        KS_HIP(hipEventRecord(ctx->ev[16], st));
+        KS_HIP(hipStreamWaitEvent(ctx->side, ctx->ev[16], 0));
+      }
+      KS_TRY(predict(halves[1], ov ? ctx->side : st));
+    }
+    KS_TRY(predict(halves[0], st));
+  }
+  KS_HIP(hipEventRecord(ctx->ev[8], st));
+  const bool lds_lut = comp && tv.nlut <= kLdsLutMax && getenv("KS_NO_LDS_LUT") == nullptr;
 #define KS_P1(J, C, L)                                                                                       \
   hipLaunchKernelGGL((k_pass1<J, C, L>), dim3(J == 1 ? gch : gch1k), dim3(J == 1 ? 256 : 1024), 0, st, g, s->seq, \
                      total, k, tv, codes, ec, visits, p1, cand, (int64_t)0, 0)
@@ -2879,12 +2894,26 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       }
     };
     if (split) {
-      // first half on the main stream; the side stream waits for it, then
-      // runs the tail chunks and the second half (pass 1 end = ev[9] on side)
-      p1p(halves[0], st);
-      KS_HIP(hipGetLastError());
-      KS_HIP(hipEventRecord(ctx->ev[12], st));
-      KS_HIP(hipStreamWaitEvent(side, ctx->ev[12], 0));
+      // first half on the highest-priority stream, the tail chunks and the
+      // second half on the (lowest-priority) side stream at once: the second
+      // half's blocks fill the CUs the first half leaves, its drain included,
+      // and the first half ends first (its carry and stitch then run under
+      // the rest of the second half).  KS_P1_SERIAL_HALVES (A/B): the side
+      // stream waits for the first half (pass 1 end = ev[9] on side).
+      if (getenv("KS_P1_SERIAL_HALVES") == nullptr) {
+        KS_HIP(hipEventRecord(ctx->ev[17], st));
+        KS_HIP(hipStreamWaitEvent(ctx->hi, ctx->ev[17], 0));
+        if (!side_forked) KS_HIP(hipStreamWaitEvent(side, ctx->ev[17], 0));
+        p1p(halves[0], ctx->hi);
+        KS_HIP(hipGetLastError());
+        KS_HIP(hipEventRecord(ctx->ev[12], ctx->hi));
+        KS_HIP(hipStreamWaitEvent(st, ctx->ev[12], 0));
+      } else {
+        p1p(halves[0], st);
+        KS_HIP(hipGetLastError());
+        KS_HIP(hipEventRecord(ctx->ev[12], st));
+        KS_HIP(hipStreamWaitEvent(side, ctx->ev[12], 0));
+      }
       if (tail) {
         if (J == 5) KS_P1T(5, false);
         else if (lds_lut) { if (J == 4) KS_P1T(4, true); else if (J == 3) KS_P1T(3, true); else KS_P1T(2, true); }
@@ -2943,7 +2972,14 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
 #undef KS_P1TC
 #undef KS_P1P
   KS_HIP(hipGetLastError());
-  KS_HIP(hipEventRecord(ctx->ev[9], split ? ctx->side : st));  // end of pass 1 (the last half's stream)
+  if (split && getenv("KS_P1_SERIAL_HALVES") == nullptr) {
+    // end of pass 1 = the later of the halves: the hi stream (idle now) joins the side stream's
+    KS_HIP(hipEventRecord(ctx->ev[18], ctx->side));
+    KS_HIP(hipStreamWaitEvent(ctx->hi, ctx->ev[18], 0));
+    KS_HIP(hipEventRecord(ctx->ev[9], ctx->hi));
+  } else {
+    KS_HIP(hipEventRecord(ctx->ev[9], split ? ctx->side : st));  // end of pass 1 (the last half's stream)
+  }
 
   // P2-P5 (without the candidates) of one half on stream strm, with its own
   // replay counter, error bits and fix list; ev[14] / ev[15] mark the last

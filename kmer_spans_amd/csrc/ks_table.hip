@@ -334,11 +334,17 @@ void pool_give(int dev, void *p, size_t bytes) {
 // KS_NO_CONTIG_EXT=1 keeps the plain allocation.
 static hipError_t ext_malloc(void **p, size_t bytes) {
   static const bool contig = !getenv("KS_NO_CONTIG_EXT");
+  static const bool dbg = getenv("KS_DEBUG_ALLOC") != nullptr;
   if (contig && bytes >= ((size_t)1 << 30)) {
-    if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
+    if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) {
+      if (dbg) fprintf(stderr, "[ext alloc] contiguous %zu bytes at %p\n", bytes, *p);
+      return hipSuccess;
+    }
     (void)hipGetLastError();
   }
-  return hipMalloc(p, bytes);
+  const hipError_t e = hipMalloc(p, bytes);
+  if (dbg) fprintf(stderr, "[ext alloc] plain %zu bytes at %p (%d)\n", bytes, *p, (int)e);
+  return e;
 }
 
 // Tables whose chunked scan predicts carry binades before pass 1: compressed

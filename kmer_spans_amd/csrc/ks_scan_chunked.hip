@@ -377,6 +377,7 @@ __global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__r
 // bases; a max-plus scan of them (k_approx_scan) predicts each chunk's entry,
 // i.e. the binade pass 1 summarises in.  Only a prediction: a wrong binade
 // costs one gathered summary (k_summ_fix), never a result.
+template <int PS>
 __global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k, const uint16_t *__restrict__ approx, int kp,
                                                   double *__restrict__ pa, double *__restrict__ pb) {
   __shared__ __half s_ap[1 << 16];
@@ -404,12 +405,8 @@ __global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k
     for (int t = 0; t < 16; ++t) {
       if (16 * t < n) {
         const uint64_t x = ((((uint64_t)wd[t] << 32) | wd[t + 1]) << bp) | (((uint64_t)wd[t + 2] << bp) >> 32);
-#ifndef KS_PRED_STRIDE
-#define KS_PRED_STRIDE 2
-#endif
         // every PS-th index, weighted PS (A/B: PS = 2 cuts the predictor 1.11 -> 0.80 ms with the
         // same 16.2 K gathered summaries at the metric config)
-        constexpr int PS = KS_PRED_STRIDE;
         float a[16 / PS];
 #pragma unroll
         for (int j = 0; j < 16; j += PS)
@@ -2824,8 +2821,16 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipMemsetAsync(W + o_pz + h.c0, 0, (size_t)(h.c1 - h.c0), strm));
       const unsigned gl =
           (unsigned)std::max<int64_t>(1, std::min<int64_t>((h.c1 - h.c0 + 1023) / 1024, ctx->num_cus));
-      hipLaunchKernelGGL(k_predict, dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx, tv.approx_k,
-                         pp.asum, pp.cexit);
+      const int ps = getenv("KS_PRED_PS") ? atoi(getenv("KS_PRED_PS")) : 2;
+      if (ps == 4)
+        hipLaunchKernelGGL(k_predict<4>, dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx, tv.approx_k,
+                           pp.asum, pp.cexit);
+      else if (ps == 8)
+        hipLaunchKernelGGL(k_predict<8>, dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx, tv.approx_k,
+                           pp.asum, pp.cexit);
+      else
+        hipLaunchKernelGGL(k_predict<2>, dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx, tv.approx_k,
+                           pp.asum, pp.cexit);
       KS_HIP(hipGetLastError());
       return ascan(pp, d_xh, h.r0, h.r1, h.t0, h.t1, strm);
     };
@@ -3013,8 +3018,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
           hipLaunchKernelGGL(k_summ_fix<false>, dim3(gf), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
                              d_fix + h.c0, d_nfix + hi, sm);
       } else {
+        // LUT reads through L2, not staged in LDS: a 54 KB LDS copy per block
+        // (2048 blocks, most without a listed chunk) cost more than the ~4 M
+        // lookups of the ~16 K listed chunks (KS_FIXW_LDS: A/B)
         const unsigned gw = (unsigned)std::max<int64_t>(1, (int64_t)ctx->num_cus * 8);
-        if (lds_lut)
+        if (lds_lut && getenv("KS_FIXW_LDS") != nullptr)
           hipLaunchKernelGGL(k_summ_fixw<true>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
                              d_fix + h.c0, d_nfix + hi, sm);
         else

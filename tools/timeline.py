@@ -11,6 +11,7 @@ for r in rows[i0:]:
     s, e = int(r['Start_Timestamp']), int(r['End_Timestamp'])
     m = re.search(r'(k_\w+|rocprim|__amd_rocclr_\w+)', r['Kernel_Name'])
     name = m.group(1) if m else r['Kernel_Name'][:40]
-    print(f"{(s - t0) / 1e3:9.1f} us  gap {(s - prev) / 1e3:7.1f}  dur {(e - s) / 1e3:8.1f}  {name}")
-    busy += e - s; prev = e
+    q = r.get('Queue_Id') or ''
+    print(f"{(s - t0) / 1e3:9.1f} us  end {(e - t0) / 1e3:9.1f}  dur {(e - s) / 1e3:8.1f}  q{q:>3}  {name}")
+    busy += e - s; prev = max(prev, e)
 print(f"span {(prev - t0) / 1e3:.1f} us, busy {busy / 1e3:.1f} us")

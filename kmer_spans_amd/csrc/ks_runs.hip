@@ -207,6 +207,8 @@ __global__ void k_split(const int64_t *__restrict__ cbase, const int64_t *__rest
   out[0] = (unsigned long long)lo;
   out[1] = (unsigned long long)cbase[lo];
   out[2] = (unsigned long long)tbase[lo];
+  out[3] = (unsigned long long)cbase[n];  // totals: one readback with the aggregates
+  out[4] = (unsigned long long)tbase[n];
 }
 
 }  // namespace
@@ -240,14 +242,11 @@ ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int t
   const double frac = getenv("KS_SPLIT_FRAC") ? atof(getenv("KS_SPLIT_FRAC")) : 0.7;
   hipLaunchKernelGGL(k_split, dim3(1), dim3(1), 0, st, lay->cbase, lay->tbase, n, frac, agg + 3);
   KS_HIP(hipGetLastError());
-  int64_t h[2] = {0, 0};
-  unsigned long long ha[6] = {0, 0, 0, 0, 0, 0};
-  KS_HIP(hipMemcpyAsync(&h[0], lay->cbase + n, 8, hipMemcpyDeviceToHost, st));
-  KS_HIP(hipMemcpyAsync(&h[1], lay->tbase + n, 8, hipMemcpyDeviceToHost, st));
-  KS_HIP(hipMemcpyAsync(ha, agg, 48, hipMemcpyDeviceToHost, st));
+  unsigned long long ha[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  KS_HIP(hipMemcpyAsync(ha, agg, 64, hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
-  lay->nch = h[0];
-  lay->ntiles = h[1];
+  lay->nch = (int64_t)ha[6];
+  lay->ntiles = (int64_t)ha[7];
   lay->scored = (int64_t)ha[0];
   lay->nscan = (int64_t)ha[1];
   lay->longest = (int64_t)ha[2];

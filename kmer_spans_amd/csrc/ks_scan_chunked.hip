@@ -397,8 +397,28 @@ __global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k
     // with the batches unrolled so the words stay in registers
     const int64_t w0 = q0 >> 4, last = total >> 4;
     uint32_t wd[18];
+    const int64_t wa = w0 & ~(int64_t)3;
+    if (wa + 20 <= last + 1) {
+      // five aligned 16-B loads (a quarter of the requests of 18 word loads:
+      // the lanes of a wave read 64 different lines per instruction), then
+      // the 18 words at offset w0 - wa selected in registers
+      uint32_t a[20];
+      const uint4 *P4 = reinterpret_cast<const uint4 *>(packed + wa);
 #pragma unroll
-    for (int t = 0; t < 18; ++t) wd[t] = packed[min(w0 + t, last)];
+      for (int t = 0; t < 5; ++t) {
+        const uint4 v = P4[t];
+        a[4 * t] = v.x;
+        a[4 * t + 1] = v.y;
+        a[4 * t + 2] = v.z;
+        a[4 * t + 3] = v.w;
+      }
+      const int o = (int)(w0 - wa);
+#pragma unroll
+      for (int t = 0; t < 18; ++t) wd[t] = o == 0 ? a[t] : (o == 1 ? a[t + 1] : (o == 2 ? a[t + 2] : a[t + 3]));
+    } else {
+#pragma unroll
+      for (int t = 0; t < 18; ++t) wd[t] = packed[min(w0 + t, last)];
+    }
     const uint32_t bp = 2u * (uint32_t)(q0 & 15);
     float tsum = 0.f, tex = 0.f;
 #pragma unroll
@@ -2834,6 +2854,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipGetLastError());
       return ascan(pp, d_xh, h.r0, h.r1, h.t0, h.t1, strm);
     };
+    // the first half's predictor and prescan first (they gate its pass 1;
+    // the predictor holds whole CUs: 128 KiB of LDS per block), then the
+    // second half's on the side stream, under the first half's pass 1
+    KS_TRY(predict(halves[0], st));
     if (split) {  // KS_NO_P0_OVERLAP (A/B): both halves' predictors on the main stream
       const bool ov = getenv("KS_NO_P0_OVERLAP") == nullptr;
       side_forked = ov;
@@ -2843,7 +2867,6 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       }
       KS_TRY(predict(halves[1], ov ? ctx->side : st));
     }
-    KS_TRY(predict(halves[0], st));
   }
   KS_HIP(hipEventRecord(ctx->ev[8], st));
   const bool lds_lut = comp && tv.nlut <= kLdsLutMax && getenv("KS_NO_LDS_LUT") == nullptr;

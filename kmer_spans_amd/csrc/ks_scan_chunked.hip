@@ -87,6 +87,21 @@ struct Carry {  // P3/P4
   int32_t *harg;
 };
 
+// Composites of the global 64-chunk tiles (chunks [64t, 64t + 64)) for the
+// carry's tile batches: k_tile_comp writes, per tile whose chunks all have a
+// summary in one binade e, the composed increment D_p of the tile and the
+// interval [LO_p, HI_p] of entry mantissas (parity p) for which every
+// chunk's trajectory stays inside the binade -- exactly the fast-tile test
+// of carry_segment, reduced over the tile.  em / ee: the entry mantissa and
+// binade of each tile the carry accepted in a batch (ee = INT32_MIN: not
+// batched), expanded per chunk by k_tile_apply.
+struct TileComp {
+  int32_t *e;                // [tiles] binade, INT32_MIN: no composite
+  long long *D, *LO, *HI;    // [2 * tiles] by entry parity
+  long long *em;             // [tiles]
+  int32_t *ee;               // [tiles]
+};
+
 struct Cand {  // closed emittable excursions of the clean trajectories (segmented append)
   long long *beg, *arg, *rst;
   double *best;
@@ -1993,7 +2008,8 @@ template <bool kCompressed>
 __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64_t c1, const uint8_t *__restrict__ seq,
                                               int64_t total, int k, const TableView &tv,
                                               const uint16_t *__restrict__ codes, const P1 &o, const Summ &sm,
-                                              const Carry &cr, unsigned long long *__restrict__ nreplay,
+                                              const Carry &cr, const TileComp &tc,
+                                              unsigned long long *__restrict__ nreplay,
                                               unsigned int *__restrict__ err, long long *__restrict__ dbg,
                                               int64_t r) {
   const int lane = threadIdx.x;
@@ -2010,9 +2026,9 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
     long long D[2], M[2], N[2];
     int A[2];
   };
-  auto load_tile = [&](int64_t cb, TileIn &t) {
+  auto load_tile = [&](int64_t cb, int64_t ce, TileIn &t) {
     const int64_t c = cb + lane;
-    const bool live = c < c1;
+    const bool live = c < ce;
     const int64_t cc = live ? c : c0;  // dead lanes read a valid chunk, values unused
     t.exit = o.cexit[cc];
     t.pmin = o.pmin[cc];
@@ -2029,15 +2045,79 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
       t.A[q] = sm.A[2 * cc + q];
     }
   };
+  // tiles are the global 64-chunk tiles (partial at the segment's ends)
+  auto tile_end = [&](int64_t cb) { return min(c1, (cb & ~(int64_t)63) + 64); };
   TileIn cur;
-  load_tile(c0, cur);
+  load_tile(c0, tile_end(c0), cur);
   long long t_fast = 0, t_rep = 0;  // diagnostics: cycles in fast tiles, in replays
-  for (int64_t cb = c0; cb < c1; cb += 64) {
+  bool try_batch = true;
+  for (int64_t cb = c0; cb < c1;) {
     const long long tt0 = dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
+    // Tile batch: up to 64 whole tiles at once from their composites (the
+    // serial fast path's test per tile, with the entries of all of them from
+    // one wave scan of the composed increments); accepted tiles are expanded
+    // per chunk by k_tile_apply.  The first rejected tile takes the per-tile
+    // path below.
+    if (tc.e && try_batch && (cb & 63) == 0 && x >= kLMin && x < 1.0e18) {
+      const int e = binade_of(x);
+      const int64_t ntl = min((int64_t)64, (c1 - cb) >> 6);
+      if (e >= 6 && e <= 58 && ntl >= 2) {
+        const int64_t t = (cb >> 6) + lane;
+        const bool in = lane < ntl;
+        const int te = in ? tc.e[t] : INT32_MIN;
+        long long d0 = 0, d1 = 0, lo0 = 0, lo1 = 0, hi0 = -1, hi1 = -1;
+        if (in) {
+          d0 = tc.D[2 * t];
+          d1 = tc.D[2 * t + 1];
+          lo0 = tc.LO[2 * t];
+          lo1 = tc.LO[2 * t + 1];
+          hi0 = tc.HI[2 * t];
+          hi1 = tc.HI[2 * t + 1];
+        }
+        if (!in || te != e) d0 = d1 = 0;  // identity beyond the first rejected tile (never used)
+        long long i0 = d0, i1 = d1;  // inclusive composed increments
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const long long p0 = __shfl_up(i0, d, 64), p1 = __shfl_up(i1, d, 64);
+          if (lane >= d) {
+            const long long n0 = p0 + ((p0 & 1) ? i1 : i0);
+            const long long n1 = p1 + (((1 + p1) & 1) ? i1 : i0);
+            i0 = n0;
+            i1 = n1;
+          }
+        }
+        long long x0 = __shfl_up(i0, 1, 64), x1 = __shfl_up(i1, 1, 64);
+        if (lane == 0) { x0 = 0; x1 = 0; }
+        const long long m0 = mant_of(x);
+        const long long mt = m0 + ((m0 & 1) ? x1 : x0);  // entry mantissa of tile t
+        const int pt = (int)(mt & 1);
+        const bool ok = in && te == e && mt >= (pt ? lo1 : lo0) && mt <= (pt ? hi1 : hi0);
+        const unsigned long long bad = __ballot(!ok);
+        const int f = bad ? __ffsll((long long)bad) - 1 : 64;
+        if (f > 0) {
+          if (lane < f) {
+            tc.em[t] = mt;
+            tc.ee[t] = e;
+          }
+          const long long mi = m0 + ((m0 & 1) ? i1 : i0);  // exit of tile t
+          x = from_mant(rl64(mi, f - 1), e);
+          n_l += 64 * f;
+          cb += 64 * f;
+          if (dbg) t_fast += (long long)__builtin_amdgcn_s_memtime() - tt0;
+          if (cb >= c1) break;
+          load_tile(cb, tile_end(cb), cur);
+          try_batch = f == 64;  // a rejected tile goes through the per-tile path first
+          continue;
+        }
+      }
+    }
+    try_batch = true;
+    const int64_t ce = tile_end(cb);
+    if (lane == 0 && tc.ee) tc.ee[cb >> 6] = INT32_MIN;  // not batched (the fallback pass reruns segments)
     TileIn nxt = cur;
-    if (cb + 64 < c1) load_tile(cb + 64, nxt);
+    if (ce < c1) load_tile(ce, tile_end(ce), nxt);
     const int64_t c = cb + lane;
-    const bool live = c < c1;
+    const bool live = c < ce;
     const double l_exit = live ? cur.exit : 0.0;
     const double l_pmin = live ? cur.pmin : 0.0;
     const double l_sabs = live ? cur.sabs : 0.0;
@@ -2055,17 +2135,21 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
         A[t] = cur.A[t];
       }
     }
-    const int nb = (int)min((int64_t)64, c1 - cb);
+    const int nb = (int)(ce - cb);
     double my_x = 0.0, my_hmax = -1.0;
     int my_mode = kModeClean, my_harg = 0, my_hq = -1;
-    // Tile fast path: every chunk has a summary for the binade of the tile's
-    // exact entry -> compose the 64 integer maps m -> m + D[m & 1] with a wave
-    // scan, then check each chunk's trajectory bounds at its exact entry.
-    bool tile_done = false;
-    if (x >= kLMin && x < 1.0e18) {
-      const int e = binade_of(x);
-      if (__all(!live || se == e)) {
-        long long i0 = live ? D[0] : 0, i1 = live ? D[1] : 0;  // inclusive composed map
+    // Runs of summary chunks: from chunk j on, the chunks that have a summary
+    // for the binade of the exact carry and stay inside it are taken at once:
+    // their integer maps m -> m + D[m & 1] composed by a wave scan (chunks
+    // before j and past the tile: identity), each checked at its exact entry.
+    // The first other chunk takes the serial step.  (A fast tile is one run
+    // from j = 0; a replay in mid-tile no longer walks the rest serially.)
+    bool tile_done = true;  // diagnostics: no serial step in this tile
+    for (int j = 0; j < nb; ++j) {
+      if (x >= kLMin && x < 1.0e18 && rl32(se, j) == binade_of(x)) {
+        const int e = binade_of(x);
+        const bool in = live && lane >= j;
+        long long i0 = in ? D[0] : 0, i1 = in ? D[1] : 0;  // inclusive composed map
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
           const long long p0 = __shfl_up(i0, d, 64), p1 = __shfl_up(i1, d, 64);
@@ -2081,23 +2165,24 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
         const long long m0 = mant_of(x);
         const long long mj = m0 + ((m0 & 1) ? x1 : x0);  // exact entry of this lane's chunk
         const int pj = (int)(mj & 1);
-        const bool ok = !live || (mj + (pj ? N[1] : N[0]) >= (1LL << 52) + 1 &&
-                                  mj + (pj ? M[1] : M[0]) <= (1LL << 53) - 2);
-        if (__all(ok)) {
-          if (live) {
+        const bool ok = lane < j || (in && se == e && mj + (pj ? N[1] : N[0]) >= (1LL << 52) + 1 &&
+                                     mj + (pj ? M[1] : M[0]) <= (1LL << 53) - 2);
+        const unsigned long long bad = __ballot(!ok);
+        const int f = bad ? __ffsll((long long)bad) - 1 : 64;  // <= nb
+        if (f > j) {
+          if (lane >= j && lane < f) {
             my_x = from_mant(mj, e);
             my_mode = kModeL;
             my_hmax = from_mant(mj + (pj ? M[1] : M[0]), e);
             my_harg = pj ? A[1] : A[0];
           }
-          const long long last = rl64(mj + (pj ? D[1] : D[0]), nb - 1);
-          x = from_mant(last, e);
-          tile_done = true;
-          n_l += nb;
+          x = from_mant(rl64(mj + (pj ? D[1] : D[0]), f - 1), e);
+          n_l += f - j;
+          j = f - 1;
+          continue;
         }
       }
-    }
-    for (int j = 0; j < nb && !tile_done; ++j) {
+      tile_done = false;
       const double cj_exit = rld(l_exit, j);
       if (lane == j) my_x = x;
       int mode = kModeU;
@@ -2177,6 +2262,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
     }
     if (dbg && tile_done) t_fast += (long long)__builtin_amdgcn_s_memtime() - tt0;
     cur = nxt;
+    cb = ce;
   }
   if (lane == 0 && replays) atomicAdd(nreplay, replays);
   if (lane == 0 && c1 < g.nch && g.run[c1] == g.run[c1 - 1] &&
@@ -2195,6 +2281,101 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
   }
 }
 
+// Tile composites (TileComp) of the global tiles of chunks [g.c0, g.nch):
+// one wave per tile, from the final summaries (after k_summ_fix).  Also
+// clears the batch marks (ee) of the range.
+__global__ void __launch_bounds__(256) k_tile_comp(Chunks g, Summ sm, TileComp tc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (g.c0 >> 6) + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (g.nch <= g.c0 || t > ((g.nch - 1) >> 6)) return;  // whole waves
+  const int64_t c = 64 * t + lane;
+  const bool live = c >= g.c0 && c < g.nch;
+  const int se = live ? sm.e[c] : INT32_MIN;
+  const int e = __builtin_amdgcn_readfirstlane(se);
+  if (lane == 0) tc.ee[t] = INT32_MIN;
+  if (e == INT32_MIN || !__all(live && se == e)) {
+    if (lane == 0) tc.e[t] = INT32_MIN;
+    return;
+  }
+  const long long D0 = sm.D[2 * c], D1 = sm.D[2 * c + 1];
+  const long long M0 = sm.M[2 * c], M1 = sm.M[2 * c + 1];
+  const long long N0 = sm.N[2 * c], N1 = sm.N[2 * c + 1];
+  long long i0 = D0, i1 = D1;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const long long p0 = __shfl_up(i0, d, 64), p1 = __shfl_up(i1, d, 64);
+    if (lane >= d) {
+      const long long n0 = p0 + ((p0 & 1) ? i1 : i0);
+      const long long n1 = p1 + (((1 + p1) & 1) ? i1 : i0);
+      i0 = n0;
+      i1 = n1;
+    }
+  }
+  long long x0 = __shfl_up(i0, 1, 64), x1 = __shfl_up(i1, 1, 64);
+  if (lane == 0) { x0 = 0; x1 = 0; }
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    // entry mantissa m (parity p): chunk lane enters at m + inc with parity pj
+    // and stays in the binade iff m + inc + N_pj >= 2^52 + 1 and
+    // m + inc + M_pj <= 2^53 - 2 (carry_segment's fast-tile test)
+    const long long inc = p ? x1 : x0;
+    const int pj = (int)((p + inc) & 1);
+    long long lo = (1LL << 52) + 1 - inc - (pj ? N1 : N0);
+    long long hi = (1LL << 53) - 2 - inc - (pj ? M1 : M0);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      lo = max(lo, (long long)__shfl_xor(lo, d, 64));
+      hi = min(hi, (long long)__shfl_xor(hi, d, 64));
+    }
+    const long long tot = __shfl(p ? i1 : i0, 63, 64);
+    if (lane == 0) {
+      tc.D[2 * t + p] = tot;
+      tc.LO[2 * t + p] = lo;
+      tc.HI[2 * t + p] = hi;
+    }
+  }
+  if (lane == 0) tc.e[t] = e;
+}
+
+// Per-chunk carry of the tiles accepted in batches (ee != INT32_MIN): the
+// fast-tile path of carry_segment from the tile's exact entry.  gated: only
+// after a fallback (bit 16 of err), for the tiles k_carry_run batched.
+__global__ void __launch_bounds__(256) k_tile_apply(Chunks g, Summ sm, TileComp tc, Carry cr,
+                                                    const unsigned int *__restrict__ err, int gated) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (g.c0 >> 6) + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (g.nch <= g.c0 || t > ((g.nch - 1) >> 6)) return;
+  if (gated && !(*(volatile const unsigned int *)err & 16u)) return;
+  const int e = tc.ee[t];
+  if (e == INT32_MIN) return;
+  const long long m = tc.em[t];
+  const int64_t c = 64 * t + lane;
+  const bool live = c < g.nch;
+  const int64_t cc = live ? c : 64 * t;
+  const long long D0 = sm.D[2 * cc], D1 = sm.D[2 * cc + 1];
+  long long i0 = live ? D0 : 0, i1 = live ? D1 : 0;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const long long p0 = __shfl_up(i0, d, 64), p1 = __shfl_up(i1, d, 64);
+    if (lane >= d) {
+      const long long n0 = p0 + ((p0 & 1) ? i1 : i0);
+      const long long n1 = p1 + (((1 + p1) & 1) ? i1 : i0);
+      i0 = n0;
+      i1 = n1;
+    }
+  }
+  long long x0 = __shfl_up(i0, 1, 64), x1 = __shfl_up(i1, 1, 64);
+  if (lane == 0) { x0 = 0; x1 = 0; }
+  if (!live) return;
+  const long long mj = m + ((m & 1) ? x1 : x0);
+  const int pj = (int)(mj & 1);
+  cr.x[c] = from_mant(mj, e);
+  cr.mode[c] = (uint8_t)kModeL;
+  cr.hq[c] = -1;
+  cr.hmax[c] = from_mant(mj + (pj ? sm.M[2 * c + 1] : sm.M[2 * c]), e);
+  cr.harg[c] = pj ? sm.A[2 * c + 1] : sm.A[2 * c];
+}
+
 // Carry by window: block w runs the segments that start in chunks
 // [64w, 64w + 64) (segment starts flagged by k_seg_marks; a segment ends at
 // the next flagged chunk, possibly windows later).
@@ -2202,7 +2383,7 @@ template <bool kCompressed>
 __global__ void __launch_bounds__(64) k_carry_win(Chunks g, const uint8_t *__restrict__ flag,
                                                   const uint8_t *__restrict__ seq, int64_t total, int k, TableView tv,
                                                   const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
-                                                  unsigned long long *__restrict__ nreplay,
+                                                  TileComp tc, unsigned long long *__restrict__ nreplay,
                                                   unsigned int *__restrict__ err, long long *__restrict__ dbg) {
   const int64_t w = g.c0 / 64 + blockIdx.x;  // segment starts in [c0, nch); segments end by nch
   const int lane = threadIdx.x;
@@ -2224,7 +2405,7 @@ __global__ void __launch_bounds__(64) k_carry_win(Chunks g, const uint8_t *__res
         }
       }
     }
-    carry_segment<kCompressed>(g, c0, c1, seq, total, k, tv, codes, o, sm, cr, nreplay, err, dbg, w);
+    carry_segment<kCompressed>(g, c0, c1, seq, total, k, tv, codes, o, sm, cr, tc, nreplay, err, dbg, w);
   }
 }
 
@@ -2234,13 +2415,13 @@ template <bool kCompressed>
 __global__ void __launch_bounds__(64) k_carry_run(Chunks g, const int64_t *__restrict__ cbase, int64_t nruns,
                                                   const uint8_t *__restrict__ seq, int64_t total, int k, TableView tv,
                                                   const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
-                                                  unsigned long long *__restrict__ nreplay,
+                                                  TileComp tc, unsigned long long *__restrict__ nreplay,
                                                   unsigned int *__restrict__ err, long long *__restrict__ dbg,
                                                   int64_t r_lo) {
   const int64_t r = r_lo + blockIdx.x;
   if (r >= nruns || !(*(volatile unsigned int *)err & 16u)) return;
   const int64_t c0 = cbase[r], c1 = cbase[r + 1];
-  if (c0 < c1) carry_segment<kCompressed>(g, c0, c1, seq, total, k, tv, codes, o, sm, cr, nreplay, err, nullptr, r);
+  if (c0 < c1) carry_segment<kCompressed>(g, c0, c1, seq, total, k, tv, codes, o, sm, cr, tc, nreplay, err, nullptr, r);
 }
 
 // Fallback preparation: after a failed segment check, the first heads pass
@@ -2700,6 +2881,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const size_t o_fix = off; off += al(nch * 8 + 16);
   const size_t o_tagg = off; off += al(ntiles * 16);  // parallel approximate scan: tile maps, tile entries
   const size_t o_tin = off; off += al(ntiles * 8);
+  const int64_t ngt = nch / 64 + 2;  // global 64-chunk tiles (carry tile batches)
+  const size_t o_gte = off; off += al(ngt * 4);
+  const size_t o_gtd = off; off += al(ngt * 8 * 6);
+  const size_t o_gtm = off; off += al(ngt * 8);
+  const size_t o_gtee = off; off += al(ngt * 4);
   void *wsp = nullptr;
   KS_TRY(ensure(ctx, SLOT_CHUNK_A, off, &wsp));
   char *W = static_cast<char *>(wsp);
@@ -2725,6 +2911,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   };
   const XTiles xagg = xtiles(W + o_xagg), xtin = xtiles(W + o_xagg + al(ntiles * 32));
   double2 *d_tagg = reinterpret_cast<double2 *>(W + o_tagg);
+  // carry tile batches (KS_NO_TILE_BATCH: A/B, the per-tile walk only)
+  const bool tile_batch = getenv("KS_NO_TILE_BATCH") == nullptr;
+  long long *gtd = reinterpret_cast<long long *>(W + o_gtd);
+  const TileComp tcomp{reinterpret_cast<int32_t *>(W + o_gte), gtd, gtd + 2 * ngt, gtd + 4 * ngt,
+                       reinterpret_cast<long long *>(W + o_gtm), reinterpret_cast<int32_t *>(W + o_gtee)};
   double *d_tin = reinterpret_cast<double *>(W + o_tin);
   // approximate max-plus scan of (sum, clean exit) over runs [r0, r1) (tiles
   // [t0, t1)): three parallel kernels, or the one-wave-per-run k_approx_scan
@@ -3067,13 +3258,23 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     // ---- P3 carry by segments + P4 heads; then the gated per-run fallback
     const int64_t wc = h.c0 / 64;
     const unsigned nwc = (unsigned)((h.c1 - 1) / 64 - wc + 1);
+    const TileComp tch = tile_batch ? tcomp : TileComp{};
+    const unsigned gtc = (unsigned)(((h.c1 - 1) / 64 - wc + 1 + 3) / 4);  // 4 tiles per block
+    if (tile_batch) {
+      hipLaunchKernelGGL(k_tile_comp, dim3(gtc), dim3(256), 0, strm, gv, sm, tch);
+      KS_HIP(hipGetLastError());
+    }
     if (comp)
       hipLaunchKernelGGL(k_carry_win<true>, dim3(nwc), dim3(64), 0, strm, gv, d_flag, s->seq, total, k, tv, codes, p1,
-                         sm, cr, rep_h, err_h, dbg);
+                         sm, cr, tch, rep_h, err_h, dbg);
     else
       hipLaunchKernelGGL(k_carry_win<false>, dim3(nwc), dim3(64), 0, strm, gv, d_flag, s->seq, total, k, tv, codes,
-                         p1, sm, cr, rep_h, err_h, dbg);
+                         p1, sm, cr, tch, rep_h, err_h, dbg);
     KS_HIP(hipGetLastError());
+    if (tile_batch) {
+      hipLaunchKernelGGL(k_tile_apply, dim3(gtc), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 0);
+      KS_HIP(hipGetLastError());
+    }
     auto heads = [&](int gated) {
 #define KS_HEADS(J, C)                                                                                           \
   hipLaunchKernelGGL((k_heads<J, C>), dim3(gch_h), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes, cr, err_h, \
@@ -3091,10 +3292,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     if (nr > 0) {
       if (comp)
         hipLaunchKernelGGL(k_carry_run<true>, dim3((unsigned)nr), dim3(64), 0, strm, gv, d_cbase, h.r1, s->seq, total,
-                           k, tv, codes, p1, sm, cr, rep_h, err_h, nullptr, h.r0);
+                           k, tv, codes, p1, sm, cr, tch, rep_h, err_h, nullptr, h.r0);
       else
         hipLaunchKernelGGL(k_carry_run<false>, dim3((unsigned)nr), dim3(64), 0, strm, gv, d_cbase, h.r1, s->seq,
-                           total, k, tv, codes, p1, sm, cr, rep_h, err_h, nullptr, h.r0);
+                           total, k, tv, codes, p1, sm, cr, tch, rep_h, err_h, nullptr, h.r0);
+      if (tile_batch) hipLaunchKernelGGL(k_tile_apply, dim3(gtc), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 1);
     }
     heads(1);
     KS_HIP(hipGetLastError());

@@ -1454,10 +1454,12 @@ __device__ __forceinline__ void ascan_pair(double &a, double &b, int lane) {
     }
   }
 }
-__global__ void __launch_bounds__(64) k_ascan_tiles(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
-                                                    int64_t nruns, P1 o, double2 *__restrict__ tagg, int64_t t_lo) {
-  const int64_t t = t_lo + blockIdx.x;
-  const int lane = threadIdx.x;
+__global__ void __launch_bounds__(256) k_ascan_tiles(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
+                                                    int64_t nruns, P1 o, double2 *__restrict__ tagg, int64_t t_lo,
+                                                    int64_t t_hi) {
+  const int64_t t = t_lo + (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);  // wave per tile
+  if (t >= t_hi) return;
+  const int lane = threadIdx.x & 63;
   int64_t r, c0, c1;
   tile_of(tbase, cbase, nruns, t, r, c0, c1);
   const int64_t c = c0 + lane;
@@ -1496,11 +1498,12 @@ __global__ void __launch_bounds__(64) k_ascan_runs(const int64_t *__restrict__ t
     if (!(carry == carry)) carry = 0.0;
   }
 }
-__global__ void __launch_bounds__(64) k_ascan_apply(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
+__global__ void __launch_bounds__(256) k_ascan_apply(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
                                                     int64_t nruns, P1 o, const double *__restrict__ tin,
-                                                    double *__restrict__ xt, int64_t t_lo) {
-  const int64_t t = t_lo + blockIdx.x;
-  const int lane = threadIdx.x;
+                                                    double *__restrict__ xt, int64_t t_lo, int64_t t_hi) {
+  const int64_t t = t_lo + (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);  // wave per tile
+  if (t >= t_hi) return;
+  const int lane = threadIdx.x & 63;
   int64_t r, c0, c1;
   tile_of(tbase, cbase, nruns, t, r, c0, c1);
   const int64_t c = c0 + lane;
@@ -1749,11 +1752,14 @@ __global__ void __launch_bounds__(256) k_summ_fixw(Chunks g, const uint8_t *__re
 // Segment starts: every run start, and after the first chunk of each
 // 64-chunk window that is predicted to clamp by a wide margin (so that the
 // exact entry, which differs from x~ by rounding only, clamps too).
-__global__ void __launch_bounds__(64) k_seg_marks(Chunks g, P1 o, const double *__restrict__ xt,
-                                                  uint8_t *__restrict__ flag) {
-  // windows of 64 chunks from the one holding c0 - 1; only this launch's
-  // chunks [c0, nch) are read and marked
-  const int64_t e = ((g.c0 > 0 ? g.c0 - 1 : 0) / 64 + (int64_t)blockIdx.x) * 64 + threadIdx.x;
+__global__ void __launch_bounds__(256) k_seg_marks(Chunks g, P1 o, const double *__restrict__ xt,
+                                                   uint8_t *__restrict__ flag, int64_t nw) {
+  // windows of 64 chunks from the one holding c0 - 1 (a wave each, nw of
+  // them); only this launch's chunks [c0, nch) are read and marked
+  const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wv >= nw) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t e = ((g.c0 > 0 ? g.c0 - 1 : 0) / 64 + wv) * 64 + lane;
   bool elig = false, next_run = false;
   if (e + 1 < g.nch && e + 1 >= g.c0) {
     next_run = g.run[e + 1] != g.run[e];
@@ -1764,7 +1770,7 @@ __global__ void __launch_bounds__(64) k_seg_marks(Chunks g, P1 o, const double *
   }
   const unsigned long long b = __ballot(elig);
   const int f = b ? __ffsll((long long)b) - 1 : 64;
-  if (e + 1 < g.nch && e + 1 >= g.c0) flag[e + 1] = (next_run || (int)threadIdx.x == f) ? 1 : 0;
+  if (e + 1 < g.nch && e + 1 >= g.c0) flag[e + 1] = (next_run || lane == f) ? 1 : 0;
   if (e == 0 && g.c0 == 0) flag[0] = 1;
 }
 
@@ -2012,7 +2018,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
                                               unsigned long long *__restrict__ nreplay,
                                               unsigned int *__restrict__ err, long long *__restrict__ dbg,
                                               int64_t r) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   double x = (c0 > 0 && g.run[c0] == g.run[c0 - 1]) ? o.cexit[c0 - 1] : 0.0;
   unsigned long long replays = 0;
   const long long t_start = dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
@@ -2380,13 +2386,15 @@ __global__ void __launch_bounds__(256) k_tile_apply(Chunks g, Summ sm, TileComp 
 // [64w, 64w + 64) (segment starts flagged by k_seg_marks; a segment ends at
 // the next flagged chunk, possibly windows later).
 template <bool kCompressed>
-__global__ void __launch_bounds__(64) k_carry_win(Chunks g, const uint8_t *__restrict__ flag,
+__global__ void __launch_bounds__(256) k_carry_win(Chunks g, const uint8_t *__restrict__ flag,
                                                   const uint8_t *__restrict__ seq, int64_t total, int k, TableView tv,
                                                   const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
                                                   TileComp tc, unsigned long long *__restrict__ nreplay,
                                                   unsigned int *__restrict__ err, long long *__restrict__ dbg) {
-  const int64_t w = g.c0 / 64 + blockIdx.x;  // segment starts in [c0, nch); segments end by nch
-  const int lane = threadIdx.x;
+  // a wave per window: segment starts in [c0, nch); segments end by nch
+  const int64_t w = g.c0 / 64 + (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (g.nch <= 0 || w > (g.nch - 1) / 64) return;
+  const int lane = threadIdx.x & 63;
   const int64_t base = w * 64;
   unsigned long long m = __ballot(base + lane >= g.c0 && base + lane < g.nch && flag[base + lane]);
   while (m) {
@@ -2725,11 +2733,12 @@ __device__ __forceinline__ XState xt_load(const XTiles &a, int64_t t) {
   return XState{a.reset[t], a.open[t], a.xb[t], a.xa[t], a.xm[t]};
 }
 
-__global__ void __launch_bounds__(64) k_stitch_tiles(Chunks g, const int64_t *__restrict__ tbase,
+__global__ void __launch_bounds__(256) k_stitch_tiles(Chunks g, const int64_t *__restrict__ tbase,
                                                      const int64_t *__restrict__ cbase, int64_t nruns, P1 o,
-                                                     Carry cr, XTiles agg, int64_t t_lo) {
-  const int64_t t = t_lo + blockIdx.x;
-  const int lane = threadIdx.x;
+                                                     Carry cr, XTiles agg, int64_t t_lo, int64_t t_hi) {
+  const int64_t t = t_lo + (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);  // wave per tile
+  if (t >= t_hi) return;
+  const int lane = threadIdx.x & 63;
   int64_t r, c0, c1;
   tile_of(tbase, cbase, nruns, t, r, c0, c1);
   const int64_t c = c0 + lane;
@@ -2768,13 +2777,15 @@ __global__ void __launch_bounds__(64) k_stitch_runs(const int64_t *__restrict__ 
   }
 }
 
-__global__ void __launch_bounds__(64) k_stitch_emit(Chunks g, const int64_t *__restrict__ tbase,
+__global__ void __launch_bounds__(256) k_stitch_emit(Chunks g, const int64_t *__restrict__ tbase,
                                                     const int64_t *__restrict__ cbase, int64_t nruns,
                                                     const int64_t *__restrict__ ra, const int32_t *__restrict__ rseq,
                                                     P1 o, Carry cr, EmitCfg ec, XTiles tin, RegionBuf out,
-                                                    Rescan rs, unsigned int *__restrict__ err, int64_t t_lo) {
-  const int64_t t = t_lo + blockIdx.x;
-  const int lane = threadIdx.x;
+                                                    Rescan rs, unsigned int *__restrict__ err, int64_t t_lo,
+                                                    int64_t t_hi) {
+  const int64_t t = t_lo + (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);  // wave per tile
+  if (t >= t_hi) return;
+  const int lane = threadIdx.x & 63;
   int64_t r, c0, c1;
   tile_of(tbase, cbase, nruns, t, r, c0, c1);
   const int64_t c = c0 + lane;
@@ -2921,6 +2932,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // [t0, t1)): three parallel kernels, or the one-wave-per-run k_approx_scan
   // with KS_SERIAL_ASCAN
   static const bool serial_ascan = getenv("KS_SERIAL_ASCAN") != nullptr;
+  // waves per block of the wave-per-tile / wave-per-window kernels (KS_WPB: A/B)
+  const int wpb = getenv("KS_WPB") ? std::max(1, std::min(4, atoi(getenv("KS_WPB")))) : 2;
   auto ascan = [&](const P1 &o, double *out, int64_t r0, int64_t r1, int64_t t0, int64_t t1,
                    hipStream_t strm) -> ks_status {
     if (r1 <= r0) return KS_OK;
@@ -2929,11 +2942,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipGetLastError());
       return KS_OK;
     }
-    hipLaunchKernelGGL(k_ascan_tiles, dim3((unsigned)(t1 - t0)), dim3(64), 0, strm, d_tbase, d_cbase, nruns, o,
-                       d_tagg, t0);
+    const unsigned g4 = (unsigned)((t1 - t0 + wpb - 1) / wpb);  // a wave per tile, wpb per block
+    hipLaunchKernelGGL(k_ascan_tiles, dim3(g4), dim3(64 * wpb), 0, strm, d_tbase, d_cbase, nruns, o, d_tagg, t0, t1);
     hipLaunchKernelGGL(k_ascan_runs, dim3((unsigned)(r1 - r0)), dim3(64), 0, strm, d_tbase, r1, d_tagg, d_tin, r0);
-    hipLaunchKernelGGL(k_ascan_apply, dim3((unsigned)(t1 - t0)), dim3(64), 0, strm, d_tbase, d_cbase, nruns, o, d_tin,
-                       out, t0);
+    hipLaunchKernelGGL(k_ascan_apply, dim3(g4), dim3(64 * wpb), 0, strm, d_tbase, d_cbase, nruns, o, d_tin, out, t0, t1);
     KS_HIP(hipGetLastError());
     return KS_OK;
   };
@@ -3215,7 +3227,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     // ---- P2 prediction, segment starts, summaries
     KS_TRY(ascan(p1, xt, h.r0, h.r1, h.t0, h.t1, strm));
     const int64_t wl = (h.c0 > 0 ? h.c0 - 1 : 0) / 64;
-    hipLaunchKernelGGL(k_seg_marks, dim3((unsigned)((h.c1 + 63) / 64 - wl)), dim3(64), 0, strm, gv, p1, xt, d_flag);
+    const int64_t nwm = (h.c1 + 63) / 64 - wl;
+    hipLaunchKernelGGL(k_seg_marks, dim3((unsigned)((nwm + wpb - 1) / wpb)), dim3(64 * wpb), 0, strm, gv, p1, xt, d_flag, nwm);
     KS_HIP(hipGetLastError());
     if (p1summ) {
       KS_HIP(hipMemsetAsync(d_nfix + hi, 0, 8, strm));
@@ -3265,10 +3278,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipGetLastError());
     }
     if (comp)
-      hipLaunchKernelGGL(k_carry_win<true>, dim3(nwc), dim3(64), 0, strm, gv, d_flag, s->seq, total, k, tv, codes, p1,
+      hipLaunchKernelGGL(k_carry_win<true>, dim3((nwc + wpb - 1) / wpb), dim3(64 * wpb), 0, strm, gv, d_flag, s->seq, total, k, tv, codes, p1,
                          sm, cr, tch, rep_h, err_h, dbg);
     else
-      hipLaunchKernelGGL(k_carry_win<false>, dim3(nwc), dim3(64), 0, strm, gv, d_flag, s->seq, total, k, tv, codes,
+      hipLaunchKernelGGL(k_carry_win<false>, dim3((nwc + wpb - 1) / wpb), dim3(64 * wpb), 0, strm, gv, d_flag, s->seq, total, k, tv, codes,
                          p1, sm, cr, tch, rep_h, err_h, dbg);
     KS_HIP(hipGetLastError());
     if (tile_batch) {
@@ -3304,8 +3317,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
 
     // ---- P5 stitch
     if (nt > 0) {
-      hipLaunchKernelGGL(k_stitch_tiles, dim3((unsigned)nt), dim3(64), 0, strm, g, d_tbase, d_cbase, nruns, p1, cr,
-                         xagg, h.t0);
+      hipLaunchKernelGGL(k_stitch_tiles, dim3((unsigned)((nt + wpb - 1) / wpb)), dim3(64 * wpb), 0, strm, g, d_tbase, d_cbase,
+                         nruns, p1, cr, xagg, h.t0, h.t1);
       KS_HIP(hipGetLastError());
     }
     if (nr > 0) {
@@ -3314,8 +3327,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipGetLastError());
     }
     if (nt > 0) {
-      hipLaunchKernelGGL(k_stitch_emit, dim3((unsigned)nt), dim3(64), 0, strm, g, d_tbase, d_cbase, nruns, runs.a,
-                         runs.seq, p1, cr, ec, xtin, rb, rs, err_h, h.t0);
+      hipLaunchKernelGGL(k_stitch_emit, dim3((unsigned)((nt + wpb - 1) / wpb)), dim3(64 * wpb), 0, strm, g, d_tbase, d_cbase,
+                         nruns, runs.a, runs.seq, p1, cr, ec, xtin, rb, rs, err_h, h.t0, h.t1);
       KS_HIP(hipGetLastError());
     }
     return KS_OK;

@@ -130,9 +130,11 @@ def score_table(api, hc, k, words, score):
 
 
 def pmc_traffic(kernel_prefix, build_id, workload):
-    """HBM bytes per launch of the dominant kernel from the committed PMC
-    passes (tools/gpu_pmc.sh -> profiles/pmc_summary.json), used only when
-    they were taken on this very build (library build id) and workload.
+    """HBM bytes per step of the dominant kernel (all its launches: pass 1
+    runs as two launches, one per part of the runs) from the committed PMC
+    passes (tools/gpu_pmc.sh + tools/pmc_assemble.py -> profiles/
+    pmc_summary.json), used only when they were taken on this very build
+    (library build id) and workload.
     FETCH_SIZE counts 64 B per memory-side read request; the kernel's only
     streaming read (the packed bases, total/4 bytes, 16-B loads) is under-
     counted by half on gfx950 (MI355X_MICROARCH.md, HBM), so that half is
@@ -144,13 +146,20 @@ def pmc_traffic(kernel_prefix, build_id, workload):
         return None, f"stale: PMC summary of build {pmc.get('build_id')}, this library is {build_id}"
     if pmc.get("workload") != workload:
         return None, "PMC summary is for another workload"
+    steps = float(pmc.get("steps", 1))
+    fetch = write = 0.0
+    names = []
     for name, cs in pmc.get("kernels", {}).items():
         if name.startswith(kernel_prefix) and "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
-            fetch = cs["FETCH_SIZE"] * 1e3
-            corr = pmc.get("streaming_read_bytes", {}).get(name, 0.0) / 2.0
-            return {"bytes": int(round(fetch + cs["WRITE_SIZE"] * 1e3 + corr)), "fetch": int(fetch),
-                    "write": int(cs["WRITE_SIZE"] * 1e3), "streaming_correction": int(corr),
-                    "read_requests": int(fetch / 64.0), "kernel": name}, "ok"
+            n = cs.get("dispatches", 1) / steps  # launches per step (pass 1: one per part of the runs)
+            fetch += cs["FETCH_SIZE"] * 1e3 * n
+            write += cs["WRITE_SIZE"] * 1e3 * n
+            names.append(name)
+    if names:
+        corr = pmc.get("streaming_read_bytes_per_step", {}).get(kernel_prefix, 0.0) / 2.0
+        return {"bytes": int(round(fetch + write + corr)), "fetch": int(fetch), "write": int(write),
+                "streaming_correction": int(corr), "read_requests": int(fetch / 64.0), "kernels": names,
+                "per": "step (all launches of the kernel)"}, "ok"
     return None, "kernel not in the PMC summary"
 
 

@@ -20,6 +20,42 @@
 namespace ks {
 namespace {
 
+// Sequence starts in [base, lim] as bits (offs[q] - base) of the LDS bitmap,
+// by the first wave: a 64-ary lower_bound over offs[0..nseq] (one dependent
+// load per 64x narrowing instead of log2(nseq) single-lane loads: the tile
+// loop's block waits on it), then the starts 64 at a time.
+__device__ __forceinline__ void mark_seq_starts(const int64_t *__restrict__ offs, int32_t nseq, int64_t base,
+                                                int64_t lim, uint32_t *bmask) {
+  const int lane = threadIdx.x & 63;
+  int64_t L = 0, R = (int64_t)nseq + 1;  // first i in [L, R) with offs[i] >= base, else R
+  while (R - L > 64) {
+    const int64_t step = (R - L + 63) / 64;
+    const int64_t pv = L + lane * step;
+    const bool lt = pv < R && offs[pv] < base;
+    const int cnt = __popcll(__ballot(lt));
+    if (cnt == 0) {
+      R = L;
+      break;
+    }
+    const int64_t last = L + (int64_t)(cnt - 1) * step;  // last pivot below base
+    L = last + 1;
+    R = min(R, last + step);
+  }
+  if (R > L) {
+    const bool lt = L + lane < R && offs[L + lane] < base;
+    L += __popcll(__ballot(lt));
+  }
+  for (int64_t q0 = L; q0 <= nseq; q0 += 64) {
+    const int64_t q = q0 + lane;
+    const bool in = q <= nseq && offs[q] <= lim;
+    if (in) {
+      const int r = (int)(offs[q] - base);
+      atomicOr(&bmask[r >> 5], 1u << (r & 31));
+    }
+    if (__ballot(in) != __ballot(true)) break;  // offsets ascend: the rest lie past lim
+  }
+}
+
 constexpr int kTile = 4096;
 constexpr int kPer = 16;
 constexpr int kLook = 16;  // look-back bytes (k - 1 <= 14)
@@ -45,17 +81,7 @@ __global__ void __launch_bounds__(256) k_count(const uint8_t *__restrict__ seq, 
     __syncthreads();
     for (int i = threadIdx.x; i < (kTile + kLook + 32) / 32 + 1; i += blockDim.x) bmask[i] = 0;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int lo = 0, hi = nseq + 1;
-      while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (offs[mid] < base) lo = mid + 1; else hi = mid;
-      }
-      for (int q = lo; q <= nseq && offs[q] <= t0 + kTile; ++q) {
-        const int r = (int)(offs[q] - base);
-        bmask[r >> 5] |= 1u << (r & 31);
-      }
-    }
+    if (threadIdx.x < 64) mark_seq_starts(offs, nseq, base, t0 + kTile, bmask);
     __syncthreads();
     const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
     if (p0 >= total) continue;
@@ -149,17 +175,7 @@ __global__ void __launch_bounds__(256) k_count_multi(const uint8_t *__restrict__
     __syncthreads();
     for (int i = threadIdx.x; i < (kTile + kLook + 32) / 32 + 1; i += blockDim.x) bmask[i] = 0;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int lo = 0, hi = nseq + 1;
-      while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (offs[mid] < base) lo = mid + 1; else hi = mid;
-      }
-      for (int q = lo; q <= nseq && offs[q] <= t0 + kTile; ++q) {
-        const int r = (int)(offs[q] - base);
-        bmask[r >> 5] |= 1u << (r & 31);
-      }
-    }
+    if (threadIdx.x < 64) mark_seq_starts(offs, nseq, base, t0 + kTile, bmask);
     __syncthreads();
     const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
     if (p0 >= total) continue;
@@ -295,17 +311,7 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
     __syncthreads();
     for (int i = threadIdx.x; i < (kPTile + kLook + 32) / 32 + 1; i += kPT) bmask[i] = 0;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int lo = 0, hi = nseq + 1;
-      while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (offs[mid] < base) lo = mid + 1; else hi = mid;
-      }
-      for (int q = lo; q <= nseq && offs[q] <= t0 + kPTile; ++q) {
-        const int r = (int)(offs[q] - base);
-        bmask[r >> 5] |= 1u << (r & 31);
-      }
-    }
+    if (threadIdx.x < 64) mark_seq_starts(offs, nseq, base, t0 + kPTile, bmask);
     __syncthreads();
     const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
     if (p0 >= total) continue;
@@ -386,17 +392,7 @@ __global__ void __launch_bounds__(kPT) k_part_scatter(const uint8_t *__restrict_
     for (int i = threadIdx.x; i < (kPTile + kLook + 32) / 32 + 1; i += kPT) bmask[i] = 0;
     for (int i = threadIdx.x; i < nb; i += kPT) cnt[i] = 0;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int lo = 0, hi = nseq + 1;
-      while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (offs[mid] < base) lo = mid + 1; else hi = mid;
-      }
-      for (int q = lo; q <= nseq && offs[q] <= t0 + kPTile; ++q) {
-        const int r = (int)(offs[q] - base);
-        bmask[r >> 5] |= 1u << (r & 31);
-      }
-    }
+    if (threadIdx.x < 64) mark_seq_starts(offs, nseq, base, t0 + kPTile, bmask);
     __syncthreads();
     const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
     uint32_t br[kPer];   // bucket << 16 | rank, or ~0u
@@ -665,7 +661,8 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   const int nb1 = 1 << g.T1, nbf = 1 << g.T;
   const int shift = 2 * k - g.T1;
   const int64_t ntiles = (total + kPTile - 1) / kPTile;
-  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(kPBlocks, ntiles));
+  const int pb = getenv("KS_PART_BLOCKS") ? atoi(getenv("KS_PART_BLOCKS")) : kPBlocks;  // A/B
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(pb > 0 ? pb : kPBlocks, ntiles));
   const int C = kSubChunks;
   const size_t m1 = (size_t)nb1 * G, m2 = g.T2 ? (size_t)nbf * C : 0;
   void *w = nullptr, *p1 = nullptr, *p2 = nullptr, *tmp = nullptr;

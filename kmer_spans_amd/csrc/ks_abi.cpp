@@ -194,6 +194,10 @@ extern "C" ks_status ks_ctx_create(int32_t device, ks_ctx **out) {
 extern "C" void ks_ctx_destroy(ks_ctx *c) {
   if (!c) return;
   if (c->pid != getpid()) return;  // inherited across fork(): its HIP handles are not ours
+  if (c->sub) {
+    ks_ctx_destroy(c->sub);
+    c->sub = nullptr;
+  }
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (auto &b : c->slots)
@@ -209,6 +213,14 @@ extern "C" void ks_ctx_destroy(ks_ctx *c) {
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
+
+namespace ks {
+ks_status ctx_sub(ks_ctx *ctx, ks_ctx **sub) {
+  if (!ctx->sub) KS_TRY(ks_ctx_create(ctx->device, &ctx->sub));
+  *sub = ctx->sub;
+  return KS_OK;
+}
+}  // namespace ks
 
 extern "C" ks_status ks_ctx_set_stream(ks_ctx *c, void *stream) {
   if (!c) return fail(KS_ERR_ARG, "null ctx");

@@ -85,6 +85,7 @@ struct ks_ctx {
   hipEvent_t ev[20] = {};
   hipStream_t side = nullptr;  // forked work that overlaps the main stream (joined by events; lowest priority)
   hipStream_t hi = nullptr;    // highest-priority stream: the first half's pass 1 (ks_scan_chunked.hip)
+  ks_ctx *sub = nullptr;       // second context of the same device: the other part of a two-part scan
   int64_t rescan_segcap = 0;  // grow-only rescan capacity per segment (tr_lr rescans outnumber regions)
 };
 
@@ -139,6 +140,7 @@ inline double now_ms() {
 ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out);
 ks_status ensure_pinned(ks_ctx *ctx, size_t bytes, void **out);
 ks_status activate(ks_ctx *ctx);  // fork check + hipSetDevice
+ks_status ctx_sub(ks_ctx *ctx, ks_ctx **sub);  // ctx->sub, created on first use
 ks_status default_ctx(ks_ctx **ctx);  // *ctx or the process default context (fork-checked)
 bool hip_usable_here();  // false in a child forked after HIP was initialised
 
@@ -199,7 +201,7 @@ struct RegionBuf {
 
 // Launch wrappers (defined in the .hip files).
 ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs, float *ms,
-                    bool want_packed = false);
+                    bool want_packed = false, int64_t p_lo = 0, int64_t p_hi = -1);
 ks_status launch_count(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const Runs &runs, int k,
                        int32_t *counts_dev, double *n_words);
 // Which span scan a call performs.  trlr = 0: kmer_regions (kmer_spans.c:

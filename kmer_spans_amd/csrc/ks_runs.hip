@@ -70,15 +70,19 @@ __device__ __forceinline__ void append_events(uint32_t starts, uint32_t ends, in
 // packed (optional): the same pass stores the 2-bit codes of the 16 bytes as
 // one word (bytes past total encode as 'N'), which the gather pass of the
 // chunked scan reads instead of the bytes (a quarter of the lines).
+// Range [p_lo, p_hi) (a part of the buffer cut at sequence boundaries, see
+// scan_impl): bytes outside it read as N, so its runs and no others come
+// out; units [u0, u1) are visited (the range plus a margin, whose packed
+// words -- pure functions of the bytes -- the part's later passes may read).
 __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ seq, int64_t total,
                                                   unsigned long long *__restrict__ ev,
                                                   unsigned long long *__restrict__ ev_count, int64_t cap,
-                                                  uint32_t *__restrict__ packed) {
-  const int64_t nunits = total / 16 + 1;  // covers position total
+                                                  uint32_t *__restrict__ packed, int64_t p_lo, int64_t p_hi,
+                                                  int64_t u0, int64_t u1) {
   constexpr int U = 4;                     // units per lane and step: U loads in flight
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
   const int lane = threadIdx.x & 63;
-  for (int64_t ub = (int64_t)blockIdx.x * blockDim.x * U; ub < nunits; ub += stride) {
+  for (int64_t ub = u0 + (int64_t)blockIdx.x * blockDim.x * U; ub < u1; ub += stride) {
     uint4 v[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) {
@@ -94,7 +98,7 @@ __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ se
       // previous unit), loaded by lane 0
       uint32_t prev_b = __shfl_up(v[j].w >> 24, 1, 64);
       if (lane == 0 || p0 + 16 > total) prev_b = p0 == 0 ? (uint32_t)'N' : (p0 - 1 < total ? seq[p0 - 1] : 'N');
-      if (u < nunits) {
+      if (u < u1) {
         uint32_t nm = 0xffffu;
         if (p0 + 16 <= total) {
           nm = n_mask4(v[j].x) | (n_mask4(v[j].y) << 4) | (n_mask4(v[j].z) << 8) | (n_mask4(v[j].w) << 12);
@@ -110,12 +114,16 @@ __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ se
           }
           if (packed) packed[u] = pw;
         }
-        const uint32_t prev_n = is_n((uint8_t)prev_b) ? 1u : 0u;
+        if (p0 < p_lo || p0 + 16 > p_hi) {  // a unit at an end of the range: outside reads as N
+          for (int q = 0; q < 16; ++q)
+            if (p0 + q < p_lo || p0 + q >= p_hi) nm |= 1u << q;
+        }
+        const uint32_t prev_n = (is_n((uint8_t)prev_b) || p0 <= p_lo || p0 - 1 >= p_hi) ? 1u : 0u;
         const uint32_t non = ~nm & 0xffffu;
         starts = non & ((nm << 1) | prev_n);
         ends = nm & ((non << 1) | (prev_n ^ 1u)) & 0xffffu;
-        if (p0 + 16 > total) {  // no events past position total
-          const int keep = (int)(total - p0) + 1;
+        if (p0 + 16 > p_hi) {  // no events past position p_hi
+          const int keep = (int)(p_hi - p0) + 1;
           const uint32_t km = keep >= 16 ? 0xffffu : ((1u << keep) - 1u);
           starts &= km;
           ends &= km;
@@ -130,11 +138,11 @@ __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ se
 // START at the boundary (emitted once per distinct offset).
 __global__ void k_seq_events(const uint8_t *__restrict__ seq, int64_t total, const int64_t *__restrict__ offs,
                              int32_t nseq, unsigned long long *__restrict__ ev,
-                             unsigned long long *__restrict__ ev_count, int64_t cap) {
+                             unsigned long long *__restrict__ ev_count, int64_t cap, int64_t p_lo, int64_t p_hi) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q < 1 || q >= nseq) return;
   const int64_t p = offs[q];
-  if (offs[q - 1] == p || p <= 0 || p >= total) return;
+  if (offs[q - 1] == p || p <= p_lo || p >= p_hi || p >= total) return;
   if (is_n(seq[p - 1]) || is_n(seq[p])) return;
   const unsigned long long slot = atomicAdd(ev_count, 2ull);
   if ((int64_t)slot + 1 < cap) {
@@ -256,7 +264,9 @@ ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int t
   return KS_OK;
 }
 
-ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs, float *ms, bool want_packed) {
+ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs, float *ms, bool want_packed,
+                    int64_t p_lo, int64_t p_hi) {
+  if (p_hi < 0) p_hi = total;
   hipStream_t st = ctx->stream;
   KS_HIP(hipEventRecord(ctx->ev[0], st));
   uint32_t *packed = nullptr;
@@ -276,14 +286,18 @@ ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs
     void *evp = nullptr;
     KS_TRY(ensure(ctx, SLOT_EVENTS, (size_t)cap * 8, &evp));
     KS_HIP(hipMemsetAsync(d_count, 0, 8, st));
-    const int64_t nunits = total / 16 + 1;
-    const unsigned grid = (unsigned)std::min<int64_t>((nunits + 1023) / 1024, (int64_t)ctx->num_cus * 16);
+    const int64_t nunits = total / 16 + 1;  // covers position total
+    constexpr int64_t kMargin = 64;          // packed words past the range's ends (pass-1 staging reach)
+    const int64_t u0 = std::max<int64_t>(0, p_lo / 16 - kMargin);
+    const int64_t u1 = std::min<int64_t>(nunits, p_hi / 16 + 1 + kMargin);
+    const unsigned grid = (unsigned)std::max<int64_t>(
+        1, std::min<int64_t>((u1 - u0 + 1023) / 1024, (int64_t)ctx->num_cus * 16));
     hipLaunchKernelGGL(k_n_events, dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp,
-                       d_count, cap, packed);
+                       d_count, cap, packed, p_lo, p_hi, u0, u1);
     KS_HIP(hipGetLastError());
     if (s->nseq > 1) {
       hipLaunchKernelGGL(k_seq_events, dim3((unsigned)((s->nseq + 255) / 256)), dim3(256), 0, st, s->seq, total,
-                         s->offsets_dev, s->nseq, (unsigned long long *)evp, d_count, cap);
+                         s->offsets_dev, s->nseq, (unsigned long long *)evp, d_count, cap, p_lo, p_hi);
       KS_HIP(hipGetLastError());
     }
     KS_HIP(hipMemcpyAsync(&n_ev, d_count, 8, hipMemcpyDeviceToHost, st));

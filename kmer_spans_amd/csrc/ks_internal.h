@@ -82,7 +82,7 @@ struct ks_ctx {
   // pinned host staging
   void *pinned = nullptr;
   size_t pinned_bytes = 0;
-  hipEvent_t ev[20] = {};
+  hipEvent_t ev[24] = {};
   hipStream_t side = nullptr;  // forked work that overlaps the main stream (joined by events; lowest priority)
   hipStream_t hi = nullptr;    // highest-priority stream: the first half's pass 1 (ks_scan_chunked.hip)
   ks_ctx *sub = nullptr;       // second context of the same device: the other part of a two-part scan

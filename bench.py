@@ -51,7 +51,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 ALGO_BYTES_PER_BASE = 9.0      # 1 B sequence + 8 B FP64 table entry (k >= 8)
-RANDOM_WALL_GPS = 48.0         # measured random-request ceiling (profiles/r1_gather_bench2.jsonl)
+RANDOM_WALL_GPS = 50.0         # measured random-request ceiling, contiguous 128 GiB table (profiles/r2/frag_probe.txt)
 METRIC = "Gbases/sec scanned (k=13, log-ratio score) at 1/2/4/8 MI355X; spans bit-exact"
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 
@@ -384,7 +384,8 @@ def main():
         ra = {"table_reads_per_launch": int(reads), "positions_per_read": J,
               "achieved_G_per_s": round(reads / (ms_kernel * 1e-3) / 1e9, 2), "wall_G_per_s": RANDOM_WALL_GPS,
               "frac": round(reads / (ms_kernel * 1e-3) / 1e9 / RANDOM_WALL_GPS, 4),
-              "wall_source": "profiles/r1_gather_bench2.jsonl (random u64 reads, 32-128 GiB tables)"}
+              "wall_source": "profiles/r2/frag_probe.txt (random 16-B reads from a physically contiguous 128 GiB "
+                             "buffer: 49.3-50.6 G/s; scattered VRAM 47.5-48.9)"}
         if traffic:
             ra["memory_read_requests_per_launch"] = traffic["read_requests"]
             ra["memory_requests_G_per_s"] = round(traffic["read_requests"] / (ms_kernel * 1e-3) / 1e9, 2)

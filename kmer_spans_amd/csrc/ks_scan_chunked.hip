@@ -1426,13 +1426,20 @@ __global__ void __launch_bounds__(64) k_approx_scan(const int64_t *__restrict__ 
   }
 }
 
+// Per-tile run map: block r writes r for the stitch tiles of run r.
+__global__ void k_tile_runs(const int64_t *__restrict__ tbase, int64_t nruns, int32_t *__restrict__ trun) {
+  const int64_t r = blockIdx.x;
+  if (r >= nruns) return;
+  for (int64_t t = tbase[r] + threadIdx.x; t < tbase[r + 1]; t += blockDim.x) trun[t] = (int32_t)r;
+}
+
+// Run of stitch tile t from the per-tile run map (k_tile_runs): one load
+// instead of a dependent binary search over the runs, which bounded the
+// wave-per-tile kernels by its latency (12 loads at 2,790 runs).
 __device__ __forceinline__ void tile_of(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
-                                        int64_t nruns, int64_t t, int64_t &r, int64_t &c0, int64_t &c1) {
-  int64_t lo = 0, hi = nruns - 1;  // last run with tbase[r] <= t
-  while (lo < hi) {
-    const int64_t mid = (lo + hi + 1) >> 1;
-    if (tbase[mid] <= t) lo = mid; else hi = mid - 1;
-  }
+                                        const int32_t *__restrict__ trun, int64_t t, int64_t &r, int64_t &c0,
+                                        int64_t &c1) {
+  const int64_t lo = trun[t];
   r = lo;
   c0 = cbase[lo] + (t - tbase[lo]) * 64;
   c1 = min(c0 + 64, cbase[lo + 1]);
@@ -1455,13 +1462,13 @@ __device__ __forceinline__ void ascan_pair(double &a, double &b, int lane) {
   }
 }
 __global__ void __launch_bounds__(256) k_ascan_tiles(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
-                                                    int64_t nruns, P1 o, double2 *__restrict__ tagg, int64_t t_lo,
+                                                    int64_t nruns, const int32_t *__restrict__ trun, P1 o, double2 *__restrict__ tagg, int64_t t_lo,
                                                     int64_t t_hi) {
   const int64_t t = t_lo + (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);  // wave per tile
   if (t >= t_hi) return;
   const int lane = threadIdx.x & 63;
   int64_t r, c0, c1;
-  tile_of(tbase, cbase, nruns, t, r, c0, c1);
+  tile_of(tbase, cbase, trun, t, r, c0, c1);
   const int64_t c = c0 + lane;
   double a = 0.0, b = -INFINITY;
   if (c < c1) {
@@ -1499,13 +1506,13 @@ __global__ void __launch_bounds__(64) k_ascan_runs(const int64_t *__restrict__ t
   }
 }
 __global__ void __launch_bounds__(256) k_ascan_apply(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
-                                                    int64_t nruns, P1 o, const double *__restrict__ tin,
+                                                    int64_t nruns, const int32_t *__restrict__ trun, P1 o, const double *__restrict__ tin,
                                                     double *__restrict__ xt, int64_t t_lo, int64_t t_hi) {
   const int64_t t = t_lo + (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);  // wave per tile
   if (t >= t_hi) return;
   const int lane = threadIdx.x & 63;
   int64_t r, c0, c1;
-  tile_of(tbase, cbase, nruns, t, r, c0, c1);
+  tile_of(tbase, cbase, trun, t, r, c0, c1);
   const int64_t c = c0 + lane;
   double a = 0.0, b = -INFINITY;
   if (c < c1) {
@@ -2734,13 +2741,13 @@ __device__ __forceinline__ XState xt_load(const XTiles &a, int64_t t) {
 }
 
 __global__ void __launch_bounds__(256) k_stitch_tiles(Chunks g, const int64_t *__restrict__ tbase,
-                                                     const int64_t *__restrict__ cbase, int64_t nruns, P1 o,
+                                                     const int64_t *__restrict__ cbase, int64_t nruns, const int32_t *__restrict__ trun, P1 o,
                                                      Carry cr, XTiles agg, int64_t t_lo, int64_t t_hi) {
   const int64_t t = t_lo + (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);  // wave per tile
   if (t >= t_hi) return;
   const int lane = threadIdx.x & 63;
   int64_t r, c0, c1;
-  tile_of(tbase, cbase, nruns, t, r, c0, c1);
+  tile_of(tbase, cbase, trun, t, r, c0, c1);
   const int64_t c = c0 + lane;
   XState f{0, 0, 0, 0, -INFINITY};
   if (c < c1) f = chunk_op(g, o, cr, c).f;
@@ -2778,7 +2785,7 @@ __global__ void __launch_bounds__(64) k_stitch_runs(const int64_t *__restrict__ 
 }
 
 __global__ void __launch_bounds__(256) k_stitch_emit(Chunks g, const int64_t *__restrict__ tbase,
-                                                    const int64_t *__restrict__ cbase, int64_t nruns,
+                                                    const int64_t *__restrict__ cbase, int64_t nruns, const int32_t *__restrict__ trun,
                                                     const int64_t *__restrict__ ra, const int32_t *__restrict__ rseq,
                                                     P1 o, Carry cr, EmitCfg ec, XTiles tin, RegionBuf out,
                                                     Rescan rs, unsigned int *__restrict__ err, int64_t t_lo,
@@ -2787,7 +2794,7 @@ __global__ void __launch_bounds__(256) k_stitch_emit(Chunks g, const int64_t *__
   if (t >= t_hi) return;
   const int lane = threadIdx.x & 63;
   int64_t r, c0, c1;
-  tile_of(tbase, cbase, nruns, t, r, c0, c1);
+  tile_of(tbase, cbase, trun, t, r, c0, c1);
   const int64_t c = c0 + lane;
   const bool live = c < c1;
   ChunkOp op;
@@ -2892,6 +2899,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const size_t o_fix = off; off += al(nch * 8 + 16);
   const size_t o_tagg = off; off += al(ntiles * 16);  // parallel approximate scan: tile maps, tile entries
   const size_t o_tin = off; off += al(ntiles * 8);
+  const size_t o_trun = off; off += al(ntiles * 4 + 4);  // stitch tile -> run (k_tile_runs)
   const int64_t ngt = nch / 64 + 2;  // global 64-chunk tiles (carry tile batches)
   const size_t o_gte = off; off += al(ngt * 4);
   const size_t o_gtd = off; off += al(ngt * 8 * 6);
@@ -2922,6 +2930,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   };
   const XTiles xagg = xtiles(W + o_xagg), xtin = xtiles(W + o_xagg + al(ntiles * 32));
   double2 *d_tagg = reinterpret_cast<double2 *>(W + o_tagg);
+  int32_t *d_trun = reinterpret_cast<int32_t *>(W + o_trun);
   // carry tile batches (KS_NO_TILE_BATCH: A/B, the per-tile walk only)
   const bool tile_batch = getenv("KS_NO_TILE_BATCH") == nullptr;
   long long *gtd = reinterpret_cast<long long *>(W + o_gtd);
@@ -2943,9 +2952,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       return KS_OK;
     }
     const unsigned g4 = (unsigned)((t1 - t0 + wpb - 1) / wpb);  // a wave per tile, wpb per block
-    hipLaunchKernelGGL(k_ascan_tiles, dim3(g4), dim3(64 * wpb), 0, strm, d_tbase, d_cbase, nruns, o, d_tagg, t0, t1);
+    hipLaunchKernelGGL(k_ascan_tiles, dim3(g4), dim3(64 * wpb), 0, strm, d_tbase, d_cbase, nruns, d_trun, o, d_tagg, t0,
+                       t1);
     hipLaunchKernelGGL(k_ascan_runs, dim3((unsigned)(r1 - r0)), dim3(64), 0, strm, d_tbase, r1, d_tagg, d_tin, r0);
-    hipLaunchKernelGGL(k_ascan_apply, dim3(g4), dim3(64 * wpb), 0, strm, d_tbase, d_cbase, nruns, o, d_tin, out, t0, t1);
+    hipLaunchKernelGGL(k_ascan_apply, dim3(g4), dim3(64 * wpb), 0, strm, d_tbase, d_cbase, nruns, d_trun, o, d_tin, out,
+                       t0, t1);
     KS_HIP(hipGetLastError());
     return KS_OK;
   };
@@ -3000,6 +3011,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   hipLaunchKernelGGL(k_make_chunks, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, st, runs.a, d_cbase,
                      nruns, k, runs.b, mode.trlr, g);
   KS_HIP(hipGetLastError());
+  if (nruns > 0) {
+    hipLaunchKernelGGL(k_tile_runs, dim3((unsigned)nruns), dim3(256), 0, st, d_tbase, nruns, d_trun);
+    KS_HIP(hipGetLastError());
+  }
   const unsigned gch = (unsigned)((nch + 255) / 256);
   const unsigned gch1k = (unsigned)((nch + 1023) / 1024);
   const int Jt = (tv.ext != nullptr) ? tv.ext_J : 1;
@@ -3318,7 +3333,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     // ---- P5 stitch
     if (nt > 0) {
       hipLaunchKernelGGL(k_stitch_tiles, dim3((unsigned)((nt + wpb - 1) / wpb)), dim3(64 * wpb), 0, strm, g, d_tbase, d_cbase,
-                         nruns, p1, cr, xagg, h.t0, h.t1);
+                         nruns, d_trun, p1, cr, xagg, h.t0, h.t1);
       KS_HIP(hipGetLastError());
     }
     if (nr > 0) {
@@ -3328,7 +3343,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     }
     if (nt > 0) {
       hipLaunchKernelGGL(k_stitch_emit, dim3((unsigned)((nt + wpb - 1) / wpb)), dim3(64 * wpb), 0, strm, g, d_tbase, d_cbase,
-                         nruns, runs.a, runs.seq, p1, cr, ec, xtin, rb, rs, err_h, h.t0, h.t1);
+                         nruns, d_trun, runs.a, runs.seq, p1, cr, ec, xtin, rb, rs, err_h, h.t0, h.t1);
       KS_HIP(hipGetLastError());
     }
     return KS_OK;

@@ -370,8 +370,10 @@ static_assert(kP1WinReach <= kP1TailMargin + 1, "pipelined windows stay inside t
 
 // ------------------------------------------------------------------- P0
 
-__global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase, int64_t nruns,
-                              int k, const int64_t *__restrict__ rbnd, int extra, Chunks g) {
+// Chunk start, length and run: a lane per chunk, its run by a binary search
+// over the chunk bases (KS_MAKE_CHUNKS_SEARCH: A/B against k_make_chunks).
+__global__ void k_make_chunks_search(const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase,
+                                     int64_t nruns, int k, const int64_t *__restrict__ rbnd, int extra, Chunks g) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
   int64_t lo = 0, hi = nruns - 1;  // last run with cbase[r] <= c
@@ -379,6 +381,20 @@ __global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__r
     const int64_t mid = (lo + hi + 1) >> 1;
     if (cbase[mid] <= c) lo = mid; else hi = mid - 1;
   }
+  const int64_t first = ra[lo] + k + (c - cbase[lo]) * CH;
+  const int64_t last = rbnd[lo] - 1 + extra;  // tr_lr: one more index (the first k-mer's own step)
+  g.start[c] = first;
+  g.n[c] = (int32_t)min((int64_t)CH, last - first + 1);
+  g.run[c] = (int32_t)lo;
+}
+__global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase,
+                              const int64_t *__restrict__ tbase, const int32_t *__restrict__ trun, int64_t ntiles,
+                              int k, const int64_t *__restrict__ rbnd, int extra, Chunks g) {
+  const int64_t t = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (t >= ntiles) return;
+  const int64_t lo = trun[t];
+  const int64_t c = cbase[lo] + (t - tbase[lo]) * 64 + (threadIdx.x & 63);
+  if (c >= cbase[lo + 1]) return;
   const int64_t first = ra[lo] + k + (c - cbase[lo]) * CH;
   const int64_t last = rbnd[lo] - 1 + extra;  // tr_lr: one more index (the first k-mer's own step)
   g.start[c] = first;
@@ -1438,8 +1454,18 @@ __global__ void k_tile_runs(const int64_t *__restrict__ tbase, int64_t nruns, in
 // wave-per-tile kernels by its latency (12 loads at 2,790 runs).
 __device__ __forceinline__ void tile_of(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
                                         const int32_t *__restrict__ trun, int64_t t, int64_t &r, int64_t &c0,
-                                        int64_t &c1) {
-  const int64_t lo = trun[t];
+                                        int64_t &c1, int64_t nruns) {
+  int64_t lo;
+  if (trun) {
+    lo = trun[t];
+  } else {  // (KS_TILE_SEARCH: the binary search, A/B)
+    lo = 0;
+    int64_t hi = nruns - 1;  // last run with tbase[r] <= t
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (tbase[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+  }
   r = lo;
   c0 = cbase[lo] + (t - tbase[lo]) * 64;
   c1 = min(c0 + 64, cbase[lo + 1]);
@@ -1468,7 +1494,7 @@ __global__ void __launch_bounds__(256) k_ascan_tiles(const int64_t *__restrict__
   if (t >= t_hi) return;
   const int lane = threadIdx.x & 63;
   int64_t r, c0, c1;
-  tile_of(tbase, cbase, trun, t, r, c0, c1);
+  tile_of(tbase, cbase, trun, t, r, c0, c1, nruns);
   const int64_t c = c0 + lane;
   double a = 0.0, b = -INFINITY;
   if (c < c1) {
@@ -1512,7 +1538,7 @@ __global__ void __launch_bounds__(256) k_ascan_apply(const int64_t *__restrict__
   if (t >= t_hi) return;
   const int lane = threadIdx.x & 63;
   int64_t r, c0, c1;
-  tile_of(tbase, cbase, trun, t, r, c0, c1);
+  tile_of(tbase, cbase, trun, t, r, c0, c1, nruns);
   const int64_t c = c0 + lane;
   double a = 0.0, b = -INFINITY;
   if (c < c1) {
@@ -2747,7 +2773,7 @@ __global__ void __launch_bounds__(256) k_stitch_tiles(Chunks g, const int64_t *_
   if (t >= t_hi) return;
   const int lane = threadIdx.x & 63;
   int64_t r, c0, c1;
-  tile_of(tbase, cbase, trun, t, r, c0, c1);
+  tile_of(tbase, cbase, trun, t, r, c0, c1, nruns);
   const int64_t c = c0 + lane;
   XState f{0, 0, 0, 0, -INFINITY};
   if (c < c1) f = chunk_op(g, o, cr, c).f;
@@ -2794,7 +2820,7 @@ __global__ void __launch_bounds__(256) k_stitch_emit(Chunks g, const int64_t *__
   if (t >= t_hi) return;
   const int lane = threadIdx.x & 63;
   int64_t r, c0, c1;
-  tile_of(tbase, cbase, trun, t, r, c0, c1);
+  tile_of(tbase, cbase, trun, t, r, c0, c1, nruns);
   const int64_t c = c0 + lane;
   const bool live = c < c1;
   ChunkOp op;
@@ -2930,7 +2956,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   };
   const XTiles xagg = xtiles(W + o_xagg), xtin = xtiles(W + o_xagg + al(ntiles * 32));
   double2 *d_tagg = reinterpret_cast<double2 *>(W + o_tagg);
-  int32_t *d_trun = reinterpret_cast<int32_t *>(W + o_trun);
+  int32_t *d_trun_map = reinterpret_cast<int32_t *>(W + o_trun);
+  int32_t *d_trun = getenv("KS_TILE_SEARCH") ? nullptr : d_trun_map;
   // carry tile batches (KS_NO_TILE_BATCH: A/B, the per-tile walk only)
   const bool tile_batch = getenv("KS_NO_TILE_BATCH") == nullptr;
   long long *gtd = reinterpret_cast<long long *>(W + o_gtd);
@@ -3008,13 +3035,19 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
 
   // ---- P0 chunks, P1 gather pass
   KS_HIP(hipEventRecord(ctx->ev[7], st));
-  hipLaunchKernelGGL(k_make_chunks, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, st, runs.a, d_cbase,
-                     nruns, k, runs.b, mode.trlr, g);
-  KS_HIP(hipGetLastError());
   if (nruns > 0) {
-    hipLaunchKernelGGL(k_tile_runs, dim3((unsigned)nruns), dim3(256), 0, st, d_tbase, nruns, d_trun);
+    hipLaunchKernelGGL(k_tile_runs, dim3((unsigned)nruns), dim3(256), 0, st, d_tbase, nruns, d_trun_map);
     KS_HIP(hipGetLastError());
   }
+  if (getenv("KS_MAKE_CHUNKS_SEARCH") == nullptr) {
+    if (ntiles > 0)
+      hipLaunchKernelGGL(k_make_chunks, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, st, runs.a, d_cbase, d_tbase,
+                         d_trun_map, ntiles, k, runs.b, mode.trlr, g);
+  } else {
+    hipLaunchKernelGGL(k_make_chunks_search, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, st, runs.a, d_cbase,
+                       nruns, k, runs.b, mode.trlr, g);
+  }
+  KS_HIP(hipGetLastError());
   const unsigned gch = (unsigned)((nch + 255) / 256);
   const unsigned gch1k = (unsigned)((nch + 1023) / 1024);
   const int Jt = (tv.ext != nullptr) ? tv.ext_J : 1;

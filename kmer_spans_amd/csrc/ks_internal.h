@@ -86,6 +86,8 @@ struct ks_ctx {
   hipStream_t side = nullptr;  // forked work that overlaps the main stream (joined by events; lowest priority)
   hipStream_t hi = nullptr;    // highest-priority stream: the first half's pass 1 (ks_scan_chunked.hip)
   ks_ctx *sub = nullptr;       // second context of the same device: the other part of a two-part scan
+  unsigned long long hreg[64] = {};  // region counters per segment read back with the chunked scan's counters
+  bool hreg_ok = false;              // (kSegs entries, valid until the next scan attempt)
   int64_t rescan_segcap = 0;  // grow-only rescan capacity per segment (tr_lr rescans outnumber regions)
 };
 
@@ -188,6 +190,7 @@ ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int t
 // segments of segcap slots, each with its own counter, so that appends from
 // thousands of waves do not serialise on one address; slot s*segcap + i.
 constexpr int kSegs = 64;
+static_assert(kSegs <= 64, "ks_ctx::hreg holds kSegs counters");
 
 struct RegionBuf {
   int32_t *seq;

@@ -361,7 +361,12 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
   unsigned long long *d_rcount = reinterpret_cast<unsigned long long *>(scal) + 16;  // [kSegs]
   std::vector<unsigned long long> hcnt(kSegs, 0);
-  auto read_counts = [&]() -> ks_status {  // -> hcnt; sync
+  auto read_counts = [&]() -> ks_status {  // -> hcnt (sync), or the copy the chunked scan made
+    if (ctx->hreg_ok) {
+      ctx->hreg_ok = false;
+      std::copy(ctx->hreg, ctx->hreg + kSegs, hcnt.begin());
+      return KS_OK;
+    }
     KS_HIP(hipMemcpyAsync(hcnt.data(), d_rcount, 8 * kSegs, hipMemcpyDeviceToHost, st));
     KS_HIP(hipStreamSynchronize(st));
     return KS_OK;
@@ -386,6 +391,7 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
     rb.cap = cap;
     rb.segcap = segcap;
     KS_HIP(hipMemsetAsync(d_rcount, 0, 8 * kSegs, st));
+    ctx->hreg_ok = false;
     KS_HIP(hipEventRecord(ctx->ev[3], st));
     if (algo == 1) {
       // visits of the chunked path go to a scratch histogram first, so that a
@@ -433,6 +439,7 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
         return KS_INTERNAL_DUAL_ABORT;  // scan_impl redoes the whole call in one part
       } else if (rc == KS_ERR_INTERNAL) {
         fprintf(stderr, "kmer_spans_amd: chunked scan fell back to the lane kernel: %s\n", ks_last_error());
+        ctx->hreg_ok = false;  // the lane kernel recounts the regions
         algo = 0;
         S->scan_algo = 0;
         KS_HIP(hipMemsetAsync(d_rcount, 0, 8 * kSegs, st));
@@ -447,9 +454,12 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
     }
     KS_HIP(hipEventRecord(ctx->ev[4], st));
     KS_TRY(read_counts());
-    float ms = 0;
-    KS_HIP(hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[4]));
-    if (algo == 0) S->ms_scan = ms;
+    if (algo == 0) {  // (the chunked scan times itself; its counters came without a sync here)
+      float ms = 0;
+      KS_HIP(hipEventSynchronize(ctx->ev[4]));
+      KS_HIP(hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[4]));
+      S->ms_scan = ms;
+    }
     const int64_t m = max_count();
     if (m <= segcap) {
       complete = true;

@@ -3403,7 +3403,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   KS_HIP(hipEventRecord(ctx->ev[11], st));
   std::vector<unsigned long long> hcv(2 * kSegs + 4);
   KS_HIP(hipMemcpyAsync(hcv.data(), cnts, 8 * (2 * kSegs + 4), hipMemcpyDeviceToHost, st));
+  // the region counters too (final: the rescans above append the last
+  // regions), so that scan_impl needs no second round trip for them
+  KS_HIP(hipMemcpyAsync(ctx->hreg, rb.count, 8 * kSegs, hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
+  ctx->hreg_ok = true;
   unsigned long long cand_max = 0, res_max = 0, res_tot = 0;
   for (int q = 0; q < kSegs; ++q) {
     cand_max = std::max(cand_max, hcv[q]);

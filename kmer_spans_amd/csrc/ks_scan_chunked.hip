@@ -102,6 +102,18 @@ struct TileComp {
   int32_t *ee;               // [tiles]
 };
 
+// Values of the chunks the carry will likely replay (no summary, a predicted
+// positive entry that does not clamp for certain), gathered ahead in
+// parallel (k_replay_gather): a replay then costs one coalesced 32-B load
+// per lane instead of the dependent base / code / LUT loads of values4.
+struct ReplayBuf {
+  int32_t *slot;             // [nch] slot of chunk c, -1: none
+  int64_t *chunk;            // [2 * cap] chunk of a slot
+  double *v;                 // [2 * cap * 256] values, lane-major (4 per lane)
+  unsigned long long *count; // [2] listed chunks per half (may exceed cap: those are not listed)
+  int64_t cap;               // slots per half
+};
+
 struct Cand {  // closed emittable excursions of the clean trajectories (segmented append)
   long long *beg, *arg, *rst;
   double *best;
@@ -1609,12 +1621,13 @@ __global__ void __launch_bounds__(256) k_summ_select(Chunks g, P1 o, const doubl
                                                      Summ sm, int64_t *__restrict__ fix,
                                                      unsigned long long *__restrict__ nfix,
                                                      const double *__restrict__ xh,
-                                                     unsigned long long *__restrict__ why) {
+                                                     unsigned long long *__restrict__ why, ReplayBuf rp, int hi) {
   const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool want = false;
+  bool want = false, rwant = false;
   if (c < g.nch) {
     sm.e[c] = INT32_MIN;
     const double x = xt[c];
+    if (rp.slot) rp.slot[c] = -1;
     if (!o.special[c] && x >= kLMin && x < 1.0e18) {
       const int e = (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
       const double lo = fmin(x, x + o.pmin[c]), hi = fmax(x, x + o.pmax[c]);
@@ -1637,6 +1650,26 @@ __global__ void __launch_bounds__(256) k_summ_select(Chunks g, P1 o, const doubl
           // diagnostics (KS_DEBUG_CARRY): no prediction / void summary / other binade
           if (why) atomicAdd(&why[sp.e[2 * c] != INT32_MIN ? 2 : (xh[c] >= kP1SumMin ? 1 : 0)], 1ull);
         }
+      }
+    }
+    // no summary will serve it: a likely replay unless it enters at 0 or
+    // clamps for certain (with a wide margin: a needless prefetch is cheap)
+    rwant = rp.slot && !want && sm.e[c] == INT32_MIN && !o.special[c] && x > 0.0 &&
+            !(x + o.pmin[c] < -ldexp(fabs(x) + o.sabs[c], -8));
+  }
+  {  // wave-aggregated append to the replay prefetch list of this half
+    const unsigned long long b = __ballot(rwant);
+    if (b) {
+      const int lane = threadIdx.x & 63;
+      const int leader = __ffsll((long long)b) - 1;
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(rp.count + hi, (unsigned long long)__popcll(b));
+      base = __shfl(base, leader, 64);
+      const unsigned long long q = base + __popcll(b & ((1ull << lane) - 1ull));
+      if (rwant && (int64_t)q < rp.cap) {
+        const int64_t sl = hi * rp.cap + (int64_t)q;
+        rp.slot[c] = (int32_t)sl;
+        rp.chunk[sl] = c;
       }
     }
   }
@@ -1679,6 +1712,30 @@ __global__ void __launch_bounds__(256) k_summ_fix(Chunks g, const uint8_t *__res
       sm.N[2 * c + t] = N[t];
       sm.A[2 * c + t] = A[t];
     }
+  }
+}
+
+// Values of the listed likely replays (k_summ_select): a wave per chunk,
+// 4 values per lane through the expanded table, stored lane-major.
+template <bool kLds>
+__global__ void __launch_bounds__(256) k_replay_gather(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
+                                                       int k, TableView tv, ReplayBuf rp, int hi) {
+  __shared__ double s_lut[kLds ? kLdsLutMax : 1];
+  if (kLds) {
+    for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t nl = min((int64_t)rp.count[hi], rp.cap);
+  for (int64_t w = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); w < nl; w += nw) {
+    const int64_t sl = hi * rp.cap + w;
+    const int64_t c = rp.chunk[sl];
+    double v[4];
+    values16_nostore<4>(g, seq, total, k, tv, c, 4 * lane, g.n[c], v, kLds ? s_lut : nullptr);
+    double2 *d = reinterpret_cast<double2 *>(rp.v + sl * 256 + 4 * lane);
+    d[0] = make_double2(v[0], v[1]);
+    d[1] = make_double2(v[2], v[3]);
   }
 }
 
@@ -2050,7 +2107,7 @@ template <bool kCompressed>
 __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64_t c1, const uint8_t *__restrict__ seq,
                                               int64_t total, int k, const TableView &tv,
                                               const uint16_t *__restrict__ codes, const P1 &o, const Summ &sm,
-                                              const Carry &cr, const TileComp &tc,
+                                              const Carry &cr, const TileComp &tc, const ReplayBuf &rp,
                                               unsigned long long *__restrict__ nreplay,
                                               unsigned int *__restrict__ err, long long *__restrict__ dbg,
                                               int64_t r) {
@@ -2064,7 +2121,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
   // behind the tile's scan)
   struct TileIn {
     double exit, pmin, sabs;
-    int spec, n, se;
+    int spec, n, se, rs;
     long long D[2], M[2], N[2];
     int A[2];
   };
@@ -2077,6 +2134,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
     t.sabs = o.sabs[cc];
     t.spec = live ? o.special[cc] : 1;
     t.n = live ? g.n[cc] : 0;
+    t.rs = (live && rp.slot) ? rp.slot[cc] : -1;
     const int se = sm.e[cc];
     t.se = live ? se : INT32_MIN;
 #pragma unroll
@@ -2261,7 +2319,17 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
         const int64_t cj = cb + j;
         const int n = rl32(l_n, j);
         double v[4];
-        values4(g, seq, total, k, tv, kCompressed ? codes : nullptr, cj, 4 * lane, n, v);
+        const int rsj = rl32(cur.rs, j);
+        if (rsj >= 0) {  // gathered ahead (k_replay_gather)
+          const double2 *d = reinterpret_cast<const double2 *>(rp.v + (int64_t)rsj * 256 + 4 * lane);
+          const double2 a = d[0], b = d[1];
+          v[0] = a.x;
+          v[1] = a.y;
+          v[2] = b.x;
+          v[3] = b.y;
+        } else {
+          values4(g, seq, total, k, tv, kCompressed ? codes : nullptr, cj, 4 * lane, n, v);
+        }
         double T = x, hmax = -1.0;
         int hq = -1, harg = 0;
         const bool par = kParReplay && replay_par(v, n, x, T, hmax, harg);
@@ -2425,7 +2493,7 @@ template <bool kCompressed>
 __global__ void __launch_bounds__(256) k_carry_win(Chunks g, const uint8_t *__restrict__ flag,
                                                   const uint8_t *__restrict__ seq, int64_t total, int k, TableView tv,
                                                   const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
-                                                  TileComp tc, unsigned long long *__restrict__ nreplay,
+                                                  TileComp tc, ReplayBuf rp, unsigned long long *__restrict__ nreplay,
                                                   unsigned int *__restrict__ err, long long *__restrict__ dbg) {
   // a wave per window: segment starts in [c0, nch); segments end by nch
   const int64_t w = g.c0 / 64 + (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -2449,7 +2517,7 @@ __global__ void __launch_bounds__(256) k_carry_win(Chunks g, const uint8_t *__re
         }
       }
     }
-    carry_segment<kCompressed>(g, c0, c1, seq, total, k, tv, codes, o, sm, cr, tc, nreplay, err, dbg, w);
+    carry_segment<kCompressed>(g, c0, c1, seq, total, k, tv, codes, o, sm, cr, tc, rp, nreplay, err, dbg, w);
   }
 }
 
@@ -2459,13 +2527,13 @@ template <bool kCompressed>
 __global__ void __launch_bounds__(64) k_carry_run(Chunks g, const int64_t *__restrict__ cbase, int64_t nruns,
                                                   const uint8_t *__restrict__ seq, int64_t total, int k, TableView tv,
                                                   const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
-                                                  TileComp tc, unsigned long long *__restrict__ nreplay,
+                                                  TileComp tc, ReplayBuf rp, unsigned long long *__restrict__ nreplay,
                                                   unsigned int *__restrict__ err, long long *__restrict__ dbg,
                                                   int64_t r_lo) {
   const int64_t r = r_lo + blockIdx.x;
   if (r >= nruns || !(*(volatile unsigned int *)err & 16u)) return;
   const int64_t c0 = cbase[r], c1 = cbase[r + 1];
-  if (c0 < c1) carry_segment<kCompressed>(g, c0, c1, seq, total, k, tv, codes, o, sm, cr, tc, nreplay, err, nullptr, r);
+  if (c0 < c1) carry_segment<kCompressed>(g, c0, c1, seq, total, k, tv, codes, o, sm, cr, tc, rp, nreplay, err, nullptr, r);
 }
 
 // Fallback preparation: after a failed segment check, the first heads pass
@@ -2934,6 +3002,12 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const size_t o_gtd = off; off += al(ngt * 8 * 6);
   const size_t o_gtm = off; off += al(ngt * 8);
   const size_t o_gtee = off; off += al(ngt * 4);
+  // likely-replay prefetch (k_summ_select lists, k_replay_gather fills)
+  const int64_t rcap_h = std::max<int64_t>(65536, nch / 128);  // slots per half
+  const size_t o_rslot = off; off += al(nch * 4);
+  const size_t o_rchunk = off; off += al(2 * rcap_h * 8);
+  const size_t o_rcnt = off; off += al(64);
+  const size_t o_rval = off; off += al(2 * rcap_h * 256 * 8);
   void *wsp = nullptr;
   KS_TRY(ensure(ctx, SLOT_CHUNK_A, off, &wsp));
   char *W = static_cast<char *>(wsp);
@@ -2966,6 +3040,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   long long *gtd = reinterpret_cast<long long *>(W + o_gtd);
   const TileComp tcomp{reinterpret_cast<int32_t *>(W + o_gte), gtd, gtd + 2 * ngt, gtd + 4 * ngt,
                        reinterpret_cast<long long *>(W + o_gtm), reinterpret_cast<int32_t *>(W + o_gtee)};
+  ReplayBuf rpb{reinterpret_cast<int32_t *>(W + o_rslot), reinterpret_cast<int64_t *>(W + o_rchunk),
+                reinterpret_cast<double *>(W + o_rval), reinterpret_cast<unsigned long long *>(W + o_rcnt), rcap_h};
   double *d_tin = reinterpret_cast<double *>(W + o_tin);
   // approximate max-plus scan of (sum, clean exit) over runs [r0, r1) (tiles
   // [t0, t1)): three parallel kernels, or the one-wave-per-run k_approx_scan
@@ -3060,6 +3136,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const bool p1summ = comp && Jt >= 2 && !lds_table && runs.packed != nullptr && tv.approx != nullptr &&
                       !kP1NoStore && getenv("KS_NO_P1_SUMMARY") == nullptr &&
                       getenv("KS_NO_PIPELINED_P1") == nullptr;
+  // (KS_NO_REPLAY_PREFETCH: A/B; the carry reads no slots unless k_summ_select wrote them)
+  if (!p1summ || getenv("KS_NO_REPLAY_PREFETCH") != nullptr) rpb.slot = nullptr;
   // Two halves of the runs (pass-1-summary path): the second half's pass 1
   // (side stream) runs while the first half's latency-bound later passes
   // (carry, stitch) run on the main stream; halves split at a run boundary,
@@ -3283,8 +3361,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     KS_HIP(hipGetLastError());
     if (p1summ) {
       KS_HIP(hipMemsetAsync(d_nfix + hi, 0, 8, strm));
+      KS_HIP(hipMemsetAsync(rpb.count + hi, 0, 8, strm));
       hipLaunchKernelGGL(k_summ_select, dim3(gch_h), dim3(256), 0, strm, gv, p1, xt, sp1, sm, d_fix + h.c0,
-                         d_nfix + hi, d_xh, dbg ? reinterpret_cast<unsigned long long *>(dbg + nwin * 9) : nullptr);
+                         d_nfix + hi, d_xh, dbg ? reinterpret_cast<unsigned long long *>(dbg + nwin * 9) : nullptr,
+                         rpb, hi);
       KS_HIP(hipGetLastError());
       const unsigned gf = (unsigned)std::max<int64_t>(1, std::min<int64_t>(gch_h, (int64_t)ctx->num_cus * 8));
       static const bool fix_serial = getenv("KS_FIX_SERIAL") != nullptr;  // A/B: lane-serial summaries
@@ -3306,6 +3386,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
         else
           hipLaunchKernelGGL(k_summ_fixw<false>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
                              d_fix + h.c0, d_nfix + hi, sm);
+      }
+      if (rpb.slot) {
+        const unsigned gw = (unsigned)std::max<int64_t>(1, (int64_t)ctx->num_cus * 8);
+        hipLaunchKernelGGL(k_replay_gather<false>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, rpb, hi);
+        KS_HIP(hipGetLastError());
       }
     } else if (lds_lut)
       hipLaunchKernelGGL((k_summaries<true, true>), dim3(gch1k), dim3(1024), 0, strm, g, s->seq, total, k, tv, codes,
@@ -3330,10 +3415,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     }
     if (comp)
       hipLaunchKernelGGL(k_carry_win<true>, dim3((nwc + wpb - 1) / wpb), dim3(64 * wpb), 0, strm, gv, d_flag, s->seq, total, k, tv, codes, p1,
-                         sm, cr, tch, rep_h, err_h, dbg);
+                         sm, cr, tch, rpb, rep_h, err_h, dbg);
     else
       hipLaunchKernelGGL(k_carry_win<false>, dim3((nwc + wpb - 1) / wpb), dim3(64 * wpb), 0, strm, gv, d_flag, s->seq, total, k, tv, codes,
-                         p1, sm, cr, tch, rep_h, err_h, dbg);
+                         p1, sm, cr, tch, rpb, rep_h, err_h, dbg);
     KS_HIP(hipGetLastError());
     if (tile_batch) {
       hipLaunchKernelGGL(k_tile_apply, dim3(gtc), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 0);
@@ -3356,10 +3441,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     if (nr > 0) {
       if (comp)
         hipLaunchKernelGGL(k_carry_run<true>, dim3((unsigned)nr), dim3(64), 0, strm, gv, d_cbase, h.r1, s->seq, total,
-                           k, tv, codes, p1, sm, cr, tch, rep_h, err_h, nullptr, h.r0);
+                           k, tv, codes, p1, sm, cr, tch, rpb, rep_h, err_h, nullptr, h.r0);
       else
         hipLaunchKernelGGL(k_carry_run<false>, dim3((unsigned)nr), dim3(64), 0, strm, gv, d_cbase, h.r1, s->seq,
-                           total, k, tv, codes, p1, sm, cr, tch, rep_h, err_h, nullptr, h.r0);
+                           total, k, tv, codes, p1, sm, cr, tch, rpb, rep_h, err_h, nullptr, h.r0);
       if (tile_batch) hipLaunchKernelGGL(k_tile_apply, dim3(gtc), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 1);
     }
     heads(1);
@@ -3430,6 +3515,12 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     KS_HIP(hipMemcpy(why, dbg + nwin * 9, 24, hipMemcpyDeviceToHost));
     fprintf(stderr, "[p1summ] chunks %lld gathered summaries %llu (no prediction %llu, void %llu, other binade %llu)\n",
             (long long)nch, nf, why[0], why[1], why[2]);
+    if (rpb.slot) {
+      unsigned long long rc[2] = {0, 0};
+      KS_HIP(hipMemcpy(rc, rpb.count, 16, hipMemcpyDeviceToHost));
+      fprintf(stderr, "[replay prefetch] listed %llu + %llu chunks (cap %lld per half)\n", rc[0], rc[1],
+              (long long)rpb.cap);
+    }
   }
   if (dbg) {
     std::vector<long long> h(nwin * 9);

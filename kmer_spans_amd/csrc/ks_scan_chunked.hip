@@ -1617,6 +1617,74 @@ __global__ void __launch_bounds__(1024) k_summaries(Chunks g, const uint8_t *__r
 // want one (same test as k_summaries) is the pass-1 one when pass 1 predicted
 // this binade; the others (no or another prediction, a tie, the tail chunks)
 // are listed for k_summ_fix.
+// The per-chunk part of k_summ_select: the selected summary (or none) of
+// chunk c; want: list it for k_summ_fix; rwant: list it for the replay
+// prefetch.
+__device__ __forceinline__ void select_one(const Chunks &g, const P1 &o, const double *__restrict__ xt,
+                                           const SummP1 &sp, const Summ &sm, const double *__restrict__ xh,
+                                           unsigned long long *__restrict__ why, const ReplayBuf &rp, int64_t c,
+                                           bool &want, bool &rwant) {
+  want = rwant = false;
+  sm.e[c] = INT32_MIN;
+  const double x = xt[c];
+  if (rp.slot) rp.slot[c] = -1;
+  if (!o.special[c] && x >= kLMin && x < 1.0e18) {
+    const int e = (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
+    const double lo = fmin(x, x + o.pmin[c]), hi = fmax(x, x + o.pmax[c]);
+    const double slack = ldexp(1.0, e - 24) + o.sabs[c] * 1e-9;
+    if (lo - slack >= ldexp(1.0, e) && hi + slack < ldexp(1.0, e + 1)) {
+      const int t = sp.e[2 * c] == e ? 0 : (sp.e[2 * c + 1] == e ? 1 : -1);
+      if (t >= 0) {
+        sm.e[c] = e;
+        const long long D = sp.D[2 * c + t], M = sp.M[2 * c + t], N = sp.N[2 * c + t];
+        const int A = sp.A[2 * c + t];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          sm.D[2 * c + q] = D;
+          sm.M[2 * c + q] = M;
+          sm.N[2 * c + q] = N;
+          sm.A[2 * c + q] = A;
+        }
+      } else {
+        want = true;
+        // diagnostics (KS_DEBUG_CARRY): no prediction / void summary / other binade
+        if (why) atomicAdd(&why[sp.e[2 * c] != INT32_MIN ? 2 : (xh[c] >= kP1SumMin ? 1 : 0)], 1ull);
+      }
+    }
+  }
+  // no summary will serve it: a likely replay unless it enters at 0 or
+  // clamps for certain (with a wide margin: a needless prefetch is cheap)
+  rwant = rp.slot && !want && sm.e[c] == INT32_MIN && !o.special[c] && x > 0.0 &&
+          !(x + o.pmin[c] < -ldexp(fabs(x) + o.sabs[c], -8));
+}
+
+// Wave-aggregated appends of the wave's listed chunks (every lane calls it).
+__device__ __forceinline__ void select_append(bool want, bool rwant, int64_t c, int64_t *__restrict__ fix,
+                                              unsigned long long *__restrict__ nfix, const ReplayBuf &rp, int hi) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long b = __ballot(want);
+  if (b) {
+    const int leader = __ffsll((long long)b) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(nfix, (unsigned long long)__popcll(b));
+    base = __shfl(base, leader, 64);
+    if (want) fix[base + __popcll(b & ((1ull << lane) - 1ull))] = c;
+  }
+  const unsigned long long br = __ballot(rwant);
+  if (br) {
+    const int leader = __ffsll((long long)br) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(rp.count + hi, (unsigned long long)__popcll(br));
+    base = __shfl(base, leader, 64);
+    const unsigned long long q = base + __popcll(br & ((1ull << lane) - 1ull));
+    if (rwant && (int64_t)q < rp.cap) {
+      const int64_t sl = hi * rp.cap + (int64_t)q;
+      rp.slot[c] = (int32_t)sl;
+      rp.chunk[sl] = c;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) k_summ_select(Chunks g, P1 o, const double *__restrict__ xt, SummP1 sp,
                                                      Summ sm, int64_t *__restrict__ fix,
                                                      unsigned long long *__restrict__ nfix,
@@ -1624,64 +1692,36 @@ __global__ void __launch_bounds__(256) k_summ_select(Chunks g, P1 o, const doubl
                                                      unsigned long long *__restrict__ why, ReplayBuf rp, int hi) {
   const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool want = false, rwant = false;
-  if (c < g.nch) {
-    sm.e[c] = INT32_MIN;
-    const double x = xt[c];
-    if (rp.slot) rp.slot[c] = -1;
-    if (!o.special[c] && x >= kLMin && x < 1.0e18) {
-      const int e = (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
-      const double lo = fmin(x, x + o.pmin[c]), hi = fmax(x, x + o.pmax[c]);
-      const double slack = ldexp(1.0, e - 24) + o.sabs[c] * 1e-9;
-      if (lo - slack >= ldexp(1.0, e) && hi + slack < ldexp(1.0, e + 1)) {
-        const int t = sp.e[2 * c] == e ? 0 : (sp.e[2 * c + 1] == e ? 1 : -1);
-        if (t >= 0) {
-          sm.e[c] = e;
-          const long long D = sp.D[2 * c + t], M = sp.M[2 * c + t], N = sp.N[2 * c + t];
-          const int A = sp.A[2 * c + t];
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            sm.D[2 * c + q] = D;
-            sm.M[2 * c + q] = M;
-            sm.N[2 * c + q] = N;
-            sm.A[2 * c + q] = A;
-          }
-        } else {
-          want = true;
-          // diagnostics (KS_DEBUG_CARRY): no prediction / void summary / other binade
-          if (why) atomicAdd(&why[sp.e[2 * c] != INT32_MIN ? 2 : (xh[c] >= kP1SumMin ? 1 : 0)], 1ull);
-        }
-      }
-    }
-    // no summary will serve it: a likely replay unless it enters at 0 or
-    // clamps for certain (with a wide margin: a needless prefetch is cheap)
-    rwant = rp.slot && !want && sm.e[c] == INT32_MIN && !o.special[c] && x > 0.0 &&
-            !(x + o.pmin[c] < -ldexp(fabs(x) + o.sabs[c], -8));
-  }
-  {  // wave-aggregated append to the replay prefetch list of this half
-    const unsigned long long b = __ballot(rwant);
-    if (b) {
-      const int lane = threadIdx.x & 63;
-      const int leader = __ffsll((long long)b) - 1;
-      unsigned long long base = 0;
-      if (lane == leader) base = atomicAdd(rp.count + hi, (unsigned long long)__popcll(b));
-      base = __shfl(base, leader, 64);
-      const unsigned long long q = base + __popcll(b & ((1ull << lane) - 1ull));
-      if (rwant && (int64_t)q < rp.cap) {
-        const int64_t sl = hi * rp.cap + (int64_t)q;
-        rp.slot[c] = (int32_t)sl;
-        rp.chunk[sl] = c;
-      }
-    }
-  }
-  // wave-aggregated append to the fix list
-  const unsigned long long b = __ballot(want);
-  if (!b) return;
+  if (c < g.nch) select_one(g, o, xt, sp, sm, xh, why, rp, c, want, rwant);
+  select_append(want, rwant, c, fix, nfix, rp, hi);
+}
+
+// k_seg_marks and k_summ_select in one pass (a wave per 64-chunk window from
+// the one holding c0 - 1): the window's segment marks, then the summaries.
+__global__ void __launch_bounds__(256) k_marks_select(Chunks g, P1 o, const double *__restrict__ xt,
+                                                      uint8_t *__restrict__ flag, int64_t nw, SummP1 sp, Summ sm,
+                                                      int64_t *__restrict__ fix, unsigned long long *__restrict__ nfix,
+                                                      const double *__restrict__ xh,
+                                                      unsigned long long *__restrict__ why, ReplayBuf rp, int hi) {
+  const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wv >= nw) return;
   const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((long long)b) - 1;
-  unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(nfix, (unsigned long long)__popcll(b));
-  base = __shfl(base, leader, 64);
-  if (want) fix[base + __popcll(b & ((1ull << lane) - 1ull))] = c;
+  const int64_t e = ((g.c0 > 0 ? g.c0 - 1 : 0) / 64 + wv) * 64 + lane;
+  bool elig = false, next_run = false;
+  if (e + 1 < g.nch && e + 1 >= g.c0) {
+    next_run = g.run[e + 1] != g.run[e];
+    if (!next_run && e >= g.c0 && !o.special[e]) {
+      const double x = xt[e];
+      elig = x + o.pmin[e] < -ldexp(fabs(x) + o.sabs[e], -20);  // false for NaN
+    }
+  }
+  const unsigned long long b = __ballot(elig);
+  const int f = b ? __ffsll((long long)b) - 1 : 64;
+  if (e + 1 < g.nch && e + 1 >= g.c0) flag[e + 1] = (next_run || lane == f) ? 1 : 0;
+  if (e == 0 && g.c0 == 0) flag[0] = 1;
+  bool want = false, rwant = false;
+  if (e >= g.c0 && e < g.nch) select_one(g, o, xt, sp, sm, xh, why, rp, e, want, rwant);
+  select_append(want, rwant, e, fix, nfix, rp, hi);
 }
 
 // Summaries of the listed chunks from gathered values (their codes were not
@@ -1758,7 +1798,8 @@ template <bool kLds>
 __global__ void __launch_bounds__(256) k_summ_fixw(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
                                                    TableView tv, const double *__restrict__ xt,
                                                    const int64_t *__restrict__ fix,
-                                                   const unsigned long long *__restrict__ nfix, Summ sm) {
+                                                   const unsigned long long *__restrict__ nfix, Summ sm,
+                                                   ReplayBuf rp, int hi) {
   __shared__ double s_lut[kLds ? kLdsLutMax : 1];
   if (kLds) {
     for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
@@ -1767,7 +1808,19 @@ __global__ void __launch_bounds__(256) k_summ_fixw(Chunks g, const uint8_t *__re
   const int lane = threadIdx.x & 63;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int64_t nf = (int64_t)*nfix;
-  for (int64_t f = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); f < nf; f += nw) {
+  // the waves past the fix list gather the listed likely replays (k_replay_gather's work)
+  const int64_t nr = rp.slot ? min((int64_t)rp.count[hi], rp.cap) : 0;
+  for (int64_t f = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); f < nf + nr; f += nw) {
+    if (f >= nf) {
+      const int64_t sl = hi * rp.cap + (f - nf);
+      const int64_t cr = rp.chunk[sl];
+      double v[4];
+      values16_nostore<4>(g, seq, total, k, tv, cr, 4 * lane, g.n[cr], v, kLds ? s_lut : nullptr);
+      double2 *d = reinterpret_cast<double2 *>(rp.v + sl * 256 + 4 * lane);
+      d[0] = make_double2(v[0], v[1]);
+      d[1] = make_double2(v[2], v[3]);
+      continue;
+    }
     const int64_t c = fix[f];
     const int e = binade_of(xt[c]);
     const double scale = ldexp(1.0, 52 - e);
@@ -3357,14 +3410,25 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     KS_TRY(ascan(p1, xt, h.r0, h.r1, h.t0, h.t1, strm));
     const int64_t wl = (h.c0 > 0 ? h.c0 - 1 : 0) / 64;
     const int64_t nwm = (h.c1 + 63) / 64 - wl;
-    hipLaunchKernelGGL(k_seg_marks, dim3((unsigned)((nwm + wpb - 1) / wpb)), dim3(64 * wpb), 0, strm, gv, p1, xt, d_flag, nwm);
-    KS_HIP(hipGetLastError());
+    // segment marks and summary selection in one pass over the chunks
+    // (KS_NO_FUSED_SELECT: k_seg_marks then k_summ_select, A/B)
+    const bool fused = p1summ && getenv("KS_NO_FUSED_SELECT") == nullptr;
+    if (!fused) {
+      hipLaunchKernelGGL(k_seg_marks, dim3((unsigned)((nwm + wpb - 1) / wpb)), dim3(64 * wpb), 0, strm, gv, p1, xt,
+                         d_flag, nwm);
+      KS_HIP(hipGetLastError());
+    }
     if (p1summ) {
       KS_HIP(hipMemsetAsync(d_nfix + hi, 0, 8, strm));
       KS_HIP(hipMemsetAsync(rpb.count + hi, 0, 8, strm));
-      hipLaunchKernelGGL(k_summ_select, dim3(gch_h), dim3(256), 0, strm, gv, p1, xt, sp1, sm, d_fix + h.c0,
-                         d_nfix + hi, d_xh, dbg ? reinterpret_cast<unsigned long long *>(dbg + nwin * 9) : nullptr,
-                         rpb, hi);
+      if (fused)
+        hipLaunchKernelGGL(k_marks_select, dim3((unsigned)((nwm + 3) / 4)), dim3(256), 0, strm, gv, p1, xt, d_flag,
+                           nwm, sp1, sm, d_fix + h.c0, d_nfix + hi, d_xh,
+                           dbg ? reinterpret_cast<unsigned long long *>(dbg + nwin * 9) : nullptr, rpb, hi);
+      else
+        hipLaunchKernelGGL(k_summ_select, dim3(gch_h), dim3(256), 0, strm, gv, p1, xt, sp1, sm, d_fix + h.c0,
+                           d_nfix + hi, d_xh, dbg ? reinterpret_cast<unsigned long long *>(dbg + nwin * 9) : nullptr,
+                           rpb, hi);
       KS_HIP(hipGetLastError());
       const unsigned gf = (unsigned)std::max<int64_t>(1, std::min<int64_t>(gch_h, (int64_t)ctx->num_cus * 8));
       static const bool fix_serial = getenv("KS_FIX_SERIAL") != nullptr;  // A/B: lane-serial summaries
@@ -3382,12 +3446,12 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
         const unsigned gw = (unsigned)std::max<int64_t>(1, (int64_t)ctx->num_cus * 8);
         if (lds_lut && getenv("KS_FIXW_LDS") != nullptr)
           hipLaunchKernelGGL(k_summ_fixw<true>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
-                             d_fix + h.c0, d_nfix + hi, sm);
+                             d_fix + h.c0, d_nfix + hi, sm, rpb, hi);
         else
           hipLaunchKernelGGL(k_summ_fixw<false>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
-                             d_fix + h.c0, d_nfix + hi, sm);
+                             d_fix + h.c0, d_nfix + hi, sm, rpb, hi);
       }
-      if (rpb.slot) {
+      if (rpb.slot && fix_serial) {  // (k_summ_fixw gathers them otherwise)
         const unsigned gw = (unsigned)std::max<int64_t>(1, (int64_t)ctx->num_cus * 8);
         hipLaunchKernelGGL(k_replay_gather<false>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, rpb, hi);
         KS_HIP(hipGetLastError());

@@ -482,7 +482,8 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
   // one block (ks_regions_free frees seq_id): [seq_id | beg | end] int32 (a
   // 3 x n matrix, the layout of the reference's `pos`), then [score | 0.0]
   // doubles (2 x n, `score`'s layout with the reference's second row, :280)
-  {
+  // (allocated while the device orders the regions)
+  auto alloc_out = [&]() -> ks_status {
     const size_t nn = (size_t)std::max<int64_t>(n, 1);
     const size_t ioff = (3 * nn * 4 + 7) & ~(size_t)7;
     char *blk = static_cast<char *>(malloc(ioff + 2 * nn * 8));
@@ -490,12 +491,14 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
       memset(out, 0, sizeof(*out));
       return fail(KS_ERR_NOMEM, "out of host memory for %lld regions", (long long)n);
     }
+    out->n = n;
     out->seq_id = reinterpret_cast<int32_t *>(blk);
     out->beg = out->seq_id + nn;
     out->end = out->beg + nn;
     out->score = reinterpret_cast<double *>(blk + ioff);
     if (n == 0) out->score[0] = 0.0;  // (n > 0: zero-filled while the D2H runs)
-  }
+    return KS_OK;
+  };
   if (n > 0) {
     void *tmpb = nullptr;
     const size_t nn = (size_t)n;
@@ -528,6 +531,7 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
     KS_TRY(ensure_pinned(ctx, blk, &hp));
     KS_HIP(hipMemcpyAsync(hp, o_seq, blk, hipMemcpyDeviceToHost, st));
     KS_HIP(hipEventRecord(ctx->ev[6], st));
+    KS_TRY(alloc_out());
     memset(out->score + nn, 0, nn * 8);  // second row of `score` (overlaps the device work)
     KS_HIP(hipStreamSynchronize(st));
     const char *h = static_cast<const char *>(hp);
@@ -536,6 +540,7 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
     memcpy(out->end, h + (reinterpret_cast<char *>(o_end) - reinterpret_cast<char *>(o_seq)), nn * 4);
     memcpy(out->score, h + (reinterpret_cast<char *>(o_score) - reinterpret_cast<char *>(o_seq)), nn * 8);
   } else {
+    KS_TRY(alloc_out());
     KS_HIP(hipEventRecord(ctx->ev[6], st));
     KS_HIP(hipStreamSynchronize(st));
   }

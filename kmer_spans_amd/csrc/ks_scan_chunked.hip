@@ -1696,6 +1696,10 @@ __global__ void __launch_bounds__(256) k_summ_select(Chunks g, P1 o, const doubl
   select_append(want, rwant, c, fix, nfix, rp, hi);
 }
 
+__global__ void k_copy_u64(const unsigned long long *__restrict__ src, unsigned long long *__restrict__ dst, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
 // k_seg_marks and k_summ_select in one pass (a wave per 64-chunk window from
 // the one holding c0 - 1): the window's segment marks, then the summaries.
 __global__ void __launch_bounds__(256) k_marks_select(Chunks g, P1 o, const double *__restrict__ xt,
@@ -3034,7 +3038,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const size_t o_mode = off; off += al(nch);
   const size_t o_hq = off; off += al(nch * 4 * 2);
   const size_t o_hmax = off; off += al(nch * 8);
-  const size_t o_cnt = off; off += al(8 * (2 * kSegs + 8));
+  const size_t o_cnt = off; off += al(8 * (3 * kSegs + 8));  // + the region counters' copy
   const size_t o_flag = off; off += al(nch + 64);
   const size_t o_xagg = off; off += al(ntiles * 32) * 2;
   // pass-1 summaries: predictor sums / exits / zero flags, predicted entries,
@@ -3550,12 +3554,15 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   KS_TRY(launch_scan_lane(ctx, s->seq, total, rs.a, rs.b, rs.seq, rcap, k, tv, mw, min_score, visits_rescan, rb,
                           rs.count, rs.segcap, mode, 0, nullptr, runs.packed));
   KS_HIP(hipEventRecord(ctx->ev[11], st));
-  std::vector<unsigned long long> hcv(2 * kSegs + 4);
-  KS_HIP(hipMemcpyAsync(hcv.data(), cnts, 8 * (2 * kSegs + 4), hipMemcpyDeviceToHost, st));
   // the region counters too (final: the rescans above append the last
-  // regions), so that scan_impl needs no second round trip for them
-  KS_HIP(hipMemcpyAsync(ctx->hreg, rb.count, 8 * kSegs, hipMemcpyDeviceToHost, st));
+  // regions), copied next to the scan's counters: one readback for both, and
+  // scan_impl needs no round trip of its own
+  hipLaunchKernelGGL(k_copy_u64, dim3(1), dim3(64), 0, st, rb.count, cnts + 2 * kSegs + 8, kSegs);
+  KS_HIP(hipGetLastError());
+  std::vector<unsigned long long> hcv(3 * kSegs + 8);
+  KS_HIP(hipMemcpyAsync(hcv.data(), cnts, 8 * (3 * kSegs + 8), hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
+  std::copy(hcv.begin() + 2 * kSegs + 8, hcv.begin() + 3 * kSegs + 8, ctx->hreg);
   ctx->hreg_ok = true;
   unsigned long long cand_max = 0, res_max = 0, res_tot = 0;
   for (int q = 0; q < kSegs; ++q) {

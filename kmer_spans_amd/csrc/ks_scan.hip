@@ -27,6 +27,7 @@ namespace ks {
 ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, const RunLayout &lay, int k,
                        const TableView &tv, uint64_t mw, double min_score, uint32_t *visits,
                        uint32_t *visits_rescan, const RegionBuf &rb, ks_scan_stats *stats, const ScanMode &mode);
+ks_status chunked_phase_times(ks_ctx *ctx, ks_scan_stats *stats);
 ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const int64_t *ra, const int64_t *rb,
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
@@ -545,6 +546,7 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
     KS_HIP(hipStreamSynchronize(st));
   }
   S->n_regions = n;
+  if (algo == 1) KS_TRY(chunked_phase_times(ctx, S));
   float ms_fin = 0, ms_tot = 0;
   KS_HIP(hipEventElapsedTime(&ms_fin, ctx->ev[5], ctx->ev[6]));
   KS_HIP(hipEventElapsedTime(&ms_tot, ctx->ev[2], ctx->ev[6]));

@@ -3643,23 +3643,29 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       if (hist[e]) fprintf(stderr, " 2^%d:%lld", e, hist[e]);
     fprintf(stderr, "\n");
   }
-  if (stats) {
-    float ms_lay = 0, ms_p1 = 0, ms_p2 = 0, ms_p34 = 0, ms_p5 = 0, ms_res = 0;
-    KS_HIP(hipEventElapsedTime(&ms_lay, ctx->ev[7], ctx->ev[8]));
-    KS_HIP(hipEventElapsedTime(&ms_p1, ctx->ev[8], ctx->ev[9]));
-    KS_HIP(hipEventElapsedTime(&ms_p2, ctx->ev[9], ctx->ev[14]));
-    KS_HIP(hipEventElapsedTime(&ms_p34, ctx->ev[14], ctx->ev[15]));
-    KS_HIP(hipEventElapsedTime(&ms_p5, ctx->ev[15], ctx->ev[10]));
-    KS_HIP(hipEventElapsedTime(&ms_res, ctx->ev[10], ctx->ev[11]));
-    stats->ms_layout = ms_lay;
-    stats->ms_scan = ms_p1;
-    stats->ms_predict = ms_p2;
-    stats->ms_carry = ms_p34;
-    stats->ms_stitch = ms_p5;
-    stats->ms_rescan = ms_res;
+  if (stats) {  // (phase times: chunked_phase_times, after the call's last sync)
     stats->n_rescan = nres;
     stats->n_replay = (int64_t)hc[2];
   }
+  return KS_OK;
+}
+
+// Phase times of the last chunked scan on ctx (its events are complete once
+// the caller has synchronised after the region readback).
+ks_status chunked_phase_times(ks_ctx *ctx, ks_scan_stats *stats) {
+  float ms_lay = 0, ms_p1 = 0, ms_p2 = 0, ms_p34 = 0, ms_p5 = 0, ms_res = 0;
+  KS_HIP(hipEventElapsedTime(&ms_lay, ctx->ev[7], ctx->ev[8]));
+  KS_HIP(hipEventElapsedTime(&ms_p1, ctx->ev[8], ctx->ev[9]));
+  KS_HIP(hipEventElapsedTime(&ms_p2, ctx->ev[9], ctx->ev[14]));
+  KS_HIP(hipEventElapsedTime(&ms_p34, ctx->ev[14], ctx->ev[15]));
+  KS_HIP(hipEventElapsedTime(&ms_p5, ctx->ev[15], ctx->ev[10]));
+  KS_HIP(hipEventElapsedTime(&ms_res, ctx->ev[10], ctx->ev[11]));
+  stats->ms_layout = ms_lay;
+  stats->ms_scan = ms_p1;
+  stats->ms_predict = ms_p2;
+  stats->ms_carry = ms_p34;
+  stats->ms_stitch = ms_p5;
+  stats->ms_rescan = ms_res;
   return KS_OK;
 }
 

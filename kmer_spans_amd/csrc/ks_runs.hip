@@ -33,6 +33,18 @@ __device__ __forceinline__ uint32_t enc_pack4(uint32_t w) {
   const uint32_t t = (w >> 1) & 0x03030303u;
   return ((t & 3u) << 6) | (((t >> 8) & 3u) << 4) | (((t >> 16) & 3u) << 2) | ((t >> 24) & 3u);
 }
+// The same with one multiply: byte i of t (i = 0..3, values 0..3) lands at
+// bit 30 - 2i; every cross term stays below bit 24 without carries.
+__device__ __forceinline__ uint32_t enc_pack4m(uint32_t w) {
+  return (((w >> 1) & 0x03030303u) * 0x40100401u) >> 24;
+}
+// n_mask4 with one multiply: the zero-byte flags at bits 0, 8, 16, 24 (after
+// >> 7) land at bits 28..31; the cross terms are distinct bits below 24.
+__device__ __forceinline__ uint32_t n_mask4m(uint32_t w) {
+  const uint32_t x = (w | 0x20202020u) ^ 0x6e6e6e6eu;
+  const uint32_t z = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+  return ((z >> 7) * 0x10204080u) >> 28;
+}
 
 // Appends the events of `cnt` set bits of starts/ends (bit i <-> p0 + i).
 __device__ __forceinline__ void append_events(uint32_t starts, uint32_t ends, int64_t p0,
@@ -74,6 +86,7 @@ __device__ __forceinline__ void append_events(uint32_t starts, uint32_t ends, in
 // scan_impl): bytes outside it read as N, so its runs and no others come
 // out; units [u0, u1) are visited (the range plus a margin, whose packed
 // words -- pure functions of the bytes -- the part's later passes may read).
+template <bool kMul>  // multiply-based byte packing (A/B: KS_NEV_SHIFTS=1 for the shift/or forms)
 __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ seq, int64_t total,
                                                   unsigned long long *__restrict__ ev,
                                                   unsigned long long *__restrict__ ev_count, int64_t cap,
@@ -101,10 +114,17 @@ __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ se
       if (u < u1) {
         uint32_t nm = 0xffffu;
         if (p0 + 16 <= total) {
-          nm = n_mask4(v[j].x) | (n_mask4(v[j].y) << 4) | (n_mask4(v[j].z) << 8) | (n_mask4(v[j].w) << 12);
-          if (packed)
-            packed[u] = (enc_pack4(v[j].x) << 24) | (enc_pack4(v[j].y) << 16) | (enc_pack4(v[j].z) << 8) |
-                        enc_pack4(v[j].w);
+          if (kMul) {
+            nm = n_mask4m(v[j].x) | (n_mask4m(v[j].y) << 4) | (n_mask4m(v[j].z) << 8) | (n_mask4m(v[j].w) << 12);
+            if (packed)
+              packed[u] = (enc_pack4m(v[j].x) << 24) | (enc_pack4m(v[j].y) << 16) | (enc_pack4m(v[j].z) << 8) |
+                          enc_pack4m(v[j].w);
+          } else {
+            nm = n_mask4(v[j].x) | (n_mask4(v[j].y) << 4) | (n_mask4(v[j].z) << 8) | (n_mask4(v[j].w) << 12);
+            if (packed)
+              packed[u] = (enc_pack4(v[j].x) << 24) | (enc_pack4(v[j].y) << 16) | (enc_pack4(v[j].z) << 8) |
+                          enc_pack4(v[j].w);
+          }
         } else {
           uint32_t pw = 0;
           for (int q = 0; q < 16; ++q) {
@@ -292,8 +312,12 @@ ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs
     const int64_t u1 = std::min<int64_t>(nunits, p_hi / 16 + 1 + kMargin);
     const unsigned grid = (unsigned)std::max<int64_t>(
         1, std::min<int64_t>((u1 - u0 + 1023) / 1024, (int64_t)ctx->num_cus * 16));
-    hipLaunchKernelGGL(k_n_events, dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp,
-                       d_count, cap, packed, p_lo, p_hi, u0, u1);
+    if (getenv("KS_NEV_SHIFTS"))
+      hipLaunchKernelGGL(k_n_events<false>, dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp,
+                         d_count, cap, packed, p_lo, p_hi, u0, u1);
+    else
+      hipLaunchKernelGGL(k_n_events<true>, dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp,
+                         d_count, cap, packed, p_lo, p_hi, u0, u1);
     KS_HIP(hipGetLastError());
     if (s->nseq > 1) {
       hipLaunchKernelGGL(k_seq_events, dim3((unsigned)((s->nseq + 255) / 256)), dim3(256), 0, st, s->seq, total,

@@ -3660,11 +3660,13 @@ ks_status chunked_phase_times(ks_ctx *ctx, ks_scan_stats *stats) {
   KS_HIP(hipEventElapsedTime(&ms_p34, ctx->ev[14], ctx->ev[15]));
   KS_HIP(hipEventElapsedTime(&ms_p5, ctx->ev[15], ctx->ev[10]));
   KS_HIP(hipEventElapsedTime(&ms_res, ctx->ev[10], ctx->ev[11]));
+  // (the second part's P2-P5 events can precede the end of the union of the
+  // pass-1 launches when it finished first: such a phase counts 0)
   stats->ms_layout = ms_lay;
   stats->ms_scan = ms_p1;
-  stats->ms_predict = ms_p2;
-  stats->ms_carry = ms_p34;
-  stats->ms_stitch = ms_p5;
+  stats->ms_predict = std::max(0.0f, ms_p2);
+  stats->ms_carry = std::max(0.0f, ms_p34);
+  stats->ms_stitch = std::max(0.0f, ms_p5);
   stats->ms_rescan = ms_res;
   return KS_OK;
 }

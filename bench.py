@@ -391,6 +391,31 @@ def main():
             ra["memory_requests_G_per_s"] = round(traffic["read_requests"] / (ms_kernel * 1e-3) / 1e9, 2)
         roofline["random_access"] = ra
 
+    # ---- the same step with the visit histogram kmer_regions_r returns
+    # (kmer_spans.c:266-267,523-537): device-resident, count-derived top-level
+    # visits + rescan visits; not `value` (the metric counts regions only)
+    visits_line = None
+    if rank == 0 and not args.trlr and stats[-1]["scan_algo"] == 1:
+        vis = torch.zeros(4 ** k, dtype=torch.int32, device=dev)
+        D.scan(ctx, ds, k, table, args.min_width, args.min_score, visits=vis)  # warm
+        vt = []
+        for _ in range(3):
+            vis.zero_()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            vpos, vscore, _ = D.scan(ctx, ds, k, table, args.min_width, args.min_score, visits=vis)
+            torch.cuda.synchronize()
+            vt.append(time.perf_counter() - t1)
+        tv = float(np.median(vt))
+        # every scored index is visited once at top level or more by rescans
+        vsum = int(vis.to(torch.int64).sum().item())
+        visits_line = {"ms": round(tv * 1e3, 3), "Gbases_per_s": round(n_bases / tv / 1e9, 3),
+                       "regions_equal": bool(np.array_equal(vpos, pos)),
+                       "scores_equal": bool(np.array_equal(vscore.view(np.uint64), score.view(np.uint64))),
+                       "visits_total": vsum, "scored_positions": int(stats[-1].get("n_scored", 0)),
+                       "note": "ks_scan_dev with the visit histogram (device-resident), median of 3"}
+        del vis, vpos, vscore
+
     # ---- PCIe-inclusive rate of the drop-in host entry point (never `value`)
     host_path = None
     need_w = (args.host_path or not args.no_cpu) and rank == 0
@@ -466,6 +491,7 @@ def main():
         "table_equal_host": table_equal_host,
         "regions": n_regions_all,
         "replayed_chunks": int(stats[-1]["n_replay"]),
+        "visits_path": visits_line,
         "host_path": host_path,
         "phase_ms": {key[3:]: round(float(np.mean([s[key] for s in stats])), 3)
                      for key in stats[-1] if key.startswith("ms_")},

@@ -86,7 +86,9 @@ __device__ __forceinline__ void append_events(uint32_t starts, uint32_t ends, in
 // scan_impl): bytes outside it read as N, so its runs and no others come
 // out; units [u0, u1) are visited (the range plus a margin, whose packed
 // words -- pure functions of the bytes -- the part's later passes may read).
-template <bool kMul>  // multiply-based byte packing (A/B: KS_NEV_SHIFTS=1 for the shift/or forms)
+// kPre: lane 0's byte before its unit is loaded with the unit loads (one
+// memory round trip per step) instead of after them (A/B: KS_NEV_LATE_PREV=1).
+template <bool kMul, bool kPre>  // multiply-based byte packing (A/B: KS_NEV_SHIFTS=1 for the shift/or forms)
 __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ seq, int64_t total,
                                                   unsigned long long *__restrict__ ev,
                                                   unsigned long long *__restrict__ ev_count, int64_t cap,
@@ -97,10 +99,13 @@ __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ se
   const int lane = threadIdx.x & 63;
   for (int64_t ub = u0 + (int64_t)blockIdx.x * blockDim.x * U; ub < u1; ub += stride) {
     uint4 v[U];
+    uint32_t pb[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const int64_t p0 = (ub + j * blockDim.x + threadIdx.x) * 16;
       v[j] = p0 + 16 <= total ? *reinterpret_cast<const uint4 *>(seq + p0) : make_uint4(0, 0, 0, 0);
+      pb[j] = 'N';
+      if (kPre && lane == 0 && p0 > 0 && p0 - 1 < total) pb[j] = seq[p0 - 1];
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
@@ -110,7 +115,10 @@ __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ se
       // the byte before the unit: lane - 1's last byte (the same step's
       // previous unit), loaded by lane 0
       uint32_t prev_b = __shfl_up(v[j].w >> 24, 1, 64);
-      if (lane == 0 || p0 + 16 > total) prev_b = p0 == 0 ? (uint32_t)'N' : (p0 - 1 < total ? seq[p0 - 1] : 'N');
+      if (kPre && lane == 0)
+        prev_b = pb[j];
+      else if (lane == 0 || p0 + 16 > total)
+        prev_b = p0 == 0 ? (uint32_t)'N' : (p0 - 1 < total ? seq[p0 - 1] : 'N');
       if (u < u1) {
         uint32_t nm = 0xffffu;
         if (p0 + 16 <= total) {
@@ -312,12 +320,11 @@ ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs
     const int64_t u1 = std::min<int64_t>(nunits, p_hi / 16 + 1 + kMargin);
     const unsigned grid = (unsigned)std::max<int64_t>(
         1, std::min<int64_t>((u1 - u0 + 1023) / 1024, (int64_t)ctx->num_cus * 16));
-    if (getenv("KS_NEV_SHIFTS"))
-      hipLaunchKernelGGL(k_n_events<false>, dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp,
-                         d_count, cap, packed, p_lo, p_hi, u0, u1);
-    else
-      hipLaunchKernelGGL(k_n_events<true>, dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp,
-                         d_count, cap, packed, p_lo, p_hi, u0, u1);
+    auto *kern = getenv("KS_NEV_SHIFTS")     ? k_n_events<false, true>
+                 : getenv("KS_NEV_LATE_PREV") ? k_n_events<true, false>
+                                              : k_n_events<true, true>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp, d_count, cap,
+                       packed, p_lo, p_hi, u0, u1);
     KS_HIP(hipGetLastError());
     if (s->nseq > 1) {
       hipLaunchKernelGGL(k_seq_events, dim3((unsigned)((s->nseq + 255) / 256)), dim3(256), 0, st, s->seq, total,

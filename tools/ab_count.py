@@ -58,6 +58,9 @@ def main():
         print(f"round {r}: " + "  ".join(f"{n} {min(v[-a.steps:]):.2f}" for n, v in res.items()), flush=True)
     for n, v in res.items():
         print(n, "min", round(min(v), 3), "median", round(statistics.median(v), 3))
+    # cross-process comparison of library builds (KS_LIB_PATH): a checksum of the histogram
+    idx = torch.arange(ref.numel(), device=ref.device, dtype=torch.int64) % 1000003 + 1
+    print("checksum", int((ref.to(torch.int64) * idx).sum().item()), "total", int(ref.to(torch.int64).sum().item()))
 
 
 if __name__ == "__main__":

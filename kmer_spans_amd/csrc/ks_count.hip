@@ -280,39 +280,6 @@ inline PartGeo part_geo(int k) {
   return {L, T, T1, T - T1};
 }
 
-// One lane's window of a partition tile (kLook bytes before its kPer
-// positions): the fast path as two 16-B loads, issued a tile ahead so that
-// the next tile's loads are in flight during this tile's LDS work.
-struct Win {
-  uint4 a, b;
-  bool ok;
-};
-__device__ __forceinline__ Win win_load(const uint8_t *__restrict__ seq, int64_t total, int64_t p0) {
-  Win w;
-  w.ok = p0 >= kLook && p0 + kPer <= total;
-  if (w.ok) {
-    w.a = *reinterpret_cast<const uint4 *>(seq + p0 - kLook);
-    w.b = *reinterpret_cast<const uint4 *>(seq + p0);
-  } else {
-    w.a = w.b = make_uint4(0, 0, 0, 0);
-  }
-  return w;
-}
-__device__ __forceinline__ void win_bytes(const Win &w, const uint8_t *__restrict__ seq, int64_t total, int64_t p0,
-                                          uint8_t *b) {
-  if (w.ok) {
-    const uint32_t x[8] = {w.a.x, w.a.y, w.a.z, w.a.w, w.b.x, w.b.y, w.b.z, w.b.w};
-#pragma unroll
-    for (int j = 0; j < kLook + kPer; ++j) b[j] = (uint8_t)(x[j >> 2] >> (8 * (j & 3)));
-  } else {
-#pragma unroll
-    for (int j = 0; j < kLook + kPer; ++j) {
-      const int64_t q = p0 - kLook + j;
-      b[j] = (q >= 0 && q < total) ? seq[q] : (uint8_t)'N';
-    }
-  }
-}
-
 __global__ void k_part_sum_last(const unsigned long long *__restrict__ mat, const unsigned long long *__restrict__ ex,
                                 size_t n, unsigned long long *__restrict__ last) {
   *last = ex[n - 1] + mat[n - 1];
@@ -338,12 +305,9 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
   }
   const uint32_t mask = (1u << (2 * k)) - 1u;
   const uint32_t pmask = (1u << shift) - 1u;
-  Win nw = win_load(seq, total, (int64_t)blockIdx.x * kPTile + (int64_t)threadIdx.x * kPer);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
     const int64_t t0 = tile * kPTile;
     const int64_t base = t0 - kLook;
-    const Win cw = nw;
-    if (tile + G < ntiles) nw = win_load(seq, total, (tile + G) * kPTile + (int64_t)threadIdx.x * kPer);
     __syncthreads();
     for (int i = threadIdx.x; i < (kPTile + kLook + 32) / 32 + 1; i += kPT) bmask[i] = 0;
     __syncthreads();
@@ -352,7 +316,19 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
     const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
     if (p0 >= total) continue;
     uint8_t b[kLook + kPer];
-    win_bytes(cw, seq, total, p0, b);
+    if (p0 >= kLook && p0 + kPer <= total) {
+      const uint4 v0 = *reinterpret_cast<const uint4 *>(seq + p0 - kLook);
+      const uint4 v1 = *reinterpret_cast<const uint4 *>(seq + p0);
+      const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+      for (int j = 0; j < kLook + kPer; ++j) b[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+    } else {
+#pragma unroll
+      for (int j = 0; j < kLook + kPer; ++j) {
+        const int64_t q = p0 - kLook + j;
+        b[j] = (q >= 0 && q < total) ? seq[q] : (uint8_t)'N';
+      }
+    }
     uint32_t code = 0;
     int len = 0;
 #pragma unroll
@@ -409,14 +385,9 @@ __global__ void __launch_bounds__(kPT) k_part_scatter(const uint8_t *__restrict_
   for (int i = threadIdx.x; i < nb; i += kPT) cur[i] = ex[(size_t)i * G + blockIdx.x];
   const uint32_t mask = (1u << (2 * k)) - 1u;
   const uint32_t pmask = (1u << shift) - 1u;
-  // u32 items (k >= 14): no register room for the prefetch, load in the tile
-  constexpr bool kAhead = sizeof(Item) == 2;
-  Win nw = win_load(seq, total, (int64_t)blockIdx.x * kPTile + (int64_t)threadIdx.x * kPer);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
     const int64_t t0 = tile * kPTile;
     const int64_t base = t0 - kLook;
-    const Win cw = kAhead ? nw : win_load(seq, total, t0 + (int64_t)threadIdx.x * kPer);
-    if (kAhead && tile + G < ntiles) nw = win_load(seq, total, (tile + G) * kPTile + (int64_t)threadIdx.x * kPer);
     __syncthreads();
     for (int i = threadIdx.x; i < (kPTile + kLook + 32) / 32 + 1; i += kPT) bmask[i] = 0;
     for (int i = threadIdx.x; i < nb; i += kPT) cnt[i] = 0;
@@ -425,17 +396,24 @@ __global__ void __launch_bounds__(kPT) k_part_scatter(const uint8_t *__restrict_
     __syncthreads();
     const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
     uint32_t br[kPer];   // bucket << 16 | rank, or ~0u
-    // payloads: u16 items two per register (keeps the next tile's window
-    // loads in registers without spills)
-    constexpr bool kPack = sizeof(Item) == 2;
-    uint32_t pay[kPack ? kPer / 2 : kPer];
+    uint32_t pay[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) br[j] = ~0u;
-#pragma unroll
-    for (int j = 0; j < (kPack ? kPer / 2 : kPer); ++j) pay[j] = 0;
     if (p0 < total) {
       uint8_t b[kLook + kPer];
-      win_bytes(cw, seq, total, p0, b);
+      if (p0 >= kLook && p0 + kPer <= total) {
+        const uint4 v0 = *reinterpret_cast<const uint4 *>(seq + p0 - kLook);
+        const uint4 v1 = *reinterpret_cast<const uint4 *>(seq + p0);
+        const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int j = 0; j < kLook + kPer; ++j) b[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+      } else {
+#pragma unroll
+        for (int j = 0; j < kLook + kPer; ++j) {
+          const int64_t q = p0 - kLook + j;
+          b[j] = (q >= 0 && q < total) ? seq[q] : (uint8_t)'N';
+        }
+      }
       uint32_t code = 0;
       int len = 0;
 #pragma unroll
@@ -455,10 +433,7 @@ __global__ void __launch_bounds__(kPT) k_part_scatter(const uint8_t *__restrict_
           if (!q1) {
             const uint32_t bk = code >> shift;
             br[j - kLook] = (bk << 16) | atomicAdd(&cnt[bk], 1u);
-            if (kPack)
-              pay[(j - kLook) >> 1] |= (code & pmask) << (16 * ((j - kLook) & 1));
-            else
-              pay[j - kLook] = code & pmask;
+            pay[j - kLook] = code & pmask;
           }
         }
       }
@@ -507,7 +482,7 @@ __global__ void __launch_bounds__(kPT) k_part_scatter(const uint8_t *__restrict_
     for (int j = 0; j < kPer; ++j)
       if (br[j] != ~0u) {
         const uint32_t bk = br[j] >> 16, pos = off[bk] + (br[j] & 0xffffu);
-        sorted[pos] = kPack ? (Item)(pay[j >> 1] >> (16 * (j & 1))) : (Item)pay[j];
+        sorted[pos] = (Item)pay[j];
         bkt[pos] = (uint16_t)bk;
       }
     __syncthreads();
@@ -655,24 +630,7 @@ __global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
   for (unsigned long long i = eb + threadIdx.x; i < e; i += kPT) atomicAdd(&h[part[i]], 1u);
   const uint4 *v = reinterpret_cast<const uint4 *>(part + ah);
   const unsigned long long nv = (eb - ah) / 8;
-  // 4 loads in flight per lane before their 32 LDS atomics
-  constexpr int kB = 4;
-  unsigned long long i = threadIdx.x;
-  for (; i + (kB - 1) * kPT < nv; i += kB * kPT) {
-    uint4 x[kB];
-#pragma unroll
-    for (int u = 0; u < kB; ++u) x[u] = v[i + u * kPT];
-#pragma unroll
-    for (int u = 0; u < kB; ++u) {
-      const uint32_t w[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        atomicAdd(&h[w[j] & 0xffffu], 1u);
-        atomicAdd(&h[w[j] >> 16], 1u);
-      }
-    }
-  }
-  for (; i < nv; i += kPT) {
+  for (unsigned long long i = threadIdx.x; i < nv; i += kPT) {
     const uint4 x = v[i];
     const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll

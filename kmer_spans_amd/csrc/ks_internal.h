@@ -89,6 +89,10 @@ struct ks_ctx {
   unsigned long long hreg[64] = {};  // region counters per segment read back with the chunked scan's counters
   bool hreg_ok = false;              // (kSegs entries, valid until the next scan attempt)
   int64_t rescan_segcap = 0;  // grow-only rescan capacity per segment (tr_lr rescans outnumber regions)
+  // top-level visits counted by another context concurrently with the scan
+  // (scan_impl): scan_core leaves the count out and says whether it did
+  bool vis_count_ext = false;
+  bool vis_count_ext_used = false;
 };
 
 struct ks_table {

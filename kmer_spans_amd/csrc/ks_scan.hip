@@ -425,7 +425,10 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
           const int64_t n = (int64_t)1 << (2 * k);
           if (!vis_atomic) {
             double words = 0;
-            KS_TRY(launch_count(ctx, s, total, runs, k, visits_dev, &words));
+            if (ctx->vis_count_ext)  // scan_impl adds the count (uint32 wrap-around makes the order free)
+              ctx->vis_count_ext_used = true;
+            else
+              KS_TRY(launch_count(ctx, s, total, runs, k, visits_dev, &words));
             if (runs.n > 0) {
               hipLaunchKernelGGL(k_visit_correct, dim3((unsigned)((runs.n + 255) / 256)), dim3(256), 0, st, runs.a,
                                  runs.b, runs.seq, runs.n, s->offsets_dev, s->seq, k, vis);
@@ -586,7 +589,54 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     const int64_t P = m > 0 ? s->offsets_host[m] : 0;
     if (m <= 0 || 5 * P < total || 5 * P > 4 * total) m = -1;  // parts of 20-80 %
   }
-  if (m < 0) return scan_core(ctx, s, total, k, t, min_width, min_score, visits_dev, out, stats, mode, nullptr);
+  if (m < 0) {
+    // Visits of the one-part chunked scan: the top-level count (the k-mer
+    // histogram, ~24 ms at k = 13, streaming + LDS work) runs on the
+    // sub-context's stream from a second host thread while the scan's gather
+    // pass (random requests) runs here; the count lands in the sub-context's
+    // histogram and is added once both are done.  KS_VISITS_SERIAL: the
+    // count after the scan on this stream (A/B).
+    const bool vis_conc = visits_dev && !mode.trlr && ctx->scan_algo != 0 && total > 0 &&
+                          getenv("KS_VISITS_ATOMIC") == nullptr && getenv("KS_VISITS_SERIAL") == nullptr;
+    if (!vis_conc) return scan_core(ctx, s, total, k, t, min_width, min_score, visits_dev, out, stats, mode, nullptr);
+    ks_ctx *vsub = nullptr;
+    KS_TRY(ctx_sub(ctx, &vsub));
+    const size_t nb = (size_t)4 << (2 * k);
+    KS_HIP(hipEventRecord(ctx->ev[19], ctx->stream));  // the count starts after the caller's uploads
+    KS_HIP(hipStreamWaitEvent(vsub->stream, ctx->ev[19], 0));
+    ks_status rc_c = KS_OK;
+    std::string err_c;
+    void *cbuf = nullptr;
+    std::thread th([&] {
+      rc_c = activate(vsub);
+      if (rc_c == KS_OK) rc_c = ensure(vsub, SLOT_COUNTS, nb, &cbuf);
+      if (rc_c == KS_OK && hipMemsetAsync(cbuf, 0, nb, vsub->stream) != hipSuccess)
+        rc_c = fail(KS_ERR_DEVICE, "hipMemsetAsync failed");
+      double words = 0;
+      Runs none;
+      if (rc_c == KS_OK) rc_c = launch_count(vsub, s, total, none, k, static_cast<int32_t *>(cbuf), &words);
+      if (rc_c != KS_OK) err_c = ks_last_error();  // (thread-local)
+    });
+    ctx->vis_count_ext = true;
+    ctx->vis_count_ext_used = false;
+    const ks_status rc = scan_core(ctx, s, total, k, t, min_width, min_score, visits_dev, out, stats, mode, nullptr);
+    ctx->vis_count_ext = false;
+    th.join();  // (launch_count ended with a synchronisation of the sub-context's stream)
+    if (rc != KS_OK) return rc;
+    if (rc_c != KS_OK) {
+      ks_regions_free(out);
+      set_error("%s", err_c.c_str());
+      return rc_c;
+    }
+    if (ctx->vis_count_ext_used) {  // (a lane-kernel fallback counted every visit itself)
+      const int64_t n = (int64_t)1 << (2 * k);
+      hipLaunchKernelGGL(k_add_hist, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0,
+                         ctx->stream, reinterpret_cast<uint32_t *>(visits_dev), static_cast<const uint32_t *>(cbuf), n);
+      KS_HIP(hipGetLastError());
+      KS_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return KS_OK;
+  }
   ks_ctx *sub = nullptr;
   KS_TRY(ctx_sub(ctx, &sub));
   const double t0 = now_ms();

@@ -85,6 +85,8 @@ def parse(argv=None):
     p.add_argument("--cpu-sample", type=float, default=2.0e8,
                    help="bases of the CPU-baseline sample besides the largest contig")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-visits", action="store_true",
+                   help="skip the visits_path line (profiling runs: its scans run beside a concurrent count)")
     p.add_argument("--no-expand", action="store_true", help="do not build the expanded (k+J-1)-mer table")
     p.add_argument("--ext-max-gib", type=float, default=None,
                    help="cap on the expanded table (GiB); default: no cap beyond HBM (J = 5, 128 GiB at k = 13) "
@@ -395,7 +397,7 @@ def main():
     # (kmer_spans.c:266-267,523-537): device-resident, count-derived top-level
     # visits + rescan visits; not `value` (the metric counts regions only)
     visits_line = None
-    if rank == 0 and not args.trlr and stats[-1]["scan_algo"] == 1:
+    if rank == 0 and not args.trlr and not args.no_visits and stats[-1]["scan_algo"] == 1:
         vis = torch.zeros(4 ** k, dtype=torch.int32, device=dev)
         D.scan(ctx, ds, k, table, args.min_width, args.min_score, visits=vis)  # warm
         vt = []

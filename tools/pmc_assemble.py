@@ -32,7 +32,9 @@ def main(bench_json, out_json, *csvs):
         "build_id": cfg["build_id"],
         "workload": {"k": cfg["k"], "score": cfg["score"], "scale": 1.0, "ncontigs": 24, "expand": True,
                      "trlr": False, "mode": cfg["mode"], "world": 1},
-        "steps": 1,
+        # scan calls in the profiled run: its steps + warmup, plus the visits
+        # line's warm call and 3 timed calls (the same scan)
+        "steps": int(b["steps"]) + int(b["warmup"]) + (4 if b.get("visits_path") else 0),
         # packed bases (total / 4 bytes per step) are the only 16-B streaming read of k_pass1p
         "streaming_read_bytes_per_step": {"k_pass1p": n_bases / 4.0},
         "kernels": kernels,

@@ -167,12 +167,16 @@ __global__ void __launch_bounds__(1024) k_remap_codes(uint16_t *__restrict__ cod
 // stores as k_build_ext_u16 (was four entries per lane as two 16-B stores
 // at a 32-B stride: 42-56 ms for the 128 GiB table at k = 13).
 __device__ __forceinline__ uint64_t c12_of(uint32_t code) { return code < 0xFFFu ? code : 0xFFFu; }
+// kU pairs per lane and trip (grid-strided), their code loads all issued
+// before the first store: a trip costs one round trip to L2 / the Infinity
+// Cache for kU x 16 B of stores (A/B: KS_EXT_U1 for one pair per trip).
+template <int kU>
 __global__ void k_build_ext_c12(const uint16_t *__restrict__ codes, int k, uint64_t nent,
                                 uint64_t *__restrict__ ext) {
   const uint64_t mk = ((uint64_t)1 << (2 * k)) - 1;
   const uint64_t npair = nent >> 1;
-  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npair;
-       p += (uint64_t)gridDim.x * blockDim.x) {
+  const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
+  auto pair = [&](uint64_t p) -> ks_u64x2 {
     const uint64_t e0 = p << 1;
     uint64_t base = 0;
 #pragma unroll
@@ -181,8 +185,17 @@ __global__ void k_build_ext_c12(const uint16_t *__restrict__ codes, int k, uint6
     ks_u64x2 o;
     o.x = base | (c12_of(w & 0xffffu) << 48);
     o.y = base | (c12_of(w >> 16) << 48);
-    __builtin_nontemporal_store(o, reinterpret_cast<ks_u64x2 *>(ext) + p);
+    return o;
+  };
+  uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; p + (kU - 1) * S < npair; p += kU * S) {
+    ks_u64x2 o[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) o[u] = pair(p + u * S);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) __builtin_nontemporal_store(o[u], reinterpret_cast<ks_u64x2 *>(ext) + p + u * S);
   }
+  for (; p < npair; p += S) __builtin_nontemporal_store(pair(p), reinterpret_cast<ks_u64x2 *>(ext) + p);
 }
 
 // Expanded table, FP64 values: J values per entry (double2 / double4).  A
@@ -496,7 +509,10 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   KS_HIP(hipEventRecord(a, st));
   const unsigned grid = (unsigned)std::min<uint64_t>((nent + 255) / 256, (uint64_t)ctx->num_cus * 32);
   if (u16 && bits == 12) {
-    hipLaunchKernelGGL(k_build_ext_c12, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
+    if (getenv("KS_EXT_U1"))
+      hipLaunchKernelGGL(k_build_ext_c12<1>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
+    else
+      hipLaunchKernelGGL(k_build_ext_c12<4>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
   } else if (u16) {
     if (J == 4) hipLaunchKernelGGL((k_build_ext_u16<4, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
     else if (J == 3) hipLaunchKernelGGL((k_build_ext_u16<3, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);

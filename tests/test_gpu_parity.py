@@ -182,6 +182,38 @@ def test_human_like_device_path(K, oracle, ctx, k, score):
     D.bind_torch_stream(ctx)
 
 
+@pytest.mark.parametrize("mode", ["concurrent", "KS_VISITS_SERIAL", "KS_VISITS_ATOMIC"])
+def test_visit_histogram_modes(K, oracle, ctx, monkeypatch, mode):
+    """The visit histogram of kmer_regions_r (kmer_spans.c:266-267) by each
+    route: the top-level count on the sub-context concurrently with the scan
+    (default), the count after the scan, one atomic per scanned index -- all
+    equal to the oracle's, with the same regions; twice in a row (the
+    sub-context's workspace is reused)."""
+    import torch
+    from kmer_spans_amd import device as D, genome
+    if mode != "concurrent":
+        monkeypatch.setenv(mode, "1")
+    k = 11
+    parts, lens = genome.human_like(scale=0.002, seed=5, device="cuda")
+    ds = D.from_parts(parts, lens, "cuda")
+    D.bind_torch_stream(ctx)
+    host = [ds.host_seq(q) for q in range(ds.nseq)]
+    n, oc = oracle.kmer_counts(host, k)
+    w = K.log2_table(oc, k)
+    o = oracle.scan(host, k, w, 0.0, 100, 20.0, visits=True)
+    tab = D.DeviceTable(ctx, w, k, 0.0, compress=True, expand=True)
+    ctx.set_scan_algo(1)
+    try:
+        for rep in range(2):
+            vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+            pos, sc, st = D.scan(ctx, ds, k, tab, 100, 20.0, vis)
+            _assert_same_regions(pos, sc, o["pos"], o["score"], (mode, rep))
+            assert np.array_equal(vis.cpu().numpy(), o["counts"]), (mode, rep)
+    finally:
+        ctx.set_scan_algo(-1)
+        tab.close()
+
+
 @pytest.mark.parametrize("k,expand", [(11, True), (11, False), (13, True)])
 def test_rank_carried_replays(K, oracle, ctx, k, expand):
     """Weighted-rank scores (config 3 shape): excursions at small S cross

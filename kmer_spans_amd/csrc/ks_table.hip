@@ -170,7 +170,7 @@ __device__ __forceinline__ uint64_t c12_of(uint32_t code) { return code < 0xFFFu
 // kU pairs per lane and trip (grid-strided), their code loads all issued
 // before the first store: a trip costs one round trip to L2 / the Infinity
 // Cache for kU x 16 B of stores (A/B: KS_EXT_U1 for one pair per trip).
-template <int kU>
+template <int kU, bool kNT = true>
 __global__ void k_build_ext_c12(const uint16_t *__restrict__ codes, int k, uint64_t nent,
                                 uint64_t *__restrict__ ext) {
   const uint64_t mk = ((uint64_t)1 << (2 * k)) - 1;
@@ -193,7 +193,12 @@ __global__ void k_build_ext_c12(const uint16_t *__restrict__ codes, int k, uint6
 #pragma unroll
     for (int u = 0; u < kU; ++u) o[u] = pair(p + u * S);
 #pragma unroll
-    for (int u = 0; u < kU; ++u) __builtin_nontemporal_store(o[u], reinterpret_cast<ks_u64x2 *>(ext) + p + u * S);
+    for (int u = 0; u < kU; ++u) {
+      if (kNT)
+        __builtin_nontemporal_store(o[u], reinterpret_cast<ks_u64x2 *>(ext) + p + u * S);
+      else
+        reinterpret_cast<ks_u64x2 *>(ext)[p + u * S] = o[u];
+    }
   }
   for (; p < npair; p += S) __builtin_nontemporal_store(pair(p), reinterpret_cast<ks_u64x2 *>(ext) + p);
 }
@@ -204,20 +209,31 @@ __global__ void k_build_ext_c12(const uint16_t *__restrict__ codes, int k, uint6
 // a lane per 32-B entry with two strided 16-B stores ran at 44.6 ms for
 // 128 GiB on scattered VRAM and 78.8 ms on contiguous VRAM.
 typedef double ks_f64x2 __attribute__((ext_vector_type(2)));
-template <int J>
+// kU slots per lane and trip (grid-strided), loads ahead of the stores as in
+// k_build_ext_c12 (A/B: KS_EXT_U1).
+template <int J, int kU = 1>
 __global__ void k_build_ext_f64(const double *__restrict__ vals, int k, uint64_t nent, double *__restrict__ ext) {
   constexpr int H = (J <= 2) ? 1 : 2;  // 16-B halves per entry
   const uint64_t mk = ((uint64_t)1 << (2 * k)) - 1;
   const uint64_t nslot = nent * H;
-  for (uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; sl < nslot;
-       sl += (uint64_t)gridDim.x * blockDim.x) {
+  const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
+  auto half = [&](uint64_t sl) -> ks_f64x2 {
     const uint64_t e = H == 2 ? sl >> 1 : sl;
     const int t0 = H == 2 ? 2 * (int)(sl & 1) : 0;  // first value of this half
     ks_f64x2 o;
     o.x = (t0 < J) ? vals[(e >> (2 * (J - 1 - t0))) & mk] : 0.0;
     o.y = (t0 + 1 < J) ? vals[(e >> (2 * (J - 2 - t0))) & mk] : 0.0;
-    __builtin_nontemporal_store(o, reinterpret_cast<ks_f64x2 *>(ext) + sl);
+    return o;
+  };
+  uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; sl + (kU - 1) * S < nslot; sl += kU * S) {
+    ks_f64x2 o[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) o[u] = half(sl + u * S);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) __builtin_nontemporal_store(o[u], reinterpret_cast<ks_f64x2 *>(ext) + sl + u * S);
   }
+  for (; sl < nslot; sl += S) __builtin_nontemporal_store(half(sl), reinterpret_cast<ks_f64x2 *>(ext) + sl);
 }
 
 // out[i] = lut[index of counts[i] in dv]: dv = the sorted distinct counts
@@ -511,6 +527,11 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   if (u16 && bits == 12) {
     if (getenv("KS_EXT_U1"))
       hipLaunchKernelGGL(k_build_ext_c12<1>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
+    else if (getenv("KS_EXT_U8"))
+      hipLaunchKernelGGL(k_build_ext_c12<8>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
+    else if (getenv("KS_EXT_PLAIN"))
+      hipLaunchKernelGGL((k_build_ext_c12<4, false>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent,
+                         (uint64_t *)ext);
     else
       hipLaunchKernelGGL(k_build_ext_c12<4>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
   } else if (u16) {
@@ -518,7 +539,9 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
     else if (J == 3) hipLaunchKernelGGL((k_build_ext_u16<3, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
     else hipLaunchKernelGGL((k_build_ext_u16<2, uint32_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint32_t *)ext);
   } else {
-    if (J == 4) hipLaunchKernelGGL(k_build_ext_f64<4>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
+    if (J == 4 && getenv("KS_EXT_F64_U4"))
+      hipLaunchKernelGGL((k_build_ext_f64<4, 4>), dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
+    else if (J == 4) hipLaunchKernelGGL(k_build_ext_f64<4>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
     else if (J == 3) hipLaunchKernelGGL(k_build_ext_f64<3>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
     else hipLaunchKernelGGL(k_build_ext_f64<2>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
   }

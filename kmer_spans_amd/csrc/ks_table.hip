@@ -74,29 +74,40 @@ __global__ void k_assign_codes(const double *__restrict__ s, const unsigned long
 // cache, so the stores are nontemporal.  The code reads repeat across the
 // wave and stay cached: the build is a write stream.
 typedef unsigned long long ks_u64x2 __attribute__((ext_vector_type(2)));
-template <int J, typename E>
+// kU pairs per lane and trip, loads ahead of the stores (as k_build_ext_c12;
+// A/B: KS_EXT_U1).
+template <int J, typename E, int kU = 1>
 __global__ void k_build_ext_u16(const uint16_t *__restrict__ codes, int k, uint64_t nent, E *__restrict__ ext) {
   const uint64_t mk = ((uint64_t)1 << (2 * k)) - 1;
   const uint64_t npair = nent >> 1;
-  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npair;
-       p += (uint64_t)gridDim.x * blockDim.x) {
+  const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
+  auto pair = [&](uint64_t p) -> ks_u64x2 {
     const uint64_t e0 = p << 1;
     uint64_t v = 0;
 #pragma unroll
     for (int t = 0; t < J - 1; ++t) v |= (uint64_t)codes[(e0 >> (2 * (J - 1 - t))) & mk] << (16 * t);
     const uint32_t w = *reinterpret_cast<const uint32_t *>(codes + (e0 & mk));
-    const uint64_t v0 = v | ((uint64_t)(w & 0xffffu) << (16 * (J - 1)));
-    const uint64_t v1 = v | ((uint64_t)(w >> 16) << (16 * (J - 1)));
-    if (sizeof(E) == 8) {
-      ks_u64x2 o;
-      o.x = v0;
-      o.y = v1;
+    ks_u64x2 o;
+    o.x = v | ((uint64_t)(w & 0xffffu) << (16 * (J - 1)));
+    o.y = v | ((uint64_t)(w >> 16) << (16 * (J - 1)));
+    return o;
+  };
+  auto put = [&](uint64_t p, const ks_u64x2 &o) {
+    if (sizeof(E) == 8)
       __builtin_nontemporal_store(o, reinterpret_cast<ks_u64x2 *>(ext) + p);
-    } else {
-      __builtin_nontemporal_store((uint64_t)(uint32_t)v0 | ((uint64_t)(uint32_t)v1 << 32),
+    else
+      __builtin_nontemporal_store((uint64_t)(uint32_t)o.x | ((uint64_t)(uint32_t)o.y << 32),
                                   reinterpret_cast<uint64_t *>(ext) + p);
-    }
+  };
+  uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; p + (kU - 1) * S < npair; p += kU * S) {
+    ks_u64x2 o[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) o[u] = pair(p + u * S);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) put(p + u * S, o[u]);
   }
+  for (; p < npair; p += S) put(p, pair(p));
 }
 
 // Position weight of every uint16 code in [lo, lo + kHistBins): number of
@@ -169,7 +180,8 @@ __global__ void __launch_bounds__(1024) k_remap_codes(uint16_t *__restrict__ cod
 __device__ __forceinline__ uint64_t c12_of(uint32_t code) { return code < 0xFFFu ? code : 0xFFFu; }
 // kU pairs per lane and trip (grid-strided), their code loads all issued
 // before the first store: a trip costs one round trip to L2 / the Infinity
-// Cache for kU x 16 B of stores (A/B: KS_EXT_U1 for one pair per trip).
+// Cache for kU x 16 B of stores (A/B: KS_EXT_U1 / KS_EXT_U4 / KS_EXT_U16 pairs per trip,
+// KS_EXT_PLAIN for plain stores).
 template <int kU, bool kNT = true>
 __global__ void k_build_ext_c12(const uint16_t *__restrict__ codes, int k, uint64_t nent,
                                 uint64_t *__restrict__ ext) {
@@ -527,20 +539,27 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   if (u16 && bits == 12) {
     if (getenv("KS_EXT_U1"))
       hipLaunchKernelGGL(k_build_ext_c12<1>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
-    else if (getenv("KS_EXT_U8"))
-      hipLaunchKernelGGL(k_build_ext_c12<8>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
-    else if (getenv("KS_EXT_PLAIN"))
-      hipLaunchKernelGGL((k_build_ext_c12<4, false>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent,
-                         (uint64_t *)ext);
-    else
+    else if (getenv("KS_EXT_U4"))
       hipLaunchKernelGGL(k_build_ext_c12<4>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
+    else if (getenv("KS_EXT_U16"))
+      hipLaunchKernelGGL(k_build_ext_c12<16>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
+    else if (getenv("KS_EXT_PLAIN"))
+      hipLaunchKernelGGL((k_build_ext_c12<8, false>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent,
+                         (uint64_t *)ext);
+    else  // 8 pairs per trip: 27.06 vs 28.2 (4), 29.3 (1) ms, plain stores 36.8 (profiles/r2/s3/ab_ext_build_*)
+      hipLaunchKernelGGL(k_build_ext_c12<8>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
   } else if (u16) {
-    if (J == 4) hipLaunchKernelGGL((k_build_ext_u16<4, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
+    if (J == 4 && getenv("KS_EXT_U1") == nullptr)
+      hipLaunchKernelGGL((k_build_ext_u16<4, uint64_t, 8>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent,
+                         (uint64_t *)ext);
+    else if (J == 4) hipLaunchKernelGGL((k_build_ext_u16<4, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
     else if (J == 3) hipLaunchKernelGGL((k_build_ext_u16<3, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
     else hipLaunchKernelGGL((k_build_ext_u16<2, uint32_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint32_t *)ext);
   } else {
     if (J == 4 && getenv("KS_EXT_F64_U4"))
       hipLaunchKernelGGL((k_build_ext_f64<4, 4>), dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
+    else if (J == 4 && getenv("KS_EXT_F64_U8"))
+      hipLaunchKernelGGL((k_build_ext_f64<4, 8>), dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
     else if (J == 4) hipLaunchKernelGGL(k_build_ext_f64<4>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
     else if (J == 3) hipLaunchKernelGGL(k_build_ext_f64<3>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
     else hipLaunchKernelGGL(k_build_ext_f64<2>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);

@@ -20,6 +20,7 @@ def main():
     p.add_argument("--k", type=int, default=13)
     p.add_argument("--score", default="log2")
     p.add_argument("--scale", type=float, default=1.0)
+    p.add_argument("--ext-max-gib", type=float, default=0.0, help="expanded-table cap (0: the library's choice)")
     a = p.parse_args()
     import numpy as np
     import torch
@@ -42,7 +43,9 @@ def main():
             old = {key: os.environ.get(key) for key in env}
             os.environ.update(env)
             try:
-                tab = D.DeviceTable.from_counts(ctx, counts, a.k, a.score, total=words, expand=True)
+                tab = D.DeviceTable.from_counts(ctx, counts, a.k, a.score, total=words,
+                                                thr=0.75 if a.score == "rank" else 0.0, expand=True,
+                                                max_ext_bytes=int(a.ext_max_gib * 2 ** 30))
                 sm = tab.setup_ms()
                 pos, score, _ = D.scan(ctx, ds, a.k, tab, 100, 20.0)
                 tab.close()

@@ -558,7 +558,7 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   } else {
     if (J == 4 && getenv("KS_EXT_F64_U4"))
       hipLaunchKernelGGL((k_build_ext_f64<4, 4>), dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
-    else if (J == 4 && getenv("KS_EXT_F64_U8"))
+    else if (J == 4 && getenv("KS_EXT_U1") == nullptr)
       hipLaunchKernelGGL((k_build_ext_f64<4, 8>), dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
     else if (J == 4) hipLaunchKernelGGL(k_build_ext_f64<4>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
     else if (J == 3) hipLaunchKernelGGL(k_build_ext_f64<3>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);

@@ -397,7 +397,7 @@ def main():
     # (kmer_spans.c:266-267,523-537): device-resident, count-derived top-level
     # visits + rescan visits; not `value` (the metric counts regions only)
     visits_line = None
-    if rank == 0 and not args.trlr and not args.no_visits and stats[-1]["scan_algo"] == 1:
+    if world == 1 and not args.trlr and not args.no_visits and stats[-1]["scan_algo"] == 1:
         vis = torch.zeros(4 ** k, dtype=torch.int32, device=dev)
         D.scan(ctx, ds, k, table, args.min_width, args.min_score, visits=vis)  # warm
         vt = []

@@ -2507,9 +2507,12 @@ __global__ void __launch_bounds__(256) k_tile_comp(Chunks g, Summ sm, TileComp t
 // Per-chunk carry of the tiles accepted in batches (ee != INT32_MIN): the
 // fast-tile path of carry_segment from the tile's exact entry.  gated: only
 // after a fallback (bit 16 of err), for the tiles k_carry_run batched.
-__device__ __forceinline__ void tile_apply_one(const Chunks &g, const Summ &sm, const TileComp &tc, const Carry &cr,
-                                               int64_t t) {
+__global__ void __launch_bounds__(256) k_tile_apply(Chunks g, Summ sm, TileComp tc, Carry cr,
+                                                    const unsigned int *__restrict__ err, int gated) {
   const int lane = threadIdx.x & 63;
+  const int64_t t = (g.c0 >> 6) + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (g.nch <= g.c0 || t > ((g.nch - 1) >> 6)) return;
+  if (gated && !(*(volatile const unsigned int *)err & 16u)) return;
   const int e = tc.ee[t];
   if (e == INT32_MIN) return;
   const long long m = tc.em[t];
@@ -2538,21 +2541,6 @@ __device__ __forceinline__ void tile_apply_one(const Chunks &g, const Summ &sm, 
   cr.hq[c] = -1;
   cr.hmax[c] = from_mant(mj + (pj ? sm.M[2 * c + 1] : sm.M[2 * c]), e);
   cr.harg[c] = pj ? sm.A[2 * c + 1] : sm.A[2 * c];
-}
-// a wave per tile; gated (after a fallback only): a small grid whose waves
-// stride over the tiles (wave-uniform, so the shuffles stay converged)
-__global__ void __launch_bounds__(256) k_tile_apply(Chunks g, Summ sm, TileComp tc, Carry cr,
-                                                    const unsigned int *__restrict__ err, int gated) {
-  const int64_t t = (g.c0 >> 6) + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  if (g.nch <= g.c0) return;
-  const int64_t tlast = (g.nch - 1) >> 6;
-  if (gated) {
-    if (!(*(volatile const unsigned int *)err & 16u)) return;
-    for (int64_t tt = t; tt <= tlast; tt += ((int64_t)gridDim.x * blockDim.x) >> 6) tile_apply_one(g, sm, tc, cr, tt);
-    return;
-  }
-  if (t > tlast) return;
-  tile_apply_one(g, sm, tc, cr, t);
 }
 
 // Carry by window: block w runs the segments that start in chunks
@@ -2623,10 +2611,13 @@ __global__ void k_fallback_prep(unsigned int *__restrict__ err, unsigned long lo
 // lane per chunk, from the exact entry.  Uncompressed tables read the
 // expanded table (J indices per read) like P1.
 template <int J, bool kCompressed>
-__device__ __forceinline__ void head_one(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
-                                         const TableView &tv, const uint16_t *__restrict__ codes, const Carry &cr,
-                                         unsigned int *__restrict__ err, int64_t c) {
+__global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
+                                               int k, TableView tv, const uint16_t *__restrict__ codes,
+                                               Carry cr, unsigned int *__restrict__ err, int gated) {
   const uint32_t *__restrict__ packed = g.packed;
+  const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= g.nch) return;
+  if (gated && !(*(volatile unsigned int *)err & 16u)) return;  // second pass only after a fallback
   const int mode = cr.mode[c];
   if (mode == kModeL || mode == kModeU) return;  // head written by the carry (summary / replay)
   cr.hq[c] = -1;
@@ -2727,24 +2718,6 @@ __device__ __forceinline__ void head_one(const Chunks &g, const uint8_t *__restr
   cr.hq[c] = hq;
   cr.hmax[c] = hmax;
   cr.harg[c] = harg;
-}
-
-// gated: the second pass, only after a fallback (bit 16 of err); launched
-// with a small grid that strides over the chunks, so that the usual no-op
-// costs one wave of blocks, not one block per 256 chunks.
-template <int J, bool kCompressed>
-__global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
-                                               int k, TableView tv, const uint16_t *__restrict__ codes,
-                                               Carry cr, unsigned int *__restrict__ err, int gated) {
-  const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gated) {
-    if (!(*(volatile unsigned int *)err & 16u)) return;
-    for (int64_t cc = c; cc < g.nch; cc += (int64_t)gridDim.x * blockDim.x)
-      head_one<J, kCompressed>(g, seq, total, k, tv, codes, cr, err, cc);
-    return;
-  }
-  if (c >= g.nch) return;
-  head_one<J, kCompressed>(g, seq, total, k, tv, codes, cr, err, c);
 }
 
 // ------------------------------------------------------------------- P5
@@ -3519,15 +3492,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       hipLaunchKernelGGL(k_tile_apply, dim3(gtc), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 0);
       KS_HIP(hipGetLastError());
     }
-    // grid of the gated second passes (KS_GATED_FULL: one block per 256 chunks / 4 tiles, A/B)
-    auto ggate = [&](unsigned full) -> unsigned {
-      static const bool gfull = getenv("KS_GATED_FULL") != nullptr;
-      return gfull ? full : std::max(1u, std::min(full, (unsigned)ctx->num_cus * 4u));
-    };
     auto heads = [&](int gated) {
 #define KS_HEADS(J, C)                                                                                           \
-  hipLaunchKernelGGL((k_heads<J, C>), dim3(gated ? ggate(gch_h) : gch_h), dim3(256), 0, strm, gv, s->seq, total, k, \
-                     tv, codes, cr, err_h, gated)
+  hipLaunchKernelGGL((k_heads<J, C>), dim3(gch_h), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes, cr, err_h, \
+                     gated)
       if (comp) KS_HEADS(1, true);
       else if (J == 4) KS_HEADS(4, false);
       else if (J == 3) KS_HEADS(3, false);
@@ -3545,7 +3513,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       else
         hipLaunchKernelGGL(k_carry_run<false>, dim3((unsigned)nr), dim3(64), 0, strm, gv, d_cbase, h.r1, s->seq,
                            total, k, tv, codes, p1, sm, cr, tch, rpb, rep_h, err_h, nullptr, h.r0);
-      if (tile_batch) hipLaunchKernelGGL(k_tile_apply, dim3(ggate(gtc)), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 1);
+      if (tile_batch) hipLaunchKernelGGL(k_tile_apply, dim3(gtc), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 1);
     }
     heads(1);
     KS_HIP(hipGetLastError());

@@ -2,26 +2,28 @@
 """Benchmark of the span-scan hot path (BASELINE.json metric):
 
   Gbases/sec scanned, k=13, log-ratio score, 3.1 Gbp human-shaped genome,
-  spans bit-exact.
+  spans bit-exact, at 1/2/4/8 MI355X.
 
 One *step* = one ks_scan_dev pass (run segmentation + scan + region
 ordering/D2H) over the device-resident sequences of a rank.  Genomes are
-synthetic (kmer_spans_amd.genome.human_like: GRCh38 contig lengths, repeats,
-N gaps), generated on the GPU from seeds; the score table is built from the
-genome's own k-mer counts before timing (the table is an input of
+synthetic (kmer_spans_amd.genome: GRCh38 contig lengths, repeats, N gaps),
+generated on the GPU from seeds; the score table is built from the genome's
+own k-mer counts before timing (the table is an input of
 kmer_regions_r), and its cost is reported beside the value as `setup_ms` and
 an end-to-end rate.
 
 Multi-GPU: `python bench.py --gpus N` starts N ranks itself
 (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE set before any HIP call in
-the children; the parent never touches the GPU), or runs as one rank under
-torchrun.  Backend "nccl" (RCCL over xGMI) when every rank has its own GPU,
-gloo for rehearsals with more ranks than GPUs.  Modes:
-  genome  (default, weak scaling) every rank scans its own genome (config 5
-          shape: genomes stay whole per GPU); records gathered to rank 0.
-  shard   (strong scaling) ONE genome, contigs LPT-sharded over the ranks;
-          per-rank counts summed with an int32 all-reduce before the table is
-          built; records gathered to rank 0 and merged (dist.merge_shards).
+the children; the parent never touches the GPU and kills the other ranks as
+soon as one fails), or runs as one rank under torchrun.  Backend "nccl" (RCCL
+over xGMI) when every rank has its own GPU, gloo for rehearsals with more
+ranks than GPUs.  Modes:
+  shard   (default; strong scaling, the north-star curve) ONE genome, contigs
+          LPT-sharded over the ranks; per-rank counts summed with an exact
+          int32 all-reduce before the table is built; records gathered to
+          rank 0 and merged (dist.merge_shards).  At N=1 this is the whole
+          genome (the same seeds as `genome`).
+  genome  (weak scaling) every rank scans its own genome.
   genomes (config 5) every rank processes --genomes-per-rank genomes; each
           timed end to end: count + table (+ expanded table) + scan.
 No collective runs on the data path: the only exchanges are the count
@@ -29,9 +31,11 @@ all-reduce (shard) and the record gather after timing.
 
 Prints ONE JSON line on rank 0 (the driver's contract) with the roofline of
 the dominant kernel (hipEvents on the library's stream inside the timed
-steps), and at N=1 the CPU oracle timed on a bounded sample (which always
-includes the largest contig, the longest exact-carry chain) plus the parity
-verdict of that sample.
+steps), and after timing: the parity verdict of EVERY contig (the CPU oracle
+on a thread pool, per rank on its own shard), at N=1 the CPU oracle timed on
+one pinned core over a bounded sample, the weighted-rank sub-line (BASELINE
+config 3, `configs.rank`, same genome and counts) with its own all-contig
+parity, the visit-histogram line and the host-pointer entry point.
 """
 from __future__ import annotations
 
@@ -42,6 +46,7 @@ import socket
 import subprocess
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import torch
@@ -71,7 +76,7 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1, help="ranks to run (one process per GPU)")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--mode", choices=["genome", "shard", "genomes"], default="genome")
+    p.add_argument("--mode", choices=["shard", "genome", "genomes"], default="shard")
     p.add_argument("--genomes-per-rank", type=int, default=2, help="--mode genomes: genomes per rank")
     p.add_argument("--scale", type=float, default=1.0, help="genome scale (1.0 = 3.09 Gbp)")
     p.add_argument("--k", type=int, default=13)
@@ -82,18 +87,26 @@ def parse(argv=None):
     p.add_argument("--min-score", type=float, default=20.0)
     p.add_argument("--algo", type=int, default=-1, help="-1 auto, 0 lane-per-run, 1 chunked")
     p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--shard-of", type=int, default=1,
+                   help="(one rank) scan only one shard of an N-way LPT split of the genome, with the whole "
+                        "genome's table: the fixed per-step cost at shard size")
+    p.add_argument("--shard-index", type=int, default=-1, help="--shard-of: which shard (default: the largest)")
     p.add_argument("--cpu-sample", type=float, default=2.0e8,
-                   help="bases of the CPU-baseline sample besides the largest contig")
-    p.add_argument("--no-cpu", action="store_true")
+                   help="bases of the timed CPU-baseline sample besides the largest contig")
+    p.add_argument("--cpu-threads", type=int, default=16, help="host threads of the (untimed) parity leg")
+    p.add_argument("--parity", choices=["all", "sample", "none"], default="all",
+                   help="contigs compared with the CPU oracle after timing")
+    p.add_argument("--no-cpu", action="store_true", help="no CPU baseline, no parity leg")
+    p.add_argument("--no-rank", action="store_true", help="skip the weighted-rank sub-line (N=1 default line)")
+    p.add_argument("--rank-steps", type=int, default=5)
     p.add_argument("--no-visits", action="store_true",
                    help="skip the visits_path line (profiling runs: its scans run beside a concurrent count)")
+    p.add_argument("--no-host-path", action="store_true", help="skip the host-pointer entry point line")
     p.add_argument("--no-expand", action="store_true", help="do not build the expanded (k+J-1)-mer table")
     p.add_argument("--ext-max-gib", type=float, default=None,
                    help="cap on the expanded table (GiB); default: no cap beyond HBM (J = 5, 128 GiB at k = 13) "
                         "for the scan modes, 32 GiB (J = 4) for --mode genomes, where it is built per genome")
     p.add_argument("--ncontigs", type=int, default=24, help="1 = the chr1-like single contig of config 2")
-    p.add_argument("--host-path", action="store_true",
-                   help="also time the host-pointer entry point (ks_kmer_regions with visits: staging + PCIe + scan)")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
     return p.parse_args(argv)
 
@@ -106,30 +119,41 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def spawn(n: int) -> int:
+def spawn(n: int, argv=None) -> int:
     """Start n ranks of this script as child processes (the parent makes no
     HIP call: it only sets the rank environment) and return the worst exit
-    code."""
+    code.  The children are polled: when one exits non-zero the others are
+    killed at once instead of blocking in a collective until its timeout."""
     port = _free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ)
         env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    return max((abs(rc) for rc in rcs), default=0)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] +
+                                      (sys.argv[1:] if argv is None else argv), env=env))
+    worst = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            worst = max(worst, abs(rc))
+            if rc != 0:
+                for q in live:
+                    q.kill()
+                for q in live:
+                    q.wait()
+                    worst = max(worst, abs(q.returncode or 0))
+                live = []
+                break
+        time.sleep(0.1)
+    return worst
 
 
 # ------------------------------------------------------------------ helpers
-
-def score_table(api, hc, k, words, score):
-    if score == "log2":
-        return api.log2_table(hc, k), 0.0
-    if score == "pm1":
-        return api.pm1_table(hc, k), 0.0
-    return api.rank_table(hc, k, words), 0.75
-
 
 def pmc_traffic(kernel_prefix, build_id, workload):
     """HBM bytes per step of the dominant kernel (all its launches: pass 1
@@ -146,7 +170,8 @@ def pmc_traffic(kernel_prefix, build_id, workload):
     pmc = json.load(open(PMC_SUMMARY))
     if pmc.get("build_id") != build_id:
         return None, f"stale: PMC summary of build {pmc.get('build_id')}, this library is {build_id}"
-    if pmc.get("workload") != workload:
+    want = {key: workload.get(key) for key in pmc.get("workload", {})}
+    if pmc.get("workload") != want:
         return None, "PMC summary is for another workload"
     steps = float(pmc.get("steps", 1))
     fetch = write = 0.0
@@ -166,8 +191,8 @@ def pmc_traffic(kernel_prefix, build_id, workload):
 
 
 def sample_ids(offsets, budget):
-    """Contigs of the CPU sample: the largest one (longest carry chain at the
-    metric config) plus the smallest ones up to `budget` more bases."""
+    """Contigs of the timed CPU sample: the largest one (longest carry chain
+    at the metric config) plus the smallest ones up to `budget` more bases."""
     lens = np.diff(offsets)
     big = int(np.argmax(lens))
     ids, acc = [big], int(lens[big])
@@ -182,15 +207,70 @@ def sample_ids(offsets, budget):
     return sorted(ids), acc
 
 
-def parity_of(pos, score, ids, o, one):
-    """GPU records of the sampled contigs (ids, in the GPU's numbering) equal
-    the oracle's records of those contigs (numbered 0.. in ids order)."""
-    sel = np.isin(pos[0] - one, ids)
-    gp = pos[:, sel].copy()
-    remap = {q: i for i, q in enumerate(ids)}
-    gp[0] = [remap[int(x) - one] + one for x in gp[0]]
-    gs = score[:, sel]
-    return bool(np.array_equal(gp, o["pos"]) and np.array_equal(gs.view(np.uint64), o["score"].view(np.uint64)))
+def host_contigs(ds):
+    """Every sequence's bytes on the host (one D2H copy), as numpy views."""
+    buf = ds.seq[:max(ds.total, 1)].cpu().numpy()
+    return [buf[int(a):int(b)] for a, b in zip(ds.offsets[:-1], ds.offsets[1:])]
+
+
+class Oracle:
+    """The CPU oracle (oracle/, test infrastructure) as the checker of one
+    scan configuration: per-contig records on a host thread pool (ctypes
+    releases the GIL), the timed single-core baseline, the all-contig
+    parity verdict."""
+
+    def __init__(self, host, k, w, thr, min_width, min_score, trlr, threads):
+        from oracle import oracle as O
+        self.O = O
+        self.host, self.k, self.w, self.thr = host, k, w, thr
+        self.mw, self.ms, self.trlr = min_width, min_score, trlr
+        self.one = 1 if trlr else 0
+        self.threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+        self.per = {}  # contig -> (pos, score) with seq id = the contig's own
+
+    def _run(self, seqs):
+        if self.trlr:
+            return self.O.tr_lr_regions(seqs, self.k, self.mw, self.w, self.w)
+        return self.O.scan(seqs, self.k, self.w, self.thr, self.mw, self.ms)
+
+    def _keep(self, ids, o):
+        for i, q in enumerate(ids):
+            sel = o["pos"][0] - self.one == i
+            p = o["pos"][:, sel].copy()
+            p[0] = q + self.one
+            self.per[q] = (p, o["score"][:, sel])
+
+    def baseline(self, ids):
+        """Single-thread timing on one pinned core (the reference is single
+        threaded); the records are kept for the parity verdict."""
+        old = os.sched_getaffinity(0)
+        os.sched_setaffinity(0, {min(old)})
+        try:
+            t0 = time.perf_counter()
+            o = self._run([self.host[q] for q in ids])
+            t = time.perf_counter() - t0
+        finally:
+            os.sched_setaffinity(0, old)
+        self._keep(ids, o)
+        return t
+
+    def fill(self, ids):
+        """Records of the given contigs (largest first) on the thread pool."""
+        todo = sorted((q for q in ids if q not in self.per), key=lambda q: -self.host[q].size)
+        with ThreadPoolExecutor(self.threads) as ex:
+            for q, o in zip(todo, ex.map(lambda q: self._run([self.host[q]]), todo)):
+                self._keep([q], o)
+
+    def parity(self, pos, score, ids):
+        """GPU records restricted to contigs ids equal the oracle's, bitwise."""
+        ids = sorted(ids)
+        sel = np.isin(pos[0] - self.one, ids)
+        ps = [self.per[q][0] for q in ids]
+        ss = [self.per[q][1] for q in ids]
+        op = np.concatenate(ps, axis=1) if ps else np.zeros((3, 0), np.int32)
+        osc = np.concatenate(ss, axis=1) if ss else np.zeros((2, 0), np.float64)
+        return bool(np.array_equal(pos[:, sel], op) and
+                    np.array_equal(score[:, sel].view(np.uint64), osc.view(np.uint64)))
 
 
 class Timer:
@@ -204,6 +284,10 @@ class Timer:
     def __exit__(self, *a):
         torch.cuda.synchronize()
         self.ms = (time.perf_counter() - self.t) * 1e3
+
+
+def phase_means(stats):
+    return {key[3:]: round(float(np.mean([s[key] for s in stats])), 3) for key in stats[-1] if key.startswith("ms_")}
 
 
 # --------------------------------------------------------------------- main
@@ -244,24 +328,27 @@ def main():
         if dist:
             tdist.barrier()
 
-    def max_over_ranks(x: float) -> float:
+    def reduce_over_ranks(x: float, op) -> float:
         if not dist:
             return x
         e = torch.tensor([x], dtype=torch.float64, device=dev if tdist.get_backend() == "nccl" else "cpu")
-        tdist.all_reduce(e, op=tdist.ReduceOp.MAX)
+        tdist.all_reduce(e, op=op)
         return float(e.item())
 
-    def make_table(counts, words, ext_gib=None, warm=True):
+    def max_over_ranks(x: float) -> float:
+        return reduce_over_ranks(x, tdist.ReduceOp.MAX if dist else None)
+
+    def make_table(counts, words, score, ext_gib=None, warm=True):
         """Score table built on the device from the device counts
         (ks_table_from_counts: no 4^k host round trip), timed; w (the
         reference's weight vector) stays on the device for the parity leg."""
         t = {}
-        thr = 0.75 if args.score == "rank" else 0.0
+        thr = 0.75 if score == "rank" else 0.0
         cap = int((ext_gib if ext_gib is not None else (args.ext_max_gib or 0.0)) * (1 << 30))
         w_dev = torch.empty(4 ** k, dtype=torch.float64, device=dev)
 
         def build():
-            return D.DeviceTable.from_counts(ctx, counts, k, args.score, total=words, thr=thr,
+            return D.DeviceTable.from_counts(ctx, counts, k, score, total=words, thr=thr,
                                              expand=not args.no_expand, max_ext_bytes=cap, w_out=w_dev)
         if warm:  # first build: grows the workspace and allocates the expanded table (fresh VRAM is
             with Timer() as tm:  # cleared by the driver: seconds for 128 GiB), reported apart
@@ -281,22 +368,49 @@ def main():
             return D.tr_lr(ctx, ds, k, table, init, args.min_width)
         return D.scan(ctx, ds, k, table, args.min_width, args.min_score)
 
+    def timed_steps(ds, table, init, steps, warmup):
+        for _ in range(warmup):
+            scan_once(ds, table, init)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        stats = []
+        out = None
+        for _ in range(steps):
+            out = scan_once(ds, table, init)
+            stats.append(out[2])
+        torch.cuda.synchronize()
+        barrier()
+        return out[0], out[1], stats, max_over_ranks(time.perf_counter() - t0)
+
     setup = {}
     extra = {}
     # ------------------------------------------------------------ the input
     t0 = time.time()
+    lens_all = [max(1, int(round(L * args.scale))) for L in genome.GRCH38[:args.ncontigs]]
+    shards = None
     if args.mode == "shard":
-        lens_all = [max(1, int(round(L * args.scale))) for L in genome.GRCH38[:args.ncontigs]]
         from kmer_spans_amd.dist import lpt_shards
-        shards = lpt_shards(lens_all, world)
-        mine = shards[rank]
-        parts = [genome.contig(lens_all[q], args.seed + q, dev) for q in mine]
-        ds = D.from_parts(parts, [lens_all[q] for q in mine], dev)
+        nsh = world if dist else max(1, args.shard_of)
+        shards = lpt_shards(lens_all, nsh)
+        if dist:
+            mine = shards[rank]
+        else:
+            idx = args.shard_index if args.shard_index >= 0 else int(np.argmax([sum(lens_all[q] for q in s)
+                                                                                for s in shards]))
+            mine = shards[idx] if nsh > 1 else list(range(len(lens_all)))
+        # --shard-of at one rank: the whole genome is counted (its table is the one the
+        # sharded run builds after the all-reduce), then only the shard is scanned
+        gen = range(len(lens_all)) if (not dist and nsh > 1) else mine
+        parts = [genome.contig(lens_all[q], args.seed + q, dev) for q in gen]
+        ds = D.from_parts(parts, [lens_all[q] for q in gen], dev)
         genome_bp = sum(lens_all)
     else:
+        mine = None
         parts, lens = genome.human_like(scale=args.scale, seed=args.seed + 1000 * rank, device=dev,
                                         ncontigs=args.ncontigs)
         ds = D.from_parts(parts, lens, dev)
+        genome_bp = None
     del parts
     torch.cuda.synchronize()
     setup["genome_s"] = round(time.time() - t0, 2)
@@ -310,7 +424,7 @@ def main():
     with Timer() as tm:
         words = D.count(ctx, ds, k, counts)
     setup["count_ms"] = round(tm.ms, 2)
-    if args.mode == "shard":  # the table of the whole genome: exact int32 sum of per-shard counts
+    if args.mode == "shard" and dist:  # the table of the whole genome: exact int32 sum of per-shard counts
         from kmer_spans_amd.dist import allreduce_histogram
         with Timer() as tm:
             if tdist.get_backend() == "nccl":
@@ -324,40 +438,27 @@ def main():
             tdist.all_reduce(wt)
             words = float(wt.item())
         setup["count_allreduce_ms"] = round(tm.ms, 2)
-    w_dev, thr, table, init_table, tt = make_table(counts, words)
+    if args.mode == "shard" and not dist and args.shard_of > 1:
+        ds = ds.subset(mine)
+        torch.cuda.empty_cache()
+        extra["shard_of"] = {"n": args.shard_of, "contigs": mine, "bp": int(ds.total),
+                             "note": "one shard of an N-way LPT split scanned with the whole genome's table"}
+    w_dev, thr, table, init_table, tt = make_table(counts, words, args.score)
     setup.update({key: round(v, 2) for key, v in tt.items()})
-    w = None  # host copy of w, fetched after timing for the oracle legs
+    table_shape = {"table_compressed": table.compressed, "table_distinct": table.distinct,
+                   "positions_per_read": table.positions_per_read, "code_bits": table.code_bits,
+                   "escape_fraction": round(table.escape_fraction, 6)}
 
     # ------------------------------------------------------------- timing
-    for _ in range(args.warmup):
-        scan_once(ds, table, init_table)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    stats = []
-    for _ in range(args.steps):
-        pos, score, st = scan_once(ds, table, init_table)
-        stats.append(st)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
+    pos, score, stats, elapsed = timed_steps(ds, table, init_table, args.steps, args.warmup)
 
     n_bases = int(stats[-1]["n_bases"])
-    total_bases = genome_bp if args.mode == "shard" else n_bases * world
+    if args.mode == "shard":
+        total_bases = genome_bp if (dist or args.shard_of <= 1) else n_bases
+    else:
+        total_bases = n_bases * world
     ms_step = elapsed / args.steps * 1e3
     value = total_bases / (elapsed / args.steps) / 1e9
-
-    # ---- span records to rank 0 (RCCL gather; not on the timed path)
-    n_regions_all = int(pos.shape[1])
-    if dist:
-        from kmer_spans_amd.dist import gather_regions, merge_shards
-        allpos, allscore = gather_regions(pos, score, dev)
-        if rank == 0:
-            n_regions_all = sum(int(p.shape[1]) for p in allpos)
-            if args.mode == "shard":
-                mpos, _ = merge_shards(shards, allpos, allscore, one_based=args.trlr)
-                extra["merged_regions"] = int(mpos.shape[1])
-                extra["merged_order_ok"] = bool(np.all(np.diff(mpos[0].astype(np.int64) * (1 << 32) + mpos[1]) > 0))
 
     # ---- dominant kernel roofline (hipEvents on the library stream)
     ms_kernel = float(np.mean([s["ms_scan"] for s in stats]))
@@ -368,7 +469,8 @@ def main():
                 "kernel": kernel, "kernel_ms": round(ms_kernel, 3), "algo_bytes_per_base": ALGO_BYTES_PER_BASE,
                 "algo_bytes_per_launch": int(ALGO_BYTES_PER_BASE * n_bases)}
     workload = {"k": k, "score": args.score, "scale": args.scale, "ncontigs": args.ncontigs,
-                "expand": not args.no_expand, "trlr": args.trlr, "mode": args.mode, "world": world}
+                "expand": not args.no_expand, "trlr": args.trlr, "mode": args.mode, "world": world,
+                "shard_of": args.shard_of}
     traffic, why = pmc_traffic(kernel, build_id, workload)
     if traffic:
         roofline["traffic"] = traffic["bytes"]
@@ -378,7 +480,7 @@ def main():
         roofline["traffic_note"] = why
     # the bound that applies to a gather pass: random requests (every table
     # read is one 64-B request whatever its width; the chip's measured ceiling
-    # for such requests from 32-128 GiB tables is ~48 G/s, tools/gather_bench2.hip)
+    # for such requests from 32-128 GiB tables is ~48-50 G/s, tools/line_bench.hip)
     if stats[-1]["scan_algo"] == 1:
         J = max(1, int(table.positions_per_read))
         n_scored = int(stats[-1]["n_scored"])
@@ -409,7 +511,6 @@ def main():
             torch.cuda.synchronize()
             vt.append(time.perf_counter() - t1)
         tv = float(np.median(vt))
-        # every scored index is visited once at top level or more by rescans
         vsum = int(vis.to(torch.int64).sum().item())
         visits_line = {"ms": round(tv * 1e3, 3), "Gbases_per_s": round(n_bases / tv / 1e9, 3),
                        "regions_equal": bool(np.array_equal(vpos, pos)),
@@ -418,24 +519,29 @@ def main():
                        "note": "ks_scan_dev with the visit histogram (device-resident), median of 3"}
         del vis, vpos, vscore
 
+    # ---- span records to rank 0 (RCCL gather; not on the timed path)
+    n_regions_all = int(pos.shape[1])
+    if dist:
+        from kmer_spans_amd.dist import gather_regions, merge_shards
+        allpos, allscore = gather_regions(pos, score, dev)
+        if rank == 0:
+            n_regions_all = sum(int(p.shape[1]) for p in allpos)
+            if args.mode == "shard":
+                mpos, _ = merge_shards(shards, allpos, allscore, one_based=args.trlr)
+                extra["merged_regions"] = int(mpos.shape[1])
+                extra["merged_order_ok"] = bool(np.all(np.diff(mpos[0].astype(np.int64) * (1 << 32) + mpos[1]) > 0))
+
+    w = w_dev.cpu().numpy()
+    host = None
+    if not args.no_cpu or not args.no_host_path:
+        host = host_contigs(ds)
+
     # ---- PCIe-inclusive rate of the drop-in host entry point (never `value`)
     host_path = None
-    need_w = (args.host_path or not args.no_cpu) and rank == 0
-    table_equal_host = None
-    if need_w:
-        w = w_dev.cpu().numpy()
-        if world == 1 and not args.no_cpu:  # the device-built table against the host builder (bitwise)
-            hc = counts.cpu().numpy()
-            wh = np.asarray(score_table(api, hc, k, words, args.score)[0], dtype=np.float64)
-            table_equal_host = bool(np.array_equal(w.view(np.uint64), wh.view(np.uint64)))
-            del hc, wh
-    if args.trlr and w is not None:
-        w = w - thr
-    if args.host_path and rank == 0 and not args.trlr and thr == 0.0:
-        hs = [ds.host_seq(q) for q in range(ds.nseq)]
-        api.kmer_regions(hs, k, w, args.min_width, args.min_score)  # warm (pinned staging, workspace)
+    if world == 1 and not args.no_host_path and not args.trlr and thr == 0.0:
+        api.kmer_regions(host, k, w, args.min_width, args.min_score)  # warm (pinned staging, workspace)
         t0 = time.perf_counter()
-        hr = api.kmer_regions(hs, k, w, args.min_width, args.min_score)
+        hr = api.kmer_regions(host, k, w, args.min_width, args.min_score)
         t_host = time.perf_counter() - t0
         host_path = {"seconds": round(t_host, 4), "Gbases_per_s": round(n_bases / t_host / 1e9, 3),
                      "regions_equal": bool(np.array_equal(hr["pos"], pos)),
@@ -443,29 +549,51 @@ def main():
                      "visits": True, "timing": hr.get("timing"),
                      "note": "ks_kmer_regions from host memory with the visit histogram: pinned staging + H2D + "
                              "table upload/compress/expand + count-derived visits + scan + D2H"}
-        del hs
+        del hr
 
-    # ---- CPU baseline (N=1 only): the oracle, single thread, bounded sample
+    # ---- CPU baseline (N=1, one pinned core, bounded sample) and the parity
+    # verdict (every contig of this rank, oracle on a host thread pool)
     cpu = None
     parity = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        from oracle import oracle as O
-        ids, acc = sample_ids(ds.offsets, args.cpu_sample)
-        host = [ds.host_seq(q) for q in ids]
-        t0 = time.perf_counter()
-        if args.trlr:
-            o = O.tr_lr_regions(host, k, args.min_width, w, w)
-        else:
-            o = O.scan(host, k, w, thr, args.min_width, args.min_score)
-        t_cpu = time.perf_counter() - t0
-        lens = np.diff(ds.offsets)
-        cpu = {"value": round(acc / t_cpu / 1e9, 5), "unit": "Gbases/s", "cores": 1, "kind": "port",
-               "sample": f"oracle/ks_oracle.c scan of {len(ids)} contigs ({acc} bp: the largest, "
-                         f"{int(lens.max())} bp, plus the smallest) of the same genome, same table",
-               "seconds": round(t_cpu, 3), "host_cpu": cpu_model(), "host_nproc": os.cpu_count()}
-        parity = parity_of(pos, score, ids, o, 1 if args.trlr else 0)
-        extra["parity_contigs"] = ids
-        extra["parity_bp"] = acc
+    table_equal_host = None
+    if not args.no_cpu:
+        if world == 1:  # the device-built table against the host builder (bitwise)
+            hc = counts.cpu().numpy()
+            wh = np.asarray(api.log2_table(hc, k) if args.score == "log2" else
+                            api.pm1_table(hc, k) if args.score == "pm1" else
+                            api.rank_table(hc, k, words), dtype=np.float64)
+            table_equal_host = bool(np.array_equal(w.view(np.uint64), wh.view(np.uint64)))
+            del hc, wh
+        orc = Oracle(host, k, (w - thr) if args.trlr else w, thr, args.min_width, args.min_score, args.trlr,
+                     args.cpu_threads)
+        if rank == 0 and world == 1:
+            ids, acc = sample_ids(ds.offsets, args.cpu_sample)
+            t_cpu = orc.baseline(ids)
+            lens = np.diff(ds.offsets)
+            cpu = {"value": round(acc / t_cpu / 1e9, 5), "unit": "Gbases/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle/ks_oracle.c scan of {len(ids)} contigs ({acc} bp: the largest, "
+                             f"{int(lens.max())} bp, plus the smallest) of the same genome, same table, "
+                             f"one thread pinned to one core",
+                   "seconds": round(t_cpu, 3), "host_cpu": cpu_model(), "host_nproc": os.cpu_count()}
+        check = list(range(ds.nseq)) if args.parity == "all" else sorted(orc.per) if args.parity == "sample" else []
+        if check:
+            t0 = time.perf_counter()
+            orc.fill(check)
+            ok = orc.parity(pos, score, check)
+            bp = int(sum(int(host[q].size) for q in check))
+            extra["parity_seconds"] = round(time.perf_counter() - t0, 2)
+            extra["parity_threads"] = orc.threads
+            parity = bool(reduce_over_ranks(1.0 if ok else 0.0, tdist.ReduceOp.MIN if dist else None) > 0.5)
+            extra["parity_bp"] = int(reduce_over_ranks(float(bp), tdist.ReduceOp.SUM if dist else None))
+            extra["parity_contigs"] = "all" if args.parity == "all" else check
+        del orc
+
+    # ---- weighted rank (BASELINE config 3) on the same genome and counts
+    rank_line = None
+    if (world == 1 and not args.no_rank and args.score == "log2" and not args.trlr and args.mode == "shard"
+            and args.shard_of <= 1):
+        table.close()
+        rank_line = rank_subline(args, ctx, ds, counts, words, make_table, timed_steps, host, D)
 
     step_ms = ms_step
     e2e_ms = setup["count_ms"] + setup["table_device"] + step_ms
@@ -475,18 +603,15 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
         "scaling": "strong" if args.mode == "shard" else "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": f"human-shaped synthetic genome ({total_bases if args.mode == 'shard' else n_bases} bp, "
+        "config": {"workload": f"human-shaped synthetic genome ({total_bases} bp, "
                                f"{args.ncontigs} contigs, scale {args.scale}), k={k}, {args.score} score from its "
                                f"own counts, min_width {args.min_width}, min_score {args.min_score}, device-resident"
                                + (", contigs LPT-sharded over the ranks" if args.mode == "shard" else
                                   ", one genome per rank"),
-                   "k": k, "score": args.score, "genome_bp": total_bases if args.mode == "shard" else n_bases,
+                   "k": k, "score": args.score, "genome_bp": total_bases,
                    "parallelism": f"{'contig-shard' if args.mode == 'shard' else 'genome-per-rank'} x{world}",
                    "mode": args.mode, "scan": "tr_lr_regions" if args.trlr else "kmer_regions",
-                   "scan_algo": int(stats[-1]["scan_algo"]), "table_compressed": table.compressed,
-                   "table_distinct": table.distinct, "positions_per_read": table.positions_per_read,
-                   "code_bits": table.code_bits, "escape_fraction": round(table.escape_fraction, 6),
-                   "build_id": build_id},
+                   "scan_algo": int(stats[-1]["scan_algo"]), **table_shape, "build_id": build_id},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "parity_sample": parity,
@@ -495,12 +620,12 @@ def main():
         "replayed_chunks": int(stats[-1]["n_replay"]),
         "visits_path": visits_line,
         "host_path": host_path,
-        "phase_ms": {key[3:]: round(float(np.mean([s[key] for s in stats])), 3)
-                     for key in stats[-1] if key.startswith("ms_")},
+        "phase_ms": phase_means(stats),
         "setup_ms": setup,
         "end_to_end": {"ms": round(e2e_ms, 2), "Gbases_per_s": round(n_bases / (e2e_ms * 1e-3) / 1e9, 3),
                        "what": "count + device score table from the counts (values, codes, 12-bit codes, "
                                "expanded table) + one scan step, per rank"},
+        "configs": {"rank": rank_line} if rank_line is not None else None,
     }
     line.update(extra)
     if rank == 0:
@@ -511,6 +636,68 @@ def main():
                 f.write(s + "\n")
     if dist:
         tdist.destroy_process_group()
+
+
+def rank_subline(args, ctx, ds, counts, words, make_table, timed_steps, host, D):
+    """BASELINE config 3 (kmer_low_comp_regions, kmer_spans.c:548-621): the
+    weighted-rank table (threshold 0.75) of the same genome's counts, scanned
+    like the metric line; parity over every contig; the CPU phases of the
+    reference operation (count, rank, scan) on one pinned core."""
+    k = args.k
+    w_dev, thr, table, init, tt = make_table(counts, words, "rank", warm=False)
+    pos, score, stats, elapsed = timed_steps(ds, table, init, args.rank_steps, 1)
+    n_bases = int(stats[-1]["n_bases"])
+    ms = elapsed / args.rank_steps * 1e3
+    out = {"what": "weighted rank (kmer_low_comp_regions, thr 0.75), k=13, same genome and counts",
+           "value": round(n_bases / (ms * 1e-3) / 1e9, 4), "unit": "Gbases/s", "ms_per_step": round(ms, 3),
+           "steps": args.rank_steps, "regions": int(pos.shape[1]), "replayed_chunks": int(stats[-1]["n_replay"]),
+           "phase_ms": phase_means(stats), "table_ms": round(tt["table_device"], 2),
+           "table_setup_ms": {key: round(v, 2) for key, v in tt.items()},
+           "positions_per_read": table.positions_per_read, "parity": None}
+    out["end_to_end"] = {"ms": round(float(tt["table_device"]) + ms, 2),
+                         "what": "device rank table + one step (the count is shared with the metric line)"}
+    table.close()
+    if args.no_cpu or host is None:
+        return out
+    from oracle import oracle as O
+    w = w_dev.cpu().numpy()
+    hc = counts.cpu().numpy()
+    old = os.sched_getaffinity(0)
+    os.sched_setaffinity(0, {min(old)})
+    try:  # the reference's rank build (glibc merge sort + sequential prefix), one core
+        t0 = time.perf_counter()
+        wo = O.rank_table(hc, k, words)
+        t_rank = time.perf_counter() - t0
+    finally:
+        os.sched_setaffinity(0, old)
+    out["table_equal_oracle"] = bool(np.array_equal(w.view(np.uint64), wo.view(np.uint64)))
+    del wo
+    orc = Oracle(host, k, w, thr, args.min_width, args.min_score, False, args.cpu_threads)
+    ids, acc = sample_ids(ds.offsets, args.cpu_sample)
+    old = os.sched_getaffinity(0)
+    os.sched_setaffinity(0, {min(old)})
+    try:
+        t0 = time.perf_counter()
+        O.kmer_counts([host[q] for q in ids], k)
+        t_count = time.perf_counter() - t0
+    finally:
+        os.sched_setaffinity(0, old)
+    t_scan = orc.baseline(ids)
+    total = float(ds.total)
+    out["cpu_baseline"] = {
+        "kind": "port", "cores": 1, "unit": "Gbases/s",
+        "value": round(total / (t_count * total / acc + t_rank + t_scan * total / acc) / 1e9, 5),
+        "scan_value": round(acc / t_scan / 1e9, 5),
+        "phases_s": {"count_sample": round(t_count, 3), "rank_table_full": round(t_rank, 3),
+                     "scan_sample": round(t_scan, 3)},
+        "sample": f"count and scan of {len(ids)} contigs ({acc} bp), extrapolated to {int(total)} bp; the rank "
+                  f"table (4^{k} entries) built once in full; oracle/ks_oracle.c, one pinned core"}
+    t0 = time.perf_counter()
+    orc.fill(range(ds.nseq))
+    out["parity"] = orc.parity(pos, score, range(ds.nseq))
+    out["parity_bp"] = int(ds.total)
+    out["parity_seconds"] = round(time.perf_counter() - t0, 2)
+    return out
 
 
 def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over_ranks, make_table, D, genome,
@@ -531,8 +718,8 @@ def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over
     def one(ds):
         counts.zero_()
         words = D.count(ctx, ds, k, counts)
-        _, _, table, init, _ = make_table(counts, words, ext_gib=args.ext_max_gib if args.ext_max_gib else 32.0,
-                                          warm=False)
+        _, _, table, init, _ = make_table(counts, words, args.score,
+                                          ext_gib=args.ext_max_gib if args.ext_max_gib else 32.0, warm=False)
         if args.trlr:
             out = D.tr_lr(ctx, ds, k, table, init, args.min_width)
         else:

@@ -203,8 +203,13 @@ ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev, int32_t k
 void ks_table_destroy(ks_table *t);
 /* The library keeps the buffer of the last destroyed expanded table (one
  * per device) for the next table that fits in it: a fresh 32-128 GiB
- * hipMalloc can take seconds (the driver clears new VRAM).  This returns it
- * to the driver (also: environment KS_EXT_POOL=0 disables the pool). */
+ * hipMalloc can take seconds (the driver clears new VRAM).  Like a caching
+ * allocator, it stays allocated after the call that destroyed the table
+ * returns (up to 128 GiB at k = 13 for a device-API table, 32 GiB for the
+ * host entry points' J = 4 tables).  This returns it to the driver; so does
+ * ks_ctx_destroy for its device; environment KS_EXT_POOL=0 disables the
+ * pool.  Workspace retained by a context (scan scratch, the table builder's
+ * sort scratch of ~20 B x 4^k) is freed by ks_ctx_destroy. */
 void ks_release_cache(void);
 /* 1 if the table is stored compressed (uint16 codes + LUT), else 0. */
 int32_t ks_table_is_compressed(const ks_table *t);

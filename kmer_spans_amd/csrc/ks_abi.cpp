@@ -211,6 +211,7 @@ extern "C" void ks_ctx_destroy(ks_ctx *c) {
       (void)hipStreamDestroy(x);
     }
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  ks::pool_release_device(c->device);  // a destroyed table's pooled expanded-table buffer (ks_table.hip)
   delete c;
 }
 

@@ -92,6 +92,7 @@ struct ks_ctx {
   // top-level visits counted by another context concurrently with the scan
   // (scan_impl): scan_core leaves the count out and says whether it did
   bool vis_count_ext = false;
+  bool chunked_events = false;  // the last scan_chunked recorded its phase events (ev[7..11], ev[14..15])
   bool vis_count_ext_used = false;
 };
 
@@ -147,6 +148,7 @@ ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out);
 ks_status ensure_pinned(ks_ctx *ctx, size_t bytes, void **out);
 ks_status activate(ks_ctx *ctx);  // fork check + hipSetDevice
 ks_status ctx_sub(ks_ctx *ctx, ks_ctx **sub);  // ctx->sub, created on first use
+void pool_release_device(int dev);             // free the device's pooled expanded-table buffer
 ks_status default_ctx(ks_ctx **ctx);  // *ctx or the process default context (fork-checked)
 bool hip_usable_here();  // false in a child forked after HIP was initialised
 

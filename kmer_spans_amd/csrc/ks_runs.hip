@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ se
         ends = nm & ((non << 1) | (prev_n ^ 1u)) & 0xffffu;
         if (p0 + 16 > p_hi) {  // no events past position p_hi
           const int keep = (int)(p_hi - p0) + 1;
-          const uint32_t km = keep >= 16 ? 0xffffu : ((1u << keep) - 1u);
+          const uint32_t km = keep <= 0 ? 0u : keep >= 16 ? 0xffffu : ((1u << keep) - 1u);
           starts &= km;
           ends &= km;
         }

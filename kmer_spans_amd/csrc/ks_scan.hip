@@ -596,7 +596,15 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     // pass (random requests) runs here; the count lands in the sub-context's
     // histogram and is added once both are done.  KS_VISITS_SERIAL: the
     // count after the scan on this stream (A/B).
-    const bool vis_conc = visits_dev && !mode.trlr && ctx->scan_algo != 0 && total > 0 &&
+    // Only when the chunked path is certain or likely: forced, or some
+    // sequence longer than the lane kernel's limit (a run longer than 2^15
+    // needs one); otherwise the lane kernel counts its own visits and a
+    // concurrent count would be thrown away.
+    int64_t longest_seq = 0;
+    for (int32_t q = 0; q < s->nseq; ++q)
+      longest_seq = std::max<int64_t>(longest_seq, s->offsets_host[q + 1] - s->offsets_host[q]);
+    const bool chunked_likely = ctx->scan_algo == 1 || (ctx->scan_algo < 0 && longest_seq > (1 << 15));
+    const bool vis_conc = visits_dev && !mode.trlr && chunked_likely && total > 0 &&
                           getenv("KS_VISITS_ATOMIC") == nullptr && getenv("KS_VISITS_SERIAL") == nullptr;
     if (!vis_conc) return scan_core(ctx, s, total, k, t, min_width, min_score, visits_dev, out, stats, mode, nullptr);
     ks_ctx *vsub = nullptr;

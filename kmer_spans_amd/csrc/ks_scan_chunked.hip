@@ -3016,6 +3016,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const int64_t total = s->offsets_host[s->nseq];
   const int64_t nruns = runs.n;
   const int64_t nch = lay.nch, ntiles = lay.ntiles;
+  ctx->chunked_events = false;
   if (nruns == 0 || nch == 0) return KS_OK;
   const int64_t *d_cbase = lay.cbase, *d_tbase = lay.tbase;
   const bool comp = tv.compressed != 0;
@@ -3647,12 +3648,17 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     stats->n_rescan = nres;
     stats->n_replay = (int64_t)hc[2];
   }
+  ctx->chunked_events = true;
   return KS_OK;
 }
 
 // Phase times of the last chunked scan on ctx (its events are complete once
 // the caller has synchronised after the region readback).
 ks_status chunked_phase_times(ks_ctx *ctx, ks_scan_stats *stats) {
+  if (!ctx->chunked_events) {  // nothing to scan (no run longer than k): no phase was recorded
+    stats->ms_layout = stats->ms_scan = stats->ms_predict = stats->ms_carry = stats->ms_stitch = stats->ms_rescan = 0;
+    return KS_OK;
+  }
   float ms_lay = 0, ms_p1 = 0, ms_p2 = 0, ms_p34 = 0, ms_p5 = 0, ms_res = 0;
   KS_HIP(hipEventElapsedTime(&ms_lay, ctx->ev[7], ctx->ev[8]));
   KS_HIP(hipEventElapsedTime(&ms_p1, ctx->ev[8], ctx->ev[9]));

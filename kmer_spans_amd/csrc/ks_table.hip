@@ -359,6 +359,13 @@ void *pool_take(int dev, size_t bytes, size_t *cap) {
 void pool_give(int dev, void *p, size_t bytes) {
   if (!p) return;
   if (pool_on() && dev >= 0 && dev < 64) {
+    // the next table's build may run on another stream: every kernel that
+    // reads this buffer must have finished before it is handed out again
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(dev);
+    (void)hipDeviceSynchronize();
+    if (cur >= 0) (void)hipSetDevice(cur);
     std::lock_guard<std::mutex> g(g_pool_mu);
     PoolBuf &b = g_pool[dev];
     if (!b.p || b.bytes < bytes) {
@@ -913,6 +920,10 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
   KS_TFC(hipStreamSynchronize(st));
 #undef KS_TFC
   cleanup();
+  if (ctx->slots[SLOT_TABLE_TMP].bytes > ((size_t)4 << 30)) {  // k >= 14: ~20 B x 4^k of sort scratch
+    (void)hipFree(ctx->slots[SLOT_TABLE_TMP].ptr);                // is not kept on the context
+    ctx->slots[SLOT_TABLE_TMP] = DevBuf();
+  }
   t->ms_compress = now_ms() - t_start - t->ms_upload;
   if (flags & KS_TABLE_EXPAND) {
     const size_t cap = max_ext_bytes > 0 ? (size_t)max_ext_bytes : (size_t)160 << 30;
@@ -942,6 +953,16 @@ extern "C" void ks_table_destroy(ks_table *t) {
   if (t->d_approx) (void)hipFree(t->d_approx);
   delete t;
 }
+
+namespace ks {
+// The pooled buffer of one device goes back to the driver (ks_ctx_destroy).
+void pool_release_device(int dev) {
+  if (dev < 0 || dev >= 64) return;
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  if (g_pool[dev].p) (void)hipFree(g_pool[dev].p);
+  g_pool[dev] = PoolBuf();
+}
+}  // namespace ks
 
 extern "C" void ks_release_cache(void) {
   if (!hip_usable_here()) return;

@@ -661,8 +661,7 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   const int nb1 = 1 << g.T1, nbf = 1 << g.T;
   const int shift = 2 * k - g.T1;
   const int64_t ntiles = (total + kPTile - 1) / kPTile;
-  const int pb = getenv("KS_PART_BLOCKS") ? atoi(getenv("KS_PART_BLOCKS")) : kPBlocks;  // A/B
-  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(pb > 0 ? pb : kPBlocks, ntiles));
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(kPBlocks, ntiles));
   const int C = kSubChunks;
   const size_t m1 = (size_t)nb1 * G, m2 = g.T2 ? (size_t)nbf * C : 0;
   void *w = nullptr, *p1 = nullptr, *p2 = nullptr, *tmp = nullptr;

@@ -88,7 +88,7 @@ __device__ __forceinline__ void append_events(uint32_t starts, uint32_t ends, in
 // words -- pure functions of the bytes -- the part's later passes may read).
 // kPre: lane 0's byte before its unit is loaded with the unit loads (one
 // memory round trip per step) instead of after them (A/B: KS_NEV_LATE_PREV=1).
-template <bool kMul, bool kPre>  // multiply-based byte packing (A/B: KS_NEV_SHIFTS=1 for the shift/or forms)
+template <bool kMul, bool kPre>  // multiply-based byte packing, lane 0's preceding byte loaded early (both A/B winners)
 __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ seq, int64_t total,
                                                   unsigned long long *__restrict__ ev,
                                                   unsigned long long *__restrict__ ev_count, int64_t cap,
@@ -274,8 +274,9 @@ ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int t
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt_c, lay->cbase, (int)(n + 1), st));
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt_t, lay->tbase, (int)(n + 1), st));
   // the first half (highest priority) ends first; its carry and stitch run
-  // under the rest of the second half (KS_SPLIT_FRAC: A/B, tools/ab_inproc.py)
-  const double frac = getenv("KS_SPLIT_FRAC") ? atof(getenv("KS_SPLIT_FRAC")) : 0.7;
+  // under the rest of the second half (A/B: 0.7 of the chunks, 17.73 vs
+  // 17.97 / 17.95 ms at 0.6 / 0.8)
+  constexpr double frac = 0.7;
   hipLaunchKernelGGL(k_split, dim3(1), dim3(1), 0, st, lay->cbase, lay->tbase, n, frac, agg + 3);
   KS_HIP(hipGetLastError());
   unsigned long long ha[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -320,10 +321,7 @@ ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs
     const int64_t u1 = std::min<int64_t>(nunits, p_hi / 16 + 1 + kMargin);
     const unsigned grid = (unsigned)std::max<int64_t>(
         1, std::min<int64_t>((u1 - u0 + 1023) / 1024, (int64_t)ctx->num_cus * 16));
-    auto *kern = getenv("KS_NEV_SHIFTS")     ? k_n_events<false, true>
-                 : getenv("KS_NEV_LATE_PREV") ? k_n_events<true, false>
-                                              : k_n_events<true, true>;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp, d_count, cap,
+    hipLaunchKernelGGL((k_n_events<true, true>), dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp, d_count, cap,
                        packed, p_lo, p_hi, u0, u1);
     KS_HIP(hipGetLastError());
     if (s->nseq > 1) {

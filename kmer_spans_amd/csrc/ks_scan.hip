@@ -308,21 +308,9 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
   return KS_OK;
 }
 
-// One part of a scan split at a sequence boundary (scan_impl): positions
-// [p_lo, p_hi), sequences [q_lo, q_hi).  The part leaves the top-level visits
-// to scan_impl (its runs and its rescan-visit histogram are handed back) and
-// never falls back to the lane kernel (KS_INTERNAL_DUAL_ABORT instead).
-struct ScanPart {
-  int64_t p_lo = 0, p_hi = 0;
-  int32_t q_lo = 0, q_hi = 0;
-  Runs runs;
-  uint32_t *vscr = nullptr;
-};
-constexpr ks_status KS_INTERNAL_DUAL_ABORT = static_cast<ks_status>(101);
-
 static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, const ks_table *t,
                            int32_t min_width, double min_score, int32_t *visits_dev, ks_regions *out,
-                           ks_scan_stats *stats, const ScanMode &mode, ScanPart *part) {
+                           ks_scan_stats *stats, const ScanMode &mode) {
   hipStream_t st = ctx->stream;
   ks_scan_stats local{};
   ks_scan_stats *S = stats ? stats : &local;
@@ -330,8 +318,7 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
   KS_HIP(hipEventRecord(ctx->ev[2], st));
   Runs runs;
   float ms_runs = 0;
-  KS_TRY(find_runs(ctx, s, total, &runs, &ms_runs, /*want_packed=*/true, part ? part->p_lo : 0,
-                   part ? part->p_hi : -1));
+  KS_TRY(find_runs(ctx, s, total, &runs, &ms_runs, /*want_packed=*/true));
   S->ms_runs = ms_runs;
   // chunk layout, statistics and algorithm choice (device-side, one sync)
   RunLayout lay;
@@ -339,7 +326,7 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
   const int64_t longest = lay.longest, scored = lay.scored;
   S->n_scored = scored;
   S->n_runs = lay.nscan;
-  for (int32_t q = part ? part->q_lo : 0; q < (part ? part->q_hi : s->nseq); ++q) {
+  for (int32_t q = 0; q < s->nseq; ++q) {
     const int64_t L = s->offsets_host[q + 1] - s->offsets_host[q];
     if (L >= k) S->n_bases += L;
   }
@@ -350,7 +337,6 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
   int algo = ctx->scan_algo;
   if (algo < 0) algo = (longest > (1 << 15)) ? 1 : 0;
   if (mode.trlr && !(mode.finite && mode.maxabs * (double)(longest + 2) < 1e300)) algo = 0;  // literal NaN rules
-  if (part && algo != 1) return KS_INTERNAL_DUAL_ABORT;
   S->scan_algo = algo;
 
   // region capacity: what the (grow-only) slot already holds, so that the
@@ -408,7 +394,7 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
       // top-level visits: from the k-mer counts (one partitioned count pass)
       // unless KS_VISITS_ATOMIC is set (one random atomic per scanned index in
       // pass 1, the former path, kept for A/B runs and tests)
-      const bool vis_atomic = getenv("KS_VISITS_ATOMIC") != nullptr && !part;
+      const bool vis_atomic = getenv("KS_VISITS_ATOMIC") != nullptr;
       ks_status rc = scan_chunked(ctx, s, runs, lay, k, tv, mw, min_score, vis_atomic ? vscr : nullptr, vscr, rb, S,
                                   mode);
       if (rc == KS_INTERNAL_RETRY) {  // a buffer did not fit: grow, rerun, visits untouched
@@ -417,10 +403,7 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
         if (m > segcap) segcap = m + m / 4 + 64;
         continue;
       }
-      if (rc == KS_OK && part) {  // visits: scan_impl, after both parts
-        part->runs = runs;
-        if (vscr) part->vscr = vscr;  // (a rerun for a larger region buffer counts no visits)
-      } else if (rc == KS_OK) {
+      if (rc == KS_OK) {
         if (vis) {
           const int64_t n = (int64_t)1 << (2 * k);
           if (!vis_atomic) {
@@ -439,8 +422,6 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
                              vis, vscr, n);
           KS_HIP(hipGetLastError());
         }
-      } else if (rc == KS_ERR_INTERNAL && part) {
-        return KS_INTERNAL_DUAL_ABORT;  // scan_impl redoes the whole call in one part
       } else if (rc == KS_ERR_INTERNAL) {
         fprintf(stderr, "kmer_spans_amd: chunked scan fell back to the lane kernel: %s\n", ks_last_error());
         ctx->hreg_ok = false;  // the lane kernel recounts the regions
@@ -559,37 +540,12 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
 }
 
 
-// Scan of one call.  A large multi-sequence input is cut at the sequence
-// boundary nearest half its bases into two parts scanned at once by two host
-// threads on two contexts (this one and its sub-context: own streams and
-// workspace, the same table): each part's run segmentation, layout and
-// predictor run under the other's gather pass, and its region ordering and
-// readback too; runs never cross a sequence, so the parts are independent
-// and their region lists (global (seq, beg) order) concatenate.  The
-// top-level visits (one count of the whole input, then each part's
-// corrections and rescan visits) follow on the main stream.  KS_NO_DUAL: one
-// part.  (Opt-in, see dual_min.)  A part that would take the lane kernel (a consistency fallback, or
-// only short runs) sends the whole call down the one-part path.
+// Scan of one call.  With the visit histogram on the chunked path, the
+// top-level count runs concurrently on the sub-context (below).
 ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, const ks_table *t,
                     int32_t min_width, double min_score, int32_t *visits_dev, ks_regions *out,
                     ks_scan_stats *stats, const ScanMode &mode) {
-  // Off by default: on the metric genome the parts' streaming run passes
-  // compete with the other part's gather pass for the same HBM and the
-  // one-part pipeline is as fast or faster (A/B: 19.02-19.31 vs 19.47-19.99
-  // ms, profiles/r2/ab_two_part_g34.json).  KS_DUAL_MIN=<bases>: the
-  // two-part path from that size on (tests/test_gpu_dual.py).
-  const int64_t dual_min = getenv("KS_DUAL_MIN") ? atoll(getenv("KS_DUAL_MIN")) : INT64_MAX;
-  int32_t m = -1;
-  if (!mode.trlr && ctx->scan_algo != 0 && total >= dual_min && s->nseq >= 2 && getenv("KS_NO_DUAL") == nullptr) {
-    int64_t best = INT64_MAX;
-    for (int32_t q = 1; q < s->nseq; ++q) {
-      const int64_t d = std::llabs(2 * s->offsets_host[q] - total);
-      if (d < best) { best = d; m = q; }
-    }
-    const int64_t P = m > 0 ? s->offsets_host[m] : 0;
-    if (m <= 0 || 5 * P < total || 5 * P > 4 * total) m = -1;  // parts of 20-80 %
-  }
-  if (m < 0) {
+  {
     // Visits of the one-part chunked scan: the top-level count (the k-mer
     // histogram, ~24 ms at k = 13, streaming + LDS work) runs on the
     // sub-context's stream from a second host thread while the scan's gather
@@ -606,7 +562,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     const bool chunked_likely = ctx->scan_algo == 1 || (ctx->scan_algo < 0 && longest_seq > (1 << 15));
     const bool vis_conc = visits_dev && !mode.trlr && chunked_likely && total > 0 &&
                           getenv("KS_VISITS_ATOMIC") == nullptr && getenv("KS_VISITS_SERIAL") == nullptr;
-    if (!vis_conc) return scan_core(ctx, s, total, k, t, min_width, min_score, visits_dev, out, stats, mode, nullptr);
+    if (!vis_conc) return scan_core(ctx, s, total, k, t, min_width, min_score, visits_dev, out, stats, mode);
     ks_ctx *vsub = nullptr;
     KS_TRY(ctx_sub(ctx, &vsub));
     const size_t nb = (size_t)4 << (2 * k);
@@ -627,7 +583,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     });
     ctx->vis_count_ext = true;
     ctx->vis_count_ext_used = false;
-    const ks_status rc = scan_core(ctx, s, total, k, t, min_width, min_score, visits_dev, out, stats, mode, nullptr);
+    const ks_status rc = scan_core(ctx, s, total, k, t, min_width, min_score, visits_dev, out, stats, mode);
     ctx->vis_count_ext = false;
     th.join();  // (launch_count ended with a synchronisation of the sub-context's stream)
     if (rc != KS_OK) return rc;
@@ -645,114 +601,6 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     }
     return KS_OK;
   }
-  ks_ctx *sub = nullptr;
-  KS_TRY(ctx_sub(ctx, &sub));
-  const double t0 = now_ms();
-  ScanPart pa, pb;
-  pa.p_lo = 0;
-  pa.p_hi = s->offsets_host[m];
-  pa.q_lo = 0;
-  pa.q_hi = m;
-  pb.p_lo = s->offsets_host[m];
-  pb.p_hi = total;
-  pb.q_lo = m;
-  pb.q_hi = s->nseq;
-  ks_regions ra{}, rb{};
-  ks_scan_stats sa{}, sb{};
-  ks_status rc_b = KS_OK;
-  std::string err_b;
-  sub->scan_algo = ctx->scan_algo;
-  // the sub-context's stream starts after the caller's work on ctx->stream
-  // (the sequence upload, the table build)
-  KS_HIP(hipEventRecord(ctx->ev[19], ctx->stream));
-  KS_HIP(hipStreamWaitEvent(sub->stream, ctx->ev[19], 0));
-  std::thread th([&] {
-    rc_b = activate(sub);
-    if (rc_b == KS_OK)
-      rc_b = scan_core(sub, s, total, k, t, min_width, min_score, visits_dev, &rb, &sb, mode, &pb);
-    if (rc_b != KS_OK) err_b = ks_last_error();  // (thread-local)
-  });
-  const ks_status rc_a = scan_core(ctx, s, total, k, t, min_width, min_score, visits_dev, &ra, &sa, mode, &pa);
-  th.join();
-  if (rc_a != KS_OK || rc_b != KS_OK) {
-    if (rc_a == KS_OK) ks_regions_free(&ra);
-    if (rc_b == KS_OK) ks_regions_free(&rb);
-    const bool abort = (rc_a == KS_OK || rc_a == KS_INTERNAL_DUAL_ABORT) &&
-                       (rc_b == KS_OK || rc_b == KS_INTERNAL_DUAL_ABORT);
-    if (!abort) {
-      if (rc_a == KS_OK) set_error("%s", err_b.c_str());
-      return rc_a != KS_OK ? rc_a : rc_b;
-    }
-    KS_HIP(hipStreamSynchronize(sub->stream));
-    return scan_core(ctx, s, total, k, t, min_width, min_score, visits_dev, out, stats, mode, nullptr);
-  }
-  hipStream_t st = ctx->stream;
-  if (visits_dev) {  // the parts' streams are idle (each ended with a readback)
-    double words = 0;
-    KS_TRY(launch_count(ctx, s, total, pa.runs, k, visits_dev, &words));
-    uint32_t *vis = reinterpret_cast<uint32_t *>(visits_dev);
-    const int64_t n = (int64_t)1 << (2 * k);
-    for (const ScanPart *p : {&pa, &pb}) {
-      if (p->runs.n > 0) {
-        hipLaunchKernelGGL(k_visit_correct, dim3((unsigned)((p->runs.n + 255) / 256)), dim3(256), 0, st, p->runs.a,
-                           p->runs.b, p->runs.seq, p->runs.n, s->offsets_dev, s->seq, k, vis);
-        KS_HIP(hipGetLastError());
-      }
-      if (p->vscr) {
-        hipLaunchKernelGGL(k_add_hist, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, st,
-                           vis, p->vscr, n);
-        KS_HIP(hipGetLastError());
-      }
-    }
-    KS_HIP(hipStreamSynchronize(st));
-  }
-  // one output block, [seq_id | beg | end] int32 then [score | 0.0] doubles
-  const int64_t n = ra.n + rb.n;
-  const size_t nn = (size_t)std::max<int64_t>(n, 1);
-  const size_t ioff = (3 * nn * 4 + 7) & ~(size_t)7;
-  char *blk = static_cast<char *>(malloc(ioff + 2 * nn * 8));
-  if (!blk) {
-    ks_regions_free(&ra);
-    ks_regions_free(&rb);
-    memset(out, 0, sizeof(*out));
-    return fail(KS_ERR_NOMEM, "out of host memory for %lld regions", (long long)n);
-  }
-  out->n = n;
-  out->seq_id = reinterpret_cast<int32_t *>(blk);
-  out->beg = out->seq_id + nn;
-  out->end = out->beg + nn;
-  out->score = reinterpret_cast<double *>(blk + ioff);
-  memset(out->score, 0, 2 * nn * 8);
-  int64_t o = 0;
-  for (const ks_regions *r : {&ra, &rb}) {
-    if (r->n > 0) {
-      memcpy(out->seq_id + o, r->seq_id, r->n * 4);
-      memcpy(out->beg + o, r->beg, r->n * 4);
-      memcpy(out->end + o, r->end, r->n * 4);
-      memcpy(out->score + o, r->score, r->n * 8);
-    }
-    o += r->n;
-  }
-  ks_regions_free(&ra);
-  ks_regions_free(&rb);
-  if (stats) {
-    *stats = sa;  // phase timings: the first part's (its own stream)
-    stats->n_bases += sb.n_bases;
-    stats->n_scored += sb.n_scored;
-    stats->n_runs += sb.n_runs;
-    stats->n_regions = n;
-    stats->n_rescan += sb.n_rescan;
-    stats->n_replay += sb.n_replay;
-    // the gather pass of the call: from the first part's start of pass 1
-    // to the later end of the two (hipEvents on both contexts' streams)
-    float b8 = 0, b9 = 0, a9 = 0;
-    KS_HIP(hipEventElapsedTime(&a9, ctx->ev[8], ctx->ev[9]));
-    KS_HIP(hipEventElapsedTime(&b8, ctx->ev[8], sub->ev[8]));
-    KS_HIP(hipEventElapsedTime(&b9, ctx->ev[8], sub->ev[9]));
-    stats->ms_scan = std::max(a9, b9) - std::min(0.0f, b8);
-    stats->ms_total = now_ms() - t0;
-  }
-  return KS_OK;
 }
 
 }  // namespace ks

@@ -104,7 +104,7 @@ struct TileComp {
 
 // Values of the chunks the carry will likely replay (no summary, a predicted
 // positive entry that does not clamp for certain), gathered ahead in
-// parallel (k_replay_gather): a replay then costs one coalesced 32-B load
+// parallel (k_summ_fixw): a replay then costs one coalesced 32-B load
 // per lane instead of the dependent base / code / LUT loads of values4.
 struct ReplayBuf {
   int32_t *slot;             // [nch] slot of chunk c, -1: none
@@ -245,7 +245,7 @@ __device__ __forceinline__ void values16_nostore(const Chunks &g, const uint8_t 
   uint64_t x = 0;
   const bool pk = packed_bits(g.packed, total, p, x);
   if (pk && tv.ext && tv.ext_J >= 2 && k + tv.ext_J - 1 + 15 <= 32) {
-    // one expanded-table read per J indices (the gathers of k_summ_fix and
+    // one expanded-table read per J indices (the gathers of k_summ_fixw and
     // the heads: 4 random requests per 16 indices at J = 5 instead of 32)
     const int J = tv.ext_J, kx = k + J - 1;
     const uint64_t xmask = (kx >= 32) ? ~0ull : ((1ull << (2 * kx)) - 1ull);
@@ -333,47 +333,29 @@ __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restri
 // its chunk (q0 = start + J - 1), loaded once (5 x 16 B) instead of one 12-B
 // load per batch, so the lane's two 128-B lines are fetched once even when
 // the random table reads evict them from L2 between batches.
-#ifdef KS_P1_NO_STAGE
-constexpr bool kP1Stage = false;
-#else
 constexpr bool kP1Stage = true;
-#endif
-#ifndef KS_P1_G
-#define KS_P1_G 4
-#endif
-// G = 8 (40 indices per batch at J = 5): twice the table reads in flight per
-// lane, at 3 waves per SIMD (768-lane blocks, <= 168 VGPRs)
-constexpr int kP1G = KS_P1_G;
-#ifndef KS_P1_BLOCK
-#define KS_P1_BLOCK (KS_P1_G > 4 ? 768 : 1024)
-#endif
-constexpr int kP1Block = KS_P1_BLOCK;  // lanes per pass-1 block (build parameter for A/B runs)
+// Table reads per batch of the pipelined pass 1: 3 leaves registers for two
+// binade summaries (G = 4 spilled: 17.10 vs 14.66 ms; G = 8 at 768-lane
+// blocks: 17.7 vs 16.4 ms).  The buffer-end margins below are computed for
+// kP1G = 4 (conservative for 3).
+constexpr int kP1GSumm = 3;
+constexpr int kP1G = 4;
+constexpr int kP1Block = 1024;  // lanes per pass-1 block (512 / 256: 147 / 108 vs 163 Gbases/s)
 // Pass-1 summaries start at predicted entries of 1024 (below, exact halves
-// make most chunks' single-trajectory summaries void; k_summ_fix does those).
+// make most chunks' single-trajectory summaries void; k_summ_fixw does those).
 constexpr double kP1SumMin = 1024.0;
-// Table reads per batch of the summarising pass 1 (no code store, so no
-// 4-codes-per-word constraint): 3 leaves registers for two summaries.
-#ifndef KS_P1_GSUMM
-#define KS_P1_GSUMM 3
-#endif
-constexpr int kP1GSumm = KS_P1_GSUMM;
 // A predicted entry within this relative distance of a binade edge is
 // summarised in the neighbouring binade too.
 constexpr double kP1Margin = 0.125;
-#ifdef KS_P1_NOSTORE  // diagnostic build: no code store in k_pass1p, later passes gather (slow, exact)
-constexpr bool kP1NoStore = true;
-#else
-constexpr bool kP1NoStore = false;
-#endif
 static_assert(kP1Block % 64 == 0 && kP1Block <= 1024, "pass-1 block is whole waves");
-constexpr int kP1StageWords = kP1G > 4 ? 24 : 20;
+constexpr int kP1StageWords = 20;
 // Bases past its chunk's first scan index a pass-1 lane may read: the
 // pipelined kernel's windows reach two batches ahead (< 256 + 2 * 40 + 3 * 16)
 // and the LDS staging reads kP1StageWords words from word (start + J - 1) / 16.
 // Lanes closer than this to the buffer end are left to k_pass1 (tail_only),
 // so every packed word they stage exists (the packed array has total / 16 + 1
 // words, ks_runs.hip).
-constexpr int kP1WinReach = 4 + 255 + 2 * 5 * kP1G + 16 * (kP1G > 4 ? 5 : 3);  // J - 1 + last b0 + 2 PB + window
+constexpr int kP1WinReach = 4 + 255 + 2 * 5 * kP1G + 16 * 3;  // J - 1 + last b0 + 2 PB + window
 constexpr int kP1StageReach = 16 * kP1StageWords + 21;
 constexpr int kP1TailMargin = kP1WinReach > kP1StageReach ? (kP1WinReach > 352 ? kP1WinReach : 352)
                                                           : (kP1StageReach > 352 ? kP1StageReach : 352);
@@ -382,26 +364,9 @@ static_assert(kP1WinReach <= kP1TailMargin + 1, "pipelined windows stay inside t
 
 // ------------------------------------------------------------------- P0
 
-// Chunk start, length and run: a lane per chunk, its run by a binary search
-// over the chunk bases (KS_MAKE_CHUNKS_SEARCH: A/B against k_make_chunks).
-__global__ void k_make_chunks_search(const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase,
-                                     int64_t nruns, int k, const int64_t *__restrict__ rbnd, int extra, Chunks g) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= g.nch) return;
-  int64_t lo = 0, hi = nruns - 1;  // last run with cbase[r] <= c
-  while (lo < hi) {
-    const int64_t mid = (lo + hi + 1) >> 1;
-    if (cbase[mid] <= c) lo = mid; else hi = mid - 1;
-  }
-  const int64_t first = ra[lo] + k + (c - cbase[lo]) * CH;
-  const int64_t last = rbnd[lo] - 1 + extra;  // tr_lr: one more index (the first k-mer's own step)
-  g.start[c] = first;
-  g.n[c] = (int32_t)min((int64_t)CH, last - first + 1);
-  g.run[c] = (int32_t)lo;
-}
-
-// The same with a wave per stitch tile (64 chunks of one run), the run from
-// the tile map of k_tile_runs (in-process A/B: 17.91-18.00 vs 18.01-18.13 ms).
+// Chunk start, length and run, a wave per stitch tile (64 chunks of one run),
+// the run from the tile map of k_tile_runs (in-process A/B against a binary
+// search per chunk: 17.91-18.00 vs 18.01-18.13 ms).
 __global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase,
                               const int64_t *__restrict__ tbase, const int32_t *__restrict__ trun, int64_t ntiles,
                               int k, const int64_t *__restrict__ rbnd, int extra, Chunks g) {
@@ -422,7 +387,7 @@ __global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__r
 // d_approx, <= 128 KiB in LDS, one block per CU), rolled from the packed
 // bases; a max-plus scan of them (k_approx_scan) predicts each chunk's entry,
 // i.e. the binade pass 1 summarises in.  Only a prediction: a wrong binade
-// costs one gathered summary (k_summ_fix), never a result.
+// costs one gathered summary (k_summ_fixw), never a result.
 template <int PS>
 __global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k, const uint16_t *__restrict__ approx, int kp,
                                                   double *__restrict__ pa, double *__restrict__ pb) {
@@ -673,15 +638,14 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
 // so the wait counts stay static, and the rare paths that do load (a third
 // escape in one batch, the candidate append) drain explicitly inside the
 // branch.  Results are identical to k_pass1.
-template <int J, bool kLds, bool kTrlr, bool kSumm>
+template <int J, bool kLds, bool kTrlr>
 __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
-                                                 TableView tv, uint16_t *__restrict__ codes, EmitCfg ec,
+                                                 TableView tv, EmitCfg ec,
                                                  uint32_t *__restrict__ visits, P1 o, Cand cand,
                                                  const uint32_t *__restrict__ packed, const double *__restrict__ xh,
                                                  SummP1 sp) {
-  constexpr int G = kSumm ? kP1GSumm : kP1G;  // table reads per batch
+  constexpr int G = kP1GSumm;           // table reads per batch
   constexpr int BS = kP1Block;          // lanes per block (LDS staging stride)
-  static_assert(kSumm || (G * J) % 4 == 0, "the code store writes 4 codes per 8-B word");
   constexpr int PB = G * J;             // scan indices per batch (8, 12, 16, 20)
   constexpr bool k12 = (J == 5);        // 12-bit codes with escapes
   using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;
@@ -716,7 +680,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
   const double first_val = (kTrlr && first) ? ec.ks[(uint32_t)(gcode >> (2 * (J - 1))) & kmask] : 0.0;
   // tail lanes (reads could pass the end of the buffer) are left to k_pass1
   if (start + n + kP1TailMargin > total) {
-    if (kSumm) sp.e[2 * c] = sp.e[2 * c + 1] = INT32_MIN;  // no pass-1 summary (the workspace is reused)
+    sp.e[2 * c] = sp.e[2 * c + 1] = INT32_MIN;  // no pass-1 summary (the workspace is reused)
     return;
   }
   // Batch m rolls the 2-bit codes of bases [q0 + m*PB, q0 + m*PB + PB) in:
@@ -788,11 +752,11 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
   int beg = -1, arg = 0;
   double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
   bool special = false;
-  // kSumm: the binade-integer summary of this chunk for the binade of its
+  // The binade-integer summary of this chunk for the binade of its
   // predicted entry xh (k_predict), single trajectory: s rounded to the binade's
   // ulp u = 2^(e-52) as (s + C) - C with C = 1.5 * 2^e, exact partial sums while
   // they stay within (-2^e, 2^e); an exact half (tie: the increment would depend
-  // on the parity of the entry) or |s| >= 2^(e-1) voids it (k_summ_fix then
+  // on the parity of the entry) or |s| >= 2^(e-1) voids it (k_summ_fixw then
   // recomputes it).  Replaces the per-position code store and k_summaries.
   // (|s| < 2^(e-1) is checked once through sabs, and the minimum through the
   // FP64 prefix minimum: N is stored as a lower bound, which keeps the carry's
@@ -802,7 +766,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
   double sC2 = 0.0, sH2 = 0.0, scur2 = 0.0, smx2 = -INFINITY;
   int sarg = 0, sarg2 = 0;
   bool sbad = false, sbad2 = false;
-  if (kSumm) {
+  {
     const double x = xh[c];
     if (x >= kP1SumMin && x < 1.0e15) {
       se = binade_of(x);
@@ -862,18 +826,11 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
     }
 #pragma unroll
     for (int gi = 0; gi < G; ++gi) {
-#if defined(KS_P1_NOTABLE)  // diagnostic build only: no table traffic (wrong values, no escapes)
-      en[gi] = (EW)(gn[gi] & (GC)0x7ff7ff7ff7ff7ffull);
-#elif defined(KS_P1_NT)
-      en[gi] = __builtin_nontemporal_load(ext + ((b0 + PB + gi * J < n) ? gn[gi] : (GC)0));
-#else
       en[gi] = ext[(b0 + PB + gi * J < n) ? gn[gi] : (GC)0];
-#endif
     }
     // 3. window of batch b+2
     win = window((q0 + b0 + 2 * PB) >> 4);
-    // 4. batch b group by group: values, packed codes, trajectory
-    uint32_t cw[PB / 2];
+    // 4. batch b group by group: values, trajectory
 #pragma unroll
     for (int gi = 0; gi < G; ++gi) {
 #pragma unroll
@@ -898,10 +855,6 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
           qq = (uint32_t)(e[gi] >> (16 * t)) & 0xffffu;
           s = kLds ? s_lut[qq] : tv.lut[qq];
         }
-        if (!kSumm) {
-          if (j & 1) cw[j >> 1] |= qq << 16;
-          else cw[j >> 1] = qq;
-        }
         if (kTrlr && first && b0 == 0 && j == 0) s = first_val;
         const int i = b0 + j;
         if (i < n) {
@@ -913,7 +866,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
           pmax = asum > pmax ? asum : pmax;
           sabs += fabs(s);
           special |= !isfinite(s);
-          if (kSumm && se != INT32_MIN) {
+          if (se != INT32_MIN) {
             const double r = (s + sC) - sC;
             sbad |= fabs(r - s) == sH;
             scur += r;
@@ -966,21 +919,12 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
       }
     }
 #pragma unroll
-    for (int r4 = 0; r4 < PB / 4; ++r4)
-      if (b0 + 4 * r4 < CH && !kP1NoStore && !kSumm)
-#ifndef KS_P1_PLAIN_CODES  // nontemporal code stores: A/B 16.19-16.21 vs 16.31-16.57 ms
-        __builtin_nontemporal_store((uint64_t)cw[2 * r4] | ((uint64_t)cw[2 * r4 + 1] << 32),
-                                    reinterpret_cast<uint64_t *>(codes + code_slot(c, b0 + 4 * r4)));
-#else
-        *reinterpret_cast<uint2 *>(codes + code_slot(c, b0 + 4 * r4)) = make_uint2(cw[2 * r4], cw[2 * r4 + 1]);
-#endif
-#pragma unroll
     for (int gi = 0; gi < G; ++gi) {
       gc[gi] = gn[gi];
       e[gi] = en[gi];
     }
   }
-  if (kSumm) {
+  {
     // valid if no tie, every |s| < 2^(e-1) (so (s + C) - C rounds s to the ulp
     // 2^(e-52)) and every partial sum inside (-2^e, 2^e) (all exact).  N is a
     // lower bound of the integer trajectory's minimum: each rounded step is
@@ -1616,9 +1560,9 @@ __global__ void __launch_bounds__(1024) k_summaries(Chunks g, const uint8_t *__r
 // Pass-1 summaries (kSumm): the summary of every chunk whose exact carry will
 // want one (same test as k_summaries) is the pass-1 one when pass 1 predicted
 // this binade; the others (no or another prediction, a tie, the tail chunks)
-// are listed for k_summ_fix.
-// The per-chunk part of k_summ_select: the selected summary (or none) of
-// chunk c; want: list it for k_summ_fix; rwant: list it for the replay
+// are listed for k_summ_fixw.
+// The per-chunk part of the selection: the selected summary (or none) of
+// chunk c; want: list it for k_summ_fixw; rwant: list it for the replay
 // prefetch.
 __device__ __forceinline__ void select_one(const Chunks &g, const P1 &o, const double *__restrict__ xt,
                                            const SummP1 &sp, const Summ &sm, const double *__restrict__ xh,
@@ -1685,22 +1629,11 @@ __device__ __forceinline__ void select_append(bool want, bool rwant, int64_t c, 
   }
 }
 
-__global__ void __launch_bounds__(256) k_summ_select(Chunks g, P1 o, const double *__restrict__ xt, SummP1 sp,
-                                                     Summ sm, int64_t *__restrict__ fix,
-                                                     unsigned long long *__restrict__ nfix,
-                                                     const double *__restrict__ xh,
-                                                     unsigned long long *__restrict__ why, ReplayBuf rp, int hi) {
-  const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool want = false, rwant = false;
-  if (c < g.nch) select_one(g, o, xt, sp, sm, xh, why, rp, c, want, rwant);
-  select_append(want, rwant, c, fix, nfix, rp, hi);
-}
-
 __global__ void k_copy_u64(const unsigned long long *__restrict__ src, unsigned long long *__restrict__ dst, int n) {
   for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
 
-// k_seg_marks and k_summ_select in one pass (a wave per 64-chunk window from
+// k_seg_marks and the summary selection in one pass (a wave per 64-chunk window from
 // the one holding c0 - 1): the window's segment marks, then the summaries.
 __global__ void __launch_bounds__(256) k_marks_select(Chunks g, P1 o, const double *__restrict__ xt,
                                                       uint8_t *__restrict__ flag, int64_t nw, SummP1 sp, Summ sm,
@@ -1728,61 +1661,6 @@ __global__ void __launch_bounds__(256) k_marks_select(Chunks g, P1 o, const doub
   select_append(want, rwant, e, fix, nfix, rp, hi);
 }
 
-// Summaries of the listed chunks from gathered values (their codes were not
-// stored): lane per listed chunk, persistent grid, count read on the device.
-template <bool kLds>
-__global__ void __launch_bounds__(256) k_summ_fix(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
-                                                  TableView tv, const double *__restrict__ xt,
-                                                  const int64_t *__restrict__ fix,
-                                                  const unsigned long long *__restrict__ nfix, Summ sm) {
-  __shared__ double s_lut[kLds ? kLdsLutMax : 1];
-  if (kLds) {
-    for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
-    __syncthreads();
-  }
-  const int64_t nf = (int64_t)*nfix;
-  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < nf; f += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t c = fix[f];
-    const double x = xt[c];
-    const int e = (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
-    long long D[2], M[2], N[2];
-    int A[2];
-    if (!chunk_summary<true, kLds>(g, seq, total, k, tv, nullptr, c, e, D, M, A, N, s_lut)) continue;
-    sm.e[c] = e;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      sm.D[2 * c + t] = D[t];
-      sm.M[2 * c + t] = M[t];
-      sm.N[2 * c + t] = N[t];
-      sm.A[2 * c + t] = A[t];
-    }
-  }
-}
-
-// Values of the listed likely replays (k_summ_select): a wave per chunk,
-// 4 values per lane through the expanded table, stored lane-major.
-template <bool kLds>
-__global__ void __launch_bounds__(256) k_replay_gather(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
-                                                       int k, TableView tv, ReplayBuf rp, int hi) {
-  __shared__ double s_lut[kLds ? kLdsLutMax : 1];
-  if (kLds) {
-    for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
-    __syncthreads();
-  }
-  const int lane = threadIdx.x & 63;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t nl = min((int64_t)rp.count[hi], rp.cap);
-  for (int64_t w = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); w < nl; w += nw) {
-    const int64_t sl = hi * rp.cap + w;
-    const int64_t c = rp.chunk[sl];
-    double v[4];
-    values16_nostore<4>(g, seq, total, k, tv, c, 4 * lane, g.n[c], v, kLds ? s_lut : nullptr);
-    double2 *d = reinterpret_cast<double2 *>(rp.v + sl * 256 + 4 * lane);
-    d[0] = make_double2(v[0], v[1]);
-    d[1] = make_double2(v[2], v[3]);
-  }
-}
-
 // Parity map of a run of steps: entry parity p -> the increment d_p of the
 // integer trajectory (exact halves round to even, so a step's increment
 // depends on the accumulator's parity).  Composition is associative.
@@ -1793,7 +1671,7 @@ __device__ __forceinline__ PMap pm_compose(const PMap &a, const PMap &b) {  // a
   return PMap{a.d0 + ((a.d0 & 1) ? b.d1 : b.d0), a.d1 + (((1 + a.d1) & 1) ? b.d1 : b.d0)};
 }
 
-// k_summ_fix with one wave per listed chunk (4 indices per lane): the values
+// Summaries of the listed chunks, one wave per listed chunk (4 indices per lane): the values
 // through the expanded table in one or two round trips, the binade-integer
 // increments as parity maps, a wave scan of the maps, and wave reductions
 // for the total, first maximum and minimum of both entry parities -- the
@@ -1812,7 +1690,7 @@ __global__ void __launch_bounds__(256) k_summ_fixw(Chunks g, const uint8_t *__re
   const int lane = threadIdx.x & 63;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int64_t nf = (int64_t)*nfix;
-  // the waves past the fix list gather the listed likely replays (k_replay_gather's work)
+  // the waves past the fix list gather the listed likely replays
   const int64_t nr = rp.slot ? min((int64_t)rp.count[hi], rp.cap) : 0;
   for (int64_t f = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); f < nf + nr; f += nw) {
     if (f >= nf) {
@@ -2172,7 +2050,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
   double x = (c0 > 0 && g.run[c0] == g.run[c0 - 1]) ? o.cexit[c0 - 1] : 0.0;
   unsigned long long replays = 0;
   const long long t_start = dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
-  long long n_l = 0, n_r = 0, n_uq = 0, n_up = 0, n_par = 0;  // diagnostics: replays that clamp, replayed indices
+  long long n_l = 0, n_r = 0, n_par = 0;  // diagnostics: replays that clamp, replayed indices
   // per-lane inputs of one 64-chunk tile; the next tile's are loaded before
   // the current one is processed (all loads independent: hides their latency
   // behind the tile's scan)
@@ -2377,7 +2255,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
         const int n = rl32(l_n, j);
         double v[4];
         const int rsj = rl32(cur.rs, j);
-        if (rsj >= 0) {  // gathered ahead (k_replay_gather)
+        if (rsj >= 0) {  // gathered ahead (k_summ_fixw)
           const double2 *d = reinterpret_cast<const double2 *>(rp.v + (int64_t)rsj * 256 + 4 * lane);
           const double2 a = d[0], b = d[1];
           v[0] = a.x;
@@ -2410,8 +2288,6 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
           my_harg = harg;
         }
         x = hq >= 0 ? cj_exit : T;
-        n_uq += hq >= 0;
-        n_up += hq >= 0 ? hq + 1 : n;
         if (dbg) t_rep += (long long)__builtin_amdgcn_s_memtime() - tr0;
       }
       if (lane == j) my_mode = mode;
@@ -2449,7 +2325,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
 }
 
 // Tile composites (TileComp) of the global tiles of chunks [g.c0, g.nch):
-// one wave per tile, from the final summaries (after k_summ_fix).  Also
+// one wave per tile, from the final summaries (after k_summ_fixw).  Also
 // clears the batch marks (ee) of the range.
 __global__ void __launch_bounds__(256) k_tile_comp(Chunks g, Summ sm, TileComp tc) {
   const int lane = threadIdx.x & 63;
@@ -3060,7 +2936,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const size_t o_gtd = off; off += al(ngt * 8 * 6);
   const size_t o_gtm = off; off += al(ngt * 8);
   const size_t o_gtee = off; off += al(ngt * 4);
-  // likely-replay prefetch (k_summ_select lists, k_replay_gather fills)
+  // likely-replay prefetch (k_marks_select lists, k_summ_fixw fills)
   const int64_t rcap_h = std::max<int64_t>(65536, nch / 128);  // slots per half
   const size_t o_rslot = off; off += al(nch * 4);
   const size_t o_rchunk = off; off += al(2 * rcap_h * 8);
@@ -3092,9 +2968,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const XTiles xagg = xtiles(W + o_xagg), xtin = xtiles(W + o_xagg + al(ntiles * 32));
   double2 *d_tagg = reinterpret_cast<double2 *>(W + o_tagg);
   int32_t *d_trun_map = reinterpret_cast<int32_t *>(W + o_trun);
-  int32_t *d_trun = getenv("KS_TILE_SEARCH") ? nullptr : d_trun_map;
-  // carry tile batches (KS_NO_TILE_BATCH: A/B, the per-tile walk only)
-  const bool tile_batch = getenv("KS_NO_TILE_BATCH") == nullptr;
+  int32_t *d_trun = d_trun_map;
   long long *gtd = reinterpret_cast<long long *>(W + o_gtd);
   const TileComp tcomp{reinterpret_cast<int32_t *>(W + o_gte), gtd, gtd + 2 * ngt, gtd + 4 * ngt,
                        reinterpret_cast<long long *>(W + o_gtm), reinterpret_cast<int32_t *>(W + o_gtee)};
@@ -3102,15 +2976,14 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                 reinterpret_cast<double *>(W + o_rval), reinterpret_cast<unsigned long long *>(W + o_rcnt), rcap_h};
   double *d_tin = reinterpret_cast<double *>(W + o_tin);
   // approximate max-plus scan of (sum, clean exit) over runs [r0, r1) (tiles
-  // [t0, t1)): three parallel kernels, or the one-wave-per-run k_approx_scan
-  // with KS_SERIAL_ASCAN
-  static const bool serial_ascan = getenv("KS_SERIAL_ASCAN") != nullptr;
-  // waves per block of the wave-per-tile / wave-per-window kernels (KS_WPB: A/B)
-  const int wpb = getenv("KS_WPB") ? std::max(1, std::min(4, atoi(getenv("KS_WPB")))) : 2;
+  // [t0, t1)): three parallel kernels (the one-wave-per-run k_approx_scan when
+  // the range has no tile)
+  // waves per block of the wave-per-tile / wave-per-window kernels (A/B: 2 of 1-4)
+  constexpr int wpb = 2;
   auto ascan = [&](const P1 &o, double *out, int64_t r0, int64_t r1, int64_t t0, int64_t t1,
                    hipStream_t strm) -> ks_status {
     if (r1 <= r0) return KS_OK;
-    if (serial_ascan || t1 <= t0) {
+    if (t1 <= t0) {
       hipLaunchKernelGGL(k_approx_scan, dim3((unsigned)(r1 - r0)), dim3(64), 0, strm, d_cbase, r1, o, out, r0);
       KS_HIP(hipGetLastError());
       return KS_OK;
@@ -3134,15 +3007,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // [2 kSegs + 2h] replays, [2 kSegs + 2h + 1] error bits (u32) of half h
   KS_HIP(hipMemsetAsync(cnts, 0, 8 * (2 * kSegs + 8), st));
   unsigned long long *d_replays = cnts + 2 * kSegs;
-  unsigned int *d_err = reinterpret_cast<unsigned int *>(cnts + 2 * kSegs + 1);
 
-  uint16_t *codes = nullptr;
-  if (comp) {
-    void *cp = nullptr;
-    const int64_t ctiles = (nch + 63) / 64;  // code store tiles (global chunk index / 64)
-    KS_TRY(ensure(ctx, SLOT_CHUNK_B, (size_t)ctiles * 64 * CH * 2, &cp));
-    codes = static_cast<uint16_t *>(cp);
-  }
   int64_t ccap = std::max<int64_t>(1 << 16, nch / 4);
   const size_t cand_bytes = ctx->slots[SLOT_CHUNK_C].bytes;  // use what the grow-only slot holds
   if (cand_bytes > 1024 && (cand_bytes - 1024) / 40 > (size_t)ccap) ccap = (int64_t)((cand_bytes - 1024) / 40);
@@ -3176,26 +3041,30 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     hipLaunchKernelGGL(k_tile_runs, dim3((unsigned)nruns), dim3(256), 0, st, d_tbase, nruns, d_trun_map);
     KS_HIP(hipGetLastError());
   }
-  if (getenv("KS_MAKE_CHUNKS_SEARCH") == nullptr) {
-    if (ntiles > 0)
-      hipLaunchKernelGGL(k_make_chunks, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, st, runs.a, d_cbase, d_tbase,
-                         d_trun_map, ntiles, k, runs.b, mode.trlr, g);
-  } else {
-    hipLaunchKernelGGL(k_make_chunks_search, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, st, runs.a, d_cbase,
-                       nruns, k, runs.b, mode.trlr, g);
-  }
+  if (ntiles > 0)
+    hipLaunchKernelGGL(k_make_chunks, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, st, runs.a, d_cbase, d_tbase,
+                       d_trun_map, ntiles, k, runs.b, mode.trlr, g);
   KS_HIP(hipGetLastError());
   const unsigned gch = (unsigned)((nch + 255) / 256);
   const unsigned gch1k = (unsigned)((nch + 1023) / 1024);
   const int Jt = (tv.ext != nullptr) ? tv.ext_J : 1;
   const bool lds_table = k <= kLdsTableK && runs.packed != nullptr && getenv("KS_NO_LDS_TABLE") == nullptr;
-  // pass-1 summaries (no per-position code store): compressed tables on the
-  // pipelined pass with a binade predictor; KS_NO_P1_SUMMARY: the code store
-  const bool p1summ = comp && Jt >= 2 && !lds_table && runs.packed != nullptr && tv.approx != nullptr &&
-                      !kP1NoStore && getenv("KS_NO_P1_SUMMARY") == nullptr &&
-                      getenv("KS_NO_PIPELINED_P1") == nullptr;
-  // (KS_NO_REPLAY_PREFETCH: A/B; the carry reads no slots unless k_summ_select wrote them)
-  if (!p1summ || getenv("KS_NO_REPLAY_PREFETCH") != nullptr) rpb.slot = nullptr;
+  // pass-1 summaries (no per-position code store): compressed expanded
+  // tables on the pipelined pass with a binade predictor (a table without
+  // one, a failed allocation of the predictor, is scanned unexpanded)
+  const bool p1summ = comp && Jt >= 2 && !lds_table && runs.packed != nullptr && tv.approx != nullptr;
+  // (the carry reads no replay slots unless k_marks_select wrote them)
+  if (!p1summ) rpb.slot = nullptr;
+  // per-index code store (uint16 per scan index, 2 B x 256 per chunk):
+  // written by the compressed unexpanded pass 1 (k_pass1<1, ...>) for the
+  // binade summaries (k_summaries)
+  uint16_t *codes = nullptr;
+  if (comp && !p1summ && !lds_table) {
+    void *cp = nullptr;
+    const int64_t ctiles = (nch + 63) / 64;  // code store tiles (global chunk index / 64)
+    KS_TRY(ensure(ctx, SLOT_CHUNK_B, (size_t)ctiles * 64 * CH * 2, &cp));
+    codes = static_cast<uint16_t *>(cp);
+  }
   // Two halves of the runs (pass-1-summary path): the second half's pass 1
   // (side stream) runs while the first half's latency-bound later passes
   // (carry, stitch) run on the main stream; halves split at a run boundary,
@@ -3205,7 +3074,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   };
   const int64_t ctail_all = nch > 1024 ? nch - 1024 : 0;
   const bool split = p1summ && lay.split_r > 0 && lay.split_r < nruns && lay.split_c >= 1024 &&
-                     lay.split_c + 1024 <= ctail_all && getenv("KS_NO_SPLIT") == nullptr;
+                     lay.split_c + 1024 <= ctail_all;
   Half halves[2];
   int nhalf = 1;
   halves[0] = Half{0, nch, 0, nruns, 0, ntiles};
@@ -3231,16 +3100,9 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipMemsetAsync(W + o_pz + h.c0, 0, (size_t)(h.c1 - h.c0), strm));
       const unsigned gl =
           (unsigned)std::max<int64_t>(1, std::min<int64_t>((h.c1 - h.c0 + 1023) / 1024, ctx->num_cus));
-      const int ps = getenv("KS_PRED_PS") ? atoi(getenv("KS_PRED_PS")) : 2;
-      if (ps == 4)
-        hipLaunchKernelGGL(k_predict<4>, dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx, tv.approx_k,
-                           pp.asum, pp.cexit);
-      else if (ps == 8)
-        hipLaunchKernelGGL(k_predict<8>, dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx, tv.approx_k,
-                           pp.asum, pp.cexit);
-      else
-        hipLaunchKernelGGL(k_predict<2>, dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx, tv.approx_k,
-                           pp.asum, pp.cexit);
+      // every second index sampled (A/B: every 4th / 8th changed nothing)
+      hipLaunchKernelGGL(k_predict<2>, dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx, tv.approx_k,
+                         pp.asum, pp.cexit);
       KS_HIP(hipGetLastError());
       return ascan(pp, d_xh, h.r0, h.r1, h.t0, h.t1, strm);
     };
@@ -3248,18 +3110,15 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     // the predictor holds whole CUs: 128 KiB of LDS per block), then the
     // second half's on the side stream, under the first half's pass 1
     KS_TRY(predict(halves[0], st));
-    if (split) {  // KS_NO_P0_OVERLAP (A/B): both halves' predictors on the main stream
-      const bool ov = getenv("KS_NO_P0_OVERLAP") == nullptr;
-      side_forked = ov;
-      if (ov) {
-        KS_HIP(hipEventRecord(ctx->ev[16], st));
-        KS_HIP(hipStreamWaitEvent(ctx->side, ctx->ev[16], 0));
-      }
-      KS_TRY(predict(halves[1], ov ? ctx->side : st));
+    if (split) {
+      side_forked = true;
+      KS_HIP(hipEventRecord(ctx->ev[16], st));
+      KS_HIP(hipStreamWaitEvent(ctx->side, ctx->ev[16], 0));
+      KS_TRY(predict(halves[1], ctx->side));
     }
   }
   KS_HIP(hipEventRecord(ctx->ev[8], st));
-  const bool lds_lut = comp && tv.nlut <= kLdsLutMax && getenv("KS_NO_LDS_LUT") == nullptr;
+  const bool lds_lut = comp && tv.nlut <= kLdsLutMax;
 #define KS_P1(J, C, L)                                                                                       \
   hipLaunchKernelGGL((k_pass1<J, C, L>), dim3(J == 1 ? gch : gch1k), dim3(J == 1 ? 256 : 1024), 0, st, g, s->seq, \
                      total, k, tv, codes, ec, visits, p1, cand, (int64_t)0, 0)
@@ -3271,23 +3130,17 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
 #define KS_P1TC(J, C, L)                                                                                       \
   hipLaunchKernelGGL((k_pass1<J, C, L>), dim3((unsigned)((nch - ctail + 1023) / 1024)), dim3(1024), 0, side, g, \
                      s->seq, total, k, tv, p1summ ? nullptr : codes, ec, visits, p1, cand, ctail, 1)
-  const int J = (tv.ext != nullptr) ? tv.ext_J : 1;
-  const bool pipelined = getenv("KS_NO_PIPELINED_P1") == nullptr && runs.packed != nullptr;
-  const unsigned gp1 = (unsigned)((nch + kP1Block - 1) / kP1Block);
+  // compressed tables are scanned expanded only on the summarising pass
+  const int J = (tv.ext != nullptr && (p1summ || !comp)) ? tv.ext_J : 1;
+  const bool pipelined = runs.packed != nullptr;
 #define KS_P1P(J, L, GV, GRID, STRM)                                                                           \
   do {                                                                                                       \
-    if (ec.trlr && p1summ)                                                                                   \
-      hipLaunchKernelGGL((k_pass1p<J, L, true, true>), dim3(GRID), dim3(kP1Block), 0, STRM, GV, s->seq, total, k, \
-                         tv, codes, ec, visits, p1, cand, runs.packed, d_xh, sp1);                           \
-    else if (ec.trlr)                                                                                        \
-      hipLaunchKernelGGL((k_pass1p<J, L, true, false>), dim3(GRID), dim3(kP1Block), 0, STRM, GV, s->seq, total, k, \
-                         tv, codes, ec, visits, p1, cand, runs.packed, d_xh, sp1);                           \
-    else if (p1summ)                                                                                         \
-      hipLaunchKernelGGL((k_pass1p<J, L, false, true>), dim3(GRID), dim3(kP1Block), 0, STRM, GV, s->seq, total, k, \
-                         tv, codes, ec, visits, p1, cand, runs.packed, d_xh, sp1);                           \
+    if (ec.trlr)                                                                                             \
+      hipLaunchKernelGGL((k_pass1p<J, L, true>), dim3(GRID), dim3(kP1Block), 0, STRM, GV, s->seq, total, k, tv, \
+                         ec, visits, p1, cand, runs.packed, d_xh, sp1);                                      \
     else                                                                                                     \
-      hipLaunchKernelGGL((k_pass1p<J, L, false, false>), dim3(GRID), dim3(kP1Block), 0, STRM, GV, s->seq, total, k, \
-                         tv, codes, ec, visits, p1, cand, runs.packed, d_xh, sp1);                           \
+      hipLaunchKernelGGL((k_pass1p<J, L, false>), dim3(GRID), dim3(kP1Block), 0, STRM, GV, s->seq, total, k, tv, \
+                         ec, visits, p1, cand, runs.packed, d_xh, sp1);                                      \
   } while (0)
   if (lds_table) {
     // small k: the whole table in LDS, persistent blocks (one per CU), no code store
@@ -3295,7 +3148,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     if (ec.trlr) hipLaunchKernelGGL(k_pass1_lds<true>, dim3(gl), dim3(1024), 0, st, g, total, k, tv, ec, visits, p1, cand);
     else hipLaunchKernelGGL(k_pass1_lds<false>, dim3(gl), dim3(1024), 0, st, g, total, k, tv, ec, visits, p1, cand);
     codes = nullptr;
-  } else if (comp && J >= 2 && pipelined) {
+  } else if (p1summ) {
     // the tail chunks (a latency-bound serial walk each) run on the side
     // stream, overlapped with the pipelined pass (of the last half)
     hipStream_t side = ctx->side;
@@ -3316,22 +3169,14 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       // second half on the (lowest-priority) side stream at once: the second
       // half's blocks fill the CUs the first half leaves, its drain included,
       // and the first half ends first (its carry and stitch then run under
-      // the rest of the second half).  KS_P1_SERIAL_HALVES (A/B): the side
-      // stream waits for the first half (pass 1 end = ev[9] on side).
-      if (getenv("KS_P1_SERIAL_HALVES") == nullptr) {
-        KS_HIP(hipEventRecord(ctx->ev[17], st));
-        KS_HIP(hipStreamWaitEvent(ctx->hi, ctx->ev[17], 0));
-        if (!side_forked) KS_HIP(hipStreamWaitEvent(side, ctx->ev[17], 0));
-        p1p(halves[0], ctx->hi);
-        KS_HIP(hipGetLastError());
-        KS_HIP(hipEventRecord(ctx->ev[12], ctx->hi));
-        KS_HIP(hipStreamWaitEvent(st, ctx->ev[12], 0));
-      } else {
-        p1p(halves[0], st);
-        KS_HIP(hipGetLastError());
-        KS_HIP(hipEventRecord(ctx->ev[12], st));
-        KS_HIP(hipStreamWaitEvent(side, ctx->ev[12], 0));
-      }
+      // the rest of the second half; serial halves cost 0.6 ms in-process).
+      KS_HIP(hipEventRecord(ctx->ev[17], st));
+      KS_HIP(hipStreamWaitEvent(ctx->hi, ctx->ev[17], 0));
+      if (!side_forked) KS_HIP(hipStreamWaitEvent(side, ctx->ev[17], 0));
+      p1p(halves[0], ctx->hi);
+      KS_HIP(hipGetLastError());
+      KS_HIP(hipEventRecord(ctx->ev[12], ctx->hi));
+      KS_HIP(hipStreamWaitEvent(st, ctx->ev[12], 0));
       if (tail) {
         if (J == 5) KS_P1T(5, false);
         else if (lds_lut) { if (J == 4) KS_P1T(4, true); else if (J == 3) KS_P1T(3, true); else KS_P1T(2, true); }
@@ -3354,8 +3199,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipGetLastError());
       if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
     }
-    if (kP1NoStore || p1summ) codes = nullptr;  // no code store: later passes gather their values
-  } else if (!comp && J >= 2 && J <= 4 && pipelined) {
+  } else if (!comp && J >= 2 && J <= 4 && pipelined) {  // FP64 expanded table (weighted rank)
     hipStream_t side = ctx->side;
     const bool tail = nch > ctail;
     if (tail) {
@@ -3376,21 +3220,17 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
 #undef KS_P1PF
     KS_HIP(hipGetLastError());
     if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
-  } else if (comp && J == 5) {
-    KS_P1(5, true, false);  // 12-bit codes: value LUT of the short codes in LDS
-  } else if (comp && lds_lut) {
-    if (J == 4) KS_P1(4, true, true); else if (J == 3) KS_P1(3, true, true); else if (J == 2) KS_P1(2, true, true); else KS_P1(1, true, false);
   } else if (comp) {
-    if (J == 4) KS_P1(4, true, false); else if (J == 3) KS_P1(3, true, false); else if (J == 2) KS_P1(2, true, false); else KS_P1(1, true, false);
+    KS_P1(1, true, false);  // unexpanded compressed table (with the code store)
   } else {
-    if (J == 4) KS_P1(4, false, false); else if (J == 3) KS_P1(3, false, false); else if (J == 2) KS_P1(2, false, false); else KS_P1(1, false, false);
+    KS_P1(1, false, false);  // (expanded FP64 tables take k_pass1pf above)
   }
 #undef KS_P1
 #undef KS_P1T
 #undef KS_P1TC
 #undef KS_P1P
   KS_HIP(hipGetLastError());
-  if (split && getenv("KS_P1_SERIAL_HALVES") == nullptr) {
+  if (split) {
     // end of pass 1 = the later of the halves: the hi stream (idle now) joins the side stream's
     KS_HIP(hipEventRecord(ctx->ev[18], ctx->side));
     KS_HIP(hipStreamWaitEvent(ctx->hi, ctx->ev[18], 0));
@@ -3416,9 +3256,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     const int64_t wl = (h.c0 > 0 ? h.c0 - 1 : 0) / 64;
     const int64_t nwm = (h.c1 + 63) / 64 - wl;
     // segment marks and summary selection in one pass over the chunks
-    // (KS_NO_FUSED_SELECT: k_seg_marks then k_summ_select, A/B)
-    const bool fused = p1summ && getenv("KS_NO_FUSED_SELECT") == nullptr;
-    if (!fused) {
+    if (!p1summ) {
       hipLaunchKernelGGL(k_seg_marks, dim3((unsigned)((nwm + wpb - 1) / wpb)), dim3(64 * wpb), 0, strm, gv, p1, xt,
                          d_flag, nwm);
       KS_HIP(hipGetLastError());
@@ -3426,41 +3264,17 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     if (p1summ) {
       KS_HIP(hipMemsetAsync(d_nfix + hi, 0, 8, strm));
       KS_HIP(hipMemsetAsync(rpb.count + hi, 0, 8, strm));
-      if (fused)
-        hipLaunchKernelGGL(k_marks_select, dim3((unsigned)((nwm + 3) / 4)), dim3(256), 0, strm, gv, p1, xt, d_flag,
-                           nwm, sp1, sm, d_fix + h.c0, d_nfix + hi, d_xh,
-                           dbg ? reinterpret_cast<unsigned long long *>(dbg + nwin * 9) : nullptr, rpb, hi);
-      else
-        hipLaunchKernelGGL(k_summ_select, dim3(gch_h), dim3(256), 0, strm, gv, p1, xt, sp1, sm, d_fix + h.c0,
-                           d_nfix + hi, d_xh, dbg ? reinterpret_cast<unsigned long long *>(dbg + nwin * 9) : nullptr,
-                           rpb, hi);
+      hipLaunchKernelGGL(k_marks_select, dim3((unsigned)((nwm + 3) / 4)), dim3(256), 0, strm, gv, p1, xt, d_flag, nwm,
+                         sp1, sm, d_fix + h.c0, d_nfix + hi, d_xh,
+                         dbg ? reinterpret_cast<unsigned long long *>(dbg + nwin * 9) : nullptr, rpb, hi);
       KS_HIP(hipGetLastError());
-      const unsigned gf = (unsigned)std::max<int64_t>(1, std::min<int64_t>(gch_h, (int64_t)ctx->num_cus * 8));
-      static const bool fix_serial = getenv("KS_FIX_SERIAL") != nullptr;  // A/B: lane-serial summaries
-      if (fix_serial) {
-        if (lds_lut)
-          hipLaunchKernelGGL(k_summ_fix<true>, dim3(gf), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
-                             d_fix + h.c0, d_nfix + hi, sm);
-        else
-          hipLaunchKernelGGL(k_summ_fix<false>, dim3(gf), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
-                             d_fix + h.c0, d_nfix + hi, sm);
-      } else {
-        // LUT reads through L2, not staged in LDS: a 54 KB LDS copy per block
-        // (2048 blocks, most without a listed chunk) cost more than the ~4 M
-        // lookups of the ~16 K listed chunks (KS_FIXW_LDS: A/B)
-        const unsigned gw = (unsigned)std::max<int64_t>(1, (int64_t)ctx->num_cus * 8);
-        if (lds_lut && getenv("KS_FIXW_LDS") != nullptr)
-          hipLaunchKernelGGL(k_summ_fixw<true>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
-                             d_fix + h.c0, d_nfix + hi, sm, rpb, hi);
-        else
-          hipLaunchKernelGGL(k_summ_fixw<false>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
-                             d_fix + h.c0, d_nfix + hi, sm, rpb, hi);
-      }
-      if (rpb.slot && fix_serial) {  // (k_summ_fixw gathers them otherwise)
-        const unsigned gw = (unsigned)std::max<int64_t>(1, (int64_t)ctx->num_cus * 8);
-        hipLaunchKernelGGL(k_replay_gather<false>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, rpb, hi);
-        KS_HIP(hipGetLastError());
-      }
+      // summaries of the listed chunks, a wave each; the LUT read through L2,
+      // not staged in LDS: a 54 KB LDS copy per block (2048 blocks, most
+      // without a listed chunk) cost more than the ~4 M lookups of the ~16 K
+      // listed chunks
+      const unsigned gw = (unsigned)std::max<int64_t>(1, (int64_t)ctx->num_cus * 8);
+      hipLaunchKernelGGL(k_summ_fixw<false>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
+                         d_fix + h.c0, d_nfix + hi, sm, rpb, hi);
     } else if (lds_lut)
       hipLaunchKernelGGL((k_summaries<true, true>), dim3(gch1k), dim3(1024), 0, strm, g, s->seq, total, k, tv, codes,
                          p1, xt, sm);
@@ -3476,9 +3290,9 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     // ---- P3 carry by segments + P4 heads; then the gated per-run fallback
     const int64_t wc = h.c0 / 64;
     const unsigned nwc = (unsigned)((h.c1 - 1) / 64 - wc + 1);
-    const TileComp tch = tile_batch ? tcomp : TileComp{};
+    const TileComp tch = tcomp;
     const unsigned gtc = (unsigned)(((h.c1 - 1) / 64 - wc + 1 + 3) / 4);  // 4 tiles per block
-    if (tile_batch) {
+    {
       hipLaunchKernelGGL(k_tile_comp, dim3(gtc), dim3(256), 0, strm, gv, sm, tch);
       KS_HIP(hipGetLastError());
     }
@@ -3489,7 +3303,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       hipLaunchKernelGGL(k_carry_win<false>, dim3((nwc + wpb - 1) / wpb), dim3(64 * wpb), 0, strm, gv, d_flag, s->seq, total, k, tv, codes,
                          p1, sm, cr, tch, rpb, rep_h, err_h, dbg);
     KS_HIP(hipGetLastError());
-    if (tile_batch) {
+    {
       hipLaunchKernelGGL(k_tile_apply, dim3(gtc), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 0);
       KS_HIP(hipGetLastError());
     }
@@ -3514,7 +3328,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       else
         hipLaunchKernelGGL(k_carry_run<false>, dim3((unsigned)nr), dim3(64), 0, strm, gv, d_cbase, h.r1, s->seq,
                            total, k, tv, codes, p1, sm, cr, tch, rpb, rep_h, err_h, nullptr, h.r0);
-      if (tile_batch) hipLaunchKernelGGL(k_tile_apply, dim3(gtc), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 1);
+      hipLaunchKernelGGL(k_tile_apply, dim3(gtc), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 1);
     }
     heads(1);
     KS_HIP(hipGetLastError());

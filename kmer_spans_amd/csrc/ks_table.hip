@@ -543,31 +543,20 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   KS_HIP(hipEventCreate(&b));
   KS_HIP(hipEventRecord(a, st));
   const unsigned grid = (unsigned)std::min<uint64_t>((nent + 255) / 256, (uint64_t)ctx->num_cus * 32);
+  // builds with several entries' code loads ahead of their (nontemporal)
+  // stores per trip: 12-bit 8 pairs 27.06 vs 28.2 (4), 29.3 (1) ms, plain
+  // stores 36.8; FP64 8 halves 28.9 vs 34.2 ms (profiles/r2/s3/ab_ext_build_*)
   if (u16 && bits == 12) {
-    if (getenv("KS_EXT_U1"))
-      hipLaunchKernelGGL(k_build_ext_c12<1>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
-    else if (getenv("KS_EXT_U4"))
-      hipLaunchKernelGGL(k_build_ext_c12<4>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
-    else if (getenv("KS_EXT_U16"))
-      hipLaunchKernelGGL(k_build_ext_c12<16>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
-    else if (getenv("KS_EXT_PLAIN"))
-      hipLaunchKernelGGL((k_build_ext_c12<8, false>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent,
-                         (uint64_t *)ext);
-    else  // 8 pairs per trip: 27.06 vs 28.2 (4), 29.3 (1) ms, plain stores 36.8 (profiles/r2/s3/ab_ext_build_*)
-      hipLaunchKernelGGL(k_build_ext_c12<8>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
+    hipLaunchKernelGGL(k_build_ext_c12<8>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
   } else if (u16) {
-    if (J == 4 && getenv("KS_EXT_U1") == nullptr)
+    if (J == 4)
       hipLaunchKernelGGL((k_build_ext_u16<4, uint64_t, 8>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent,
                          (uint64_t *)ext);
-    else if (J == 4) hipLaunchKernelGGL((k_build_ext_u16<4, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
     else if (J == 3) hipLaunchKernelGGL((k_build_ext_u16<3, uint64_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint64_t *)ext);
     else hipLaunchKernelGGL((k_build_ext_u16<2, uint32_t>), dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nent, (uint32_t *)ext);
   } else {
-    if (J == 4 && getenv("KS_EXT_F64_U4"))
-      hipLaunchKernelGGL((k_build_ext_f64<4, 4>), dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
-    else if (J == 4 && getenv("KS_EXT_U1") == nullptr)
+    if (J == 4)
       hipLaunchKernelGGL((k_build_ext_f64<4, 8>), dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
-    else if (J == 4) hipLaunchKernelGGL(k_build_ext_f64<4>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
     else if (J == 3) hipLaunchKernelGGL(k_build_ext_f64<3>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
     else hipLaunchKernelGGL(k_build_ext_f64<2>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nent, (double *)ext);
   }

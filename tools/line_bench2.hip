@@ -1,0 +1,233 @@
+// line_bench2.hip -- the memory pattern of a pass 1 that reads one random
+// 64-B or 128-B table line per lane per batch (continuation-line table):
+// every lane owns a sequence of random lines; a wave fetches its 64 lanes'
+// lines cooperatively (L/16 lanes per line, one 16-B piece each: a wave
+// instruction touches 64/(L/16) lines, the shape that reaches ~50 G lines/s,
+// tools/line_bench.hip), and each owner then reads 3 x 8 B of its own line.
+//   glds : global_load_lds_dwordx4 straight into an LDS ring of NB batches
+//          (lines land in owner order: no transpose), owner reads from LDS
+//   reg  : global_load_dwordx4 into VGPRs, ds_write_b128 into LDS, owner reads
+//   lane : (reference) each owner loads its 3 pieces itself, 8-B loads
+// Prints G lines/s per variant.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
+
+__device__ __forceinline__ uint64_t mix(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+  return x;
+}
+
+// LB = line bytes (64 or 128); NB = batches in flight (LDS ring depth); W = waves per block
+template <int LB, int NB, int W>
+__global__ void __launch_bounds__(64 * W) k_glds(const uint8_t *__restrict__ tab, uint64_t line_mask, int batches,
+                                                 uint32_t *out) {
+  constexpr int PL = LB / 16;          // lanes per line
+  constexpr int NI = 64 / (64 / PL);   // = PL: instructions per batch (each loads 64 / PL lines)
+  constexpr int BB = 64 * LB;          // bytes per batch per wave
+  __shared__ __attribute__((aligned(16))) uint8_t ring[W][NB][BB];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t acc = 0;
+  auto issue = [&](int b) {
+    const uint64_t myline = mix(gid * 1000003ull + (uint64_t)b) & line_mask;
+    uint8_t *dst = ring[wv][b % NB];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      // instruction i loads the lines of owners i*(64/PL) .. +64/PL-1; lane -> (owner, piece)
+      const int owner = i * (64 / PL) + lane / PL;
+      const uint64_t ln = __shfl(myline, owner);
+      const uint8_t *src = tab + ln * LB + (lane % PL) * 16;
+      __builtin_amdgcn_global_load_lds((const void *)src, (void *)(dst + i * 1024), 16, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int b = 0; b < NB - 1; ++b) issue(b);
+  for (int b = 0; b < batches; ++b) {
+    if (b + NB - 1 < batches) issue(b + NB - 1);
+    // wait for batch b: leave (NB - 1) batches x NI instructions in flight
+    __builtin_amdgcn_s_waitcnt(0);  // simple: drain (k_glds_c refines)
+    const uint8_t *mine = ring[wv][b % NB] + lane * LB;
+    const uint64_t r = mix(gid + b);
+    const uint2 a = *reinterpret_cast<const uint2 *>(mine + 8 * (r & (PL * 2 - 1)));
+    const uint2 c = *reinterpret_cast<const uint2 *>(mine + 8 * ((r >> 8) & (PL * 2 - 1)));
+    const uint2 d = *reinterpret_cast<const uint2 *>(mine);
+    acc += a.x ^ c.y ^ d.x;
+  }
+  if (acc == 0x12345u) out[0] = acc;
+}
+
+// the same with counted waits: vmcnt((NB-1) * NI) leaves the younger batches in flight
+template <int LB, int NB, int W>
+__global__ void __launch_bounds__(64 * W) k_glds_c(const uint8_t *__restrict__ tab, uint64_t line_mask, int batches,
+                                                   uint32_t *out) {
+  constexpr int PL = LB / 16;
+  constexpr int NI = PL;
+  constexpr int BB = 64 * LB;
+  __shared__ __attribute__((aligned(16))) uint8_t ring[W][NB][BB];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t acc = 0;
+  auto issue = [&](int b) {
+    const uint64_t myline = mix(gid * 1000003ull + (uint64_t)b) & line_mask;
+    uint8_t *dst = ring[wv][b % NB];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int owner = i * (64 / PL) + lane / PL;
+      const uint64_t ln = __shfl(myline, owner);
+      const uint8_t *src = tab + ln * LB + (lane % PL) * 16;
+      __builtin_amdgcn_global_load_lds((const void *)src, (void *)(dst + i * 1024), 16, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int b = 0; b < NB - 1; ++b) issue(b);
+  for (int b = 0; b < batches; ++b) {
+    const bool more = b + NB - 1 < batches;
+    if (more) issue(b + NB - 1);
+    // vmcnt field: bits 3:0 and 15:14; expcnt 6:4 = 7, lgkmcnt 11:8 = 15 (no wait)
+    constexpr int keep = (NB - 1) * NI;
+    constexpr int enc = (keep & 0xf) | ((keep >> 4) << 14) | (0x7 << 4) | (0xf << 8);
+    if (more) __builtin_amdgcn_s_waitcnt(enc);
+    else __builtin_amdgcn_s_waitcnt(0x0F70 & ~0xf);
+    const uint8_t *mine = ring[wv][b % NB] + lane * LB;
+    const uint64_t r = mix(gid + b);
+    const uint2 a = *reinterpret_cast<const uint2 *>(mine + 8 * (r & (PL * 2 - 1)));
+    const uint2 c = *reinterpret_cast<const uint2 *>(mine + 8 * ((r >> 8) & (PL * 2 - 1)));
+    const uint2 d = *reinterpret_cast<const uint2 *>(mine);
+    acc += a.x ^ c.y ^ d.x;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): reads of this slot done before it is reissued
+  }
+  if (acc == 0x12345u) out[0] = acc;
+}
+
+// register staging: loads of batch b+1 in VGPRs while batch b is processed
+template <int LB, int W>
+__global__ void __launch_bounds__(64 * W) k_reg(const uint8_t *__restrict__ tab, uint64_t line_mask, int batches,
+                                                uint32_t *out) {
+  constexpr int PL = LB / 16;
+  constexpr int NI = PL;
+  constexpr int BB = 64 * LB;
+  __shared__ __attribute__((aligned(16))) uint8_t ring[W][BB];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t acc = 0;
+  uint4 v[NI];
+  auto issue = [&](int b) {
+    const uint64_t myline = mix(gid * 1000003ull + (uint64_t)b) & line_mask;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int owner = i * (64 / PL) + lane / PL;
+      const uint64_t ln = __shfl(myline, owner);
+      v[i] = *reinterpret_cast<const uint4 *>(tab + ln * LB + (lane % PL) * 16);
+    }
+  };
+  issue(0);
+  for (int b = 0; b < batches; ++b) {
+    uint8_t *dst = ring[wv];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) *reinterpret_cast<uint4 *>(dst + i * 1024 + lane * 16) = v[i];
+    if (b + 1 < batches) issue(b + 1);
+    const uint8_t *mine = ring[wv] + lane * LB;
+    const uint64_t r = mix(gid + b);
+    const uint2 a = *reinterpret_cast<const uint2 *>(mine + 8 * (r & (PL * 2 - 1)));
+    const uint2 c = *reinterpret_cast<const uint2 *>(mine + 8 * ((r >> 8) & (PL * 2 - 1)));
+    const uint2 d = *reinterpret_cast<const uint2 *>(mine);
+    acc += a.x ^ c.y ^ d.x;
+  }
+  if (acc == 0x12345u) out[0] = acc;
+}
+
+// reference: each owner loads 3 x 8 B of its own line itself
+template <int LB, int W, int U>
+__global__ void __launch_bounds__(64 * W) k_lane3(const uint8_t *__restrict__ tab, uint64_t line_mask, int batches,
+                                                  uint32_t *out) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t acc = 0;
+  for (int b = 0; b < batches; b += U) {
+    uint2 a[U], c[U], d[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t ln = mix(gid * 1000003ull + (uint64_t)(b + u)) & line_mask;
+      const uint64_t r = mix(gid + b + u);
+      const uint8_t *l = tab + ln * LB;
+      a[u] = *reinterpret_cast<const uint2 *>(l + 8 * (r & (LB / 8 - 1)));
+      c[u] = *reinterpret_cast<const uint2 *>(l + 8 * ((r >> 8) & (LB / 8 - 1)));
+      d[u] = *reinterpret_cast<const uint2 *>(l);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += a[u].x ^ c[u].y ^ d[u].x;
+  }
+  if (acc == 0x12345u) out[0] = acc;
+}
+
+template <typename F>
+float best_ms(F f, int reps) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  f(); CK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(a));
+    f();
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+    float ms = 0; CK(hipEventElapsedTime(&ms, a, b));
+    if (ms < best) best = ms;
+  }
+  return best;
+}
+
+static const uint8_t *g_tab;
+static size_t g_bytes;
+static uint32_t *g_out;
+static int g_cus;
+
+template <typename K>
+void run(const char *name, K kern, int lb, int nb, int w, int blocks_per_cu) {
+  const uint64_t lines = g_bytes / lb;
+  const int grid = g_cus * blocks_per_cu;
+  const int lanes = grid * 64 * w;
+  const int batches = (int)(((int64_t)1 << 31) / lanes);
+  const double n = (double)batches * lanes;
+  float ms = best_ms([&] { hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * w), 0, 0, g_tab, lines - 1, batches, g_out); }, 3);
+  printf("{\"kernel\":\"%s\",\"line_B\":%d,\"ring\":%d,\"waves_per_block\":%d,\"blocks_per_cu\":%d,\"G_lines_per_s\":%.2f}\n",
+         name, lb, nb, w, blocks_per_cu, n / (ms * 1e6));
+  fflush(stdout);
+}
+
+int main(int argc, char **argv) {
+  const size_t gib = (size_t)1 << 30;
+  g_bytes = (argc > 1 ? (size_t)atoi(argv[1]) : 128) * gib;
+  void *tab = nullptr;
+  if (hipExtMallocWithFlags(&tab, g_bytes, hipDeviceMallocContiguous) != hipSuccess) {
+    (void)hipGetLastError();
+    CK(hipMalloc(&tab, g_bytes));
+    printf("# plain hipMalloc\n");
+  }
+  CK(hipMemsetD32Async((hipDeviceptr_t)tab, 0x01010101, g_bytes / 4, nullptr));
+  CK(hipMalloc(&g_out, 64));
+  CK(hipDeviceSynchronize());
+  hipDeviceProp_t p;
+  CK(hipGetDeviceProperties(&p, 0));
+  g_cus = p.multiProcessorCount;
+  g_tab = (const uint8_t *)tab;
+  run("lane3", k_lane3<128, 4, 4>, 128, 0, 4, 8);
+  run("lane3", k_lane3<128, 4, 2>, 128, 0, 4, 8);
+  run("lane3", k_lane3<64, 4, 4>, 64, 0, 4, 8);
+  run("reg", k_reg<128, 4>, 128, 1, 4, 4);
+  run("reg", k_reg<128, 4>, 128, 1, 4, 8);
+  run("reg", k_reg<64, 4>, 64, 1, 4, 8);
+  run("glds_drain", k_glds<128, 2, 4>, 128, 2, 4, 2);
+  run("glds", k_glds_c<128, 2, 4>, 128, 2, 4, 2);
+  run("glds", k_glds_c<128, 3, 4>, 128, 3, 4, 1);
+  run("glds", k_glds_c<128, 2, 8>, 128, 2, 8, 1);
+  run("glds", k_glds_c<128, 2, 2>, 128, 2, 2, 4);
+  run("glds", k_glds_c<128, 3, 2>, 128, 3, 2, 3);
+  run("glds", k_glds_c<128, 4, 2>, 128, 4, 2, 2);
+  run("glds", k_glds_c<64, 2, 4>, 64, 2, 4, 4);
+  run("glds", k_glds_c<64, 3, 4>, 64, 3, 4, 3);
+  run("glds", k_glds_c<64, 4, 4>, 64, 4, 4, 2);
+  return 0;
+}

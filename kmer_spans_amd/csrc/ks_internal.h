@@ -109,7 +109,14 @@ struct ks_table {
   // codes) of its J consecutive k-mers, so one random request serves J scan
   // indices.  J = 1: not built.
   int ext_J = 1;
-  void *d_ext = nullptr;        // uint64 (J <= 4 codes) or double[4] (J <= 3 values)
+  void *d_ext = nullptr;        // uint64 (J <= 4 codes) or double[4] (J <= 3 values), or a line table
+  // Line table (line_kind != 0; d_ext holds it, ext_J = its positions per
+  // line): one 64-B line per m-mer (m = k + line_own - 1) with the values of
+  // its line_own k-mers and of every one- and two-base continuation (uint16
+  // codes, line_kind 1, ext_J = own + 2) or one-base continuation (FP64,
+  // line_kind 2, ext_J = own + 1); see k_build_line_u16 / k_pass1l.
+  int line_kind = 0;
+  int line_own = 0;
   size_t ext_bytes = 0;
   size_t ext_cap = 0;           // bytes of the allocation (a pooled buffer may be larger)
   int device = 0;

@@ -958,6 +958,288 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
   }
 }
 
+// ------------------------------------------------------------------- P1 (line tables)
+
+// Pass 1 on a line table (ks_table line_kind; k_build_line_u16 / _f64 in
+// ks_table.hip): a lane scans its chunk in steps of J = own + LV indices (LV
+// = 2 continuation levels for uint16 codes, 1 for FP64 values).  Step s reads
+// the line of the m-mer (m = k + own - 1) ending at base start - 1 + sJ +
+// own - 1: its own entries are indices sJ .. sJ + own - 1, its continuation
+// entries, selected by the next LV bases, the following LV indices.  So the
+// step's key is the (k + J - 1)-mer ending at base start + sJ + J - 2, as
+// for the expanded tables, and one random 64-B request serves J indices.
+// Lines are fetched cooperatively: four lanes load the four 16-B pieces of
+// one lane's line (global_load_lds_dwordx4: a wave instruction touches 16
+// whole lines; random 64-B lines come at ~50 G/s from a 64-128 GiB table,
+// against 25-38 G/s when each lane loads its own entry, tools/line_bench*.hip,
+// profiles/r3/line_bench*.txt), straight into a two-slot LDS ring per wave:
+// the lines land in lane order (lane L's line at L x 64 B), and the next
+// step's lines are in flight while a step is processed.  The loads are inline
+// asm (the compiler would otherwise drain every LDS-DMA before each LDS
+// read); the only ordinary memory accesses in the loop are the rare candidate
+// appends, and the bases come from the packed 2-bit codes loaded into
+// registers once per lane.  Same outputs as k_pass1p (kSumm: compressed
+// tables also summarise in the predicted binades) / k_pass1pf (FP64).
+constexpr int kLineLutMax = 7168;  // LDS LUT entries of the uint16 line pass (ring 96 KiB + 56 KiB)
+constexpr int kLineWords = 20;     // packed words per lane: <= 15 + 17 + 255 + J bases
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+// One global_load_lds_dwordx4: 16 B from each lane's gsrc to LDS address
+// lds + 16 x lane (lds wave-uniform).
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds)
+               : "memory");
+}
+
+template <int OWN, bool kF64, bool kLdsLut, bool kTrlr>
+__global__ void __launch_bounds__(kF64 ? 1024 : 768) k_pass1l(Chunks g, int64_t total, int k, TableView tv,
+                                                              EmitCfg ec, uint32_t *__restrict__ visits, P1 o,
+                                                              Cand cand, const double *__restrict__ xh, SummP1 sp) {
+  constexpr int BS = kF64 ? 1024 : 768;  // 16 / 12 waves: ring 128 / 96 KiB (+ the LUT)
+  constexpr int LV = kF64 ? 1 : 2;
+  constexpr int J = OWN + LV;
+  constexpr int NS = (CH + J - 1) / J;  // steps per chunk (the same for the whole wave)
+  constexpr bool kSumm = !kF64;
+  constexpr bool kLut = !kF64 && kLdsLut;
+  static_assert(kF64 ? OWN + 4 <= 8 : OWN + 20 <= 32, "line layout");
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[(BS / 64) * 2 * 4096];
+  __shared__ double s_lut[kLut ? kLineLutMax : 1];
+  if (kLut) {
+    for (int i = threadIdx.x; i < tv.nlut; i += BS) s_lut[i] = tv.lut[i];
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t c = g.c0 + (int64_t)blockIdx.x * BS + threadIdx.x;
+  if (c - lane >= g.nch) return;  // the whole wave is past the end (the other lanes still fetch for theirs)
+  const bool live = c < g.nch;
+  const int64_t start = live ? g.start[c] : (int64_t)k;
+  const int n = live ? g.n[c] : 0;
+  const bool first = live && (c == 0 || g.run[c - 1] != g.run[c]);
+  const uint32_t kmask = (1u << (2 * k)) - 1u;
+
+  // ---- the lane's bases: packed words from the one holding base start - k
+  uint32_t a[kLineWords];
+  {
+    const uint32_t *__restrict__ packed = g.packed;
+    const int64_t w0 = (start - k) >> 4, wlast = total >> 4;  // words 0 .. total >> 4 exist
+    const int64_t wa = w0 & ~(int64_t)3;
+    if (wa + 24 <= wlast + 1) {
+      uint32_t v[24];
+      const uint4 *P4 = reinterpret_cast<const uint4 *>(packed + wa);
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {
+        const uint4 q = P4[t];
+        v[4 * t] = q.x;
+        v[4 * t + 1] = q.y;
+        v[4 * t + 2] = q.z;
+        v[4 * t + 3] = q.w;
+      }
+      const int off = (int)(w0 - wa);
+#pragma unroll
+      for (int t = 0; t < kLineWords; ++t)
+        a[t] = off == 0 ? v[t] : (off == 1 ? v[t + 1] : (off == 2 ? v[t + 2] : v[t + 3]));
+    } else {
+#pragma unroll
+      for (int t = 0; t < kLineWords; ++t) a[t] = packed[min(w0 + t, wlast)];
+    }
+  }
+  // rolling supply: acc holds na bases in its top 2 na bits; a refill appends
+  // the next word when 16 or fewer are left and shifts the word array down
+  uint64_t acc = 0;
+  int na = 0;
+  auto refill = [&]() {
+    const bool r = na <= 16;
+    acc |= r ? ((uint64_t)a[0] << (32 - 2 * na)) : 0ull;
+    na += r ? 16 : 0;
+#pragma unroll
+    for (int t = 0; t < kLineWords - 1; ++t) a[t] = r ? a[t + 1] : a[t];
+  };
+  auto take = [&](int nb) -> uint64_t {  // nb <= 17 bases (after a refill), first base most significant
+    const uint64_t v = acc >> (64 - 2 * nb);
+    acc <<= 2 * nb;
+    na -= nb;
+    return v;
+  };
+  refill();
+  refill();
+  {
+    const int sk = (int)((start - k) & 15);
+    acc <<= 2 * sk;
+    na -= sk;
+  }
+  refill();
+  const int kx = k + J - 1;  // key length (<= 17)
+  const uint64_t xmask = (1ull << (2 * kx)) - 1ull;
+  uint64_t x = take(kx);     // key of step 0
+  // tr_lr: the run's first scan index scores the first k-mer's own score
+  const double first_val = (kTrlr && first) ? ec.ks[(uint32_t)(x >> (2 * (J - 1))) & kmask] : 0.0;
+
+  // ---- the ring: lane L's line of slot q at ring + q x 4096 + L x 64
+  uint8_t *const ring = s_ring + wv * 8192;
+  const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+  const uint8_t *__restrict__ lines = tv.line;
+  auto issue = [&](uint32_t idx, int slot) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t li = (uint32_t)__shfl((int)idx, 16 * q + (lane >> 2));
+      glds16(lines + (size_t)li * 64 + (lane & 3) * 16, ring_lds + (uint32_t)(slot * 4096 + q * 1024));
+    }
+  };
+  double prev = 0.0, best = 0.0;
+  int beg = -1, arg = 0;
+  double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
+  bool special = false;
+  // binade summaries (compressed tables), as in k_pass1p
+  int se = INT32_MIN, se2 = INT32_MIN;
+  double sC = 0.0, sH = 0.0, scur = 0.0, smx = -INFINITY;
+  double sC2 = 0.0, sH2 = 0.0, scur2 = 0.0, smx2 = -INFINITY;
+  int sarg = 0, sarg2 = 0;
+  bool sbad = false, sbad2 = false;
+  if (kSumm && live) {
+    const double xp = xh[c];
+    if (xp >= kP1SumMin && xp < 1.0e15) {
+      se = binade_of(xp);
+      sC = 1.5 * ldexp(1.0, se);
+      sH = ldexp(1.0, se - 53);
+      const double lo = ldexp(1.0, se);
+      if (xp < lo * (1.0 + kP1Margin)) se2 = se - 1;
+      else if (xp > 2.0 * lo * (1.0 - kP1Margin)) se2 = se + 1;
+      if (se2 != INT32_MIN) {
+        sC2 = 1.5 * ldexp(1.0, se2);
+        sH2 = ldexp(1.0, se2 - 53);
+      }
+    }
+  }
+  const int f0 = first ? 0 : -1;
+  issue((uint32_t)(x >> (2 * LV)), 0);
+  for (int st = 0; st < NS; ++st) {
+    const uint64_t xs = x;  // key of this step
+    if (st + 1 < NS) {      // the next step's lines in flight, then this step's complete
+      refill();
+      x = ((x << (2 * J)) | take(J)) & xmask;
+      issue((uint32_t)(x >> (2 * LV)), (st + 1) & 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const uint8_t *ln = ring + (st & 1) * 4096 + lane * 64;
+    double v[J];
+    if (!kF64) {
+      uint32_t h[16];  // halfwords 0 .. 15 of the line (own + L1 <= 9 codes: 0 .. 8)
+      const uint4 q0 = *reinterpret_cast<const uint4 *>(ln);
+      h[0] = q0.x & 0xffffu; h[1] = q0.x >> 16; h[2] = q0.y & 0xffffu; h[3] = q0.y >> 16;
+      h[4] = q0.z & 0xffffu; h[5] = q0.z >> 16; h[6] = q0.w & 0xffffu; h[7] = q0.w >> 16;
+      if (OWN + 4 > 8) {
+        const uint4 q1 = *reinterpret_cast<const uint4 *>(ln + 16);
+        h[8] = q1.x & 0xffffu; h[9] = q1.x >> 16; h[10] = q1.y & 0xffffu; h[11] = q1.y >> 16;
+        h[12] = q1.z & 0xffffu; h[13] = q1.z >> 16; h[14] = q1.w & 0xffffu; h[15] = q1.w >> 16;
+      }
+      const uint32_t c1 = (uint32_t)(xs >> 2) & 3u, c2 = (uint32_t)xs & 3u;
+      uint32_t cs[J];
+#pragma unroll
+      for (int t = 0; t < OWN; ++t) cs[t] = h[t];
+      cs[OWN] = c1 == 0 ? h[OWN] : (c1 == 1 ? h[OWN + 1] : (c1 == 2 ? h[OWN + 2] : h[OWN + 3]));
+      cs[OWN + 1] = *reinterpret_cast<const uint16_t *>(ln + 2 * (OWN + 4 + 4 * c1 + c2));
+#pragma unroll
+      for (int t = 0; t < J; ++t) v[t] = kLut ? s_lut[cs[t]] : tv.lut[cs[t]];
+    } else {
+      const double *lv = reinterpret_cast<const double *>(ln);
+#pragma unroll
+      for (int t = 0; t < OWN; ++t) v[t] = lv[t];
+      v[OWN] = lv[OWN + ((int)xs & 3)];
+    }
+#pragma unroll
+    for (int t = 0; t < J; ++t) {
+      const int i = st * J + t;
+      if (i < n) {
+        double s = v[t];
+        if (kTrlr && first && i == 0) s = first_val;
+        if (visits) atomicAdd(&visits[(uint32_t)(xs >> (2 * (J - 1 - t))) & kmask], 1u);
+        asum += s;
+        pmin = asum < pmin ? asum : pmin;
+        pmax = asum > pmax ? asum : pmax;
+        sabs += fabs(s);
+        special |= !isfinite(s);
+        if (kSumm && se != INT32_MIN) {
+          const double r = (s + sC) - sC;
+          sbad |= fabs(r - s) == sH;
+          scur += r;
+          const bool su = scur > smx;
+          smx = su ? scur : smx;
+          sarg = su ? i : sarg;
+          if (se2 != INT32_MIN) {
+            const double r2 = (s + sC2) - sC2;
+            sbad2 |= fabs(r2 - s) == sH2;
+            scur2 += r2;
+            const bool su2 = scur2 > smx2;
+            smx2 = su2 ? scur2 : smx2;
+            sarg2 = su2 ? i : sarg2;
+          }
+        }
+        // clean trajectory (k_pass1p)
+        const double tt = prev + s;
+        const double S = tt > 0 ? tt : 0.0;
+        const bool open = (prev == 0) & (S > 0);
+        const bool close = (prev > 0) & (S == 0);
+        const long long ml = kTrlr ? ec.min_len : 0;
+        const bool want =
+            kTrlr ? (close & (((long long)((arg != f0 ? arg - 1 : arg) - (beg != f0 ? beg - 1 : beg)) >= ml) |
+                              ((long long)((i != f0 ? i - 1 : i) - (arg != f0 ? arg - 1 : arg) - 1) >=
+                               (ml > 1 ? ml : 1LL))))
+                  : (close & ((uint64_t)(int64_t)(arg - beg) >= ec.mw) & (best >= ec.min_score));
+        if (want) {
+          const int64_t slot = append_one(cand.count, cand.segcap);
+          if (slot >= 0) {
+            cand.beg[slot] = start + beg;
+            cand.arg[slot] = start + arg;
+            cand.rst[slot] = start + i;
+            cand.best[slot] = best;
+          }
+        }
+        const bool up = open | (S > best);
+        best = up ? S : best;
+        arg = up ? i : arg;
+        beg = open ? i : (close ? -1 : beg);
+        prev = S;
+      }
+    }
+  }
+  if (!live) return;
+  if (kSumm) {  // as in k_pass1p
+    auto put = [&](int t, int e, bool bad, double cur, double mx, int aa) {
+      const double lim = ldexp(1.0, e);
+      const bool ok = e != INT32_MIN && !bad && sabs < 0.5 * lim && mx < 0.5 * lim && pmin > -0.5 * lim;
+      sp.e[2 * c + t] = ok ? e : INT32_MIN;
+      if (ok) {
+        const double sc = ldexp(1.0, 52 - e);
+        sp.D[2 * c + t] = (long long)(cur * sc);
+        sp.M[2 * c + t] = (long long)(mx * sc);
+        sp.N[2 * c + t] = (long long)floor((pmin - sabs * 0x1p-44) * sc) - 130;
+        sp.A[2 * c + t] = aa;
+      }
+    };
+    put(0, se, sbad, scur, smx, sarg);
+    put(1, se2, sbad2, scur2, smx2, sarg2);
+  }
+  o.cexit[c] = prev;
+  o.asum[c] = asum;
+  o.pmin[c] = pmin;
+  o.pmax[c] = pmax;
+  o.sabs[c] = sabs;
+  o.special[c] = special ? 1 : 0;
+  if (prev > 0) {
+    o.tbeg[c] = beg; o.tmax[c] = best; o.targ[c] = arg;
+  } else {
+    o.tbeg[c] = -1; o.tmax[c] = 0.0; o.targ[c] = 0;
+  }
+}
+
 // Pass 1 for small k (north_star: "the frequency table LDS-staged for small
 // k"): the 4^k FP64 values s[code] (k <= 7: <= 128 KiB) are staged in LDS
 // once per persistent block, so every scanned index costs one LDS read and no
@@ -3052,7 +3334,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // pass-1 summaries (no per-position code store): compressed expanded
   // tables on the pipelined pass with a binade predictor (a table without
   // one, a failed allocation of the predictor, is scanned unexpanded)
-  const bool p1summ = comp && Jt >= 2 && !lds_table && runs.packed != nullptr && tv.approx != nullptr;
+  const bool line = tv.line != nullptr && !lds_table && runs.packed != nullptr;  // line table: k_pass1l
+  const bool p1summ = comp && (Jt >= 2 || line) && !lds_table && runs.packed != nullptr && tv.approx != nullptr;
   // (the carry reads no replay slots unless k_marks_select wrote them)
   if (!p1summ) rpb.slot = nullptr;
   // per-index code store (uint16 per scan index, 2 B x 256 per chunk):
@@ -3148,6 +3431,53 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     if (ec.trlr) hipLaunchKernelGGL(k_pass1_lds<true>, dim3(gl), dim3(1024), 0, st, g, total, k, tv, ec, visits, p1, cand);
     else hipLaunchKernelGGL(k_pass1_lds<false>, dim3(gl), dim3(1024), 0, st, g, total, k, tv, ec, visits, p1, cand);
     codes = nullptr;
+  } else if (line && (p1summ || !comp)) {
+    // line tables: every chunk (no tail: a lane's bases come from guarded loads)
+    const bool lut = tv.nlut <= kLineLutMax;
+#define KS_P1L(O, F, L, GV, GRID, STRM)                                                                        \
+  do {                                                                                                       \
+    if (ec.trlr)                                                                                             \
+      hipLaunchKernelGGL((k_pass1l<O, F, L, true>), dim3(GRID), dim3(F ? 1024 : 768), 0, STRM, GV, total, k, tv, ec, \
+                         visits, p1, cand, d_xh, sp1);                                                       \
+    else                                                                                                     \
+      hipLaunchKernelGGL((k_pass1l<O, F, L, false>), dim3(GRID), dim3(F ? 1024 : 768), 0, STRM, GV, total, k, tv, \
+                         ec, visits, p1, cand, d_xh, sp1);                                                   \
+  } while (0)
+    auto p1l = [&](const Half &h, hipStream_t strm) {
+      const Chunks gv = view(h);
+      const int bs = comp ? 768 : 1024;
+      const unsigned grid = (unsigned)((h.c1 - h.c0 + bs - 1) / bs);
+      const int own = tv.line_own;
+      if (!comp) {
+        if (own == 4) KS_P1L(4, true, false, gv, grid, strm);
+        else if (own == 3) KS_P1L(3, true, false, gv, grid, strm);
+        else KS_P1L(2, true, false, gv, grid, strm);
+      } else if (lut) {
+        if (own == 5) KS_P1L(5, false, true, gv, grid, strm);
+        else if (own == 4) KS_P1L(4, false, true, gv, grid, strm);
+        else if (own == 3) KS_P1L(3, false, true, gv, grid, strm);
+        else KS_P1L(2, false, true, gv, grid, strm);
+      } else {
+        if (own == 5) KS_P1L(5, false, false, gv, grid, strm);
+        else if (own == 4) KS_P1L(4, false, false, gv, grid, strm);
+        else if (own == 3) KS_P1L(3, false, false, gv, grid, strm);
+        else KS_P1L(2, false, false, gv, grid, strm);
+      }
+    };
+#undef KS_P1L
+    if (split) {  // the halves at once, as the expanded-table pass below
+      KS_HIP(hipEventRecord(ctx->ev[17], st));
+      KS_HIP(hipStreamWaitEvent(ctx->hi, ctx->ev[17], 0));
+      if (!side_forked) KS_HIP(hipStreamWaitEvent(ctx->side, ctx->ev[17], 0));
+      p1l(halves[0], ctx->hi);
+      KS_HIP(hipGetLastError());
+      KS_HIP(hipEventRecord(ctx->ev[12], ctx->hi));
+      KS_HIP(hipStreamWaitEvent(st, ctx->ev[12], 0));
+      p1l(halves[1], ctx->side);
+    } else {
+      p1l(halves[0], st);
+    }
+    KS_HIP(hipGetLastError());
   } else if (p1summ) {
     // the tail chunks (a latency-bound serial walk each) run on the side
     // stream, overlapped with the pipelined pass (of the last half)

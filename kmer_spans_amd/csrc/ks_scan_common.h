@@ -20,6 +20,9 @@ struct TableView {
   const uint16_t *map12;
   const uint16_t *approx;  // fp16 prefix means (ks_table::d_approx), nullptr if absent
   int approx_k;
+  const uint8_t *line;     // line table (ks_table line_kind), nullptr if absent; ext is then nullptr
+  int line_kind;           // 1: uint16 codes, 2: FP64 values
+  int line_own;
 };
 
 // LUT entries that fit the LDS copy used by the streaming passes (64 KiB).

@@ -248,6 +248,68 @@ __global__ void k_build_ext_f64(const double *__restrict__ vals, int k, uint64_t
   for (; sl < nslot; sl += S) __builtin_nontemporal_store(half(sl), reinterpret_cast<ks_f64x2 *>(ext) + sl);
 }
 
+// Line tables (ks_table::line_kind): one 64-B line per m-mer x (m = k + own
+// - 1), holding the values of the own k-mers inside x and of the k-mers one
+// and two bases past it for every continuation:
+//   uint16 codes: [own][L1: x.c for c in ACTG order][L2: x.c1.c2], own + 20 <= 32
+//   FP64 values:  [own][L1], own + 4 <= 8
+// (zeros pad the line).  own k-mer t is (x >> 2 (own - 1 - t)) & mask; L1 c
+// is ((x << 2) | c) & mask, L2 c1 c2 is ((x << 4) | c1 c2) & mask: the L1 /
+// L2 entries of consecutive lines are consecutive code-table entries.  Four
+// lanes build a line, a 16-B piece each (codes / values 8p .. 8p + 7 /
+// 2p, 2p + 1), so one store instruction writes 16 whole lines (1 KiB); the
+// code reads repeat across the wave and stay cached: the build is a write
+// stream of nontemporal stores.
+typedef uint32_t ks_u32x4 __attribute__((ext_vector_type(4)));
+template <int OWN>
+__device__ __forceinline__ uint32_t line_kmer(uint64_t x, int j, uint32_t kmask) {
+  if (j < OWN) return (uint32_t)(x >> (2 * (OWN - 1 - j))) & kmask;
+  if (j < OWN + 4) return ((uint32_t)(x << 2) | (uint32_t)(j - OWN)) & kmask;
+  return ((uint32_t)(x << 4) | (uint32_t)(j - OWN - 4)) & kmask;
+}
+
+template <int OWN>
+__global__ void __launch_bounds__(256) k_build_line_u16(const uint16_t *__restrict__ codes, int k, uint64_t nlines,
+                                                        ks_u32x4 *__restrict__ out) {
+  static_assert(OWN + 20 <= 32, "a uint16 line holds 32 codes");
+  const uint32_t kmask = (uint32_t)(((uint64_t)1 << (2 * k)) - 1);
+  const uint64_t npiece = nlines * 4;
+  const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npiece; q += S) {
+    const uint64_t x = q >> 2;
+    const int p = (int)(q & 3);
+    uint32_t h[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = 8 * p + u;
+      h[u] = j < OWN + 20 ? (uint32_t)codes[line_kmer<OWN>(x, j, kmask)] : 0u;
+    }
+    ks_u32x4 v;
+    v.x = h[0] | (h[1] << 16);
+    v.y = h[2] | (h[3] << 16);
+    v.z = h[4] | (h[5] << 16);
+    v.w = h[6] | (h[7] << 16);
+    __builtin_nontemporal_store(v, out + q);
+  }
+}
+
+template <int OWN>
+__global__ void __launch_bounds__(256) k_build_line_f64(const double *__restrict__ vals, int k, uint64_t nlines,
+                                                        ks_f64x2 *__restrict__ out) {
+  static_assert(OWN + 4 <= 8, "an FP64 line holds 8 values");
+  const uint32_t kmask = (uint32_t)(((uint64_t)1 << (2 * k)) - 1);
+  const uint64_t npiece = nlines * 4;
+  const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npiece; q += S) {
+    const uint64_t x = q >> 2;
+    const int j = 2 * (int)(q & 3);
+    ks_f64x2 v;
+    v.x = j < OWN + 4 ? vals[line_kmer<OWN>(x, j, kmask)] : 0.0;
+    v.y = j + 1 < OWN + 4 ? vals[line_kmer<OWN>(x, j + 1, kmask)] : 0.0;
+    __builtin_nontemporal_store(v, out + q);
+  }
+}
+
 // out[i] = lut[index of counts[i] in dv]: dv = the sorted distinct counts
 // (every count occurs in it), staged in LDS with the LUT when they fit.
 constexpr int kMapLds = 8192;
@@ -467,6 +529,103 @@ static ks_status choose_code12(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev
   return KS_OK;
 }
 
+// Allocation of an expanded / line table: a pooled buffer of a destroyed
+// table when it fits, else contiguous VRAM (ext_malloc).  nullptr: no memory.
+static void *ext_alloc(ks_ctx *ctx, size_t bytes, size_t *cap) {
+  *cap = bytes;
+  void *ext = pool_take(ctx->device, bytes, cap);
+  if (ext) return ext;
+  *cap = bytes;
+  if (ext_malloc(&ext, bytes) == hipSuccess) return ext;
+  (void)hipGetLastError();
+  {  // a pooled buffer too small for this table may be what is in the way
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    if (ctx->device >= 0 && ctx->device < 64 && g_pool[ctx->device].p) {
+      (void)hipFree(g_pool[ctx->device].p);
+      g_pool[ctx->device] = PoolBuf();
+    }
+  }
+  if (ext_malloc(&ext, bytes) == hipSuccess) return ext;
+  (void)hipGetLastError();
+  return nullptr;
+}
+
+// Binade predictor of the pass-1 summaries (k_predict), built with the
+// expanded / line table of a compressed table.
+static ks_status build_approx(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev) {
+  if (!k_approx_ok(t)) return KS_OK;
+  const int kp = std::min(t->k, 8);
+  if (hipMalloc(&t->d_approx, ((size_t)2 << (2 * kp)) + 16) != hipSuccess) {
+    (void)hipGetLastError();
+    t->d_approx = nullptr;
+    return KS_OK;
+  }
+  t->approx_k = kp;
+  hipLaunchKernelGGL(k_build_approx, dim3((unsigned)std::min<int64_t>(((int64_t)1 << (2 * kp)) / 256 + 1, 4096)),
+                     dim3(256), 0, ctx->stream, t->d_codes, t->d_lut, t->d_vals, freq_dev, t->k, kp, t->d_approx);
+  KS_HIP(hipGetLastError());
+  return KS_OK;
+}
+
+// Line table of k in [8, 13] (k <= 7 scans with its table in LDS): the
+// largest own count (m = k + own - 1 <= 15, own <= 5 / 4) whose 4^m x 64 B
+// fit the budget, own >= 2.  Sets *built.
+static ks_status table_lines(ks_ctx *ctx, ks_table *t, size_t budget, const int32_t *freq_dev, bool *built) {
+  *built = false;
+  const bool u16 = t->compressed;
+  if (t->k < 8 || t->k > 13 || getenv("KS_NO_LINES")) return KS_OK;
+  int own = std::min(u16 ? 5 : 4, 16 - t->k);
+  for (; own >= 2; --own)
+    if (((size_t)64 << (2 * (t->k + own - 1))) <= budget) break;
+  if (own < 2) return KS_OK;
+  const int m = t->k + own - 1;
+  const uint64_t nlines = (uint64_t)1 << (2 * m);
+  const size_t bytes = nlines * 64;
+  const double ta = now_ms();
+  size_t cap = 0;
+  void *ext = ext_alloc(ctx, bytes, &cap);
+  if (!ext) return KS_OK;
+  t->ms_ext_alloc = now_ms() - ta;
+  t->ext_cap = cap;
+  hipStream_t st = ctx->stream;
+  hipEvent_t a, b;
+  KS_HIP(hipEventCreate(&a));
+  KS_HIP(hipEventCreate(&b));
+  KS_HIP(hipEventRecord(a, st));
+  const unsigned grid = (unsigned)std::min<uint64_t>((nlines * 4 + 255) / 256, (uint64_t)ctx->num_cus * 32);
+#define KS_LINE_BUILD(O)                                                                                       \
+  do {                                                                                                         \
+    if (u16)                                                                                                   \
+      hipLaunchKernelGGL(k_build_line_u16<O>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nlines, (ks_u32x4 *)ext); \
+    else                                                                                                       \
+      hipLaunchKernelGGL(k_build_line_f64<O>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nlines,          \
+                         (ks_f64x2 *)ext);                                                                     \
+  } while (0)
+  if (own == 5) {
+    if (u16) hipLaunchKernelGGL(k_build_line_u16<5>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nlines, (ks_u32x4 *)ext);
+  } else if (own == 4) KS_LINE_BUILD(4);
+  else if (own == 3) KS_LINE_BUILD(3);
+  else KS_LINE_BUILD(2);
+#undef KS_LINE_BUILD
+  KS_HIP(hipGetLastError());
+  KS_HIP(hipEventRecord(b, st));
+  KS_HIP(hipEventSynchronize(b));
+  float ms = 0;
+  KS_HIP(hipEventElapsedTime(&ms, a, b));
+  KS_HIP(hipEventDestroy(a));
+  KS_HIP(hipEventDestroy(b));
+  KS_TRY(build_approx(ctx, t, freq_dev));
+  t->d_ext = ext;
+  t->line_kind = u16 ? 1 : 2;
+  t->line_own = own;
+  t->ext_J = own + (u16 ? 2 : 1);
+  t->ext_bits = u16 ? 16 : 64;
+  t->ext_bytes = bytes;
+  t->ms_ext = ms;
+  *built = true;
+  return KS_OK;
+}
+
 ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t *freq_dev) {
   if (t->d_ext || t->ext_J > 1) return KS_OK;
   const bool u16 = t->compressed;
@@ -479,13 +638,18 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   // leave room for the sequences and the scan workspace
   const size_t reserve = std::max<size_t>((size_t)32 << 30, total_b / 4);
   const size_t budget = std::min(max_bytes, free_b > reserve ? free_b - reserve : (size_t)0);
+  const char *jmax_env = getenv("KS_EXT_MAX_J");  // tests: cap J to exercise every table form
+  if (!jmax_env) {  // line tables first (k_pass1l); KS_NO_LINES: the (k+J-1)-mer forms below
+    bool built = false;
+    KS_TRY(table_lines(ctx, t, budget, freq_dev, &built));
+    if (built) return KS_OK;
+  }
   // candidates, best first: (J, code bits); (k+J-1)-mer indices up to 34 bits
   struct Cand { int J, bits; };
   const Cand cands_u16[] = {{5, 12}, {4, 16}, {3, 16}, {2, 16}};
   const Cand cands_f64[] = {{4, 64}, {3, 64}, {2, 64}};
   const Cand *cands = u16 ? cands_u16 : cands_f64;
   const int ncand = u16 ? 4 : 3;
-  const char *jmax_env = getenv("KS_EXT_MAX_J");  // tests: cap J to exercise every table form
   const int jmax = jmax_env ? atoi(jmax_env) : 5;
   const char *esc_env = getenv("KS_EXT_ESCAPE_MAX");
   const double max_escape = esc_env ? atof(esc_env) : 0.01;
@@ -515,27 +679,10 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   const uint64_t nent = (uint64_t)1 << (2 * kx);
   const size_t bytes = nent * ext_entry_bytes(u16, J);
   hipStream_t st = ctx->stream;
-  void *ext = nullptr;
   const double ta = now_ms();
-  size_t cap = bytes;
-  ext = pool_take(ctx->device, bytes, &cap);
-  if (!ext) {
-    cap = bytes;
-    if (ext_malloc(&ext, bytes) != hipSuccess) {
-      (void)hipGetLastError();
-      {  // a pooled buffer too small for this table may be what is in the way
-        std::lock_guard<std::mutex> g(g_pool_mu);
-        if (ctx->device >= 0 && ctx->device < 64 && g_pool[ctx->device].p) {
-          (void)hipFree(g_pool[ctx->device].p);
-          g_pool[ctx->device] = PoolBuf();
-        }
-      }
-      if (ext_malloc(&ext, bytes) != hipSuccess) {
-        (void)hipGetLastError();
-        return KS_OK;
-      }
-    }
-  }
+  size_t cap = 0;
+  void *ext = ext_alloc(ctx, bytes, &cap);
+  if (!ext) return KS_OK;
   t->ms_ext_alloc = now_ms() - ta;
   t->ext_cap = cap;
   hipEvent_t a, b;
@@ -573,18 +720,7 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
     t->d_map12 = nullptr;
     t->d_lut12 = nullptr;
   }
-  if (k_approx_ok(t)) {  // binade predictor of the pass-1 summaries (k_predict)
-    const int kp = std::min(t->k, 8);
-    if (hipMalloc(&t->d_approx, ((size_t)2 << (2 * kp)) + 16) == hipSuccess) {
-      t->approx_k = kp;
-      hipLaunchKernelGGL(k_build_approx, dim3((unsigned)std::min<int64_t>(((int64_t)1 << (2 * kp)) / 256 + 1, 4096)),
-                         dim3(256), 0, st, t->d_codes, t->d_lut, t->d_vals, freq_dev, t->k, kp, t->d_approx);
-      KS_HIP(hipGetLastError());
-    } else {
-      (void)hipGetLastError();
-      t->d_approx = nullptr;
-    }
-  }
+  KS_TRY(build_approx(ctx, t, freq_dev));
   t->d_ext = ext;
   t->ext_J = J;
   t->ext_bits = bits;

@@ -1,0 +1,108 @@
+"""GPU parity of pass 1 on line tables (k_pass1l): every line form -- uint16
+codes with own = 2..5 k-mers per line (J = own + 2 scan indices per 64-B
+line) and FP64 values with own = 2..4 (J = own + 1) -- forced by the
+expanded-table byte cap, for kmer_regions (log2 / +-1 / weighted rank,
+with the visit histogram through both the count-derived and the atomic
+route) and tr_lr, against the oracle (kmer_spans.c:243-307, :329-395)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GiB = 1 << 30
+
+
+def _same(pos, sc, opos, osc, what):
+    assert pos.shape == opos.shape, (what, pos.shape, opos.shape)
+    assert np.array_equal(pos, opos), what
+    assert np.array_equal(sc.view(np.uint64), osc.view(np.uint64)), what
+
+
+@pytest.fixture(scope="module")
+def setup():
+    import torch
+    from kmer_spans_amd import _lib, device as D, genome
+    ctx = _lib.context(0)
+    D.bind_torch_stream(ctx)
+    parts, lens = genome.human_like(scale=0.0015, seed=77, device="cuda", ncontigs=6)
+    ds = D.from_parts(parts, lens, "cuda")
+    host = [ds.host_seq(q) for q in range(ds.nseq)]
+    return ctx, ds, host, torch
+
+
+# (k, cap GiB) -> own of the uint16 line (m = k + own - 1, 4^m x 64 B <= cap)
+@pytest.mark.parametrize("k,cap,own_u16,own_f64", [(11, 80, 5, 4), (11, 20, 4, 4), (11, 5, 3, 3), (11, 1.5, 2, 2),
+                                                   (13, 80, 3, 3), (12, 20, 3, 3), (9, 1.0, 4, 4)])
+@pytest.mark.parametrize("score", ["log2", "pm1", "rank"])
+def test_line_forms(oracle, setup, monkeypatch, k, cap, own_u16, own_f64, score):
+    ctx, ds, host, torch = setup
+    from kmer_spans_amd import device as D
+    counts = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+    words = D.count(ctx, ds, k, counts)
+    thr = 0.75 if score == "rank" else 0.0
+    w = torch.empty(4 ** k, dtype=torch.float64, device="cuda")
+    tab = D.DeviceTable.from_counts(ctx, counts, k, score, total=words, thr=thr, expand=True,
+                                    max_ext_bytes=int(cap * GiB), w_out=w)
+    own = own_f64 if score == "rank" else own_u16
+    J = own + (1 if score == "rank" else 2)
+    assert tab.positions_per_read == J, (score, k, cap, tab.positions_per_read)
+    wh = w.cpu().numpy()
+    o = oracle.scan(host, k, wh, thr, 100 if score != "pm1" else 20, 20.0 if score != "pm1" else 5.0, visits=True)
+    mw, ms = (100, 20.0) if score != "pm1" else (20, 5.0)
+    for route in ("count", "atomic"):
+        if route == "atomic":
+            monkeypatch.setenv("KS_VISITS_ATOMIC", "1")
+        ctx.set_scan_algo(1)
+        vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+        pos, sc, st = D.scan(ctx, ds, k, tab, mw, ms, vis)
+        assert st["scan_algo"] == 1
+        _same(pos, sc, o["pos"], o["score"], (score, k, cap, route))
+        assert np.array_equal(vis.cpu().numpy(), o["counts"]), (score, k, cap, route, "visits")
+        monkeypatch.delenv("KS_VISITS_ATOMIC", raising=False)
+    ctx.set_scan_algo(-1)
+    tab.close()
+
+
+@pytest.mark.parametrize("k,cap", [(13, 80), (11, 5)])
+def test_line_trlr(oracle, setup, k, cap):
+    """tr_lr regions through the line pass (the first k-mer's own score at
+    each run start, 1-based records), log2 table as both tables."""
+    ctx, ds, host, torch = setup
+    from kmer_spans_amd import device as D
+    counts = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+    words = D.count(ctx, ds, k, counts)
+    w = torch.empty(4 ** k, dtype=torch.float64, device="cuda")
+    tab = D.DeviceTable.from_counts(ctx, counts, k, "log2", total=words, expand=True, max_ext_bytes=int(cap * GiB),
+                                    w_out=w)
+    assert tab.positions_per_read >= 4
+    wh = w.cpu().numpy()
+    init = D.DeviceTable(ctx, wh, k, 0.0, compress=False)
+    o = oracle.tr_lr_regions(host, k, 50, wh, wh)
+    ctx.set_scan_algo(1)
+    pos, sc, st = D.tr_lr(ctx, ds, k, tab, init, 50)
+    ctx.set_scan_algo(-1)
+    _same(pos, sc, o["pos"], o["score"], ("trlr", k, cap))
+    tab.close()
+    init.close()
+
+
+def test_line_vs_expanded_same_regions(setup, monkeypatch):
+    """The metric-shaped config (k = 13, log2) through the line table and
+    through the J = 5 expanded table: identical regions and scores."""
+    ctx, ds, host, torch = setup
+    from kmer_spans_amd import device as D
+    k = 13
+    counts = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+    words = D.count(ctx, ds, k, counts)
+    out = []
+    for lines in (True, False):
+        if not lines:
+            monkeypatch.setenv("KS_NO_LINES", "1")
+        tab = D.DeviceTable.from_counts(ctx, counts, k, "log2", total=words, expand=True)
+        assert tab.positions_per_read == 5
+        assert tab.code_bits == (16 if lines else 12)
+        ctx.set_scan_algo(1)
+        out.append(D.scan(ctx, ds, k, tab, 100, 20.0)[:2])
+        ctx.set_scan_algo(-1)
+        tab.close()
+    _same(out[0][0], out[0][1], out[1][0], out[1][1], "line vs expanded")

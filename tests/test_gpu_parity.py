@@ -437,6 +437,7 @@ def test_code12_tables(K, oracle, ctx, monkeypatch, k, ndist, force):
     (k+4)-mer indices beyond 32 bits at k=13."""
     import torch
     from kmer_spans_amd import device as D, genome
+    monkeypatch.setenv("KS_NO_LINES", "1")  # the (k+4)-mer form, not a line table
     if force:
         monkeypatch.setenv("KS_EXT_ESCAPE_MAX", "1.0")
     torch.cuda.empty_cache()  # the 128 GiB J = 5 table at k = 13 must fit beside torch's cache

@@ -1117,17 +1117,20 @@ __global__ void __launch_bounds__(kF64 ? 1024 : 768) k_pass1l(Chunks g, int64_t 
     }
   }
   const int f0 = first ? 0 : -1;
+  // keys of the step being processed and of the two in flight
+  uint64_t x1 = 0, x2 = 0;
+  auto next_key = [&](uint64_t xp) -> uint64_t {
+    refill();
+    return ((xp << (2 * J)) | take(J)) & xmask;
+  };
   issue((uint32_t)(x >> (2 * LV)), 0);
+  x1 = next_key(x);
+  issue((uint32_t)(x1 >> (2 * LV)), 1);
   for (int st = 0; st < NS; ++st) {
     const uint64_t xs = x;  // key of this step
-    if (st + 1 < NS) {      // the next step's lines in flight, then this step's complete
-      refill();
-      x = ((x << (2 * J)) | take(J)) & xmask;
-      issue((uint32_t)(x >> (2 * LV)), (st + 1) & 1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // this step's lines complete (the next step's four loads may stay in flight)
+    if (st + 1 < NS) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint8_t *ln = ring + (st & 1) * 4096 + lane * 64;
     double v[J];
     if (!kF64) {
@@ -1153,6 +1156,15 @@ __global__ void __launch_bounds__(kF64 ? 1024 : 768) k_pass1l(Chunks g, int64_t 
 #pragma unroll
       for (int t = 0; t < OWN; ++t) v[t] = lv[t];
       v[OWN] = lv[OWN + ((int)xs & 3)];
+    }
+    // the step after next into the slot just read: two steps in flight
+    // while this one is processed
+    x = x1;
+    if (st + 2 < NS) {
+      x2 = next_key(x1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done before it is refilled
+      issue((uint32_t)(x2 >> (2 * LV)), st & 1);
+      x1 = x2;
     }
 #pragma unroll
     for (int t = 0; t < J; ++t) {

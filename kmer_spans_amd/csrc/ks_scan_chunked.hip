@@ -232,6 +232,66 @@ __device__ __forceinline__ void load_codes16(const uint16_t *__restrict__ codes,
   }
 }
 
+// Values of NV consecutive scan indices from a line table (ks_table
+// line_kind), OWN + 1 per line read: the line's own entries and the L1 entry
+// chosen by the next base (its first 16-32 B; lane-wise reads, for the
+// passes after pass 1).  x: 64 bits of packed bases from the first base of
+// index b0's k-mer; indices past n read nothing and get 0.
+template <int OWN, int NV>
+__device__ __forceinline__ void line_values(const TableView &tv, uint64_t x, int k, int b0, int n, double v[NV],
+                                            const double *s_lut) {
+  constexpr int JL = OWN + 1;
+  const int kx = k + OWN;  // the (m + 1)-mer: line index and the L1 base
+  const uint64_t xmask = (1ull << (2 * kx)) - 1ull;
+#pragma unroll
+  for (int o = 0; o < NV; o += JL) {
+    double lv[JL];
+#pragma unroll
+    for (int t = 0; t < JL; ++t) lv[t] = 0.0;
+    if (b0 + o < n) {
+      const uint64_t gx = (x >> (64 - 2 * (o + kx))) & xmask;
+      const uint8_t *ln = tv.line + (size_t)(gx >> 2) * 64;
+      const uint32_t c1 = (uint32_t)gx & 3u;
+      if (tv.line_kind == 1) {
+        uint32_t h[16];
+        const uint4 q0 = *reinterpret_cast<const uint4 *>(ln);
+        h[0] = q0.x & 0xffffu; h[1] = q0.x >> 16; h[2] = q0.y & 0xffffu; h[3] = q0.y >> 16;
+        h[4] = q0.z & 0xffffu; h[5] = q0.z >> 16; h[6] = q0.w & 0xffffu; h[7] = q0.w >> 16;
+        if (OWN + 4 > 8) {
+          const uint4 q1 = *reinterpret_cast<const uint4 *>(ln + 16);
+          h[8] = q1.x & 0xffffu; h[9] = q1.x >> 16; h[10] = q1.y & 0xffffu; h[11] = q1.y >> 16;
+          h[12] = q1.z & 0xffffu; h[13] = q1.z >> 16; h[14] = q1.w & 0xffffu; h[15] = q1.w >> 16;
+        }
+        uint32_t cs[JL];
+#pragma unroll
+        for (int t = 0; t < OWN; ++t) cs[t] = h[t];
+        cs[OWN] = c1 == 0 ? h[OWN] : (c1 == 1 ? h[OWN + 1] : (c1 == 2 ? h[OWN + 2] : h[OWN + 3]));
+#pragma unroll
+        for (int t = 0; t < JL; ++t) lv[t] = s_lut ? s_lut[cs[t]] : tv.lut[cs[t]];
+      } else {
+        const double *d = reinterpret_cast<const double *>(ln);
+#pragma unroll
+        for (int t = 0; t < OWN; ++t) lv[t] = d[t];
+        lv[OWN] = d[OWN + c1];
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < JL; ++t)
+      if (o + t < NV) v[o + t] = (b0 + o + t < n) ? lv[t] : 0.0;
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void line_values_any(const TableView &tv, uint64_t x, int k, int b0, int n, double v[NV],
+                                                const double *s_lut) {
+  switch (tv.line_own) {
+    case 2: line_values<2, NV>(tv, x, k, b0, n, v, s_lut); break;
+    case 3: line_values<3, NV>(tv, x, k, b0, n, v, s_lut); break;
+    case 4: line_values<4, NV>(tv, x, k, b0, n, v, s_lut); break;
+    default: line_values<5, NV>(tv, x, k, b0, n, v, s_lut); break;
+  }
+}
+
 // Values of scan indices b0 .. b0+15 of chunk c (0 past n) of a compressed
 // table whose per-index codes were not stored (small-k pass 1): the 16
 // k-mers from one 64-bit window of packed bases (bytes near the buffer end),
@@ -244,6 +304,10 @@ __device__ __forceinline__ void values16_nostore(const Chunks &g, const uint8_t 
   const uint32_t kmask = (1u << (2 * k)) - 1u;
   uint64_t x = 0;
   const bool pk = packed_bits(g.packed, total, p, x);
+  if (pk && tv.line) {  // line table: OWN + 1 indices per read
+    line_values_any<NV>(tv, x, k, b0, n, v, s_lut);
+    return;
+  }
   if (pk && tv.ext && tv.ext_J >= 2 && k + tv.ext_J - 1 + 15 <= 32) {
     // one expanded-table read per J indices (the gathers of k_summ_fixw and
     // the heads: 4 random requests per 16 indices at J = 5 instead of 32)
@@ -305,6 +369,13 @@ __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restri
     return;
   }
   const int64_t p = g.start[c] + i0;
+  if (tv.line) {  // line table: OWN + 1 indices per read
+    uint64_t xp = 0;
+    if (packed_bits(g.packed, total, p - k, xp)) {
+      line_values_any<4>(tv, xp, k, i0, n, v, nullptr);
+      return;
+    }
+  }
   if (!tv.compressed && tv.ext && tv.ext_J == 4) {  // FP64 expanded table: the 4 values in one 32-B entry
     uint64_t xp = 0;
     const uint64_t gcode = packed_bits(g.packed, total, p - k, xp) ? (xp >> (64 - 2 * (k + 3)))

@@ -484,12 +484,15 @@ def main():
     if stats[-1]["scan_algo"] == 1:
         J = max(1, int(table.positions_per_read))
         n_scored = int(stats[-1]["n_scored"])
-        reads = n_scored / J + (n_scored * float(table.escape_fraction) if table.code_bits == 12 else 0.0)
+        esc = float(table.escape_fraction)
+        # escapes: 12-bit (k+4)-mer table: per scan index; wide lines (13-bit): per line (its L3 index)
+        reads = n_scored / J + (n_scored * esc if table.code_bits == 12 else
+                                n_scored / J * esc if table.code_bits == 13 else 0.0)
         ra = {"table_reads_per_launch": int(reads), "positions_per_read": J,
               "achieved_G_per_s": round(reads / (ms_kernel * 1e-3) / 1e9, 2), "wall_G_per_s": RANDOM_WALL_GPS,
               "frac": round(reads / (ms_kernel * 1e-3) / 1e9 / RANDOM_WALL_GPS, 4),
-              "wall_source": "profiles/r2/frag_probe.txt (random 16-B reads from a physically contiguous 128 GiB "
-                             "buffer: 49.3-50.6 G/s; scattered VRAM 47.5-48.9)"}
+              "wall_source": "profiles/r3/line_bench.txt (random 16-128-B lines from a physically contiguous "
+                             "128 GiB buffer, fetched by 1-8 lanes each: 49.9-50.3 G lines/s)"}
         if traffic:
             ra["memory_read_requests_per_launch"] = traffic["read_requests"]
             ra["memory_requests_G_per_s"] = round(traffic["read_requests"] / (ms_kernel * 1e-3) / 1e9, 2)

@@ -159,13 +159,20 @@ typedef struct ks_dev_seqs {
  *  KS_TABLE_COMPRESS  if the table has at most 65536 distinct values, store
  *                     it as a uint16 code table plus an FP64 value LUT
  *                     (exact: the LUT holds the very same doubles);
- *  KS_TABLE_EXPAND    also build the expanded table: one entry per
- *                     (k+J-1)-mer holding the J codes/values of its J
- *                     consecutive k-mers (J <= 5, up to 128 GiB of the
- *                     GPU's HBM), so the scan issues one random read per J
- *                     scan indices.  J = 5 uses 12-bit codes for the 4095
- *                     values covering most positions and an escape to the
- *                     base table for the rest.  Skipped when it does not fit. */
+ *  KS_TABLE_EXPAND    also build an expanded table, so the scan issues one
+ *                     random read per J scan indices (up to 128 GiB of the
+ *                     GPU's HBM; skipped when it does not fit):
+ *                     k = 8..13: a line table, one 64-B line per m-mer (m =
+ *                     k + own - 1 <= 15) holding the codes / values of its
+ *                     own k-mers and of every one- and two-base (FP64: one-
+ *                     base) continuation, J = own + 2 (own + 1); at k = 12,
+ *                     13 with <= 7168 distinct values, 128-B lines with
+ *                     13-bit codes and the three-base continuations as
+ *                     11-bit codes (escape to the base table), J = own + 3
+ *                     (6 at k = 13);
+ *                     other k: one entry per (k+J-1)-mer holding the J
+ *                     codes / values of its J consecutive k-mers (J <= 5;
+ *                     J = 5 with 12-bit codes and an escape). */
 #define KS_TABLE_COMPRESS 1
 #define KS_TABLE_EXPAND 2
 typedef struct ks_table ks_table;
@@ -217,11 +224,13 @@ int64_t ks_table_distinct(const ks_table *t);
 /* Scan indices served per random table read (J of the expanded table, 1 if
  * it was not built). */
 int32_t ks_table_positions_per_read(const ks_table *t);
-/* Bits per value code in the expanded table (12 or 16), 16 for a compressed
- * table without one, 64 for an FP64 table. */
+/* Bits per value code in the expanded table (12, 13 for 128-B lines, 16),
+ * 16 for a compressed table without one, 64 for an FP64 table. */
 int32_t ks_table_code_bits(const ks_table *t);
 /* Share of positions (by the hint, else by k-mer multiplicity) whose value
- * escapes the 12-bit codes; 0 unless code bits are 12. */
+ * escapes the short codes: the 12-bit codes (code bits 12, every index) or
+ * the 11-bit three-base continuations of 128-B lines (code bits 13, one
+ * index per line); 0 otherwise. */
 double ks_table_escape_fraction(const ks_table *t);
 
 /* Shape and setup cost of a device table (host wall clock around the

@@ -250,9 +250,24 @@ __device__ __forceinline__ void line_values(const TableView &tv, uint64_t x, int
     for (int t = 0; t < JL; ++t) lv[t] = 0.0;
     if (b0 + o < n) {
       const uint64_t gx = (x >> (64 - 2 * (o + kx))) & xmask;
-      const uint8_t *ln = tv.line + (size_t)(gx >> 2) * 64;
+      const uint8_t *ln = tv.line + (size_t)(gx >> 2) * (tv.line_kind == 3 ? 128 : 64);
       const uint32_t c1 = (uint32_t)gx & 3u;
-      if (tv.line_kind == 1) {
+      if (tv.line_kind == 3) {  // wide: 13-bit own / L1 codes in the first 16 B
+        const uint4 q0 = *reinterpret_cast<const uint4 *>(ln);
+        const uint64_t lo = (uint64_t)q0.x | ((uint64_t)q0.y << 32), hi = (uint64_t)q0.z | ((uint64_t)q0.w << 32);
+        auto f13 = [&](int b) -> uint32_t {
+          const uint64_t w = b < 64 ? ((lo >> b) | (b > 51 ? (hi << (64 - b)) : 0ull)) : (hi >> (b - 64));
+          return (uint32_t)w & 0x1fffu;
+        };
+        uint32_t cs[JL];
+#pragma unroll
+        for (int t = 0; t < OWN; ++t) cs[t] = f13(13 * t);
+        const uint32_t l0 = f13(13 * OWN), l1 = f13(13 * (OWN + 1)), l2 = f13(13 * (OWN + 2)),
+                       l3 = f13(13 * (OWN + 3));
+        cs[OWN] = c1 == 0 ? l0 : (c1 == 1 ? l1 : (c1 == 2 ? l2 : l3));
+#pragma unroll
+        for (int t = 0; t < JL; ++t) lv[t] = s_lut ? s_lut[cs[t]] : tv.lut[cs[t]];
+      } else if (tv.line_kind == 1) {
         uint32_t h[16];
         const uint4 q0 = *reinterpret_cast<const uint4 *>(ln);
         h[0] = q0.x & 0xffffu; h[1] = q0.x >> 16; h[2] = q0.y & 0xffffu; h[3] = q0.y >> 16;
@@ -1068,6 +1083,191 @@ __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds) {
                : "memory");
 }
 
+// Per-lane state of a line pass over one chunk: the clean-entry trajectory,
+// its aggregates, closed candidates and (kSumm) the binade-integer summaries
+// in the predicted binade and its neighbour -- the per-index work of
+// k_pass1p, shared by k_pass1l and k_pass1w.
+template <bool kSumm, bool kTrlr>
+struct P1Lane {
+  int64_t start;
+  int n, f0;
+  double prev = 0.0, best = 0.0;
+  int beg = -1, arg = 0;
+  double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
+  bool special = false;
+  int se = INT32_MIN, se2 = INT32_MIN;
+  double sC = 0.0, sH = 0.0, scur = 0.0, smx = -INFINITY;
+  double sC2 = 0.0, sH2 = 0.0, scur2 = 0.0, smx2 = -INFINITY;
+  int sarg = 0, sarg2 = 0;
+  bool sbad = false, sbad2 = false;
+
+  __device__ __forceinline__ void init(int64_t st, int nn, bool first, bool live, double xp) {
+    start = st;
+    n = nn;
+    f0 = first ? 0 : -1;
+    if (kSumm && live && xp >= kP1SumMin && xp < 1.0e15) {
+      se = binade_of(xp);
+      sC = 1.5 * ldexp(1.0, se);
+      sH = ldexp(1.0, se - 53);
+      const double lo = ldexp(1.0, se);
+      if (xp < lo * (1.0 + kP1Margin)) se2 = se - 1;
+      else if (xp > 2.0 * lo * (1.0 - kP1Margin)) se2 = se + 1;
+      if (se2 != INT32_MIN) {
+        sC2 = 1.5 * ldexp(1.0, se2);
+        sH2 = ldexp(1.0, se2 - 53);
+      }
+    }
+  }
+
+  // scan index i (< n) with value s
+  __device__ __forceinline__ void step(double s, int i, const EmitCfg &ec, const Cand &cand) {
+    asum += s;
+    pmin = asum < pmin ? asum : pmin;
+    pmax = asum > pmax ? asum : pmax;
+    sabs += fabs(s);
+    special |= !isfinite(s);
+    if (kSumm && se != INT32_MIN) {
+      const double r = (s + sC) - sC;
+      sbad |= fabs(r - s) == sH;
+      scur += r;
+      const bool su = scur > smx;
+      smx = su ? scur : smx;
+      sarg = su ? i : sarg;
+      if (se2 != INT32_MIN) {
+        const double r2 = (s + sC2) - sC2;
+        sbad2 |= fabs(r2 - s) == sH2;
+        scur2 += r2;
+        const bool su2 = scur2 > smx2;
+        smx2 = su2 ? scur2 : smx2;
+        sarg2 = su2 ? i : sarg2;
+      }
+    }
+    // clean trajectory (k_pass1p)
+    const double tt = prev + s;
+    const double S = tt > 0 ? tt : 0.0;
+    const bool open = (prev == 0) & (S > 0);
+    const bool close = (prev > 0) & (S == 0);
+    const long long ml = kTrlr ? ec.min_len : 0;
+    const bool want =
+        kTrlr ? (close & (((long long)((arg != f0 ? arg - 1 : arg) - (beg != f0 ? beg - 1 : beg)) >= ml) |
+                          ((long long)((i != f0 ? i - 1 : i) - (arg != f0 ? arg - 1 : arg) - 1) >=
+                           (ml > 1 ? ml : 1LL))))
+              : (close & ((uint64_t)(int64_t)(arg - beg) >= ec.mw) & (best >= ec.min_score));
+    if (want) {
+      const int64_t slot = append_one(cand.count, cand.segcap);
+      if (slot >= 0) {
+        cand.beg[slot] = start + beg;
+        cand.arg[slot] = start + arg;
+        cand.rst[slot] = start + i;
+        cand.best[slot] = best;
+      }
+    }
+    const bool up = open | (S > best);
+    best = up ? S : best;
+    arg = up ? i : arg;
+    beg = open ? i : (close ? -1 : beg);
+    prev = S;
+  }
+
+  __device__ __forceinline__ void finish(int64_t c, const P1 &o, const SummP1 &sp) {
+    if (kSumm) {  // as in k_pass1p
+      auto put = [&](int t, int e, bool bad, double cur, double mx, int aa) {
+        const double lim = ldexp(1.0, e);
+        const bool ok = e != INT32_MIN && !bad && sabs < 0.5 * lim && mx < 0.5 * lim && pmin > -0.5 * lim;
+        sp.e[2 * c + t] = ok ? e : INT32_MIN;
+        if (ok) {
+          const double sc = ldexp(1.0, 52 - e);
+          sp.D[2 * c + t] = (long long)(cur * sc);
+          sp.M[2 * c + t] = (long long)(mx * sc);
+          sp.N[2 * c + t] = (long long)floor((pmin - sabs * 0x1p-44) * sc) - 130;
+          sp.A[2 * c + t] = aa;
+        }
+      };
+      put(0, se, sbad, scur, smx, sarg);
+      put(1, se2, sbad2, scur2, smx2, sarg2);
+    }
+    o.cexit[c] = prev;
+    o.asum[c] = asum;
+    o.pmin[c] = pmin;
+    o.pmax[c] = pmax;
+    o.sabs[c] = sabs;
+    o.special[c] = special ? 1 : 0;
+    if (prev > 0) {
+      o.tbeg[c] = beg; o.tmax[c] = best; o.targ[c] = arg;
+    } else {
+      o.tbeg[c] = -1; o.tmax[c] = 0.0; o.targ[c] = 0;
+    }
+  }
+};
+
+// The lane's packed 2-bit bases from the word holding base p0 on, kLineWords
+// words in registers (guarded at the end of the packed array), and a rolling
+// supply: acc holds na bases in its top 2 na bits; refill() appends the next
+// word when 16 or fewer are left and shifts the word array down.
+struct LaneBases {
+  uint32_t a[kLineWords];
+  uint64_t acc = 0;
+  int na = 0;
+
+  __device__ __forceinline__ void load(const uint32_t *__restrict__ packed, int64_t total, int64_t p0) {
+    const int64_t w0 = p0 >> 4, wlast = total >> 4;  // words 0 .. total >> 4 exist
+    const int64_t wa = w0 & ~(int64_t)3;
+    if (wa + 24 <= wlast + 1) {
+      uint32_t v[24];
+      const uint4 *P4 = reinterpret_cast<const uint4 *>(packed + wa);
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {
+        const uint4 q = P4[t];
+        v[4 * t] = q.x;
+        v[4 * t + 1] = q.y;
+        v[4 * t + 2] = q.z;
+        v[4 * t + 3] = q.w;
+      }
+      const int off = (int)(w0 - wa);
+#pragma unroll
+      for (int t = 0; t < kLineWords; ++t)
+        a[t] = off == 0 ? v[t] : (off == 1 ? v[t + 1] : (off == 2 ? v[t + 2] : v[t + 3]));
+    } else {
+#pragma unroll
+      for (int t = 0; t < kLineWords; ++t) a[t] = packed[min(w0 + t, wlast)];
+    }
+    refill();
+    refill();
+    const int sk = (int)(p0 & 15);
+    acc <<= 2 * sk;
+    na -= sk;
+  }
+  __device__ __forceinline__ void refill() {
+    const bool r = na <= 16;
+    acc |= r ? ((uint64_t)a[0] << (32 - 2 * na)) : 0ull;
+    na += r ? 16 : 0;
+#pragma unroll
+    for (int t = 0; t < kLineWords - 1; ++t) a[t] = r ? a[t + 1] : a[t];
+  }
+  // nb <= 16 bases (after a refill), first base most significant
+  __device__ __forceinline__ uint64_t take(int nb) {
+    const uint64_t v = acc >> (64 - 2 * nb);
+    acc <<= 2 * nb;
+    na -= nb;
+    return v;
+  }
+  // the (kx)-mer of the next kx bases (kx <= 32), then steps of J bases
+  __device__ __forceinline__ uint64_t first_key(int kx) {
+    uint64_t x = 0;
+    for (int left = kx; left > 0;) {
+      refill();
+      const int nb = left < 16 ? left : 16;
+      x = (x << (2 * nb)) | take(nb);
+      left -= nb;
+    }
+    return x;
+  }
+  __device__ __forceinline__ uint64_t next_key(uint64_t xp, int J, uint64_t xmask) {
+    refill();
+    return ((xp << (2 * J)) | take(J)) & xmask;
+  }
+};
+
 template <int OWN, bool kF64, bool kLdsLut, bool kTrlr>
 __global__ void __launch_bounds__(kF64 ? 1024 : 768) k_pass1l(Chunks g, int64_t total, int k, TableView tv,
                                                               EmitCfg ec, uint32_t *__restrict__ visits, P1 o,
@@ -1093,61 +1293,13 @@ __global__ void __launch_bounds__(kF64 ? 1024 : 768) k_pass1l(Chunks g, int64_t 
   const int n = live ? g.n[c] : 0;
   const bool first = live && (c == 0 || g.run[c - 1] != g.run[c]);
   const uint32_t kmask = (1u << (2 * k)) - 1u;
-
-  // ---- the lane's bases: packed words from the one holding base start - k
-  uint32_t a[kLineWords];
-  {
-    const uint32_t *__restrict__ packed = g.packed;
-    const int64_t w0 = (start - k) >> 4, wlast = total >> 4;  // words 0 .. total >> 4 exist
-    const int64_t wa = w0 & ~(int64_t)3;
-    if (wa + 24 <= wlast + 1) {
-      uint32_t v[24];
-      const uint4 *P4 = reinterpret_cast<const uint4 *>(packed + wa);
-#pragma unroll
-      for (int t = 0; t < 6; ++t) {
-        const uint4 q = P4[t];
-        v[4 * t] = q.x;
-        v[4 * t + 1] = q.y;
-        v[4 * t + 2] = q.z;
-        v[4 * t + 3] = q.w;
-      }
-      const int off = (int)(w0 - wa);
-#pragma unroll
-      for (int t = 0; t < kLineWords; ++t)
-        a[t] = off == 0 ? v[t] : (off == 1 ? v[t + 1] : (off == 2 ? v[t + 2] : v[t + 3]));
-    } else {
-#pragma unroll
-      for (int t = 0; t < kLineWords; ++t) a[t] = packed[min(w0 + t, wlast)];
-    }
-  }
-  // rolling supply: acc holds na bases in its top 2 na bits; a refill appends
-  // the next word when 16 or fewer are left and shifts the word array down
-  uint64_t acc = 0;
-  int na = 0;
-  auto refill = [&]() {
-    const bool r = na <= 16;
-    acc |= r ? ((uint64_t)a[0] << (32 - 2 * na)) : 0ull;
-    na += r ? 16 : 0;
-#pragma unroll
-    for (int t = 0; t < kLineWords - 1; ++t) a[t] = r ? a[t + 1] : a[t];
-  };
-  auto take = [&](int nb) -> uint64_t {  // nb <= 17 bases (after a refill), first base most significant
-    const uint64_t v = acc >> (64 - 2 * nb);
-    acc <<= 2 * nb;
-    na -= nb;
-    return v;
-  };
-  refill();
-  refill();
-  {
-    const int sk = (int)((start - k) & 15);
-    acc <<= 2 * sk;
-    na -= sk;
-  }
-  refill();
+  P1Lane<kSumm, kTrlr> L;
+  L.init(start, n, first, live, (kSumm && live) ? xh[c] : 0.0);
+  LaneBases B;
+  B.load(g.packed, total, start - k);
   const int kx = k + J - 1;  // key length (<= 17)
   const uint64_t xmask = (1ull << (2 * kx)) - 1ull;
-  uint64_t x = take(kx);     // key of step 0
+  uint64_t x = B.first_key(kx);  // key of step 0
   // tr_lr: the run's first scan index scores the first k-mer's own score
   const double first_val = (kTrlr && first) ? ec.ks[(uint32_t)(x >> (2 * (J - 1))) & kmask] : 0.0;
 
@@ -1162,40 +1314,10 @@ __global__ void __launch_bounds__(kF64 ? 1024 : 768) k_pass1l(Chunks g, int64_t 
       glds16(lines + (size_t)li * 64 + (lane & 3) * 16, ring_lds + (uint32_t)(slot * 4096 + q * 1024));
     }
   };
-  double prev = 0.0, best = 0.0;
-  int beg = -1, arg = 0;
-  double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
-  bool special = false;
-  // binade summaries (compressed tables), as in k_pass1p
-  int se = INT32_MIN, se2 = INT32_MIN;
-  double sC = 0.0, sH = 0.0, scur = 0.0, smx = -INFINITY;
-  double sC2 = 0.0, sH2 = 0.0, scur2 = 0.0, smx2 = -INFINITY;
-  int sarg = 0, sarg2 = 0;
-  bool sbad = false, sbad2 = false;
-  if (kSumm && live) {
-    const double xp = xh[c];
-    if (xp >= kP1SumMin && xp < 1.0e15) {
-      se = binade_of(xp);
-      sC = 1.5 * ldexp(1.0, se);
-      sH = ldexp(1.0, se - 53);
-      const double lo = ldexp(1.0, se);
-      if (xp < lo * (1.0 + kP1Margin)) se2 = se - 1;
-      else if (xp > 2.0 * lo * (1.0 - kP1Margin)) se2 = se + 1;
-      if (se2 != INT32_MIN) {
-        sC2 = 1.5 * ldexp(1.0, se2);
-        sH2 = ldexp(1.0, se2 - 53);
-      }
-    }
-  }
-  const int f0 = first ? 0 : -1;
   // keys of the step being processed and of the two in flight
   uint64_t x1 = 0, x2 = 0;
-  auto next_key = [&](uint64_t xp) -> uint64_t {
-    refill();
-    return ((xp << (2 * J)) | take(J)) & xmask;
-  };
   issue((uint32_t)(x >> (2 * LV)), 0);
-  x1 = next_key(x);
+  x1 = B.next_key(x, J, xmask);
   issue((uint32_t)(x1 >> (2 * LV)), 1);
   for (int st = 0; st < NS; ++st) {
     const uint64_t xs = x;  // key of this step
@@ -1232,7 +1354,7 @@ __global__ void __launch_bounds__(kF64 ? 1024 : 768) k_pass1l(Chunks g, int64_t 
     // while this one is processed
     x = x1;
     if (st + 2 < NS) {
-      x2 = next_key(x1);
+      x2 = B.next_key(x1, J, xmask);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done before it is refilled
       issue((uint32_t)(x2 >> (2 * LV)), st & 1);
       x1 = x2;
@@ -1241,86 +1363,168 @@ __global__ void __launch_bounds__(kF64 ? 1024 : 768) k_pass1l(Chunks g, int64_t 
     for (int t = 0; t < J; ++t) {
       const int i = st * J + t;
       if (i < n) {
-        double s = v[t];
-        if (kTrlr && first && i == 0) s = first_val;
+        double sv = v[t];
+        if (kTrlr && first && i == 0) sv = first_val;
         if (visits) atomicAdd(&visits[(uint32_t)(xs >> (2 * (J - 1 - t))) & kmask], 1u);
-        asum += s;
-        pmin = asum < pmin ? asum : pmin;
-        pmax = asum > pmax ? asum : pmax;
-        sabs += fabs(s);
-        special |= !isfinite(s);
-        if (kSumm && se != INT32_MIN) {
-          const double r = (s + sC) - sC;
-          sbad |= fabs(r - s) == sH;
-          scur += r;
-          const bool su = scur > smx;
-          smx = su ? scur : smx;
-          sarg = su ? i : sarg;
-          if (se2 != INT32_MIN) {
-            const double r2 = (s + sC2) - sC2;
-            sbad2 |= fabs(r2 - s) == sH2;
-            scur2 += r2;
-            const bool su2 = scur2 > smx2;
-            smx2 = su2 ? scur2 : smx2;
-            sarg2 = su2 ? i : sarg2;
-          }
-        }
-        // clean trajectory (k_pass1p)
-        const double tt = prev + s;
-        const double S = tt > 0 ? tt : 0.0;
-        const bool open = (prev == 0) & (S > 0);
-        const bool close = (prev > 0) & (S == 0);
-        const long long ml = kTrlr ? ec.min_len : 0;
-        const bool want =
-            kTrlr ? (close & (((long long)((arg != f0 ? arg - 1 : arg) - (beg != f0 ? beg - 1 : beg)) >= ml) |
-                              ((long long)((i != f0 ? i - 1 : i) - (arg != f0 ? arg - 1 : arg) - 1) >=
-                               (ml > 1 ? ml : 1LL))))
-                  : (close & ((uint64_t)(int64_t)(arg - beg) >= ec.mw) & (best >= ec.min_score));
-        if (want) {
-          const int64_t slot = append_one(cand.count, cand.segcap);
-          if (slot >= 0) {
-            cand.beg[slot] = start + beg;
-            cand.arg[slot] = start + arg;
-            cand.rst[slot] = start + i;
-            cand.best[slot] = best;
-          }
-        }
-        const bool up = open | (S > best);
-        best = up ? S : best;
-        arg = up ? i : arg;
-        beg = open ? i : (close ? -1 : beg);
-        prev = S;
+        L.step(sv, i, ec, cand);
       }
     }
   }
-  if (!live) return;
-  if (kSumm) {  // as in k_pass1p
-    auto put = [&](int t, int e, bool bad, double cur, double mx, int aa) {
-      const double lim = ldexp(1.0, e);
-      const bool ok = e != INT32_MIN && !bad && sabs < 0.5 * lim && mx < 0.5 * lim && pmin > -0.5 * lim;
-      sp.e[2 * c + t] = ok ? e : INT32_MIN;
-      if (ok) {
-        const double sc = ldexp(1.0, 52 - e);
-        sp.D[2 * c + t] = (long long)(cur * sc);
-        sp.M[2 * c + t] = (long long)(mx * sc);
-        sp.N[2 * c + t] = (long long)floor((pmin - sabs * 0x1p-44) * sc) - 130;
-        sp.A[2 * c + t] = aa;
+  if (live) L.finish(c, o, sp);
+}
+
+// Pass 1 on a wide line table (line_kind 3, 128-B lines, k_build_line_wide):
+// own / L1 / L2 entries as 13-bit codes (the uint16 codes of a table with at
+// most kLineLutMax distinct values: never an escape), the 64 L3 entries (the
+// three-base continuations) as 11-bit codes, 2047 escaping to the base code
+// table.  J = own + 3 indices per random request (6 at k = 13: 0.51 G
+// requests per 3.06 G indices instead of 0.61 G), at 128 B per request: the
+// size at which random lines still come at ~50 G/s (6.4 TB/s,
+// profiles/r3/line_bench.txt).  Eight lanes load a line.  A step's L3 escape
+// (one at most) is loaded right after its line is decoded
+// (global_load_lds_dword of the code pair; a lane without one reads the
+// table's first pair), and the step is processed one step later, when it
+// has landed: every step then needs one counted wait, whatever the escapes.
+constexpr int kWideBlock = 384;  // 6 waves: ring 96 KiB + LUT 56 KiB + escape slots 3 KiB
+
+// One global_load_lds_dword: 4 B from each lane's gsrc to LDS lds + 4 x lane.
+__device__ __forceinline__ void glds4(const void *gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds)
+               : "memory");
+}
+
+// nb-bit field at bit b of a line in LDS (b dynamic; two dwords).
+__device__ __forceinline__ uint32_t wide_field(const uint8_t *ln, uint32_t b, uint32_t mask) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(ln) + (b >> 5);
+  const uint64_t v = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  return (uint32_t)(v >> (b & 31)) & mask;
+}
+
+template <int OWN, bool kTrlr>
+__global__ void __launch_bounds__(kWideBlock) k_pass1w(Chunks g, int64_t total, int k, TableView tv, EmitCfg ec,
+                                                       uint32_t *__restrict__ visits, P1 o, Cand cand,
+                                                       const double *__restrict__ xh, SummP1 sp) {
+  constexpr int BS = kWideBlock;
+  constexpr int J = OWN + 3;
+  constexpr int NS = (CH + J - 1) / J;
+  constexpr int N13 = OWN + 20;
+  constexpr uint32_t B3 = 13 * N13;  // first L3 bit
+  static_assert(13 * (OWN + 4) <= 128, "own + L1 in the first 16 B");
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[(BS / 64) * 2 * 8192];
+  __shared__ __attribute__((aligned(16))) uint32_t s_esc[(BS / 64) * 2 * 64];
+  __shared__ double s_lut[kLineLutMax];
+  for (int i = threadIdx.x; i < tv.nlut; i += BS) s_lut[i] = tv.lut[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t c = g.c0 + (int64_t)blockIdx.x * BS + threadIdx.x;
+  if (c - lane >= g.nch) return;
+  const bool live = c < g.nch;
+  const int64_t start = live ? g.start[c] : (int64_t)k;
+  const int n = live ? g.n[c] : 0;
+  const bool first = live && (c == 0 || g.run[c - 1] != g.run[c]);
+  const uint32_t kmask = (1u << (2 * k)) - 1u;
+  P1Lane<true, kTrlr> L;
+  L.init(start, n, first, live, live ? xh[c] : 0.0);
+  LaneBases B;
+  B.load(g.packed, total, start - k);
+  const int kx = k + J - 1;  // key length (<= 18)
+  const uint64_t xmask = (1ull << (2 * kx)) - 1ull;
+  uint64_t x = B.first_key(kx);
+  const double first_val = (kTrlr && first) ? ec.ks[(uint32_t)(x >> (2 * (J - 1))) & kmask] : 0.0;
+
+  uint8_t *const ring = s_ring + wv * 16384;
+  uint32_t *const esc = s_esc + wv * 128;
+  const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+  const uint32_t esc_lds = __builtin_amdgcn_readfirstlane(lds_addr(esc));
+  const uint8_t *__restrict__ lines = tv.line;
+  auto issue = [&](uint32_t idx, int slot) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint32_t li = (uint32_t)__shfl((int)idx, 8 * q + (lane >> 3));
+      glds16(lines + (size_t)li * 128 + (lane & 7) * 16, ring_lds + (uint32_t)(slot * 8192 + q * 1024));
+    }
+  };
+  // the step processed one iteration late: its values, key, escape
+  double vp[J];
+  uint64_t xp = 0;
+  bool ep = false;
+  auto process = [&](int sp_, const double *vv, uint64_t xk, bool e) {
+    double v5 = vv[J - 1];
+    if (e) {  // the escaped L3 value: its code pair landed in the escape slot
+      const uint32_t pr = esc[(sp_ & 1) * 64 + lane];
+      const uint32_t km = (uint32_t)xk & kmask;
+      v5 = s_lut[(km & 1u) ? (pr >> 16) : (pr & 0xffffu)];
+    }
+#pragma unroll
+    for (int t = 0; t < J; ++t) {
+      const int i = sp_ * J + t;
+      if (i < n) {
+        double sv = t == J - 1 ? v5 : vv[t];
+        if (kTrlr && first && i == 0) sv = first_val;
+        if (visits) atomicAdd(&visits[(uint32_t)(xk >> (2 * (J - 1 - t))) & kmask], 1u);
+        L.step(sv, i, ec, cand);
       }
-    };
-    put(0, se, sbad, scur, smx, sarg);
-    put(1, se2, sbad2, scur2, smx2, sarg2);
+    }
+  };
+  uint64_t x1 = 0, x2 = 0;
+  issue((uint32_t)(x >> 6), 0);
+  x1 = B.next_key(x, J, xmask);
+  issue((uint32_t)(x1 >> 6), 1);
+  for (int st = 0; st < NS; ++st) {
+    const uint64_t xs = x;
+    // this step's lines and the previous step's escape complete (the next
+    // step's eight loads may stay in flight)
+    if (st + 1 < NS) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint8_t *ln = ring + (st & 1) * 8192 + lane * 128;
+    double v[J];
+    bool e = false;
+    {
+      const uint4 q0 = *reinterpret_cast<const uint4 *>(ln);
+      const uint64_t lo = (uint64_t)q0.x | ((uint64_t)q0.y << 32), hi = (uint64_t)q0.z | ((uint64_t)q0.w << 32);
+      auto f13 = [&](int b) -> uint32_t {  // static b < 128 - 13
+        const uint64_t w = b < 64 ? ((lo >> b) | (b > 51 ? (hi << (64 - b)) : 0ull)) : (hi >> (b - 64));
+        return (uint32_t)w & 0x1fffu;
+      };
+      const uint32_t c1 = (uint32_t)(xs >> 4) & 3u, c2 = (uint32_t)(xs >> 2) & 3u, c3 = (uint32_t)xs & 3u;
+      uint32_t cs[J];
+#pragma unroll
+      for (int t = 0; t < OWN; ++t) cs[t] = f13(13 * t);
+      const uint32_t l0 = f13(13 * OWN), l1 = f13(13 * (OWN + 1)), l2 = f13(13 * (OWN + 2)),
+                     l3 = f13(13 * (OWN + 3));
+      cs[OWN] = c1 == 0 ? l0 : (c1 == 1 ? l1 : (c1 == 2 ? l2 : l3));
+      cs[OWN + 1] = wide_field(ln, 13u * (OWN + 4 + 4 * c1 + c2), 0x1fffu);
+      const uint32_t c11 = wide_field(ln, B3 + 11u * (16 * c1 + 4 * c2 + c3), 0x7ffu);
+      e = c11 == 0x7ffu;
+      cs[OWN + 2] = e ? 0u : c11;
+#pragma unroll
+      for (int t = 0; t < J; ++t) v[t] = s_lut[cs[t]];
+    }
+    // this step's escape (every lane: a lane without one reads the first pair)
+    {
+      const uint32_t km = (uint32_t)xs & kmask;
+      const uint16_t *src = e ? tv.codes + (km & ~1u) : tv.codes;
+      glds4(src, esc_lds + (uint32_t)((st & 1) * 256));
+    }
+    x = x1;
+    if (st + 2 < NS) {
+      x2 = B.next_key(x1, J, xmask);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done before it is refilled
+      issue((uint32_t)(x2 >> 6), st & 1);
+      x1 = x2;
+    }
+    if (st > 0) process(st - 1, vp, xp, ep);
+#pragma unroll
+    for (int t = 0; t < J; ++t) vp[t] = v[t];
+    xp = xs;
+    ep = e;
   }
-  o.cexit[c] = prev;
-  o.asum[c] = asum;
-  o.pmin[c] = pmin;
-  o.pmax[c] = pmax;
-  o.sabs[c] = sabs;
-  o.special[c] = special ? 1 : 0;
-  if (prev > 0) {
-    o.tbeg[c] = beg; o.tmax[c] = best; o.targ[c] = arg;
-  } else {
-    o.tbeg[c] = -1; o.tmax[c] = 0.0; o.targ[c] = 0;
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  process(NS - 1, vp, xp, ep);
+  if (live) L.finish(c, o, sp);
 }
 
 // Pass 1 for small k (north_star: "the frequency table LDS-staged for small
@@ -3528,9 +3732,24 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   } while (0)
     auto p1l = [&](const Half &h, hipStream_t strm) {
       const Chunks gv = view(h);
+      const int own = tv.line_own;
+      if (tv.line_kind == 3) {  // wide lines
+        const unsigned grid = (unsigned)((h.c1 - h.c0 + kWideBlock - 1) / kWideBlock);
+#define KS_P1W(O)                                                                                             \
+  do {                                                                                                      \
+    if (ec.trlr)                                                                                            \
+      hipLaunchKernelGGL((k_pass1w<O, true>), dim3(grid), dim3(kWideBlock), 0, strm, gv, total, k, tv, ec, visits, \
+                         p1, cand, d_xh, sp1);                                                              \
+    else                                                                                                    \
+      hipLaunchKernelGGL((k_pass1w<O, false>), dim3(grid), dim3(kWideBlock), 0, strm, gv, total, k, tv, ec, visits, \
+                         p1, cand, d_xh, sp1);                                                              \
+  } while (0)
+        if (own == 3) KS_P1W(3); else KS_P1W(4);
+#undef KS_P1W
+        return;
+      }
       const int bs = comp ? 768 : 1024;
       const unsigned grid = (unsigned)((h.c1 - h.c0 + bs - 1) / bs);
-      const int own = tv.line_own;
       if (!comp) {
         if (own == 4) KS_P1L(4, true, false, gv, grid, strm);
         else if (own == 3) KS_P1L(3, true, false, gv, grid, strm);

@@ -293,6 +293,50 @@ __global__ void __launch_bounds__(256) k_build_line_u16(const uint16_t *__restri
   }
 }
 
+// Wide line (line_kind 3, 128 B): own / L1 / L2 entries as 13-bit codes at
+// bits 13 j (j < own + 20), the 64 L3 entries (k-mer ((x << 6) | c1 c2 c3) &
+// mask) as 11-bit codes from bit 13 (own + 20): the uint16 code when below
+// 2047, else 2047 (escape to the base code table).  Little-endian bit order
+// (bit b is bit b % 64 of the line's 64-bit word b / 64).  Eight lanes build
+// a line, one 16-B piece (bits 128 p .. 128 p + 127) each.
+template <int OWN>
+__global__ void __launch_bounds__(256) k_build_line_wide(const uint16_t *__restrict__ codes, int k, uint64_t nlines,
+                                                         ks_u32x4 *__restrict__ out) {
+  constexpr int N13 = OWN + 20, B3 = 13 * N13;
+  static_assert(B3 + 64 * 11 <= 1024, "a wide line holds 1024 bits");
+  const uint32_t kmask = (uint32_t)(((uint64_t)1 << (2 * k)) - 1);
+  const uint64_t npiece = nlines * 8;
+  const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npiece; q += S) {
+    const uint64_t x = q >> 3;
+    const int p = (int)(q & 7);
+    const int lo = 128 * p, hi = lo + 128;
+    unsigned __int128 acc = 0;
+    // 13-bit entries overlapping the piece
+    for (int j = lo / 13; j < N13 && 13 * j < hi; ++j) {
+      const uint32_t km = line_kmer<OWN>(x, j, kmask);
+      const unsigned __int128 v = (unsigned __int128)(codes[km] & 0x1fffu);
+      const int b = 13 * j - lo;
+      acc |= b >= 0 ? (v << b) : (v >> (-b));
+    }
+    // 11-bit L3 entries overlapping the piece
+    const int j3 = lo > B3 ? (lo - B3) / 11 : 0;
+    for (int j = j3; j < 64 && B3 + 11 * j < hi; ++j) {
+      const uint32_t km = ((uint32_t)(x << 6) | (uint32_t)j) & kmask;
+      const uint32_t cd = codes[km];
+      const unsigned __int128 v = (unsigned __int128)(cd < 2047u ? cd : 2047u);
+      const int b = B3 + 11 * j - lo;
+      acc |= b >= 0 ? (v << b) : (v >> (-b));
+    }
+    ks_u32x4 w;
+    w.x = (uint32_t)acc;
+    w.y = (uint32_t)(acc >> 32);
+    w.z = (uint32_t)(acc >> 64);
+    w.w = (uint32_t)(acc >> 96);
+    __builtin_nontemporal_store(w, out + q);
+  }
+}
+
 template <int OWN>
 __global__ void __launch_bounds__(256) k_build_line_f64(const double *__restrict__ vals, int k, uint64_t nlines,
                                                         ks_f64x2 *__restrict__ out) {
@@ -475,7 +519,8 @@ static size_t ext_entry_bytes(bool u16, int J) {
 // so that the 4095 heaviest codes are their own 12-bit codes (0..4094) and
 // every other code escapes.  Sets *use = false (and changes nothing) if the
 // escape share is above max_escape.
-static ks_status choose_code12(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev, double max_escape, bool *use) {
+static ks_status choose_code12(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev, double max_escape, bool *use,
+                               int64_t ndirect_max = 4095) {
   *use = false;
   hipStream_t st = ctx->stream;
   const int64_t n = (int64_t)1 << (2 * t->k);
@@ -497,7 +542,7 @@ static ks_status choose_code12(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev
   std::vector<int32_t> order(nu);
   for (int64_t i = 0; i < nu; ++i) order[i] = (int32_t)i;
   std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return h[a] > h[b]; });
-  const int64_t ndirect = std::min<int64_t>(nu, 4095);
+  const int64_t ndirect = std::min<int64_t>(nu, ndirect_max);
   long double tot = 0, cov = 0;
   for (int64_t i = 0; i < nu; ++i) tot += h[order[i]];
   for (int64_t i = 0; i < ndirect; ++i) cov += h[order[i]];
@@ -550,6 +595,10 @@ static void *ext_alloc(ks_ctx *ctx, size_t bytes, size_t *cap) {
   return nullptr;
 }
 
+// Distinct values of a wide line table (13-bit codes, LUT staged in LDS by
+// k_pass1w: ks_scan_chunked.hip kLineLutMax).
+constexpr int64_t kWideLut = 7168;
+
 // Binade predictor of the pass-1 summaries (k_predict), built with the
 // expanded / line table of a compressed table.
 static ks_status build_approx(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev) {
@@ -574,6 +623,62 @@ static ks_status table_lines(ks_ctx *ctx, ks_table *t, size_t budget, const int3
   *built = false;
   const bool u16 = t->compressed;
   if (t->k < 8 || t->k > 13 || getenv("KS_NO_LINES")) return KS_OK;
+  // wide 128-B lines (J = own + 3) where they beat the 64-B ones: k = 12, 13
+  // (m = 15), at most kWideLut distinct values (13-bit codes), and an L3
+  // escape share (positions whose value is not among the 2047 heaviest) of
+  // at most 10 %.  KS_NO_WIDE_LINES: the 64-B forms.
+  if (u16 && t->k >= 12 && t->distinct <= kWideLut && ((size_t)128 << 30) <= budget &&
+      !getenv("KS_NO_WIDE_LINES")) {
+    bool use = false;
+    const double t0 = now_ms();
+    KS_TRY(choose_code12(ctx, t, freq_dev, 0.10, &use, 2047));  // renumbers the codes by weight
+    t->ms_codes12 = now_ms() - t0;
+    if (t->d_map12) (void)hipFree(t->d_map12);
+    if (t->d_lut12) (void)hipFree(t->d_lut12);
+    t->d_map12 = nullptr;
+    t->d_lut12 = nullptr;
+    if (use) {
+      const int own = 16 - t->k;
+      const uint64_t nlines = (uint64_t)1 << 30;
+      const size_t bytes = nlines * 128;
+      const double ta = now_ms();
+      size_t cap = 0;
+      void *ext = ext_alloc(ctx, bytes, &cap);
+      if (ext) {
+        t->ms_ext_alloc = now_ms() - ta;
+        t->ext_cap = cap;
+        hipStream_t st = ctx->stream;
+        hipEvent_t a, b;
+        KS_HIP(hipEventCreate(&a));
+        KS_HIP(hipEventCreate(&b));
+        KS_HIP(hipEventRecord(a, st));
+        const unsigned grid = (unsigned)std::min<uint64_t>((nlines * 8 + 255) / 256, (uint64_t)ctx->num_cus * 32);
+        if (own == 3)
+          hipLaunchKernelGGL(k_build_line_wide<3>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nlines,
+                             (ks_u32x4 *)ext);
+        else
+          hipLaunchKernelGGL(k_build_line_wide<4>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nlines,
+                             (ks_u32x4 *)ext);
+        KS_HIP(hipGetLastError());
+        KS_HIP(hipEventRecord(b, st));
+        KS_HIP(hipEventSynchronize(b));
+        float ms = 0;
+        KS_HIP(hipEventElapsedTime(&ms, a, b));
+        KS_HIP(hipEventDestroy(a));
+        KS_HIP(hipEventDestroy(b));
+        KS_TRY(build_approx(ctx, t, freq_dev));
+        t->d_ext = ext;
+        t->line_kind = 3;
+        t->line_own = own;
+        t->ext_J = own + 3;
+        t->ext_bits = 13;
+        t->ext_bytes = bytes;
+        t->ms_ext = ms;
+        *built = true;
+        return KS_OK;
+      }
+    }
+  }
   int own = std::min(u16 ? 5 : 4, 16 - t->k);
   for (; own >= 2; --own)
     if (((size_t)64 << (2 * (t->k + own - 1))) <= budget) break;
@@ -1126,5 +1231,7 @@ extern "C" ks_status ks_table_get_info(const ks_table *t, ks_table_info *out) {
 }
 
 extern "C" double ks_table_escape_fraction(const ks_table *t) {
-  return (t && t->ext_bits == 12) ? t->escape_frac : 0.0;
+  // 12-bit (k+4)-mer tables: share of scan indices that escape; wide lines
+  // (13): share of the L3 indices (one per line) that escape
+  return (t && (t->ext_bits == 12 || t->ext_bits == 13)) ? t->escape_frac : 0.0;
 }

@@ -99,10 +99,58 @@ def test_line_vs_expanded_same_regions(setup, monkeypatch):
         if not lines:
             monkeypatch.setenv("KS_NO_LINES", "1")
         tab = D.DeviceTable.from_counts(ctx, counts, k, "log2", total=words, expand=True)
-        assert tab.positions_per_read == 5
-        assert tab.code_bits == (16 if lines else 12)
+        assert tab.positions_per_read == (6 if lines else 5)  # wide 128-B lines / the (k+4)-mer table
+        assert tab.code_bits == (13 if lines else 12)
         ctx.set_scan_algo(1)
         out.append(D.scan(ctx, ds, k, tab, 100, 20.0)[:2])
         ctx.set_scan_algo(-1)
         tab.close()
     _same(out[0][0], out[0][1], out[1][0], out[1][1], "line vs expanded")
+
+
+def _skewed_table(rng, k, nhead, ntail, tail_share):
+    """w with nhead frequent values and ntail rare ones (tail_share of the
+    k-mers): the wide line's 11-bit L3 codes escape for the rare ones."""
+    head = np.round(rng.normal(size=nhead) * 64) / 64 + rng.normal(size=nhead) * 1e-3
+    tail = rng.normal(size=ntail) * 3.0
+    n = 4 ** k
+    w = head[rng.integers(0, nhead, size=n)]
+    sel = rng.random(n) < tail_share
+    w[sel] = tail[rng.integers(0, ntail, size=int(sel.sum()))]
+    return w
+
+
+@pytest.mark.parametrize("k,ntail,share", [(13, 5000, 0.06), (12, 4000, 0.03), (13, 0, 0.0)])
+def test_wide_lines(oracle, setup, monkeypatch, k, ntail, share):
+    """Wide 128-B lines (13-bit own / L1 / L2 codes, 11-bit L3 codes with
+    escapes to the base code table, J = own + 3): regions, scores and both
+    visit routes against the oracle, on tables with escapes."""
+    ctx, ds, host, torch = setup
+    from kmer_spans_amd import device as D
+    rng = np.random.default_rng(k + ntail)
+    w = _skewed_table(rng, k, 600, ntail, share) if ntail else \
+        np.round(rng.normal(size=4 ** k) * 8) / 8  # few distinct values: no escape
+    thr = 0.02
+    tab = D.DeviceTable(ctx, w, k, thr, compress=True, expand=True)
+    assert tab.positions_per_read == 16 - k + 3 and tab.code_bits == 13, (tab.positions_per_read, tab.code_bits)
+    if ntail:
+        assert 0 < tab.escape_fraction <= 0.10, tab.escape_fraction
+    o = oracle.scan(host, k, w, thr, 30, 3.0, visits=True)
+    for route in ("count", "atomic"):
+        if route == "atomic":
+            monkeypatch.setenv("KS_VISITS_ATOMIC", "1")
+        ctx.set_scan_algo(1)
+        vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+        pos, sc, st = D.scan(ctx, ds, k, tab, 30, 3.0, vis)
+        _same(pos, sc, o["pos"], o["score"], ("wide", k, route))
+        assert np.array_equal(vis.cpu().numpy(), o["counts"]), ("wide visits", k, route)
+        monkeypatch.delenv("KS_VISITS_ATOMIC", raising=False)
+    # tr_lr through the wide pass
+    init = D.DeviceTable(ctx, w - thr, k, 0.0, compress=False)
+    trans = D.DeviceTable(ctx, w - thr, k, 0.0, compress=True, expand=True)
+    ot = oracle.tr_lr_regions(host, k, 40, w - thr, w - thr)
+    pos, sc, st = D.tr_lr(ctx, ds, k, trans, init, 40)
+    _same(pos, sc, ot["pos"], ot["score"], ("wide trlr", k))
+    ctx.set_scan_algo(-1)
+    for t_ in (tab, init, trans):
+        t_.close()

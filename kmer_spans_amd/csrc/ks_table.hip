@@ -255,102 +255,103 @@ __global__ void k_build_ext_f64(const double *__restrict__ vals, int k, uint64_t
 //   FP64 values:  [own][L1], own + 4 <= 8
 // (zeros pad the line).  own k-mer t is (x >> 2 (own - 1 - t)) & mask; L1 c
 // is ((x << 2) | c) & mask, L2 c1 c2 is ((x << 4) | c1 c2) & mask: the L1 /
-// L2 entries of consecutive lines are consecutive code-table entries.  Four
-// lanes build a line, a 16-B piece each (codes / values 8p .. 8p + 7 /
-// 2p, 2p + 1), so one store instruction writes 16 whole lines (1 KiB); the
-// code reads repeat across the wave and stay cached: the build is a write
-// stream of nontemporal stores.
+// L2 entries of consecutive lines are consecutive code-table entries.
 typedef uint32_t ks_u32x4 __attribute__((ext_vector_type(4)));
-template <int OWN>
-__device__ __forceinline__ uint32_t line_kmer(uint64_t x, int j, uint32_t kmask) {
-  if (j < OWN) return (uint32_t)(x >> (2 * (OWN - 1 - j))) & kmask;
-  if (j < OWN + 4) return ((uint32_t)(x << 2) | (uint32_t)(j - OWN)) & kmask;
-  return ((uint32_t)(x << 4) | (uint32_t)(j - OWN - 4)) & kmask;
-}
 
-template <int OWN>
-__global__ void __launch_bounds__(256) k_build_line_u16(const uint16_t *__restrict__ codes, int k, uint64_t nlines,
-                                                        ks_u32x4 *__restrict__ out) {
-  static_assert(OWN + 20 <= 32, "a uint16 line holds 32 codes");
+// Line builds, lane per line: the lane reads its line's entries (own
+// k-mers: three scattered reads; the L1 / L2 / L3 continuations: 4 / 16 / 64
+// consecutive code-table entries from ((x << 2 lev) & mask)) and packs them
+// with compile-time offsets.  The lines are walked as x = (hi << lb) | lo
+// with lo (the low lb = 2k - 2 levmax bits, which alone decide the L-region
+// reads) fixed per lane and hi the loop: a block re-reads the same few KiB
+// of the code table on every trip (L1 / L2 hits), and a wave's 64 lines are
+// consecutive, so after a transpose through LDS each 16-B store instruction
+// writes 1 KiB of whole lines.  Mode 0: uint16 64-B lines, 1: FP64 64-B
+// lines, 2: wide 128-B lines (13-bit own / L1 / L2 codes at bits 13 j, the
+// 64 L3 codes as 11-bit codes from bit 13 (own + 20), >= 2047 -> 2047).
+template <int OWN, int kMode>
+__global__ void __launch_bounds__(256) k_build_lines(const uint16_t *__restrict__ codes,
+                                                     const double *__restrict__ vals, int k, int m,
+                                                     ks_u32x4 *__restrict__ out) {
+  constexpr int LB = kMode == 2 ? 128 : 64;  // line bytes
+  constexpr int NP = LB / 16;               // 16-B pieces per line
+  constexpr int LEV = kMode == 0 ? 2 : (kMode == 1 ? 1 : 3);
+  __shared__ ks_u32x4 s_t[4][64 * NP];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t kmask = (uint32_t)(((uint64_t)1 << (2 * k)) - 1);
-  const uint64_t npiece = nlines * 4;
-  const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npiece; q += S) {
-    const uint64_t x = q >> 2;
-    const int p = (int)(q & 3);
-    uint32_t h[8];
+  const int lb = 2 * k - 2 * LEV;
+  const uint64_t nhi = ((uint64_t)1 << (2 * m - lb)) / gridDim.y;  // hi range of this block row
+  const uint64_t lo = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t hi = blockIdx.y * nhi; hi < (blockIdx.y + 1) * nhi; ++hi) {
+    const uint64_t x = (hi << lb) | lo;
+    uint32_t w[LB / 4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int j = 8 * p + u;
-      h[u] = j < OWN + 20 ? (uint32_t)codes[line_kmer<OWN>(x, j, kmask)] : 0u;
+    for (int q = 0; q < LB / 4; ++q) w[q] = 0;
+    if (kMode == 1) {  // FP64: [own][L1]
+      double d[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) d[t] = 0.0;
+#pragma unroll
+      for (int t = 0; t < OWN; ++t) d[t] = vals[(uint32_t)(x >> (2 * (OWN - 1 - t))) & kmask];
+      const double2 *l1 = reinterpret_cast<const double2 *>(vals + (((uint32_t)(x << 2)) & kmask));
+      const double2 a0 = l1[0], a1 = l1[1];
+      d[OWN] = a0.x; d[OWN + 1] = a0.y; d[OWN + 2] = a1.x; d[OWN + 3] = a1.y;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        w[2 * t] = (uint32_t)__double_as_longlong(d[t]);
+        w[2 * t + 1] = (uint32_t)((uint64_t)__double_as_longlong(d[t]) >> 32);
+      }
+    } else {
+      uint32_t h[OWN + 20];
+#pragma unroll
+      for (int t = 0; t < OWN; ++t) h[t] = codes[(uint32_t)(x >> (2 * (OWN - 1 - t))) & kmask];
+      const uint2 l1 = *reinterpret_cast<const uint2 *>(codes + (((uint32_t)(x << 2)) & kmask));
+      h[OWN] = l1.x & 0xffffu; h[OWN + 1] = l1.x >> 16; h[OWN + 2] = l1.y & 0xffffu; h[OWN + 3] = l1.y >> 16;
+      const uint4 *l2 = reinterpret_cast<const uint4 *>(codes + (((uint32_t)(x << 4)) & kmask));
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const uint4 v = l2[q];
+        const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          h[OWN + 4 + 8 * q + 2 * r] = vw[r] & 0xffffu;
+          h[OWN + 4 + 8 * q + 2 * r + 1] = vw[r] >> 16;
+        }
+      }
+      if (kMode == 0) {
+#pragma unroll
+        for (int j = 0; j < OWN + 20; ++j) w[j >> 1] |= h[j] << (16 * (j & 1));
+      } else {
+        auto put = [&](int b, uint32_t v) {  // compile-time b after unrolling
+          w[b >> 5] |= v << (b & 31);
+          if ((b & 31) != 0) w[(b >> 5) + 1] |= v >> (32 - (b & 31));
+        };
+#pragma unroll
+        for (int j = 0; j < OWN + 20; ++j) put(13 * j, h[j] & 0x1fffu);
+        const uint4 *l3 = reinterpret_cast<const uint4 *>(codes + (((uint32_t)(x << 6)) & kmask));
+        constexpr int B3 = 13 * (OWN + 20);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint4 v = l3[q];
+          const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const uint32_t cd = (vw[r >> 1] >> (16 * (r & 1))) & 0xffffu;
+            put(B3 + 11 * (8 * q + r), cd < 2047u ? cd : 2047u);
+          }
+        }
+      }
     }
-    ks_u32x4 v;
-    v.x = h[0] | (h[1] << 16);
-    v.y = h[2] | (h[3] << 16);
-    v.z = h[4] | (h[5] << 16);
-    v.w = h[6] | (h[7] << 16);
-    __builtin_nontemporal_store(v, out + q);
-  }
-}
-
-// Wide line (line_kind 3, 128 B): own / L1 / L2 entries as 13-bit codes at
-// bits 13 j (j < own + 20), the 64 L3 entries (k-mer ((x << 6) | c1 c2 c3) &
-// mask) as 11-bit codes from bit 13 (own + 20): the uint16 code when below
-// 2047, else 2047 (escape to the base code table).  Little-endian bit order
-// (bit b is bit b % 64 of the line's 64-bit word b / 64).  Eight lanes build
-// a line, one 16-B piece (bits 128 p .. 128 p + 127) each.
-template <int OWN>
-__global__ void __launch_bounds__(256) k_build_line_wide(const uint16_t *__restrict__ codes, int k, uint64_t nlines,
-                                                         ks_u32x4 *__restrict__ out) {
-  constexpr int N13 = OWN + 20, B3 = 13 * N13;
-  static_assert(B3 + 64 * 11 <= 1024, "a wide line holds 1024 bits");
-  const uint32_t kmask = (uint32_t)(((uint64_t)1 << (2 * k)) - 1);
-  const uint64_t npiece = nlines * 8;
-  const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npiece; q += S) {
-    const uint64_t x = q >> 3;
-    const int p = (int)(q & 7);
-    const int lo = 128 * p, hi = lo + 128;
-    unsigned __int128 acc = 0;
-    // 13-bit entries overlapping the piece
-    for (int j = lo / 13; j < N13 && 13 * j < hi; ++j) {
-      const uint32_t km = line_kmer<OWN>(x, j, kmask);
-      const unsigned __int128 v = (unsigned __int128)(codes[km] & 0x1fffu);
-      const int b = 13 * j - lo;
-      acc |= b >= 0 ? (v << b) : (v >> (-b));
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      ks_u32x4 v;
+      v.x = w[4 * p]; v.y = w[4 * p + 1]; v.z = w[4 * p + 2]; v.w = w[4 * p + 3];
+      s_t[wv][lane * NP + p] = v;
     }
-    // 11-bit L3 entries overlapping the piece
-    const int j3 = lo > B3 ? (lo - B3) / 11 : 0;
-    for (int j = j3; j < 64 && B3 + 11 * j < hi; ++j) {
-      const uint32_t km = ((uint32_t)(x << 6) | (uint32_t)j) & kmask;
-      const uint32_t cd = codes[km];
-      const unsigned __int128 v = (unsigned __int128)(cd < 2047u ? cd : 2047u);
-      const int b = B3 + 11 * j - lo;
-      acc |= b >= 0 ? (v << b) : (v >> (-b));
-    }
-    ks_u32x4 w;
-    w.x = (uint32_t)acc;
-    w.y = (uint32_t)(acc >> 32);
-    w.z = (uint32_t)(acc >> 64);
-    w.w = (uint32_t)(acc >> 96);
-    __builtin_nontemporal_store(w, out + q);
-  }
-}
-
-template <int OWN>
-__global__ void __launch_bounds__(256) k_build_line_f64(const double *__restrict__ vals, int k, uint64_t nlines,
-                                                        ks_f64x2 *__restrict__ out) {
-  static_assert(OWN + 4 <= 8, "an FP64 line holds 8 values");
-  const uint32_t kmask = (uint32_t)(((uint64_t)1 << (2 * k)) - 1);
-  const uint64_t npiece = nlines * 4;
-  const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npiece; q += S) {
-    const uint64_t x = q >> 2;
-    const int j = 2 * (int)(q & 3);
-    ks_f64x2 v;
-    v.x = j < OWN + 4 ? vals[line_kmer<OWN>(x, j, kmask)] : 0.0;
-    v.y = j + 1 < OWN + 4 ? vals[line_kmer<OWN>(x, j + 1, kmask)] : 0.0;
-    __builtin_nontemporal_store(v, out + q);
+    // (a wave's LDS accesses execute in order: no barrier for its own image)
+    const uint64_t x0 = x - lane;  // the wave's first line
+#pragma unroll
+    for (int p = 0; p < NP; ++p) __builtin_nontemporal_store(s_t[wv][p * 64 + lane], out + x0 * NP + p * 64 + lane);
   }
 }
 
@@ -599,6 +600,19 @@ static void *ext_alloc(ks_ctx *ctx, size_t bytes, size_t *cap) {
 // k_pass1w: ks_scan_chunked.hip kLineLutMax).
 constexpr int64_t kWideLut = 7168;
 
+// Launch of k_build_lines: 2^lb lanes (lb = 2k - 2 levmax), the hi range
+// split over grid rows until ~2^20 lanes run.
+template <int OWN, int kMode>
+static void launch_build_lines(hipStream_t st, const ks_table *t, int m, void *out) {
+  const int lev = kMode == 0 ? 2 : (kMode == 1 ? 1 : 3);
+  const int lb = 2 * t->k - 2 * lev;
+  const int hb = 2 * m - lb;
+  int ys = 0;
+  while (lb + ys < 20 && ys < hb) ++ys;
+  hipLaunchKernelGGL((k_build_lines<OWN, kMode>), dim3((unsigned)(((uint64_t)1 << lb) / 256), 1u << ys), dim3(256), 0,
+                     st, t->d_codes, t->d_vals, t->k, m, (ks_u32x4 *)out);
+}
+
 // Binade predictor of the pass-1 summaries (k_predict), built with the
 // expanded / line table of a compressed table.
 static ks_status build_approx(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev) {
@@ -652,13 +666,8 @@ static ks_status table_lines(ks_ctx *ctx, ks_table *t, size_t budget, const int3
         KS_HIP(hipEventCreate(&a));
         KS_HIP(hipEventCreate(&b));
         KS_HIP(hipEventRecord(a, st));
-        const unsigned grid = (unsigned)std::min<uint64_t>((nlines * 8 + 255) / 256, (uint64_t)ctx->num_cus * 32);
-        if (own == 3)
-          hipLaunchKernelGGL(k_build_line_wide<3>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nlines,
-                             (ks_u32x4 *)ext);
-        else
-          hipLaunchKernelGGL(k_build_line_wide<4>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nlines,
-                             (ks_u32x4 *)ext);
+        if (own == 3) launch_build_lines<3, 2>(st, t, 15, ext);
+        else launch_build_lines<4, 2>(st, t, 15, ext);
         KS_HIP(hipGetLastError());
         KS_HIP(hipEventRecord(b, st));
         KS_HIP(hipEventSynchronize(b));
@@ -697,21 +706,16 @@ static ks_status table_lines(ks_ctx *ctx, ks_table *t, size_t budget, const int3
   KS_HIP(hipEventCreate(&a));
   KS_HIP(hipEventCreate(&b));
   KS_HIP(hipEventRecord(a, st));
-  const unsigned grid = (unsigned)std::min<uint64_t>((nlines * 4 + 255) / 256, (uint64_t)ctx->num_cus * 32);
-#define KS_LINE_BUILD(O)                                                                                       \
-  do {                                                                                                         \
-    if (u16)                                                                                                   \
-      hipLaunchKernelGGL(k_build_line_u16<O>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nlines, (ks_u32x4 *)ext); \
-    else                                                                                                       \
-      hipLaunchKernelGGL(k_build_line_f64<O>, dim3(grid), dim3(256), 0, st, t->d_vals, t->k, nlines,          \
-                         (ks_f64x2 *)ext);                                                                     \
-  } while (0)
-  if (own == 5) {
-    if (u16) hipLaunchKernelGGL(k_build_line_u16<5>, dim3(grid), dim3(256), 0, st, t->d_codes, t->k, nlines, (ks_u32x4 *)ext);
-  } else if (own == 4) KS_LINE_BUILD(4);
-  else if (own == 3) KS_LINE_BUILD(3);
-  else KS_LINE_BUILD(2);
-#undef KS_LINE_BUILD
+  if (u16) {
+    if (own == 5) launch_build_lines<5, 0>(st, t, m, ext);
+    else if (own == 4) launch_build_lines<4, 0>(st, t, m, ext);
+    else if (own == 3) launch_build_lines<3, 0>(st, t, m, ext);
+    else launch_build_lines<2, 0>(st, t, m, ext);
+  } else {
+    if (own == 4) launch_build_lines<4, 1>(st, t, m, ext);
+    else if (own == 3) launch_build_lines<3, 1>(st, t, m, ext);
+    else launch_build_lines<2, 1>(st, t, m, ext);
+  }
   KS_HIP(hipGetLastError());
   KS_HIP(hipEventRecord(b, st));
   KS_HIP(hipEventSynchronize(b));

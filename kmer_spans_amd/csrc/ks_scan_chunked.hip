@@ -1385,7 +1385,12 @@ __global__ void __launch_bounds__(kF64 ? 1024 : 768) k_pass1l(Chunks g, int64_t 
 // (global_load_lds_dword of the code pair; a lane without one reads the
 // table's first pair), and the step is processed one step later, when it
 // has landed: every step then needs one counted wait, whatever the escapes.
-constexpr int kWideBlock = 384;  // 6 waves: ring 96 KiB + LUT 56 KiB + escape slots 3 KiB
+// A step needs at most 7 of a line's 32 dwords (own + L1: 0 .. 2; the L2
+// and L3 codes: two dwords each), so eight lanes gather exactly those
+// dwords of a line (global_load_lds_dword; one line request either way):
+// 2 KiB of ring per wave and step instead of 8, which leaves room for 12
+// waves per CU beside the LUT (the whole 128-B lines fit 6).
+constexpr int kWideBlock = 768;  // 12 waves: ring 48 KiB + LUT 56 KiB + escape slots 6 KiB
 
 // One global_load_lds_dword: 4 B from each lane's gsrc to LDS lds + 4 x lane.
 __device__ __forceinline__ void glds4(const void *gsrc, uint32_t lds) {
@@ -1394,13 +1399,6 @@ __device__ __forceinline__ void glds4(const void *gsrc, uint32_t lds) {
                : "=&s"(keep)
                : "v"(gsrc), "s"(lds)
                : "memory");
-}
-
-// nb-bit field at bit b of a line in LDS (b dynamic; two dwords).
-__device__ __forceinline__ uint32_t wide_field(const uint8_t *ln, uint32_t b, uint32_t mask) {
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(ln) + (b >> 5);
-  const uint64_t v = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-  return (uint32_t)(v >> (b & 31)) & mask;
 }
 
 template <int OWN, bool kTrlr>
@@ -1412,8 +1410,9 @@ __global__ void __launch_bounds__(kWideBlock) k_pass1w(Chunks g, int64_t total, 
   constexpr int NS = (CH + J - 1) / J;
   constexpr int N13 = OWN + 20;
   constexpr uint32_t B3 = 13 * N13;  // first L3 bit
-  static_assert(13 * (OWN + 4) <= 128, "own + L1 in the first 16 B");
-  __shared__ __attribute__((aligned(16))) uint8_t s_ring[(BS / 64) * 2 * 8192];
+  constexpr int NO = (13 * (OWN + 4) + 31) / 32;  // dwords of own + L1 (3 or 4)
+  static_assert(NO + 4 <= 8, "own + L1, L2, L3 dwords in 8 lanes");
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[(BS / 64) * 2 * 2048];
   __shared__ __attribute__((aligned(16))) uint32_t s_esc[(BS / 64) * 2 * 64];
   __shared__ double s_lut[kLineLutMax];
   for (int i = threadIdx.x; i < tv.nlut; i += BS) s_lut[i] = tv.lut[i];
@@ -1435,16 +1434,31 @@ __global__ void __launch_bounds__(kWideBlock) k_pass1w(Chunks g, int64_t total, 
   uint64_t x = B.first_key(kx);
   const double first_val = (kTrlr && first) ? ec.ks[(uint32_t)(x >> (2 * (J - 1))) & kmask] : 0.0;
 
-  uint8_t *const ring = s_ring + wv * 16384;
+  uint8_t *const ring = s_ring + wv * 4096;
   uint32_t *const esc = s_esc + wv * 128;
   const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(lds_addr(ring));
   const uint32_t esc_lds = __builtin_amdgcn_readfirstlane(lds_addr(esc));
   const uint8_t *__restrict__ lines = tv.line;
-  auto issue = [&](uint32_t idx, int slot) {
+  // the dwords a step reads from its line (key xk): 0 .. NO - 1, the L2
+  // code's two, the L3 code's two (a spare lane reloads dword 0)
+  auto dwords = [&](uint64_t xk) -> uint32_t {
+    const uint32_t c1 = (uint32_t)(xk >> 4) & 3u, c2 = (uint32_t)(xk >> 2) & 3u, c3 = (uint32_t)xk & 3u;
+    const uint32_t d2 = (13u * (OWN + 4 + 4 * c1 + c2)) >> 5, d3 = (B3 + 11u * (16 * c1 + 4 * c2 + c3)) >> 5;
+    return d2 | (d3 << 8);
+  };
+  auto issue = [&](uint64_t xk, int slot) {
+    const uint32_t idx = (uint32_t)(xk >> 6), dd = dwords(xk);
+    const int j = lane & 7;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const uint32_t li = (uint32_t)__shfl((int)idx, 8 * q + (lane >> 3));
-      glds16(lines + (size_t)li * 128 + (lane & 7) * 16, ring_lds + (uint32_t)(slot * 8192 + q * 1024));
+      const int ow = 8 * q + (lane >> 3);
+      const uint32_t li = (uint32_t)__shfl((int)idx, ow);
+      const uint32_t od = (uint32_t)__shfl((int)dd, ow);
+      const uint32_t d2 = od & 0xffu, d3 = od >> 8;
+      const uint32_t dw = j < NO ? (uint32_t)j
+                                 : (j < NO + 2 ? d2 + (uint32_t)(j - NO)
+                                               : (j < NO + 4 ? min(d3 + (uint32_t)(j - NO - 2), 31u) : 0u));
+      glds4(lines + (size_t)li * 128 + dw * 4, ring_lds + (uint32_t)(slot * 2048 + q * 256));
     }
   };
   // the step processed one iteration late: its values, key, escape
@@ -1470,21 +1484,24 @@ __global__ void __launch_bounds__(kWideBlock) k_pass1w(Chunks g, int64_t total, 
     }
   };
   uint64_t x1 = 0, x2 = 0;
-  issue((uint32_t)(x >> 6), 0);
+  issue(x, 0);
   x1 = B.next_key(x, J, xmask);
-  issue((uint32_t)(x1 >> 6), 1);
+  issue(x1, 1);
   for (int st = 0; st < NS; ++st) {
     const uint64_t xs = x;
     // this step's lines and the previous step's escape complete (the next
     // step's eight loads may stay in flight)
     if (st + 1 < NS) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint8_t *ln = ring + (st & 1) * 8192 + lane * 128;
+    const uint8_t *ln = ring + (st & 1) * 2048 + lane * 32;  // the step's 8 dwords (dwords())
     double v[J];
     bool e = false;
     {
       const uint4 q0 = *reinterpret_cast<const uint4 *>(ln);
-      const uint64_t lo = (uint64_t)q0.x | ((uint64_t)q0.y << 32), hi = (uint64_t)q0.z | ((uint64_t)q0.w << 32);
+      const uint4 q1 = *reinterpret_cast<const uint4 *>(ln + 16);
+      const uint32_t D[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+      const uint64_t lo = (uint64_t)D[0] | ((uint64_t)D[1] << 32);
+      const uint64_t hi = (uint64_t)D[2] | (NO > 3 ? ((uint64_t)D[3] << 32) : 0ull);
       auto f13 = [&](int b) -> uint32_t {  // static b < 128 - 13
         const uint64_t w = b < 64 ? ((lo >> b) | (b > 51 ? (hi << (64 - b)) : 0ull)) : (hi >> (b - 64));
         return (uint32_t)w & 0x1fffu;
@@ -1496,8 +1513,9 @@ __global__ void __launch_bounds__(kWideBlock) k_pass1w(Chunks g, int64_t total, 
       const uint32_t l0 = f13(13 * OWN), l1 = f13(13 * (OWN + 1)), l2 = f13(13 * (OWN + 2)),
                      l3 = f13(13 * (OWN + 3));
       cs[OWN] = c1 == 0 ? l0 : (c1 == 1 ? l1 : (c1 == 2 ? l2 : l3));
-      cs[OWN + 1] = wide_field(ln, 13u * (OWN + 4 + 4 * c1 + c2), 0x1fffu);
-      const uint32_t c11 = wide_field(ln, B3 + 11u * (16 * c1 + 4 * c2 + c3), 0x7ffu);
+      const uint32_t b2 = 13u * (OWN + 4 + 4 * c1 + c2), b3 = B3 + 11u * (16 * c1 + 4 * c2 + c3);
+      cs[OWN + 1] = (uint32_t)(((uint64_t)D[NO] | ((uint64_t)D[NO + 1] << 32)) >> (b2 & 31)) & 0x1fffu;
+      const uint32_t c11 = (uint32_t)(((uint64_t)D[NO + 2] | ((uint64_t)D[NO + 3] << 32)) >> (b3 & 31)) & 0x7ffu;
       e = c11 == 0x7ffu;
       cs[OWN + 2] = e ? 0u : c11;
 #pragma unroll
@@ -1513,7 +1531,7 @@ __global__ void __launch_bounds__(kWideBlock) k_pass1w(Chunks g, int64_t total, 
     if (st + 2 < NS) {
       x2 = B.next_key(x1, J, xmask);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done before it is refilled
-      issue((uint32_t)(x2 >> 6), st & 1);
+      issue(x2, st & 1);
       x1 = x2;
     }
     if (st > 0) process(st - 1, vp, xp, ep);

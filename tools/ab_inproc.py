@@ -30,6 +30,9 @@ def main():
     p.add_argument("--out", default=None)
     p.add_argument("--rebuild", action="store_true",
                    help="rebuild the table every round (with KS_EXT_POOL=0: a new expanded-table allocation)")
+    p.add_argument("--table-per-variant", action="store_true",
+                   help="build one table per variant with its environment set (table-form A/Bs: KS_NO_LINES, "
+                        "KS_NO_WIDE_LINES); all tables stay resident")
     a = p.parse_args()
     import numpy as np
     import torch
@@ -42,12 +45,27 @@ def main():
     counts = torch.zeros(4 ** a.k, dtype=torch.int32, device="cuda")
     words = D.count(ctx, ds, a.k, counts)
     thr = 0.75 if a.score == "rank" else 0.0
-    tab = D.DeviceTable.from_counts(ctx, counts, a.k, a.score, total=words, thr=thr, expand=True)
     variants = []
     for v in a.variants:
         name, _, envs = v.partition(":")
         env = dict(e.split("=", 1) for e in envs.split(",") if e)
         variants.append((name, env))
+    tabs = {}
+    if a.table_per_variant:
+        for name, env in variants:
+            old = {key: os.environ.get(key) for key in env}
+            os.environ.update(env)
+            tabs[name] = D.DeviceTable.from_counts(ctx, counts, a.k, a.score, total=words, thr=thr, expand=True)
+            for key, v in old.items():
+                if v is None:
+                    os.environ.pop(key, None)
+                else:
+                    os.environ[key] = v
+            print(name, "table J", tabs[name].positions_per_read, "code bits", tabs[name].code_bits,
+                  tabs[name].setup_ms(), flush=True)
+        tab = tabs[variants[0][0]]
+    else:
+        tab = D.DeviceTable.from_counts(ctx, counts, a.k, a.score, total=words, thr=thr, expand=True)
     res = {n: [] for n, _ in variants}
     phases = {}
     ref = None
@@ -63,7 +81,7 @@ def main():
                 for _ in range(a.steps):
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
-                    pos, sc, st = D.scan(ctx, ds, a.k, tab, 100, 20.0)
+                    pos, sc, st = D.scan(ctx, ds, a.k, tabs.get(name, tab), 100, 20.0)
                     torch.cuda.synchronize()
                     ms = (time.perf_counter() - t0) * 1e3
                     res[name].append(ms)
@@ -91,7 +109,8 @@ def main():
     if a.out:
         with open(a.out, "w") as f:
             json.dump(out, f, indent=1)
-    tab.close()
+    for t_ in set(list(tabs.values()) + [tab]):
+        t_.close()
 
 
 if __name__ == "__main__":

@@ -446,6 +446,7 @@ def main():
     w_dev, thr, table, init_table, tt = make_table(counts, words, args.score)
     setup.update({key: round(v, 2) for key, v in tt.items()})
     table_shape = {"table_compressed": table.compressed, "table_distinct": table.distinct,
+                   "line_kind": table.line_kind, "pass1_kernel": table.pass1_kernel,
                    "positions_per_read": table.positions_per_read, "code_bits": table.code_bits,
                    "escape_fraction": round(table.escape_fraction, 6)}
 
@@ -463,7 +464,7 @@ def main():
     # ---- dominant kernel roofline (hipEvents on the library stream)
     ms_kernel = float(np.mean([s["ms_scan"] for s in stats]))
     achieved = ALGO_BYTES_PER_BASE * n_bases / (ms_kernel * 1e-3) / 1e9
-    kernel = "k_scan_lane" if stats[-1]["scan_algo"] == 0 else "k_pass1p"
+    kernel = "k_scan_lane" if stats[-1]["scan_algo"] == 0 else table.pass1_kernel
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                 "kernel": kernel, "kernel_ms": round(ms_kernel, 3), "algo_bytes_per_base": ALGO_BYTES_PER_BASE,

@@ -245,6 +245,8 @@ typedef struct ks_table_info {
   double ms_ext_alloc; /* hipMalloc of the expanded table                        */
   double ms_ext_build; /* expanded-table build kernel                            */
   double ms_total;
+  int32_t line_kind;   /* 0: no line table; 1: uint16 64-B lines, 2: FP64 64-B lines, 3: 128-B lines */
+  int32_t line_own;    /* own k-mers per line (m = k + line_own - 1)              */
 } ks_table_info;
 ks_status ks_table_get_info(const ks_table *t, ks_table_info *out);
 

@@ -52,7 +52,7 @@ class TableInfo(C.Structure):
                 ("code_bits", C.c_int32), ("distinct", C.c_int64), ("ext_bytes", C.c_int64),
                 ("escape_fraction", C.c_double), ("ms_upload", C.c_double), ("ms_compress", C.c_double),
                 ("ms_codes12", C.c_double), ("ms_ext_alloc", C.c_double), ("ms_ext_build", C.c_double),
-                ("ms_total", C.c_double)]
+                ("ms_total", C.c_double), ("line_kind", C.c_int32), ("line_own", C.c_int32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

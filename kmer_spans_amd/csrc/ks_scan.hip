@@ -281,15 +281,16 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                            const unsigned long long *d_cnt, int64_t segcap, const ScanMode &mode, int init_step,
                            const int64_t *offs, const uint32_t *packed) {
   if (n <= 0) return KS_OK;
-  const int J = tv.ext ? tv.ext_J : 1;
+  // line tables: own + 1 indices per read (gather_group's line form)
+  const int J = tv.line ? tv.line_own + 1 : (tv.ext ? tv.ext_J : 1);
   if (mode.trlr) {
 #define KS_LANE_T(J, C)                                                                                   \
   hipLaunchKernelGGL((k_scan_lane_trlr<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, \
                      total, ra, rb, rs, n, k, tv, mode.ks, mode.min_len, out, d_cnt, segcap, init_step, offs)
     if (tv.compressed) {
-      if (J == 5) KS_LANE_T(5, true); else if (J == 4) KS_LANE_T(4, true); else if (J == 3) KS_LANE_T(3, true); else if (J == 2) KS_LANE_T(2, true); else KS_LANE_T(1, true);
+      if (J == 6) KS_LANE_T(6, true); else if (J == 5) KS_LANE_T(5, true); else if (J == 4) KS_LANE_T(4, true); else if (J == 3) KS_LANE_T(3, true); else if (J == 2) KS_LANE_T(2, true); else KS_LANE_T(1, true);
     } else {
-      if (J == 4) KS_LANE_T(4, false); else if (J == 3) KS_LANE_T(3, false); else if (J == 2) KS_LANE_T(2, false); else KS_LANE_T(1, false);
+      if (J == 5) KS_LANE_T(5, false); else if (J == 4) KS_LANE_T(4, false); else if (J == 3) KS_LANE_T(3, false); else if (J == 2) KS_LANE_T(2, false); else KS_LANE_T(1, false);
     }
 #undef KS_LANE_T
     KS_HIP(hipGetLastError());
@@ -299,9 +300,9 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
   hipLaunchKernelGGL((k_scan_lane<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, total, \
                      ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed)
   if (tv.compressed) {
-    if (J == 5) KS_LANE(5, true); else if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
+    if (J == 6) KS_LANE(6, true); else if (J == 5) KS_LANE(5, true); else if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
   } else {
-    if (J == 4) KS_LANE(4, false); else if (J == 3) KS_LANE(3, false); else if (J == 2) KS_LANE(2, false); else KS_LANE(1, false);
+    if (J == 5) KS_LANE(5, false); else if (J == 4) KS_LANE(4, false); else if (J == 3) KS_LANE(3, false); else if (J == 2) KS_LANE(2, false); else KS_LANE(1, false);
   }
 #undef KS_LANE
   KS_HIP(hipGetLastError());

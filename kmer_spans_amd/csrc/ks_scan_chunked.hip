@@ -248,48 +248,7 @@ __device__ __forceinline__ void line_values(const TableView &tv, uint64_t x, int
     double lv[JL];
 #pragma unroll
     for (int t = 0; t < JL; ++t) lv[t] = 0.0;
-    if (b0 + o < n) {
-      const uint64_t gx = (x >> (64 - 2 * (o + kx))) & xmask;
-      const uint8_t *ln = tv.line + (size_t)(gx >> 2) * (tv.line_kind == 3 ? 128 : 64);
-      const uint32_t c1 = (uint32_t)gx & 3u;
-      if (tv.line_kind == 3) {  // wide: 13-bit own / L1 codes in the first 16 B
-        const uint4 q0 = *reinterpret_cast<const uint4 *>(ln);
-        const uint64_t lo = (uint64_t)q0.x | ((uint64_t)q0.y << 32), hi = (uint64_t)q0.z | ((uint64_t)q0.w << 32);
-        auto f13 = [&](int b) -> uint32_t {
-          const uint64_t w = b < 64 ? ((lo >> b) | (b > 51 ? (hi << (64 - b)) : 0ull)) : (hi >> (b - 64));
-          return (uint32_t)w & 0x1fffu;
-        };
-        uint32_t cs[JL];
-#pragma unroll
-        for (int t = 0; t < OWN; ++t) cs[t] = f13(13 * t);
-        const uint32_t l0 = f13(13 * OWN), l1 = f13(13 * (OWN + 1)), l2 = f13(13 * (OWN + 2)),
-                       l3 = f13(13 * (OWN + 3));
-        cs[OWN] = c1 == 0 ? l0 : (c1 == 1 ? l1 : (c1 == 2 ? l2 : l3));
-#pragma unroll
-        for (int t = 0; t < JL; ++t) lv[t] = s_lut ? s_lut[cs[t]] : tv.lut[cs[t]];
-      } else if (tv.line_kind == 1) {
-        uint32_t h[16];
-        const uint4 q0 = *reinterpret_cast<const uint4 *>(ln);
-        h[0] = q0.x & 0xffffu; h[1] = q0.x >> 16; h[2] = q0.y & 0xffffu; h[3] = q0.y >> 16;
-        h[4] = q0.z & 0xffffu; h[5] = q0.z >> 16; h[6] = q0.w & 0xffffu; h[7] = q0.w >> 16;
-        if (OWN + 4 > 8) {
-          const uint4 q1 = *reinterpret_cast<const uint4 *>(ln + 16);
-          h[8] = q1.x & 0xffffu; h[9] = q1.x >> 16; h[10] = q1.y & 0xffffu; h[11] = q1.y >> 16;
-          h[12] = q1.z & 0xffffu; h[13] = q1.z >> 16; h[14] = q1.w & 0xffffu; h[15] = q1.w >> 16;
-        }
-        uint32_t cs[JL];
-#pragma unroll
-        for (int t = 0; t < OWN; ++t) cs[t] = h[t];
-        cs[OWN] = c1 == 0 ? h[OWN] : (c1 == 1 ? h[OWN + 1] : (c1 == 2 ? h[OWN + 2] : h[OWN + 3]));
-#pragma unroll
-        for (int t = 0; t < JL; ++t) lv[t] = s_lut ? s_lut[cs[t]] : tv.lut[cs[t]];
-      } else {
-        const double *d = reinterpret_cast<const double *>(ln);
-#pragma unroll
-        for (int t = 0; t < OWN; ++t) lv[t] = d[t];
-        lv[OWN] = d[OWN + c1];
-      }
-    }
+    if (b0 + o < n) line_entries<OWN>(tv, (x >> (64 - 2 * (o + kx))) & xmask, lv, s_lut);
 #pragma unroll
     for (int t = 0; t < JL; ++t)
       if (o + t < NV) v[o + t] = (b0 + o + t < n) ? lv[t] : 0.0;

@@ -32,11 +32,62 @@ __device__ __forceinline__ double tv_get(const TableView &t, uint32_t code) {
   return t.compressed ? t.lut[t.codes[code]] : t.vals[code];
 }
 
+// The own + 1 values one line-table read serves (ks_table line_kind; the
+// passes after pass 1): the line of the m-mer key >> 2 (m = k + OWN - 1), its
+// OWN own entries and the L1 entry of continuation key & 3, from the line's
+// first 16-32 B.  key: the (k + OWN)-mer ending at the last index's k-mer.
+// s_lut: the LUT in LDS, or nullptr (global).
+template <int OWN>
+__device__ __forceinline__ void line_entries(const TableView &t, uint64_t key, double lv[OWN + 1],
+                                             const double *s_lut) {
+  constexpr int JL = OWN + 1;
+  const uint8_t *ln = t.line + (size_t)(key >> 2) * (t.line_kind == 3 ? 128 : 64);
+  const uint32_t c1 = (uint32_t)key & 3u;
+  if (t.line_kind == 2) {  // FP64 values
+    const double *d = reinterpret_cast<const double *>(ln);
+#pragma unroll
+    for (int q = 0; q < OWN; ++q) lv[q] = d[q];
+    lv[OWN] = d[OWN + c1];
+    return;
+  }
+  uint32_t cs[JL];
+  const uint4 q0 = *reinterpret_cast<const uint4 *>(ln);
+  if (t.line_kind == 3) {  // wide: 13-bit own / L1 codes in the first 16 B
+    const uint64_t lo = (uint64_t)q0.x | ((uint64_t)q0.y << 32), hi = (uint64_t)q0.z | ((uint64_t)q0.w << 32);
+    auto f13 = [&](int b) -> uint32_t {
+      const uint64_t w = b < 64 ? ((lo >> b) | (b > 51 ? (hi << (64 - b)) : 0ull)) : (hi >> (b - 64));
+      return (uint32_t)w & 0x1fffu;
+    };
+#pragma unroll
+    for (int q = 0; q < OWN; ++q) cs[q] = f13(13 * q);
+    const uint32_t l0 = f13(13 * OWN), l1 = f13(13 * (OWN + 1)), l2 = f13(13 * (OWN + 2)), l3 = f13(13 * (OWN + 3));
+    cs[OWN] = c1 == 0 ? l0 : (c1 == 1 ? l1 : (c1 == 2 ? l2 : l3));
+  } else {  // uint16 codes
+    uint32_t h[16];
+    h[0] = q0.x & 0xffffu; h[1] = q0.x >> 16; h[2] = q0.y & 0xffffu; h[3] = q0.y >> 16;
+    h[4] = q0.z & 0xffffu; h[5] = q0.z >> 16; h[6] = q0.w & 0xffffu; h[7] = q0.w >> 16;
+    if (OWN + 4 > 8) {
+      const uint4 q1 = *reinterpret_cast<const uint4 *>(ln + 16);
+      h[8] = q1.x & 0xffffu; h[9] = q1.x >> 16; h[10] = q1.y & 0xffffu; h[11] = q1.y >> 16;
+      h[12] = q1.z & 0xffffu; h[13] = q1.z >> 16; h[14] = q1.w & 0xffffu; h[15] = q1.w >> 16;
+    }
+#pragma unroll
+    for (int q = 0; q < OWN; ++q) cs[q] = h[q];
+    cs[OWN] = c1 == 0 ? h[OWN] : (c1 == 1 ? h[OWN + 1] : (c1 == 2 ? h[OWN + 2] : h[OWN + 3]));
+  }
+#pragma unroll
+  for (int q = 0; q < JL; ++q) lv[q] = s_lut ? s_lut[cs[q]] : t.lut[cs[q]];
+}
+
 // The J values of one expanded-table read: scan indices served by the
 // (k+J-1)-mer `gcode` (J = 1: the base table entry of the k-mer).  J = 5
 // (compressed) holds 12-bit codes; 0xFFF escapes to the base table.
 template <int J, bool kCompressed, typename GC>
 __device__ __forceinline__ void gather_group(const TableView &t, GC gcode, uint32_t kmask, double v[J]) {
+  if (J >= 3 && t.line) {  // line table (the dispatch sets J = own + 1): gcode is the (k + own)-mer
+    line_entries<(J >= 3 ? J - 1 : 2)>(t, (uint64_t)gcode, v, nullptr);
+    return;
+  }
   if (J == 1) {
     v[0] = kCompressed ? t.lut[t.codes[gcode]] : t.vals[gcode];
   } else if (kCompressed && J == 5) {

@@ -1231,6 +1231,8 @@ extern "C" ks_status ks_table_get_info(const ks_table *t, ks_table_info *out) {
   out->ms_ext_alloc = t->ms_ext_alloc;
   out->ms_ext_build = t->ms_ext;
   out->ms_total = t->ms_total;
+  out->line_kind = t->line_kind;
+  out->line_own = t->line_own;
   return KS_OK;
 }
 

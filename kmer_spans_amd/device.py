@@ -146,6 +146,26 @@ class DeviceTable:
         return int(load().ks_table_positions_per_read(self._h))
 
     @property
+    def line_kind(self) -> int:
+        """0: no line table; 1: uint16 64-B lines (k_pass1l); 2: FP64 64-B lines
+        (k_pass1l); 3: 128-B lines (k_pass1w)."""
+        return int(self.info()["line_kind"])
+
+    @property
+    def pass1_kernel(self) -> str:
+        """The pass-1 kernel the chunked scan runs on this table."""
+        lk = self.line_kind
+        if lk == 3:
+            return "k_pass1w"
+        if lk:
+            return "k_pass1l"
+        if self.k <= 7:
+            return "k_pass1_lds"
+        if self.positions_per_read > 1:
+            return "k_pass1p" if self.compressed else "k_pass1pf"
+        return "k_pass1"
+
+    @property
     def distinct(self) -> int:
         return int(load().ks_table_distinct(self._h))
 

@@ -43,11 +43,15 @@ __device__ __forceinline__ void line_entries(const TableView &t, uint64_t key, d
   constexpr int JL = OWN + 1;
   const uint8_t *ln = t.line + (size_t)(key >> 2) * (t.line_kind == 3 ? 128 : 64);
   const uint32_t c1 = (uint32_t)key & 3u;
-  if (t.line_kind == 2) {  // FP64 values
-    const double *d = reinterpret_cast<const double *>(ln);
+  if (t.line_kind == 2) {  // FP64 values: the own ones in 16-B loads, the L1 one alone
+    const double2 *d2 = reinterpret_cast<const double2 *>(ln);
 #pragma unroll
-    for (int q = 0; q < OWN; ++q) lv[q] = d[q];
-    lv[OWN] = d[OWN + c1];
+    for (int q = 0; q < OWN; q += 2) {
+      const double2 e = d2[q >> 1];
+      lv[q] = e.x;
+      if (q + 1 < OWN) lv[q + 1] = e.y;
+    }
+    lv[OWN] = reinterpret_cast<const double *>(ln)[OWN + c1];
     return;
   }
   uint32_t cs[JL];

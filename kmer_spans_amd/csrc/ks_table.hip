@@ -263,10 +263,11 @@ typedef uint32_t ks_u32x4 __attribute__((ext_vector_type(4)));
 // consecutive code-table entries from ((x << 2 lev) & mask)) and packs them
 // with compile-time offsets.  The lines are walked as x = (hi << lb) | lo
 // with lo (the low lb = 2k - 2 levmax bits, which alone decide the L-region
-// reads) fixed per lane and hi the loop: a block re-reads the same few KiB
-// of the code table on every trip (L1 / L2 hits), and a wave's 64 lines are
-// consecutive, so after a transpose through LDS each 16-B store instruction
-// writes 1 KiB of whole lines.  Mode 0: uint16 64-B lines, 1: FP64 64-B
+// reads) fixed per lane -- a block's 64 consecutive lo values, the same for
+// its four waves -- and hi the loop (four values per trip, one per wave): a
+// block re-reads the same 2-8 KiB of the code table on every trip (L1
+// hits), and a wave's 64 lines are consecutive, so after a transpose through
+// LDS each 16-B store instruction writes 1 KiB of whole lines.  Mode 0: uint16 64-B lines, 1: FP64 64-B
 // lines, 2: wide 128-B lines (13-bit own / L1 / L2 codes at bits 13 j, the
 // 64 L3 codes as 11-bit codes from bit 13 (own + 20), >= 2047 -> 2047).
 template <int OWN, int kMode>
@@ -280,9 +281,9 @@ __global__ void __launch_bounds__(256) k_build_lines(const uint16_t *__restrict_
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t kmask = (uint32_t)(((uint64_t)1 << (2 * k)) - 1);
   const int lb = 2 * k - 2 * LEV;
-  const uint64_t nhi = ((uint64_t)1 << (2 * m - lb)) / gridDim.y;  // hi range of this block row
-  const uint64_t lo = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (uint64_t hi = blockIdx.y * nhi; hi < (blockIdx.y + 1) * nhi; ++hi) {
+  const uint64_t nhi = ((uint64_t)1 << (2 * m - lb)) / gridDim.y;  // hi range of this block row (>= 4)
+  const uint64_t lo = (uint64_t)blockIdx.x * 64 + lane;
+  for (uint64_t hi = blockIdx.y * nhi + wv; hi < (blockIdx.y + 1) * nhi; hi += 4) {
     const uint64_t x = (hi << lb) | lo;
     uint32_t w[LB / 4];
 #pragma unroll
@@ -606,10 +607,10 @@ template <int OWN, int kMode>
 static void launch_build_lines(hipStream_t st, const ks_table *t, int m, void *out) {
   const int lev = kMode == 0 ? 2 : (kMode == 1 ? 1 : 3);
   const int lb = 2 * t->k - 2 * lev;
-  const int hb = 2 * m - lb;
+  const int hb = 2 * m - lb;  // >= 4 (m >= k + 1, levmax >= 1)
   int ys = 0;
-  while (lb + ys < 20 && ys < hb) ++ys;
-  hipLaunchKernelGGL((k_build_lines<OWN, kMode>), dim3((unsigned)(((uint64_t)1 << lb) / 256), 1u << ys), dim3(256), 0,
+  while (lb + ys < 22 && ys + 2 < hb) ++ys;
+  hipLaunchKernelGGL((k_build_lines<OWN, kMode>), dim3((unsigned)(((uint64_t)1 << lb) / 64), 1u << ys), dim3(256), 0,
                      st, t->d_codes, t->d_vals, t->k, m, (ks_u32x4 *)out);
 }
 

@@ -704,6 +704,16 @@ def rank_subline(args, ctx, ds, counts, words, make_table, timed_steps, host, D)
     return out
 
 
+def reduce_parity(ok, dist, tdist):
+    """True iff every rank's parity verdict is true (gloo/nccl MIN)."""
+    if not dist:
+        return ok
+    t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64,
+                     device=torch.device("cuda", torch.cuda.current_device()) if tdist.get_backend() == "nccl" else "cpu")
+    tdist.all_reduce(t, op=tdist.ReduceOp.MIN)
+    return float(t.item()) > 0.5
+
+
 def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over_ranks, make_table, D, genome,
                 build_id):
     """Config 5: G genomes per rank, each end to end (count -> table ->
@@ -743,6 +753,23 @@ def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over
     elapsed = max_over_ranks(time.perf_counter() - t0)
     bases = sum(int(r[2]["n_bases"]) for r in results) * world
     n_regions = sum(int(r[0].shape[1]) for r in results)
+    # parity of every genome of this rank after timing (each genome's own
+    # table, rebuilt: the timed loop closed it), the oracle on a thread pool
+    parity = None
+    if not args.no_cpu and args.parity != "none":
+        ok = True
+        for ds, r in zip(dss, results):
+            counts.zero_()
+            words = D.count(ctx, ds, k, counts)
+            w_dev, thr, table, init, _ = make_table(counts, words, args.score, ext_gib=1.0, warm=False)
+            table.close()
+            if init is not None:
+                init.close()
+            orc = Oracle(host_contigs(ds), k, (w_dev.cpu().numpy() - thr) if args.trlr else w_dev.cpu().numpy(), thr,
+                         args.min_width, args.min_score, args.trlr, args.cpu_threads)
+            orc.fill(range(ds.nseq))
+            ok &= orc.parity(r[0], r[1], range(ds.nseq))
+        parity = bool(reduce_parity(ok, dist, tdist))
     if dist:
         from kmer_spans_amd.dist import gather_regions
         pos = np.concatenate([r[0] for r in results], axis=1)
@@ -758,7 +785,7 @@ def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over
                                    f"{args.score}, each: count + table + expanded table + scan",
                        "k": k, "score": args.score, "genomes": G * world, "mode": "genomes",
                        "parallelism": f"genome-per-rank x{world}", "build_id": build_id},
-            "regions": n_regions}
+            "regions": n_regions, "parity_sample": parity, "parity_genomes": G * world if parity is not None else 0}
     if rank == 0:
         s = json.dumps(line)
         print(s, flush=True)

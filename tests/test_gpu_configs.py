@@ -99,3 +99,71 @@ def test_k15_scan(oracle, compress):
     ctx.set_scan_algo(-1)
     tab.close()
     assert o["pos"].shape[1] > 0
+
+
+def test_rank_k15(oracle):
+    """Config 4 as surveyed (weighted rank at k = 15, kmer_spans.c:189-202,
+    :548-621 with no k limit): device count of a ~3 Mbp genome, the device
+    (count, index) sort of 4^15 pairs and closed-form FP64 rank table (equal
+    to the host builder, itself pinned to the oracle's sequential prefix in
+    tests/test_lib.py), its expanded FP64 table, and the chunked scan (thr
+    0.75) against the oracle."""
+    import torch
+    from kmer_spans_amd import _lib, api, device as D, genome
+    ctx = _lib.context(0)
+    D.bind_torch_stream(ctx)
+    k = 15
+    torch.cuda.empty_cache()
+    s = genome.contig(3_000_000, 515, device="cuda", repeats=True)
+    ds = D.from_parts([s], [s.numel()], "cuda")
+    host = [ds.host_seq(0)]
+    counts = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+    words = D.count(ctx, ds, k, counts)
+    w = torch.empty(4 ** k, dtype=torch.float64, device="cuda")
+    tab = D.DeviceTable.from_counts(ctx, counts, k, "rank", total=words, thr=0.75, expand=True, w_out=w)
+    assert not tab.compressed and tab.positions_per_read >= 2
+    wh = w.cpu().numpy()
+    hc = counts.cpu().numpy()
+    ref = np.asarray(api.rank_table(hc, k, words), dtype=np.float64)
+    assert np.array_equal(wh.view(np.uint64), ref.view(np.uint64)), "device rank table vs host builder"
+    del ref, hc
+    o = oracle.scan(host, k, wh, 0.75, 100, 20.0, visits=True)
+    ctx.set_scan_algo(1)
+    vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+    pos, sc, st = D.scan(ctx, ds, k, tab, 100, 20.0, vis)
+    ctx.set_scan_algo(-1)
+    _same(pos, sc, o, "rank k=15")
+    assert np.array_equal(vis.cpu().numpy(), o["counts"]), "rank k=15 visits"
+    assert pos.shape[1] > 0
+    tab.close()
+
+
+def test_genomes_mode(oracle):
+    """Config 5 logic (bench.py --mode genomes, test.R:550-567's per-scaffold
+    pattern at genome scale): several genomes scanned one after another on
+    one context, each with its own device count -> device log2 table (a
+    32 GiB cap, as the mode builds it per genome) -> scan with the visit
+    histogram; every genome's regions, scores and visits against the
+    oracle with that genome's table."""
+    import torch
+    from kmer_spans_amd import _lib, device as D, genome
+    ctx = _lib.context(0)
+    D.bind_torch_stream(ctx)
+    k = 13
+    counts = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+    for g in range(3):
+        parts, lens = genome.human_like(scale=0.002, seed=1 + 1000 * g, device="cuda", ncontigs=24)
+        ds = D.from_parts(parts, lens, "cuda")
+        host = [ds.host_seq(q) for q in range(ds.nseq)]
+        counts.zero_()
+        words = D.count(ctx, ds, k, counts)
+        w = torch.empty(4 ** k, dtype=torch.float64, device="cuda")
+        tab = D.DeviceTable.from_counts(ctx, counts, k, "log2", total=words, expand=True,
+                                        max_ext_bytes=32 << 30, w_out=w)
+        vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+        pos, sc, st = D.scan(ctx, ds, k, tab, 100, 20.0, vis)
+        o = oracle.scan(host, k, w.cpu().numpy(), 0.0, 100, 20.0, visits=True)
+        _same(pos, sc, o, ("genome", g))
+        assert np.array_equal(vis.cpu().numpy(), o["counts"]), ("genome visits", g)
+        assert st["n_bases"] == sum(lens)
+        tab.close()

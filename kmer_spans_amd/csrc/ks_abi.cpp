@@ -512,11 +512,15 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
   for (int32_t q = 0; q < nseq; ++q)
     if (lens[q] >= k) n += (double)lens[q];                   // :535
   *n_bases = n;
+  static const bool dbg = getenv("KS_DEBUG_HOST") != nullptr;  // phase times to stderr
+  const double t0 = now_ms();
   Staged st;
   KS_TRY(stage(ctx, seqs, lens, nseq, &st));
+  const double t1 = now_ms();
   ks_table *t = nullptr;
   KS_TRY(table_create(ctx, w, k, 0.0, (k >= 9 ? KS_TABLE_COMPRESS : 0) | KS_TABLE_EXPAND, nullptr,
                       host_ext_cap(st.total), &t));
+  const double t2 = now_ms();
   const size_t nb = (size_t)4 << (2 * k);
   void *d_vis = nullptr;
   ks_status rc = KS_OK;
@@ -527,11 +531,15 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
   }
   if (rc == KS_OK)
     rc = scan_impl(ctx, &st.dev, st.total, k, t, min_width, min_score, (int32_t *)d_vis, out, nullptr);
+  const double t3 = now_ms();
   if (rc == KS_OK && visits) {
     if (hipMemcpyAsync(visits, d_vis, nb, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
         hipStreamSynchronize(ctx->stream) != hipSuccess)
       rc = fail(KS_ERR_DEVICE, "visit histogram copy failed");
   }
+  if (dbg)
+    fprintf(stderr, "[host kmer_regions] stage %.2f table %.2f (J %d) scan %.2f visits D2H %.2f ms\n", t1 - t0,
+            t2 - t1, t->ext_J, t3 - t2, now_ms() - t3);
   ks_table_destroy(t);
   if (rc != KS_OK) ks_regions_free(out);
   return rc;

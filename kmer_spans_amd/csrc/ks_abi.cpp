@@ -11,6 +11,8 @@
 #include <atomic>
 #include <condition_variable>
 #include <mutex>
+#include <tmmintrin.h>
+#include <string>
 #include <thread>
 
 #include <unistd.h>
@@ -105,6 +107,57 @@ ks_status ensure_pinned(ks_ctx *ctx, size_t bytes, void **out) {
 namespace {
 
 // Stage host sequences into the ctx's device buffer (16-byte aligned base).
+// 4-bit staging.  What the scan, the count and the runs read of a base is
+// its class: 'n' or 'N' (LC(c) == 'n', kmer_spans.c:265) or the 2-bit code
+// (c >> 1) & 3 (UPDATE_OFFSET, :34).  So the host sends one nibble per base,
+// 0..3 = that code and 4 = N, half the PCIe bytes, and the device rewrites
+// each nibble as a byte of the same class ('A' 'C' 'T' 'G' 'N').
+__attribute__((target("ssse3"))) void pack_nib(uint8_t *dst, const char *src, size_t n) {
+  // dst[j] = class(src[2j]) | class(src[2j + 1]) << 4; n even
+  const __m128i lc = _mm_set1_epi8(0x20), nn = _mm_set1_epi8('n'), three = _mm_set1_epi8(3),
+                four = _mm_set1_epi8(4), mul = _mm_set1_epi16(0x1001);
+  size_t i = 0;
+  for (; i + 32 <= n; i += 32) {
+    __m128i p[2];
+    for (int h = 0; h < 2; ++h) {
+      const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 16 * h));
+      const __m128i isn = _mm_cmpeq_epi8(_mm_or_si128(x, lc), nn);
+      const __m128i code = _mm_and_si128(_mm_srli_epi16(x, 1), three);  // bits 1-2 of each byte
+      const __m128i cls = _mm_or_si128(_mm_andnot_si128(isn, code), _mm_and_si128(isn, four));
+      p[h] = _mm_maddubs_epi16(cls, mul);  // even + 16 x odd
+    }
+    _mm_storeu_si128(reinterpret_cast<__m128i *>(dst + i / 2), _mm_packus_epi16(p[0], p[1]));
+  }
+  for (; i < n; i += 2) {
+    const uint8_t a = (uint8_t)src[i], b = (uint8_t)src[i + 1];
+    dst[i / 2] = (uint8_t)((is_n(a) ? 4 : (a >> 1) & 3) | (is_n(b) ? 4 : (b >> 1) & 3) << 4);
+  }
+}
+
+inline uint8_t nib_class(char c) { return is_n((uint8_t)c) ? 4 : ((uint8_t)c >> 1) & 3; }
+
+// 16 bases per thread: 8 packed bytes in, 16 class bytes out
+__global__ void k_unpack_nib(const uint2 *__restrict__ in, uint4 *__restrict__ out, int64_t n16) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n16) return;
+  const uint2 v = in[i];
+  const uint32_t w[2] = {v.x, v.y};
+  uint32_t o[4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      uint32_t r = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t nib = (w[h] >> (16 * b + 4 * j)) & 15u;
+        r |= (uint32_t)((0x4E47544341ull >> (8 * nib)) & 0xff) << (8 * j);  // A C T G N
+      }
+      o[2 * h + b] = r;
+    }
+  out[i] = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 struct Staged {
   ks_dev_seqs dev{};
   std::vector<int64_t> offs;
@@ -118,31 +171,62 @@ struct Staged {
 // (Was: one single-threaded memcpy of everything, then one H2D.)
 constexpr size_t kStageChunk = (size_t)64 << 20;
 
-ks_status stage(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq, Staged *st) {
+ks_status stage(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq, Staged *st,
+                bool nib = false) {
   st->offs.assign((size_t)nseq + 1, 0);
   for (int32_t q = 0; q < nseq; ++q) st->offs[q + 1] = st->offs[q] + std::max<int64_t>(lens[q], 0);
   st->total = st->offs[nseq];
-  void *d_seq = nullptr, *d_offs = nullptr, *h = nullptr;
-  KS_TRY(ensure(ctx, SLOT_SEQ, (size_t)st->total + 32, &d_seq));
-  KS_TRY(ensure(ctx, SLOT_OFFS, ((size_t)nseq + 1) * 8, &d_offs));
-  KS_TRY(ensure_pinned(ctx, (size_t)st->total + 32, &h));
-  char *hp = static_cast<char *>(h);
   const size_t total = (size_t)st->total;
+  nib = nib && total >= ((size_t)1 << 20) && !getenv("KS_STAGE_BYTES");
+  void *d_seq = nullptr, *d_offs = nullptr, *h = nullptr, *d_nib = nullptr;
+  KS_TRY(ensure(ctx, SLOT_SEQ, total + 32, &d_seq));
+  KS_TRY(ensure(ctx, SLOT_OFFS, ((size_t)nseq + 1) * 8, &d_offs));
+  if (nib) KS_TRY(ensure(ctx, SLOT_STAGE_NIB, total / 2 + 64, &d_nib));
+  KS_TRY(ensure_pinned(ctx, (nib ? total / 2 : total) + 32, &h));
+  char *hp = static_cast<char *>(h);
+  uint8_t *hn = static_cast<uint8_t *>(h);
   const size_t nchunk = (total + kStageChunk - 1) / kStageChunk;
   // fill chunk c: the parts of the sequences overlapping [c x S, (c + 1) x S)
   auto fill = [&](size_t c) {
     const int64_t lo = (int64_t)(c * kStageChunk), hi = std::min<int64_t>(lo + (int64_t)kStageChunk, (int64_t)total);
     int32_t q = (int32_t)(std::upper_bound(st->offs.begin(), st->offs.end(), lo) - st->offs.begin()) - 1;
     for (; q < nseq && st->offs[q] < hi; ++q) {
-      const int64_t a = std::max(lo, st->offs[q]), b = std::min(hi, st->offs[q + 1]);
-      if (b > a) memcpy(hp + a, seqs[q] + (a - st->offs[q]), (size_t)(b - a));
+      int64_t a = std::max(lo, st->offs[q]);
+      const int64_t b = std::min(hi, st->offs[q + 1]);
+      if (b <= a) continue;
+      const char *src = seqs[q] + (a - st->offs[q]);
+      if (!nib) {
+        memcpy(hp + a, src, (size_t)(b - a));
+        continue;
+      }
+      // nibble p of byte p / 2 (low = even); a sequence may start or end
+      // mid-byte (chunks start on even positions, so a byte is one thread's)
+      if (a & 1) {
+        hn[a / 2] = (uint8_t)((hn[a / 2] & 15u) | nib_class(*src) << 4);
+        ++a;
+        ++src;
+      }
+      const int64_t even = (b - a) & ~(int64_t)1;
+      pack_nib(hn + a / 2, src, (size_t)even);
+      if (a + even < b) hn[(a + even) / 2] = nib_class(src[even]);
     }
+  };
+  // device: bases [off, off + n) from their nibbles (off even; the odd tail
+  // of the last chunk rounds up into the 32 B of slack after the buffer)
+  auto unpack = [&](size_t off, size_t n) -> hipError_t {
+    const int64_t n16 = (int64_t)((n + 15) / 16);
+    hipLaunchKernelGGL(k_unpack_nib, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, ctx->stream,
+                       reinterpret_cast<const uint2 *>(static_cast<uint8_t *>(d_nib) + off / 2),
+                       reinterpret_cast<uint4 *>(static_cast<uint8_t *>(d_seq) + off), n16);
+    return hipGetLastError();
   };
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const size_t nthr = std::min<size_t>(std::min<size_t>(16, hw), nchunk);
   if (nthr <= 1) {
     for (size_t c = 0; c < nchunk; ++c) fill(c);
-    if (total) KS_HIP(hipMemcpyAsync(d_seq, h, total, hipMemcpyHostToDevice, ctx->stream));
+    if (total) KS_HIP(hipMemcpyAsync(nib ? d_nib : d_seq, h, nib ? (total + 1) / 2 : total, hipMemcpyHostToDevice,
+                                     ctx->stream));
+    if (nib) KS_HIP(unpack(0, total));
   } else {
     std::atomic<size_t> next{0};
     std::vector<std::atomic<uint8_t>> done(nchunk);
@@ -168,8 +252,13 @@ ks_status stage(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32
         cv.wait(g, [&] { return done[c].load(std::memory_order_acquire) != 0; });
       }
       const size_t off = c * kStageChunk, n = std::min(kStageChunk, total - off);
-      if (err == hipSuccess)
+      if (err == hipSuccess && nib) {
+        err = hipMemcpyAsync(static_cast<uint8_t *>(d_nib) + off / 2, hn + off / 2, (n + 1) / 2,
+                             hipMemcpyHostToDevice, ctx->stream);
+        if (err == hipSuccess) err = unpack(off, n);
+      } else if (err == hipSuccess) {
         err = hipMemcpyAsync(static_cast<char *>(d_seq) + off, hp + off, n, hipMemcpyHostToDevice, ctx->stream);
+      }
     }
     for (auto &th : pool) th.join();
     if (err != hipSuccess) return fail(KS_ERR_DEVICE, "sequence upload failed: %s", hipGetErrorString(err));
@@ -181,6 +270,35 @@ ks_status stage(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32
   st->dev.offsets_dev = static_cast<const int64_t *>(d_offs);
   st->dev.offsets_host = st->offs.data();
   st->dev.nseq = nseq;
+  return KS_OK;
+}
+
+// memcpy with up to 16 threads (host results out of the pinned buffer)
+void par_memcpy(void *dst, const void *src, size_t n) {
+  const size_t nthr = std::min<size_t>(std::min<size_t>(16, std::max(1u, std::thread::hardware_concurrency())),
+                                       std::max<size_t>(1, n >> 24));
+  if (nthr <= 1) {
+    memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  const size_t per = (n + nthr - 1) / nthr;
+  for (size_t t = 0; t < nthr; ++t)
+    pool.emplace_back([=] {
+      const size_t a = t * per, b = std::min(n, a + per);
+      if (b > a) memcpy(static_cast<char *>(dst) + a, static_cast<const char *>(src) + a, b - a);
+    });
+  for (auto &th : pool) th.join();
+}
+
+// Device -> pageable host through the ctx's pinned buffer (the runtime's
+// own staging of a pageable destination runs at a fraction of PCIe speed).
+ks_status copy_out(ks_ctx *ctx, void *dst, const void *src_dev, size_t n) {
+  void *h = nullptr;
+  KS_TRY(ensure_pinned(ctx, n, &h));
+  KS_HIP(hipMemcpyAsync(h, src_dev, n, hipMemcpyDeviceToHost, ctx->stream));
+  KS_HIP(hipStreamSynchronize(ctx->stream));
+  par_memcpy(dst, h, n);
   return KS_OK;
 }
 
@@ -514,32 +632,62 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
   *n_bases = n;
   static const bool dbg = getenv("KS_DEBUG_HOST") != nullptr;  // phase times to stderr
   const double t0 = now_ms();
-  Staged st;
-  KS_TRY(stage(ctx, seqs, lens, nseq, &st));
-  const double t1 = now_ms();
+  // The score table's upload and compression (host w, independent of the
+  // sequences) run on the sub-context from a second host thread while the
+  // sequences are staged; its expansion waits for the k-mer count.
+  ks_ctx *sub = nullptr;
+  KS_TRY(ctx_sub(ctx, &sub));
   ks_table *t = nullptr;
-  KS_TRY(table_create(ctx, w, k, 0.0, (k >= 9 ? KS_TABLE_COMPRESS : 0) | KS_TABLE_EXPAND, nullptr,
-                      host_ext_cap(st.total), &t));
-  const double t2 = now_ms();
+  ks_status rc_t = KS_OK;
+  std::string err_t;
+  std::thread th([&] {
+    rc_t = activate(sub);
+    if (rc_t == KS_OK) rc_t = table_create(sub, w, k, 0.0, k >= 9 ? KS_TABLE_COMPRESS : 0, nullptr, 0, &t);
+    if (rc_t == KS_OK && hipStreamSynchronize(sub->stream) != hipSuccess)
+      rc_t = fail(KS_ERR_DEVICE, "table upload failed");
+    if (rc_t != KS_OK) err_t = ks_last_error();  // (thread-local)
+  });
+  Staged st;
+  ks_status rc = stage(ctx, seqs, lens, nseq, &st, true);
+  th.join();
+  if (rc == KS_OK && rc_t != KS_OK) {
+    set_error("%s", err_t.c_str());
+    rc = rc_t;
+  }
+  if (rc != KS_OK) {
+    ks_table_destroy(t);
+    return rc;
+  }
+  const double t1 = now_ms();
+  // the top-level visits: sequence_kmer_count's histogram (one partitioned
+  // count pass), also the table's position-frequency hint (the binade
+  // predictor of the scan's pass-1 summaries is built from it: without it a
+  // metric-size scan spends ~27 ms more on summary fixes)
   const size_t nb = (size_t)4 << (2 * k);
-  void *d_vis = nullptr;
-  ks_status rc = KS_OK;
-  if (visits) {
-    rc = ensure(ctx, SLOT_COUNTS, nb, &d_vis);
-    if (rc == KS_OK && hipMemsetAsync(d_vis, 0, nb, ctx->stream) != hipSuccess)
-      rc = fail(KS_ERR_DEVICE, "hipMemsetAsync failed");
+  void *d_cnt = nullptr;
+  double words = 0;
+  Runs none;
+  rc = ensure(ctx, SLOT_COUNTS, nb, &d_cnt);
+  if (rc == KS_OK && hipMemsetAsync(d_cnt, 0, nb, ctx->stream) != hipSuccess)
+    rc = fail(KS_ERR_DEVICE, "hipMemsetAsync failed");
+  if (rc == KS_OK) rc = launch_count(ctx, &st.dev, st.total, none, k, static_cast<int32_t *>(d_cnt), &words);
+  const double t2 = now_ms();
+  if (rc == KS_OK) {
+    t->ctx = ctx;
+    rc = table_expand(ctx, t, (size_t)host_ext_cap(st.total), static_cast<const int32_t *>(d_cnt));
   }
-  if (rc == KS_OK)
-    rc = scan_impl(ctx, &st.dev, st.total, k, t, min_width, min_score, (int32_t *)d_vis, out, nullptr);
   const double t3 = now_ms();
-  if (rc == KS_OK && visits) {
-    if (hipMemcpyAsync(visits, d_vis, nb, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
-        hipStreamSynchronize(ctx->stream) != hipSuccess)
-      rc = fail(KS_ERR_DEVICE, "visit histogram copy failed");
+  if (rc == KS_OK) {
+    ScanMode mode;
+    mode.visits_counted = true;
+    rc = scan_impl(ctx, &st.dev, st.total, k, t, min_width, min_score, visits ? (int32_t *)d_cnt : nullptr, out,
+                   nullptr, mode);
   }
+  const double t4 = now_ms();
+  if (rc == KS_OK && visits) rc = copy_out(ctx, visits, d_cnt, nb);
   if (dbg)
-    fprintf(stderr, "[host kmer_regions] stage %.2f table %.2f (J %d) scan %.2f visits D2H %.2f ms\n", t1 - t0,
-            t2 - t1, t->ext_J, t3 - t2, now_ms() - t3);
+    fprintf(stderr, "[host kmer_regions] stage + table upload %.2f count %.2f expand %.2f (J %d) scan %.2f "
+            "visits D2H %.2f ms\n", t1 - t0, t2 - t1, t3 - t2, t->ext_J, t4 - t3, now_ms() - t4);
   ks_table_destroy(t);
   if (rc != KS_OK) ks_regions_free(out);
   return rc;

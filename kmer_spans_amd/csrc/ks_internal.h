@@ -61,6 +61,7 @@ enum Slot : int {
   SLOT_TABLE_TMP,
   SLOT_LAYOUT,      // run layout (chunk / tile bases)
   SLOT_PACKED,      // 2-bit base codes of the whole buffer (find_runs, want_packed)
+  SLOT_STAGE_NIB,   // host entry staging: 4-bit base classes as sent over PCIe
   SLOT_COUNT
 };
 
@@ -234,6 +235,10 @@ struct ScanMode {
   int64_t min_len = 0;
   int finite = 1;
   double maxabs = 0.0;
+  // visits_dev already holds the top-level k-mer count of the input
+  // (sequence_kmer_count's histogram, e.g. the one the caller built the
+  // table's hint from): the scan applies its corrections and rescans only
+  bool visits_counted = false;
 };
 
 ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, const ks_table *t,

@@ -413,16 +413,21 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
           const int64_t n = (int64_t)1 << (2 * k);
           if (!vis_atomic) {
             double words = 0;
-            if (ctx->vis_count_ext)  // scan_impl adds the count (uint32 wrap-around makes the order free)
+            if (mode.visits_counted) {
+              // (the caller's count is already in visits_dev)
+            } else if (ctx->vis_count_ext) {  // scan_impl adds the count (uint32 wrap-around makes the order free)
               ctx->vis_count_ext_used = true;
-            else
+            } else {
               KS_TRY(launch_count(ctx, s, total, runs, k, visits_dev, &words));
+            }
             if (runs.n > 0) {
               hipLaunchKernelGGL(k_visit_correct, dim3((unsigned)((runs.n + 255) / 256)), dim3(256), 0, st, runs.a,
                                  runs.b, runs.seq, runs.n, s->offsets_dev, s->seq, k, vis);
               KS_HIP(hipGetLastError());
             }
           }
+          else if (mode.visits_counted)  // the atomic route counts the top level itself
+            KS_HIP(hipMemsetAsync(vis, 0, (size_t)n * 4, st));
           hipLaunchKernelGGL(k_add_hist, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, st,
                              vis, vscr, n);
           KS_HIP(hipGetLastError());
@@ -438,6 +443,8 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
       }
     }
     if (algo == 0) {
+      if (vis && mode.visits_counted)  // the lane kernel counts every visit itself
+        KS_HIP(hipMemsetAsync(vis, 0, (size_t)4 << (2 * k), st));
       if (runs.n)
         KS_TRY(launch_scan_lane(ctx, s->seq, total, runs.a, runs.b, runs.seq, runs.n, k, tv, mw, min_score, vis, rb,
                                 nullptr, 0, mode, 1, s->offsets_dev, runs.packed));
@@ -565,7 +572,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
     for (int32_t q = 0; q < s->nseq; ++q)
       longest_seq = std::max<int64_t>(longest_seq, s->offsets_host[q + 1] - s->offsets_host[q]);
     const bool chunked_likely = ctx->scan_algo == 1 || (ctx->scan_algo < 0 && longest_seq > (1 << 15));
-    const bool vis_conc = visits_dev && !mode.trlr && chunked_likely && total > 0 &&
+    const bool vis_conc = visits_dev && !mode.trlr && !mode.visits_counted && chunked_likely && total > 0 &&
                           getenv("KS_VISITS_ATOMIC") == nullptr && getenv("KS_VISITS_SERIAL") == nullptr;
     if (!vis_conc) return scan_core(ctx, s, total, k, t, min_width, min_score, visits_dev, out, stats, mode);
     ks_ctx *vsub = nullptr;

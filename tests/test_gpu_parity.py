@@ -146,6 +146,27 @@ def test_config1_uniform_pm1_k7(K, oracle):
     assert np.array_equal(g["counts"], o["counts"])
 
 
+def test_host_entry_nibble_staging(K, oracle):
+    """Host entry at >= 1 MiB stages one nibble per base (the base's class:
+    N or (c >> 1) & 3): odd-length sequences (bytes shared by two
+    sequences), lower case, N runs and non-ACGT letters, against the oracle."""
+    rng = np.random.default_rng(21)
+    alpha = np.frombuffer(b"ACGTACGTACGTacgtNnRYx", dtype=np.uint8)
+    seqs = []
+    for ln in [1, 3, 700_001, 2, 5, 1_200_003, 0, 999_999, 1, 17]:
+        b = alpha[rng.integers(0, len(alpha), size=ln)].copy()
+        if ln > 1000:
+            b[ln // 3: ln // 3 + 500] = ord("N")
+        seqs.append(b.tobytes().decode())
+    k = 7
+    w = rng.normal(size=4 ** k) * 0.5 + 0.05
+    g = K.kmer_regions(seqs, k, w, 20, 3.0)
+    o = oracle.kmer_regions(seqs, k, w, 20, 3.0)
+    assert o["n"] > 100
+    _assert_same_regions(g["pos"], g["score"], o["pos"], o["score"], "nibble staging")
+    assert np.array_equal(g["counts"], o["counts"])
+
+
 @pytest.mark.parametrize("k,score", [(9, "log2"), (11, "log2"), (9, "pm1"), (8, "rank")])
 def test_human_like_device_path(K, oracle, ctx, k, score):
     """Scaled config-3 genome (~6 Mbp, repeats + N gaps), device-resident

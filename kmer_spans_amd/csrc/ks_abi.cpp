@@ -7,11 +7,11 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <vector>
 #include <atomic>
 #include <condition_variable>
 #include <mutex>
-#include <tmmintrin.h>
 #include <string>
 #include <thread>
 
@@ -105,202 +105,6 @@ ks_status ensure_pinned(ks_ctx *ctx, size_t bytes, void **out) {
 }
 
 namespace {
-
-// Stage host sequences into the ctx's device buffer (16-byte aligned base).
-// 4-bit staging.  What the scan, the count and the runs read of a base is
-// its class: 'n' or 'N' (LC(c) == 'n', kmer_spans.c:265) or the 2-bit code
-// (c >> 1) & 3 (UPDATE_OFFSET, :34).  So the host sends one nibble per base,
-// 0..3 = that code and 4 = N, half the PCIe bytes, and the device rewrites
-// each nibble as a byte of the same class ('A' 'C' 'T' 'G' 'N').
-__attribute__((target("ssse3"))) void pack_nib(uint8_t *dst, const char *src, size_t n) {
-  // dst[j] = class(src[2j]) | class(src[2j + 1]) << 4; n even
-  const __m128i lc = _mm_set1_epi8(0x20), nn = _mm_set1_epi8('n'), three = _mm_set1_epi8(3),
-                four = _mm_set1_epi8(4), mul = _mm_set1_epi16(0x1001);
-  size_t i = 0;
-  for (; i + 32 <= n; i += 32) {
-    __m128i p[2];
-    for (int h = 0; h < 2; ++h) {
-      const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 16 * h));
-      const __m128i isn = _mm_cmpeq_epi8(_mm_or_si128(x, lc), nn);
-      const __m128i code = _mm_and_si128(_mm_srli_epi16(x, 1), three);  // bits 1-2 of each byte
-      const __m128i cls = _mm_or_si128(_mm_andnot_si128(isn, code), _mm_and_si128(isn, four));
-      p[h] = _mm_maddubs_epi16(cls, mul);  // even + 16 x odd
-    }
-    _mm_storeu_si128(reinterpret_cast<__m128i *>(dst + i / 2), _mm_packus_epi16(p[0], p[1]));
-  }
-  for (; i < n; i += 2) {
-    const uint8_t a = (uint8_t)src[i], b = (uint8_t)src[i + 1];
-    dst[i / 2] = (uint8_t)((is_n(a) ? 4 : (a >> 1) & 3) | (is_n(b) ? 4 : (b >> 1) & 3) << 4);
-  }
-}
-
-inline uint8_t nib_class(char c) { return is_n((uint8_t)c) ? 4 : ((uint8_t)c >> 1) & 3; }
-
-// 16 bases per thread: 8 packed bytes in, 16 class bytes out
-__global__ void k_unpack_nib(const uint2 *__restrict__ in, uint4 *__restrict__ out, int64_t n16) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n16) return;
-  const uint2 v = in[i];
-  const uint32_t w[2] = {v.x, v.y};
-  uint32_t o[4];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      uint32_t r = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t nib = (w[h] >> (16 * b + 4 * j)) & 15u;
-        r |= (uint32_t)((0x4E47544341ull >> (8 * nib)) & 0xff) << (8 * j);  // A C T G N
-      }
-      o[2 * h + b] = r;
-    }
-  out[i] = make_uint4(o[0], o[1], o[2], o[3]);
-}
-
-struct Staged {
-  ks_dev_seqs dev{};
-  std::vector<int64_t> offs;
-  int64_t total = 0;
-};
-
-// The bytes go through the ctx's pinned buffer in 64 MiB chunks: worker
-// threads fill the chunks in order (host memory bandwidth, not one core's
-// memcpy) and each chunk's H2D copy is queued as soon as it is full, so the
-// PCIe transfer overlaps the fill; one synchronisation at the end.
-// (Was: one single-threaded memcpy of everything, then one H2D.)
-constexpr size_t kStageChunk = (size_t)64 << 20;
-
-ks_status stage(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq, Staged *st,
-                bool nib = false) {
-  st->offs.assign((size_t)nseq + 1, 0);
-  for (int32_t q = 0; q < nseq; ++q) st->offs[q + 1] = st->offs[q] + std::max<int64_t>(lens[q], 0);
-  st->total = st->offs[nseq];
-  const size_t total = (size_t)st->total;
-  nib = nib && total >= ((size_t)1 << 20) && !getenv("KS_STAGE_BYTES");
-  void *d_seq = nullptr, *d_offs = nullptr, *h = nullptr, *d_nib = nullptr;
-  KS_TRY(ensure(ctx, SLOT_SEQ, total + 32, &d_seq));
-  KS_TRY(ensure(ctx, SLOT_OFFS, ((size_t)nseq + 1) * 8, &d_offs));
-  if (nib) KS_TRY(ensure(ctx, SLOT_STAGE_NIB, total / 2 + 64, &d_nib));
-  KS_TRY(ensure_pinned(ctx, (nib ? total / 2 : total) + 32, &h));
-  char *hp = static_cast<char *>(h);
-  uint8_t *hn = static_cast<uint8_t *>(h);
-  const size_t nchunk = (total + kStageChunk - 1) / kStageChunk;
-  // fill chunk c: the parts of the sequences overlapping [c x S, (c + 1) x S)
-  auto fill = [&](size_t c) {
-    const int64_t lo = (int64_t)(c * kStageChunk), hi = std::min<int64_t>(lo + (int64_t)kStageChunk, (int64_t)total);
-    int32_t q = (int32_t)(std::upper_bound(st->offs.begin(), st->offs.end(), lo) - st->offs.begin()) - 1;
-    for (; q < nseq && st->offs[q] < hi; ++q) {
-      int64_t a = std::max(lo, st->offs[q]);
-      const int64_t b = std::min(hi, st->offs[q + 1]);
-      if (b <= a) continue;
-      const char *src = seqs[q] + (a - st->offs[q]);
-      if (!nib) {
-        memcpy(hp + a, src, (size_t)(b - a));
-        continue;
-      }
-      // nibble p of byte p / 2 (low = even); a sequence may start or end
-      // mid-byte (chunks start on even positions, so a byte is one thread's)
-      if (a & 1) {
-        hn[a / 2] = (uint8_t)((hn[a / 2] & 15u) | nib_class(*src) << 4);
-        ++a;
-        ++src;
-      }
-      const int64_t even = (b - a) & ~(int64_t)1;
-      pack_nib(hn + a / 2, src, (size_t)even);
-      if (a + even < b) hn[(a + even) / 2] = nib_class(src[even]);
-    }
-  };
-  // device: bases [off, off + n) from their nibbles (off even; the odd tail
-  // of the last chunk rounds up into the 32 B of slack after the buffer)
-  auto unpack = [&](size_t off, size_t n) -> hipError_t {
-    const int64_t n16 = (int64_t)((n + 15) / 16);
-    hipLaunchKernelGGL(k_unpack_nib, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, ctx->stream,
-                       reinterpret_cast<const uint2 *>(static_cast<uint8_t *>(d_nib) + off / 2),
-                       reinterpret_cast<uint4 *>(static_cast<uint8_t *>(d_seq) + off), n16);
-    return hipGetLastError();
-  };
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const size_t nthr = std::min<size_t>(std::min<size_t>(16, hw), nchunk);
-  if (nthr <= 1) {
-    for (size_t c = 0; c < nchunk; ++c) fill(c);
-    if (total) KS_HIP(hipMemcpyAsync(nib ? d_nib : d_seq, h, nib ? (total + 1) / 2 : total, hipMemcpyHostToDevice,
-                                     ctx->stream));
-    if (nib) KS_HIP(unpack(0, total));
-  } else {
-    std::atomic<size_t> next{0};
-    std::vector<std::atomic<uint8_t>> done(nchunk);
-    for (auto &d : done) d.store(0, std::memory_order_relaxed);
-    std::mutex mu;
-    std::condition_variable cv;
-    std::vector<std::thread> pool;
-    for (size_t t = 0; t < nthr; ++t)
-      pool.emplace_back([&] {
-        for (size_t c; (c = next.fetch_add(1)) < nchunk;) {
-          fill(c);
-          {
-            std::lock_guard<std::mutex> g(mu);
-            done[c].store(1, std::memory_order_release);
-          }
-          cv.notify_one();
-        }
-      });
-    hipError_t err = hipSuccess;
-    for (size_t c = 0; c < nchunk; ++c) {  // queue each chunk's copy once it is full, in order
-      {
-        std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return done[c].load(std::memory_order_acquire) != 0; });
-      }
-      const size_t off = c * kStageChunk, n = std::min(kStageChunk, total - off);
-      if (err == hipSuccess && nib) {
-        err = hipMemcpyAsync(static_cast<uint8_t *>(d_nib) + off / 2, hn + off / 2, (n + 1) / 2,
-                             hipMemcpyHostToDevice, ctx->stream);
-        if (err == hipSuccess) err = unpack(off, n);
-      } else if (err == hipSuccess) {
-        err = hipMemcpyAsync(static_cast<char *>(d_seq) + off, hp + off, n, hipMemcpyHostToDevice, ctx->stream);
-      }
-    }
-    for (auto &th : pool) th.join();
-    if (err != hipSuccess) return fail(KS_ERR_DEVICE, "sequence upload failed: %s", hipGetErrorString(err));
-  }
-  KS_HIP(hipMemcpyAsync(d_offs, st->offs.data(), ((size_t)nseq + 1) * 8, hipMemcpyHostToDevice,
-                        ctx->stream));
-  KS_HIP(hipStreamSynchronize(ctx->stream));
-  st->dev.seq = static_cast<const uint8_t *>(d_seq);
-  st->dev.offsets_dev = static_cast<const int64_t *>(d_offs);
-  st->dev.offsets_host = st->offs.data();
-  st->dev.nseq = nseq;
-  return KS_OK;
-}
-
-// memcpy with up to 16 threads (host results out of the pinned buffer)
-void par_memcpy(void *dst, const void *src, size_t n) {
-  const size_t nthr = std::min<size_t>(std::min<size_t>(16, std::max(1u, std::thread::hardware_concurrency())),
-                                       std::max<size_t>(1, n >> 24));
-  if (nthr <= 1) {
-    memcpy(dst, src, n);
-    return;
-  }
-  std::vector<std::thread> pool;
-  const size_t per = (n + nthr - 1) / nthr;
-  for (size_t t = 0; t < nthr; ++t)
-    pool.emplace_back([=] {
-      const size_t a = t * per, b = std::min(n, a + per);
-      if (b > a) memcpy(static_cast<char *>(dst) + a, static_cast<const char *>(src) + a, b - a);
-    });
-  for (auto &th : pool) th.join();
-}
-
-// Device -> pageable host through the ctx's pinned buffer (the runtime's
-// own staging of a pageable destination runs at a fraction of PCIe speed).
-ks_status copy_out(ks_ctx *ctx, void *dst, const void *src_dev, size_t n) {
-  void *h = nullptr;
-  KS_TRY(ensure_pinned(ctx, n, &h));
-  KS_HIP(hipMemcpyAsync(h, src_dev, n, hipMemcpyDeviceToHost, ctx->stream));
-  KS_HIP(hipStreamSynchronize(ctx->stream));
-  par_memcpy(dst, h, n);
-  return KS_OK;
-}
 
 ks_status check_seqs(const char *const *seqs, const int64_t *lens, int32_t nseq) {
   if (nseq < 1 || !seqs || !lens)
@@ -640,16 +444,57 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
   ks_table *t = nullptr;
   ks_status rc_t = KS_OK;
   std::string err_t;
+  double t_table = 0, t_stage = 0;
   std::thread th([&] {
     rc_t = activate(sub);
     if (rc_t == KS_OK) rc_t = table_create(sub, w, k, 0.0, k >= 9 ? KS_TABLE_COMPRESS : 0, nullptr, 0, &t);
     if (rc_t == KS_OK && hipStreamSynchronize(sub->stream) != hipSuccess)
       rc_t = fail(KS_ERR_DEVICE, "table upload failed");
     if (rc_t != KS_OK) err_t = ks_last_error();  // (thread-local)
+    t_table = now_ms();
   });
+  // the top-level visits: sequence_kmer_count's histogram (the partitioned
+  // count), also the table's position-frequency hint (the binade predictor
+  // of the scan's pass-1 summaries is built from it: without it a
+  // metric-size scan spends ~27 ms more on summary fixes).  Where the
+  // partitioned count takes position ranges, each ~eighth of the staged
+  // bases is counted on the side stream while the rest crosses PCIe.
+  const size_t nb = (size_t)4 << (2 * k);
+  int64_t total_in = 0;
+  for (int32_t q = 0; q < nseq; ++q) total_in += std::max<int64_t>(lens[q], 0);
+  void *d_cnt = nullptr;
+  ks_status rc = ensure(ctx, SLOT_COUNTS, nb, &d_cnt);
+  if (rc == KS_OK && hipMemsetAsync(d_cnt, 0, nb, ctx->stream) != hipSuccess)
+    rc = fail(KS_ERR_DEVICE, "hipMemsetAsync failed");
+  const bool piecewise = count_range_ok(k, total_in) && !getenv("KS_HOST_COUNT_AFTER");
+  const int64_t align = std::max<int64_t>(count_range_align(), stage_chunk_bases());
+  const int64_t piece = std::max<int64_t>(align, (total_in / 8 + align - 1) / align * align);
+  int64_t counted = 0;
+  struct Ev {
+    hipEvent_t e = nullptr;
+    ~Ev() {
+      if (e) (void)hipEventDestroy(e);
+    }
+  } ev;
+  if (rc == KS_OK && piecewise && hipEventCreateWithFlags(&ev.e, hipEventDisableTiming) != hipSuccess)
+    rc = fail(KS_ERR_DEVICE, "hipEventCreate failed");
+  hipEvent_t ev_piece = ev.e;
+  if (getenv("KS_HOST_TABLE_FIRST")) th.join();  // (experiment: the table crosses PCIe before the bases)
   Staged st;
-  ks_status rc = stage(ctx, seqs, lens, nseq, &st, true);
-  th.join();
+  auto on_bytes = [&](int64_t p1) -> ks_status {
+    if (p1 < total_in && p1 - counted < piece) return KS_OK;
+    KS_TRY(launch_count_range(ctx, ctx->side, &st.dev, counted, p1, k, static_cast<int32_t *>(d_cnt)));
+    counted = p1;
+    return KS_OK;
+  };
+  if (rc == KS_OK)
+    rc = stage(ctx, seqs, lens, nseq, &st, true, piecewise ? std::function<ks_status(int64_t)>(on_bytes) : nullptr);
+  t_stage = now_ms();
+  if (rc == KS_OK && piecewise) {  // the main stream waits for the last piece's count
+    if (hipEventRecord(ev_piece, ctx->side) != hipSuccess || hipStreamWaitEvent(ctx->stream, ev_piece, 0) != hipSuccess)
+      rc = fail(KS_ERR_DEVICE, "count join failed");
+  }
+  if (th.joinable()) th.join();
   if (rc == KS_OK && rc_t != KS_OK) {
     set_error("%s", err_t.c_str());
     rc = rc_t;
@@ -659,18 +504,10 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
     return rc;
   }
   const double t1 = now_ms();
-  // the top-level visits: sequence_kmer_count's histogram (one partitioned
-  // count pass), also the table's position-frequency hint (the binade
-  // predictor of the scan's pass-1 summaries is built from it: without it a
-  // metric-size scan spends ~27 ms more on summary fixes)
-  const size_t nb = (size_t)4 << (2 * k);
-  void *d_cnt = nullptr;
   double words = 0;
   Runs none;
-  rc = ensure(ctx, SLOT_COUNTS, nb, &d_cnt);
-  if (rc == KS_OK && hipMemsetAsync(d_cnt, 0, nb, ctx->stream) != hipSuccess)
-    rc = fail(KS_ERR_DEVICE, "hipMemsetAsync failed");
-  if (rc == KS_OK) rc = launch_count(ctx, &st.dev, st.total, none, k, static_cast<int32_t *>(d_cnt), &words);
+  if (rc == KS_OK && !piecewise)
+    rc = launch_count(ctx, &st.dev, st.total, none, k, static_cast<int32_t *>(d_cnt), &words);
   const double t2 = now_ms();
   if (rc == KS_OK) {
     t->ctx = ctx;
@@ -686,8 +523,9 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
   const double t4 = now_ms();
   if (rc == KS_OK && visits) rc = copy_out(ctx, visits, d_cnt, nb);
   if (dbg)
-    fprintf(stderr, "[host kmer_regions] stage + table upload %.2f count %.2f expand %.2f (J %d) scan %.2f "
-            "visits D2H %.2f ms\n", t1 - t0, t2 - t1, t3 - t2, t->ext_J, t4 - t3, now_ms() - t4);
+    fprintf(stderr, "[host kmer_regions] stage %.2f table %.2f (upload %.2f compress %.2f) (both %.2f) count %.2f "
+            "expand %.2f (J %d) scan %.2f visits D2H %.2f ms\n", t_stage - t0, t_table - t0, t->ms_upload,
+            t->ms_compress, t1 - t0, t2 - t1, t3 - t2, t->ext_J, t4 - t3, now_ms() - t4);
   ks_table_destroy(t);
   if (rc != KS_OK) ks_regions_free(out);
   return rc;

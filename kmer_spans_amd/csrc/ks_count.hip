@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
                                               const int64_t *__restrict__ offs, int32_t nseq, int k, int shift,
                                               unsigned long long *__restrict__ mat,
                                               const unsigned long long *__restrict__ bstart,
-                                              Item *__restrict__ part, int64_t ntiles) {
+                                              Item *__restrict__ part, int64_t tile0, int64_t ntiles) {
   __shared__ uint32_t lds_b[1 << kT1];
   __shared__ uint32_t bmask[(kPTile + kLook + 32) / 32 + 1];
   const int nb = 1 << (2 * k - shift);
@@ -306,7 +306,7 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
   const uint32_t mask = (1u << (2 * k)) - 1u;
   const uint32_t pmask = (1u << shift) - 1u;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
-    const int64_t t0 = tile * kPTile;
+    const int64_t t0 = (tile0 + tile) * kPTile;
     const int64_t base = t0 - kLook;
     __syncthreads();
     for (int i = threadIdx.x; i < (kPTile + kLook + 32) / 32 + 1; i += kPT) bmask[i] = 0;
@@ -372,7 +372,7 @@ template <typename Item>
 __global__ void __launch_bounds__(kPT) k_part_scatter(const uint8_t *__restrict__ seq, int64_t total,
                                                       const int64_t *__restrict__ offs, int32_t nseq, int k, int shift,
                                                       const unsigned long long *__restrict__ ex,
-                                                      Item *__restrict__ part, int64_t ntiles) {
+                                                      Item *__restrict__ part, int64_t tile0, int64_t ntiles) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
   Item *sorted = reinterpret_cast<Item *>(dyn);               // [kPTile]
   uint16_t *bkt = reinterpret_cast<uint16_t *>(dyn + sizeof(Item) * kPTile);  // [kPTile]
@@ -386,7 +386,7 @@ __global__ void __launch_bounds__(kPT) k_part_scatter(const uint8_t *__restrict_
   const uint32_t mask = (1u << (2 * k)) - 1u;
   const uint32_t pmask = (1u << shift) - 1u;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
-    const int64_t t0 = tile * kPTile;
+    const int64_t t0 = (tile0 + tile) * kPTile;
     const int64_t base = t0 - kLook;
     __syncthreads();
     for (int i = threadIdx.x; i < (kPTile + kLook + 32) / 32 + 1; i += kPT) bmask[i] = 0;
@@ -653,14 +653,18 @@ __global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
 
 }  // namespace
 
-// Partitioned count of one k into counts_dev (accumulated).
+// Partitioned count of one k into counts_dev (accumulated): the k-mers
+// ending at positions [p_lo, total) (p_lo a multiple of kPTile; the bytes
+// before p_lo are read as their left context), on stream st.  n_words null:
+// no read-back of the k-mer total (and no synchronisation).
 static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, int32_t *counts_dev,
-                                   double *n_words) {
-  hipStream_t st = ctx->stream;
+                                   double *n_words, int64_t p_lo = 0, hipStream_t st = nullptr) {
+  if (!st) st = ctx->stream;
   const PartGeo g = part_geo(k);
   const int nb1 = 1 << g.T1, nbf = 1 << g.T;
   const int shift = 2 * k - g.T1;
-  const int64_t ntiles = (total + kPTile - 1) / kPTile;
+  const int64_t tile0 = p_lo / kPTile;
+  const int64_t ntiles = (total + kPTile - 1) / kPTile - tile0;
   const int G = (int)std::max<int64_t>(1, std::min<int64_t>(kPBlocks, ntiles));
   const int C = kSubChunks;
   const size_t m1 = (size_t)nb1 * G, m2 = g.T2 ? (size_t)nbf * C : 0;
@@ -674,8 +678,8 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   unsigned long long *sf = s1 + nb1 + 1;        // [nbf + 1]
   unsigned long long *last = sf + nbf + 1;      // [2]
   const size_t item1 = g.T2 ? 4 : 2;
-  KS_TRY(ensure(ctx, SLOT_CHUNK_B, (size_t)total * item1 + 64, &p1));
-  if (g.T2) KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)total * 2 + 64, &p2));
+  KS_TRY(ensure(ctx, SLOT_CHUNK_B, (size_t)(total - p_lo) * item1 + 64, &p1));
+  if (g.T2) KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)(total - p_lo) * 2 + 64, &p2));
   size_t tb = 0, tb2 = 0;
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, mat1, ex1, (int64_t)m1, st));
   if (m2) KS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, mat2, ex2, (int64_t)m2, st));
@@ -684,10 +688,10 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   // level 1
   if (g.T2) {
     hipLaunchKernelGGL((k_part<1, uint32_t>), dim3(G), dim3(kPT), 0, st, s->seq, total, s->offsets_dev, s->nseq, k,
-                       shift, mat1, nullptr, nullptr, ntiles);
+                       shift, mat1, nullptr, nullptr, tile0, ntiles);
   } else {
     hipLaunchKernelGGL((k_part<1, uint16_t>), dim3(G), dim3(kPT), 0, st, s->seq, total, s->offsets_dev, s->nseq, k,
-                       shift, mat1, nullptr, nullptr, ntiles);
+                       shift, mat1, nullptr, nullptr, tile0, ntiles);
   }
   KS_HIP(hipGetLastError());
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, mat1, ex1, (int64_t)m1, st));
@@ -698,13 +702,13 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
     KS_HIP(hipFuncSetAttribute((const void *)k_part_scatter<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
     hipLaunchKernelGGL(k_part_scatter<uint32_t>, dim3(G), dim3(kPT), lds, st, s->seq, total, s->offsets_dev, s->nseq,
-                       k, shift, ex1, static_cast<uint32_t *>(p1), ntiles);
+                       k, shift, ex1, static_cast<uint32_t *>(p1), tile0, ntiles);
   } else {
     const size_t lds = (size_t)kPTile * (2 + 2);
     KS_HIP(hipFuncSetAttribute((const void *)k_part_scatter<uint16_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
     hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(G), dim3(kPT), lds, st, s->seq, total, s->offsets_dev, s->nseq,
-                       k, shift, ex1, static_cast<uint16_t *>(p1), ntiles);
+                       k, shift, ex1, static_cast<uint16_t *>(p1), tile0, ntiles);
   }
   KS_HIP(hipGetLastError());
   const uint16_t *bins = static_cast<const uint16_t *>(p1);
@@ -733,11 +737,24 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
     hipLaunchKernelGGL(k_bins<false>, dim3(nbf * split), dim3(kPT), lds_h, st, bins, bstart, g.L, split,
                        (uint32_t *)counts_dev);
   KS_HIP(hipGetLastError());
+  if (!n_words) return KS_OK;
   unsigned long long words = 0;
   KS_HIP(hipMemcpyAsync(&words, last, 8, hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
   *n_words = (double)words;
   return KS_OK;
+}
+
+bool count_range_ok(int k, int64_t total) {
+  return k >= kPartMinK && total > 0 && total < ((int64_t)1 << 32) && !getenv("KS_COUNT_ATOMIC");
+}
+
+int64_t count_range_align() { return kPTile; }
+
+ks_status launch_count_range(ks_ctx *ctx, hipStream_t st, const ks_dev_seqs *s, int64_t p_lo, int64_t p_hi, int k,
+                             int32_t *counts_dev) {
+  if (p_lo % kPTile != 0 || p_hi <= p_lo) return fail(KS_ERR_ARG, "launch_count_range: bad range");
+  return count_partitioned(ctx, s, p_hi, k, counts_dev, nullptr, p_lo, st);
 }
 
 ks_status launch_count(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const Runs &, int k,

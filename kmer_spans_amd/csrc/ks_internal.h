@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -154,6 +155,29 @@ inline double now_ms() {
 
 ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out);
 ks_status ensure_pinned(ks_ctx *ctx, size_t bytes, void **out);
+// Host sequences staged on the device for a host entry point (ks_stage.cpp).
+struct Staged {
+  ks_dev_seqs dev{};
+  std::vector<int64_t> offs;
+  int64_t total = 0;
+};
+// Stage into the ctx's SLOT_SEQ (16-byte aligned; 32 B of slack after the
+// bases).  compact: the bases cross PCIe as 2-bit codes + N runs / 4-bit
+// classes and are rewritten as bytes of the same class on the device.
+// on_bytes (optional): called on the host after each chunk is queued, with
+// the end of the bases queued so far, which are then ready in ctx->side
+// order; st->dev is valid from the first call.  Synchronises ctx->stream at
+// the end (work the caller queued on ctx->side is the caller's to join).
+ks_status stage(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq, Staged *st,
+                bool compact = false, const std::function<ks_status(int64_t)> &on_bytes = nullptr);
+int64_t stage_chunk_bases();
+// memcpy with up to 16 threads
+void par_memcpy(void *dst, const void *src, size_t n);
+// device -> pageable host through the ctx's pinned buffer (synchronises)
+ks_status copy_out(ks_ctx *ctx, void *dst, const void *src_dev, size_t n);
+// pageable host -> device through the ctx's pinned buffer, nthr fill threads
+// (synchronises ctx->stream)
+ks_status h2d_pinned(ks_ctx *ctx, void *dst_dev, const void *src, size_t n, int nthr);
 ks_status activate(ks_ctx *ctx);  // fork check + hipSetDevice
 ks_status ctx_sub(ks_ctx *ctx, ks_ctx **sub);  // ctx->sub, created on first use
 void pool_release_device(int dev);             // free the device's pooled expanded-table buffer
@@ -221,6 +245,14 @@ ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs
                     bool want_packed = false, int64_t p_lo = 0, int64_t p_hi = -1);
 ks_status launch_count(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const Runs &runs, int k,
                        int32_t *counts_dev, double *n_words);
+// The partitioned count of the k-mers ending at [p_lo, p_hi) on stream st
+// (accumulated into counts_dev; p_lo a multiple of count_range_align(); no
+// synchronisation): the host entry counts each staged piece while the next
+// one is still crossing PCIe.  Only where count_range_ok(k, total).
+bool count_range_ok(int k, int64_t total);
+int64_t count_range_align();
+ks_status launch_count_range(ks_ctx *ctx, hipStream_t st, const ks_dev_seqs *s, int64_t p_lo, int64_t p_hi, int k,
+                             int32_t *counts_dev);
 // Which span scan a call performs.  trlr = 0: kmer_regions (kmer_spans.c:
 // 243-307).  trlr = 1: find_kmer_tr_lr_regions (:329-395): the table holds the
 // transition scores, ks the first-k-mer scores, regions need

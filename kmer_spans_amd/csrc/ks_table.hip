@@ -890,7 +890,16 @@ ks_status ks::table_create(ks_ctx *ctx, const double *w_host, int32_t k, double 
   KS_TBL_HIP(hipMalloc(&d_w, n * sizeof(double)));
   KS_TBL_HIP(hipMalloc(&t->d_vals, n * sizeof(double)));
   if (allow_compress) KS_TBL_HIP(hipMalloc(&d_bits, n * sizeof(unsigned long long)));
-  KS_TBL_HIP(hipMemcpyAsync(d_w, w_host, n * sizeof(double), hipMemcpyHostToDevice, st));
+  if (n * sizeof(double) >= ((size_t)64 << 20)) {  // (one hipMemcpy from pageable memory: 20-55 GB/s)
+    const ks_status rc = h2d_pinned(ctx, d_w, w_host, n * sizeof(double), 8);
+    if (rc != KS_OK) {
+      cleanup();
+      ks_table_destroy(t);
+      return rc;
+    }
+  } else {
+    KS_TBL_HIP(hipMemcpyAsync(d_w, w_host, n * sizeof(double), hipMemcpyHostToDevice, st));
+  }
   const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(k_sub_thr, dim3(grid), dim3(256), 0, st, d_w, thr, t->d_vals, d_bits, n);
   KS_TBL_HIP(hipGetLastError());

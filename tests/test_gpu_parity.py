@@ -146,12 +146,20 @@ def test_config1_uniform_pm1_k7(K, oracle):
     assert np.array_equal(g["counts"], o["counts"])
 
 
-def test_host_entry_nibble_staging(K, oracle):
-    """Host entry at >= 1 MiB stages one nibble per base (the base's class:
-    N or (c >> 1) & 3): odd-length sequences (bytes shared by two
-    sequences), lower case, N runs and non-ACGT letters, against the oracle."""
+@pytest.mark.parametrize("alpha,env", [(b"ACGTACGTACGTacgtNnRYx", None),  # dense Ns: 4-bit chunks
+                                       (b"ACGT" * 400 + b"acgtRYxn", None),  # sparse Ns: 2-bit codes + N runs
+                                       (b"ACGT" * 400 + b"acgtRYxn", "KS_STAGE_NIB"),
+                                       (b"ACGT" * 400 + b"acgtRYxn", "KS_STAGE_BYTES")])
+def test_host_entry_compact_staging(K, oracle, monkeypatch, alpha, env):
+    """Host entry at >= 1 MiB stages each base as its class (N or
+    (c >> 1) & 3): 2-bit codes + N runs, or 4-bit classes where a chunk has
+    too many N runs.  Odd-length sequences (bytes shared by sequences, starts
+    at every offset mod 4), lower case, N runs and non-ACGT letters, against
+    the oracle."""
+    if env:
+        monkeypatch.setenv(env, "1")
     rng = np.random.default_rng(21)
-    alpha = np.frombuffer(b"ACGTACGTACGTacgtNnRYx", dtype=np.uint8)
+    alpha = np.frombuffer(alpha, dtype=np.uint8)
     seqs = []
     for ln in [1, 3, 700_001, 2, 5, 1_200_003, 0, 999_999, 1, 17]:
         b = alpha[rng.integers(0, len(alpha), size=ln)].copy()
@@ -164,6 +172,33 @@ def test_host_entry_nibble_staging(K, oracle):
     o = oracle.kmer_regions(seqs, k, w, 20, 3.0)
     assert o["n"] > 100
     _assert_same_regions(g["pos"], g["score"], o["pos"], o["score"], "nibble staging")
+    assert np.array_equal(g["counts"], o["counts"])
+
+
+@pytest.mark.parametrize("piecewise,alpha", [(True, b"ACGTACGTACGTACGTacgN"), (False, b"ACGTACGTACGTACGTacgN"),
+                                             (True, b"ACGT" * 300 + b"acgN")])
+def test_host_entry_counted_in_pieces(K, oracle, monkeypatch, piecewise, alpha):
+    """Host entry at k >= 11 over ~150 Mbp: the staged bases are counted in
+    64 Mi-base pieces on a side stream while later pieces cross PCIe (k-mers
+    straddling a piece boundary belong to the later piece); the count is the
+    visit histogram and the table's frequency hint.  Against the oracle,
+    and the same with the count after staging (KS_HOST_COUNT_AFTER)."""
+    if not piecewise:
+        monkeypatch.setenv("KS_HOST_COUNT_AFTER", "1")
+    rng = np.random.default_rng(5)
+    alpha = np.frombuffer(alpha, dtype=np.uint8)
+    seqs = []
+    for ln in [67_108_863, 3, 50_000_001, 33_554_435]:
+        b = alpha[rng.integers(0, len(alpha), size=ln)]
+        b[(ln // 7) * np.arange(1, 7)] = ord("N")
+        b[ln // 2: ln // 2 + 3_000_017] = ord("n")  # a gap over chunk boundaries
+        seqs.append(b.tobytes().decode())
+    k = 11
+    w = np.round(rng.normal(size=4 ** k) * 4) / 4 + 0.3
+    g = K.kmer_regions(seqs, k, w, 40, 8.0)
+    o = oracle.kmer_regions(seqs, k, w, 40, 8.0)
+    assert o["n"] > 1000
+    _assert_same_regions(g["pos"], g["score"], o["pos"], o["score"], ("pieces", piecewise))
     assert np.array_equal(g["counts"], o["counts"])
 
 

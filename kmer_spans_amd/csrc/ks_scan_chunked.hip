@@ -326,6 +326,28 @@ __device__ __forceinline__ void values16_nostore(const Chunks &g, const uint8_t 
   }
 }
 
+// Values of scan indices b0 .. b0+15 of a chunk starting at start (0 past
+// n) from an FP64 table: the line table (OWN + 1 indices per read) where the
+// packed bases cover the window, else the base table by rolling codes.
+// code: the k-mer of index b0 on entry, of b0 + 16 on exit.
+__device__ __forceinline__ void values16_f64(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
+                                             const TableView &tv, int64_t start, int b0, int n, uint32_t &code,
+                                             uint32_t mask, double v[NB]) {
+  uint64_t xb = 0;
+  if (tv.line && packed_bits(g.packed, total, start + b0 - k, xb)) {
+    line_values_any<NB>(tv, xb, k, b0, n, v, nullptr);
+    code = (uint32_t)(xb >> (64 - 2 * (NB + k))) & mask;
+    return;
+  }
+  uint8_t by[16];
+  load16(seq, start + b0, total, by);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    v[j] = (b0 + j < n) ? tv.vals[code] : 0.0;
+    code = roll(code, by[j], mask);
+  }
+}
+
 // Values of scan indices i0 .. i0+3 of chunk c (0 past n): one 8-byte code
 // load (compressed) or one k-mer prime plus three rolls.
 __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
@@ -1758,13 +1780,7 @@ __device__ int chunk_summary_impl(const Chunks &g, const uint8_t *__restrict__ s
 #pragma unroll
       for (int j = 0; j < NB; ++j) v[j] = tv.lut[(w[j >> 1] >> (16 * (j & 1))) & 0xffffu];
     } else {
-      uint8_t by[16];
-      load16(seq, start + b0, total, by);
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        v[j] = (b0 + j < n) ? tv.vals[code] : 0.0;
-        code = roll(code, by[j], mask);
-      }
+      values16_f64(g, seq, total, k, tv, start, b0, n, code, mask, v);
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -1871,13 +1887,7 @@ __device__ int chunk_summary_fast(const Chunks &g, const uint8_t *__restrict__ s
         for (int t = 0; t < 4; ++t) code = roll(code, by[4 * gq + t], mask);
       }
     } else {
-      uint8_t by[16];
-      load16(seq, start + b0, total, by);
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        v[j] = (b0 + j < n) ? tv.vals[code] : 0.0;
-        code = roll(code, by[j], mask);
-      }
+      values16_f64(g, seq, total, k, tv, start, b0, n, code, mask, v);
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -3062,6 +3072,25 @@ __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restri
 #pragma unroll
         for (int j = 0; j < NB; ++j) v[j] = tv.lut[(w[j >> 1] >> (16 * (j & 1))) & 0xffffu];
       }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int i = b0 + j;
+        if (i < n && hq < 0) {
+          const double t = T + v[j];
+          T = t > 0 ? t : 0.0;
+          if (T == 0.0) hq = i;
+          else if (T > hmax) { hmax = T; harg = i; }
+        }
+      }
+    }
+  } else if (tv.line) {  // FP64 line table: OWN + 1 indices per read
+    const uint32_t mask = (1u << (2 * k)) - 1u;
+    uint64_t xp = 0;
+    uint32_t code = packed_bits(packed, total, start - k, xp) ? (uint32_t)(xp >> (64 - 2 * k))
+                                                              : prime_code_guarded(seq, start - k, k, total);
+    for (int b0 = 0; b0 < n && hq < 0; b0 += NB) {
+      double v[NB];
+      values16_f64(g, seq, total, k, tv, start, b0, n, code, mask, v);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int i = b0 + j;

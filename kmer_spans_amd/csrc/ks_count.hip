@@ -368,131 +368,137 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
 // contiguously at the block's cursor: consecutive lanes store consecutive
 // addresses (a lane-per-k-mer scatter issues one memory request per k-mer
 // and is request-bound at ~100 G/s).
-template <typename Item>
-__global__ void __launch_bounds__(kPT) k_part_scatter(const uint8_t *__restrict__ seq, int64_t total,
+template <typename Item, int kT>
+__global__ void __launch_bounds__(kT) k_part_scatter(const uint8_t *__restrict__ seq, int64_t total,
                                                       const int64_t *__restrict__ offs, int32_t nseq, int k, int shift,
                                                       const unsigned long long *__restrict__ ex,
                                                       Item *__restrict__ part, int64_t tile0, int64_t ntiles) {
+  constexpr int kTile = kT * kPer;  // positions per sub-tile
+  static_assert(kPTile % kTile == 0, "sub-tiles");
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
-  Item *sorted = reinterpret_cast<Item *>(dyn);               // [kPTile]
-  uint16_t *bkt = reinterpret_cast<uint16_t *>(dyn + sizeof(Item) * kPTile);  // [kPTile]
+  Item *sorted = reinterpret_cast<Item *>(dyn);               // [kTile]
+  uint16_t *bkt = reinterpret_cast<uint16_t *>(dyn + sizeof(Item) * kTile);  // [kTile]
   __shared__ unsigned long long cur[1 << kT1];
   __shared__ uint32_t cnt[1 << kT1], off[1 << kT1];
-  __shared__ uint32_t wtot[kPT / 64];
-  __shared__ uint32_t bmask[(kPTile + kLook + 32) / 32 + 1];
+  __shared__ uint32_t wtot[kT / 64];
+  __shared__ uint32_t bmask[(kTile + kLook + 32) / 32 + 1];
   const int nb = 1 << (2 * k - shift);
   const int G = gridDim.x;
-  for (int i = threadIdx.x; i < nb; i += kPT) cur[i] = ex[(size_t)i * G + blockIdx.x];
+  for (int i = threadIdx.x; i < nb; i += kT) cur[i] = ex[(size_t)i * G + blockIdx.x];
   const uint32_t mask = (1u << (2 * k)) - 1u;
   const uint32_t pmask = (1u << shift) - 1u;
+  // the positions k_part<1>'s block counted: its kPTile-position tiles, each
+  // as kPTile / kTile sub-tiles in order
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
-    const int64_t t0 = (tile0 + tile) * kPTile;
-    const int64_t base = t0 - kLook;
-    __syncthreads();
-    for (int i = threadIdx.x; i < (kPTile + kLook + 32) / 32 + 1; i += kPT) bmask[i] = 0;
-    for (int i = threadIdx.x; i < nb; i += kPT) cnt[i] = 0;
-    __syncthreads();
-    if (threadIdx.x < 64) mark_seq_starts(offs, nseq, base, t0 + kPTile, bmask);
-    __syncthreads();
-    const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
-    uint32_t br[kPer];   // bucket << 16 | rank, or ~0u
-    uint32_t pay[kPer];
+    for (int sub = 0; sub < kPTile / kTile; ++sub) {
+      const int64_t t0 = (tile0 + tile) * kPTile + (int64_t)sub * kTile;
+      const int64_t base = t0 - kLook;
+      __syncthreads();
+      for (int i = threadIdx.x; i < (kTile + kLook + 32) / 32 + 1; i += kT) bmask[i] = 0;
+      for (int i = threadIdx.x; i < nb; i += kT) cnt[i] = 0;
+      __syncthreads();
+      if (threadIdx.x < 64) mark_seq_starts(offs, nseq, base, t0 + kTile, bmask);
+      __syncthreads();
+      const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
+      uint32_t br[kPer];   // bucket << 16 | rank, or ~0u
+      uint32_t pay[kPer];
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) br[j] = ~0u;
-    if (p0 < total) {
-      uint8_t b[kLook + kPer];
-      if (p0 >= kLook && p0 + kPer <= total) {
-        const uint4 v0 = *reinterpret_cast<const uint4 *>(seq + p0 - kLook);
-        const uint4 v1 = *reinterpret_cast<const uint4 *>(seq + p0);
-        const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      for (int j = 0; j < kPer; ++j) br[j] = ~0u;
+      if (p0 < total) {
+        uint8_t b[kLook + kPer];
+        if (p0 >= kLook && p0 + kPer <= total) {
+          const uint4 v0 = *reinterpret_cast<const uint4 *>(seq + p0 - kLook);
+          const uint4 v1 = *reinterpret_cast<const uint4 *>(seq + p0);
+          const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-        for (int j = 0; j < kLook + kPer; ++j) b[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
-      } else {
-#pragma unroll
-        for (int j = 0; j < kLook + kPer; ++j) {
-          const int64_t q = p0 - kLook + j;
-          b[j] = (q >= 0 && q < total) ? seq[q] : (uint8_t)'N';
-        }
-      }
-      uint32_t code = 0;
-      int len = 0;
-#pragma unroll
-      for (int j = 1; j < kLook + kPer; ++j) {
-        const int64_t q = p0 - kLook + j;
-        const int r = (int)(q - base);
-        if ((bmask[r >> 5] >> (r & 31)) & 1u) len = 0;
-        if (!is_n(b[j])) {
-          code = ((code << 2) | enc(b[j])) & mask;
-          ++len;
+          for (int j = 0; j < kLook + kPer; ++j) b[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
         } else {
-          len = 0;
+#pragma unroll
+          for (int j = 0; j < kLook + kPer; ++j) {
+            const int64_t q = p0 - kLook + j;
+            b[j] = (q >= 0 && q < total) ? seq[q] : (uint8_t)'N';
+          }
         }
-        if (j >= kLook && q < total && len >= k) {
-          const int r1 = r + 1;
-          const bool q1 = (len == k) && ((bmask[r1 >> 5] >> (r1 & 31)) & 1u);
-          if (!q1) {
-            const uint32_t bk = code >> shift;
-            br[j - kLook] = (bk << 16) | atomicAdd(&cnt[bk], 1u);
-            pay[j - kLook] = code & pmask;
+        uint32_t code = 0;
+        int len = 0;
+#pragma unroll
+        for (int j = 1; j < kLook + kPer; ++j) {
+          const int64_t q = p0 - kLook + j;
+          const int r = (int)(q - base);
+          if ((bmask[r >> 5] >> (r & 31)) & 1u) len = 0;
+          if (!is_n(b[j])) {
+            code = ((code << 2) | enc(b[j])) & mask;
+            ++len;
+          } else {
+            len = 0;
+          }
+          if (j >= kLook && q < total && len >= k) {
+            const int r1 = r + 1;
+            const bool q1 = (len == k) && ((bmask[r1 >> 5] >> (r1 & 31)) & 1u);
+            if (!q1) {
+              const uint32_t bk = code >> shift;
+              br[j - kLook] = (bk << 16) | atomicAdd(&cnt[bk], 1u);
+              pay[j - kLook] = code & pmask;
+            }
           }
         }
       }
-    }
-    __syncthreads();
-    {  // exclusive scan of the (<= 2048) bucket counts: two per thread, wave
-       // scans, then the 16 wave totals
-      constexpr int kPerT = (1 << kT1) / kPT;
-      static_assert(kPerT * kPT == (1 << kT1), "buckets per thread");
-      uint32_t v[kPerT], sum = 0;
-#pragma unroll
-      for (int i = 0; i < kPerT; ++i) {
-        const int bi = threadIdx.x * kPerT + i;
-        v[i] = bi < nb ? cnt[bi] : 0;
-        sum += v[i];
-      }
-      const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-      uint32_t inc = sum;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += o;
-      }
-      if (lane == 63) wtot[wv] = inc;
       __syncthreads();
-      if (threadIdx.x < 64) {
-        uint32_t t = threadIdx.x < kPT / 64 ? wtot[threadIdx.x] : 0, ti = t;
+      {  // exclusive scan of the (<= 2048) bucket counts: two per thread, wave
+         // scans, then the 16 wave totals
+        constexpr int kPerT = (1 << kT1) / kT;
+        static_assert(kPerT * kT == (1 << kT1), "buckets per thread");
+        uint32_t v[kPerT], sum = 0;
+#pragma unroll
+        for (int i = 0; i < kPerT; ++i) {
+          const int bi = threadIdx.x * kPerT + i;
+          v[i] = bi < nb ? cnt[bi] : 0;
+          sum += v[i];
+        }
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        uint32_t inc = sum;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
-          const uint32_t o = __shfl_up(ti, d, 64);
-          if ((int)threadIdx.x >= d) ti += o;
+          const uint32_t o = __shfl_up(inc, d, 64);
+          if (lane >= d) inc += o;
         }
-        if (threadIdx.x < kPT / 64) wtot[threadIdx.x] = ti - t;  // exclusive
+        if (lane == 63) wtot[wv] = inc;
+        __syncthreads();
+        if (threadIdx.x < 64) {
+          uint32_t t = threadIdx.x < kT / 64 ? wtot[threadIdx.x] : 0, ti = t;
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(ti, d, 64);
+            if ((int)threadIdx.x >= d) ti += o;
+          }
+          if (threadIdx.x < kT / 64) wtot[threadIdx.x] = ti - t;  // exclusive
+        }
+        __syncthreads();
+        uint32_t run = wtot[wv] + inc - sum;
+#pragma unroll
+        for (int i = 0; i < kPerT; ++i) {
+          const int bi = threadIdx.x * kPerT + i;
+          if (bi < nb) off[bi] = run;
+          run += v[i];
+        }
       }
       __syncthreads();
-      uint32_t run = wtot[wv] + inc - sum;
 #pragma unroll
-      for (int i = 0; i < kPerT; ++i) {
-        const int bi = threadIdx.x * kPerT + i;
-        if (bi < nb) off[bi] = run;
-        run += v[i];
+      for (int j = 0; j < kPer; ++j)
+        if (br[j] != ~0u) {
+          const uint32_t bk = br[j] >> 16, pos = off[bk] + (br[j] & 0xffffu);
+          sorted[pos] = (Item)pay[j];
+          bkt[pos] = (uint16_t)bk;
+        }
+      __syncthreads();
+      const uint32_t n_items = off[nb - 1] + cnt[nb - 1];
+      for (uint32_t i = threadIdx.x; i < n_items; i += kT) {
+        const uint32_t bk = bkt[i];
+        part[cur[bk] + (i - off[bk])] = sorted[i];
       }
+      __syncthreads();
+      for (int i = threadIdx.x; i < nb; i += kT) cur[i] += cnt[i];
     }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kPer; ++j)
-      if (br[j] != ~0u) {
-        const uint32_t bk = br[j] >> 16, pos = off[bk] + (br[j] & 0xffffu);
-        sorted[pos] = (Item)pay[j];
-        bkt[pos] = (uint16_t)bk;
-      }
-    __syncthreads();
-    const uint32_t n_items = off[nb - 1] + cnt[nb - 1];
-    for (uint32_t i = threadIdx.x; i < n_items; i += kPT) {
-      const uint32_t bk = bkt[i];
-      part[cur[bk] + (i - off[bk])] = sorted[i];
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < nb; i += kPT) cur[i] += cnt[i];
   }
 }
 
@@ -699,15 +705,23 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   hipLaunchKernelGGL(k_part_starts, dim3((nb1 + 1 + 255) / 256), dim3(256), 0, st, ex1, G, nb1, s1, last);
   if (g.T2) {
     const size_t lds = (size_t)kPTile * (4 + 2);  // items + u16 bucket tags
-    KS_HIP(hipFuncSetAttribute((const void *)k_part_scatter<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)lds));
-    hipLaunchKernelGGL(k_part_scatter<uint32_t>, dim3(G), dim3(kPT), lds, st, s->seq, total, s->offsets_dev, s->nseq,
+    KS_HIP(hipFuncSetAttribute((const void *)k_part_scatter<uint32_t, kPT>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((k_part_scatter<uint32_t, kPT>), dim3(G), dim3(kPT), lds, st, s->seq, total, s->offsets_dev, s->nseq,
                        k, shift, ex1, static_cast<uint32_t *>(p1), tile0, ntiles);
   } else {
-    const size_t lds = (size_t)kPTile * (2 + 2);
-    KS_HIP(hipFuncSetAttribute((const void *)k_part_scatter<uint16_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)lds));
-    hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(G), dim3(kPT), lds, st, s->seq, total, s->offsets_dev, s->nseq,
+    // single level (k <= 13): 512-lane blocks on 8K-position sub-tiles, half
+    // the LDS, two blocks per CU (KS_SCATTER_1024: the 1024-lane form)
+    const bool big = getenv("KS_SCATTER_1024") != nullptr;
+    const int kt = big ? kPT : kPT / 2;
+    const size_t lds = (size_t)kt * kPer * (2 + 2);
+    const void *fn = big ? (const void *)k_part_scatter<uint16_t, kPT> : (const void *)k_part_scatter<uint16_t, kPT / 2>;
+    KS_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (big)
+      hipLaunchKernelGGL((k_part_scatter<uint16_t, kPT>), dim3(G), dim3(kPT), lds, st, s->seq, total, s->offsets_dev,
+                         s->nseq, k, shift, ex1, static_cast<uint16_t *>(p1), tile0, ntiles);
+    else
+      hipLaunchKernelGGL((k_part_scatter<uint16_t, kPT / 2>), dim3(G), dim3(kPT / 2), lds, st, s->seq, total, s->offsets_dev, s->nseq,
                        k, shift, ex1, static_cast<uint16_t *>(p1), tile0, ntiles);
   }
   KS_HIP(hipGetLastError());

@@ -479,7 +479,6 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
   if (rc == KS_OK && piecewise && hipEventCreateWithFlags(&ev.e, hipEventDisableTiming) != hipSuccess)
     rc = fail(KS_ERR_DEVICE, "hipEventCreate failed");
   hipEvent_t ev_piece = ev.e;
-  if (getenv("KS_HOST_TABLE_FIRST")) th.join();  // (experiment: the table crosses PCIe before the bases)
   Staged st;
   auto on_bytes = [&](int64_t p1) -> ks_status {
     if (p1 < total_in && p1 - counted < piece) return KS_OK;

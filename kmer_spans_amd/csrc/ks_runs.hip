@@ -234,6 +234,12 @@ __global__ void k_run_counts(const int64_t *__restrict__ ra, const int64_t *__re
 // cbase[r] >= frac * cbase[n] (out: r, cbase[r], tbase[r]).
 __global__ void k_split(const int64_t *__restrict__ cbase, const int64_t *__restrict__ tbase, int64_t n,
                         double frac, unsigned long long *__restrict__ out) {
+  // frac < 0: by size -- 0.7 for a genome (the second part's pass 1 covers
+  // the first part's post-processing), 0.8 at shard sizes (<= 2 M chunks,
+  // ~500 Mbp), where that post-processing is short and the second part's
+  // own tail dominates (in-process A/B at the 8-way shard: 2.47 vs 2.58 ms;
+  // 4-way equal; 2-way and the whole genome 0.7)
+  if (frac < 0) frac = cbase[n] <= (2ll << 20) ? 0.8 : 0.7;
   const int64_t half = (int64_t)((double)cbase[n] * frac);
   int64_t lo = 0, hi = n;
   while (lo < hi) {
@@ -275,7 +281,7 @@ ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int t
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt_t, lay->tbase, (int)(n + 1), st));
   // the first half (highest priority) ends first; its carry and stitch run
   // under the rest of the second half (KS_SPLIT_FRAC: the first part's share)
-  const double frac = getenv("KS_SPLIT_FRAC") ? atof(getenv("KS_SPLIT_FRAC")) : 0.7;
+  const double frac = getenv("KS_SPLIT_FRAC") ? atof(getenv("KS_SPLIT_FRAC")) : -1.0;  // (-1: by size)
   hipLaunchKernelGGL(k_split, dim3(1), dim3(1), 0, st, lay->cbase, lay->tbase, n, frac, agg + 3);
   KS_HIP(hipGetLastError());
   unsigned long long ha[8] = {0, 0, 0, 0, 0, 0, 0, 0};

@@ -28,6 +28,8 @@ def main():
     p.add_argument("--scale", type=float, default=1.0)
     p.add_argument("--ncontigs", type=int, default=24)
     p.add_argument("--out", default=None)
+    p.add_argument("--shard-of", type=int, default=1,
+                   help="scan only the largest of N LPT shards (the whole genome's count and table)")
     p.add_argument("--rebuild", action="store_true",
                    help="rebuild the table every round (with KS_EXT_POOL=0: a new expanded-table allocation)")
     p.add_argument("--table-per-variant", action="store_true",
@@ -66,6 +68,12 @@ def main():
         tab = tabs[variants[0][0]]
     else:
         tab = D.DeviceTable.from_counts(ctx, counts, a.k, a.score, total=words, thr=thr, expand=True)
+    if a.shard_of > 1:
+        from kmer_spans_amd.dist import lpt_shards
+        shards = lpt_shards([int(x) for x in lens], a.shard_of)
+        mine = max(shards, key=lambda sh: sum(int(lens[q]) for q in sh))
+        ds = ds.subset(sorted(mine))
+        print("shard", a.shard_of, "contigs", sorted(mine), "bp", int(ds.total), flush=True)
     res = {n: [] for n, _ in variants}
     phases = {}
     ref = None

@@ -91,6 +91,8 @@ def parse(argv=None):
                    help="(one rank) scan only one shard of an N-way LPT split of the genome, with the whole "
                         "genome's table: the fixed per-step cost at shard size")
     p.add_argument("--shard-index", type=int, default=-1, help="--shard-of: which shard (default: the largest)")
+    p.add_argument("--whole-contigs", action="store_true",
+                   help="shard mode: LPT over whole contigs instead of pieces cut inside N gaps")
     p.add_argument("--cpu-sample", type=float, default=2.0e8,
                    help="bases of the timed CPU-baseline sample besides the largest contig")
     p.add_argument("--cpu-threads", type=int, default=16, help="host threads of the (untimed) parity leg")
@@ -389,21 +391,47 @@ def main():
     t0 = time.time()
     lens_all = [max(1, int(round(L * args.scale))) for L in genome.GRCH38[:args.ncontigs]]
     shards = None
+    offsets = None  # per shard: each local sequence's start inside its contig (pieces)
+    pieces_mine = None
     if args.mode == "shard":
-        from kmer_spans_amd.dist import lpt_shards
+        from kmer_spans_amd.dist import gap_cuts, lpt_pieces, lpt_shards
         nsh = world if dist else max(1, args.shard_of)
-        shards = lpt_shards(lens_all, nsh)
-        if dist:
-            mine = shards[rank]
+        if nsh > 1 and not args.whole_contigs:
+            # LPT over pieces cut inside N gaps (exact: runs never cross an N,
+            # dist.gap_cuts); every rank generates the genome and makes the
+            # same cut, so every rank knows every shard's pieces
+            parts_all = [genome.contig(lens_all[q], args.seed + q, dev) for q in range(len(lens_all))]
+            cuts = [gap_cuts(x) for x in parts_all]
+            psh = lpt_pieces(lens_all, cuts, nsh)
+            shards = [[q for q, _, _ in sh] for sh in psh]
+            offsets = [[lo for _, lo, _ in sh] for sh in psh]
+            if dist:
+                pieces_mine = psh[rank]
+            else:
+                idx = args.shard_index if args.shard_index >= 0 else int(np.argmax([sum(hi - lo for _, lo, hi in sh)
+                                                                                    for sh in psh]))
+                pieces_mine = psh[idx]
+            mine = [q for q, _, _ in pieces_mine]
+            if dist:
+                parts = [parts_all[q][lo:hi] for q, lo, hi in pieces_mine]
+                ds = D.from_parts(parts, [hi - lo for _, lo, hi in pieces_mine], dev)
+            else:  # --shard-of: the whole genome is counted, then only the shard is scanned
+                parts = parts_all
+                ds = D.from_parts(parts, lens_all, dev)
+            del parts_all
         else:
-            idx = args.shard_index if args.shard_index >= 0 else int(np.argmax([sum(lens_all[q] for q in s)
-                                                                                for s in shards]))
-            mine = shards[idx] if nsh > 1 else list(range(len(lens_all)))
-        # --shard-of at one rank: the whole genome is counted (its table is the one the
-        # sharded run builds after the all-reduce), then only the shard is scanned
-        gen = range(len(lens_all)) if (not dist and nsh > 1) else mine
-        parts = [genome.contig(lens_all[q], args.seed + q, dev) for q in gen]
-        ds = D.from_parts(parts, [lens_all[q] for q in gen], dev)
+            shards = lpt_shards(lens_all, nsh)
+            if dist:
+                mine = shards[rank]
+            else:
+                idx = args.shard_index if args.shard_index >= 0 else int(np.argmax([sum(lens_all[q] for q in s)
+                                                                                    for s in shards]))
+                mine = shards[idx] if nsh > 1 else list(range(len(lens_all)))
+            # --shard-of at one rank: the whole genome is counted (its table is the one the
+            # sharded run builds after the all-reduce), then only the shard is scanned
+            gen = range(len(lens_all)) if (not dist and nsh > 1) else mine
+            parts = [genome.contig(lens_all[q], args.seed + q, dev) for q in gen]
+            ds = D.from_parts(parts, [lens_all[q] for q in gen], dev)
         genome_bp = sum(lens_all)
     else:
         mine = None
@@ -439,10 +467,18 @@ def main():
             words = float(wt.item())
         setup["count_allreduce_ms"] = round(tm.ms, 2)
     if args.mode == "shard" and not dist and args.shard_of > 1:
-        ds = ds.subset(mine)
+        if pieces_mine is not None:
+            full = ds
+            ds = D.from_parts([full.seq[int(full.offsets[q]) + lo:int(full.offsets[q]) + hi] for q, lo, hi in pieces_mine],
+                              [hi - lo for _, lo, hi in pieces_mine], dev)
+            del full
+        else:
+            ds = ds.subset(mine)
         torch.cuda.empty_cache()
-        extra["shard_of"] = {"n": args.shard_of, "contigs": mine, "bp": int(ds.total),
-                             "note": "one shard of an N-way LPT split scanned with the whole genome's table"}
+        extra["shard_of"] = {"n": args.shard_of, "contigs": sorted(set(mine)), "bp": int(ds.total),
+                             "pieces": len(pieces_mine) if pieces_mine is not None else None,
+                             "note": "one shard of an N-way LPT split (contigs cut inside N gaps) scanned with "
+                                     "the whole genome's table"}
     w_dev, thr, table, init_table, tt = make_table(counts, words, args.score)
     setup.update({key: round(v, 2) for key, v in tt.items()})
     table_shape = {"table_compressed": table.compressed, "table_distinct": table.distinct,
@@ -533,7 +569,7 @@ def main():
         if rank == 0:
             n_regions_all = sum(int(p.shape[1]) for p in allpos)
             if args.mode == "shard":
-                mpos, _ = merge_shards(shards, allpos, allscore, one_based=args.trlr)
+                mpos, _ = merge_shards(shards, allpos, allscore, one_based=args.trlr, offsets=offsets)
                 extra["merged_regions"] = int(mpos.shape[1])
                 extra["merged_order_ok"] = bool(np.all(np.diff(mpos[0].astype(np.int64) * (1 << 32) + mpos[1]) > 0))
 
@@ -619,7 +655,7 @@ def main():
         "config": {"workload": f"human-shaped synthetic genome ({total_bases} bp, "
                                f"{args.ncontigs} contigs, scale {args.scale}), k={k}, {args.score} score from its "
                                f"own counts, min_width {args.min_width}, min_score {args.min_score}, device-resident"
-                               + (", contigs LPT-sharded over the ranks" if args.mode == "shard" else
+                               + (", contigs (cut inside N gaps) LPT-sharded over the ranks" if args.mode == "shard" else
                                   ", one genome per rank"),
                    "k": k, "score": args.score, "genome_bp": total_bases,
                    "parallelism": f"{'contig-shard' if args.mode == 'shard' else 'genome-per-rank'} x{world}",

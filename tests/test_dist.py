@@ -140,3 +140,39 @@ def test_sharded_equals_unsharded_gloo_world2(oracle):
     assert tfull["pos"].shape[1] > 5
     assert np.array_equal(tpos, tfull["pos"])
     assert np.array_equal(tscore.view(np.uint64), tfull["score"].view(np.uint64))
+
+
+def test_pieces_cut_in_n_gaps_equal_whole(oracle):
+    """Contigs cut in the middle of their N gaps (dist.gap_cuts), the pieces
+    LPT-sharded over three shards, scanned and counted per shard, merged with
+    the pieces' offsets == the whole genome's scan and counts, bit for bit
+    (kmer_regions and 1-based tr_lr)."""
+    import torch
+    from kmer_spans_amd import dist
+    O = oracle
+    k = 6
+    seqs, lens = _genome(11)
+    cuts = [dist.gap_cuts(torch.from_numpy(np.frombuffer(s, np.uint8).copy()), min_gap=40) for s in seqs]
+    assert sum(len(c) for c in cuts) >= 3
+    psh = dist.lpt_pieces(lens, cuts, 3)
+    assert sorted((q, lo, hi) for sh in psh for q, lo, hi in sh) == sorted(
+        (q, b[i], b[i + 1]) for q in range(len(lens)) for b in [[0] + cuts[q] + [lens[q]]] for i in range(len(b) - 1))
+    ids = [[q for q, _, _ in sh] for sh in psh]
+    offs = [[lo for _, lo, _ in sh] for sh in psh]
+    piece_seqs = [[seqs[q][lo:hi] for q, lo, hi in sh] for sh in psh]
+    h = sum(O.kmer_counts(ps, k)[1].astype(np.int64) for ps in piece_seqs if ps)
+    _, c = O.kmer_counts(seqs, k)
+    assert np.array_equal(h, c)
+    w = O.log2_table(c, k)
+    full = O.scan(seqs, k, w, 0.0, 20, 3.0)
+    rs = [O.scan(ps, k, w, 0.0, 20, 3.0) for ps in piece_seqs]
+    pos, score = dist.merge_shards(ids, [r["pos"] for r in rs], [r["score"] for r in rs], offsets=offs)
+    assert full["pos"].shape[1] > 5
+    assert np.array_equal(pos, full["pos"])
+    assert np.array_equal(score.view(np.uint64), full["score"].view(np.uint64))
+    tfull = O.tr_lr_regions(seqs, k, 15, w, w)
+    ts = [O.tr_lr_regions(ps, k, 15, w, w) for ps in piece_seqs]
+    tpos, tscore = dist.merge_shards(ids, [t["pos"] for t in ts], [t["score"] for t in ts], one_based=True,
+                                     offsets=offs)
+    assert np.array_equal(tpos, tfull["pos"])
+    assert np.array_equal(tscore.view(np.uint64), tfull["score"].view(np.uint64))

@@ -24,6 +24,7 @@ def main(bench_json, out_json, *csvs):
                 kernels.setdefault(name, {})[c] = sum(vals) / len(vals)
                 kernels[name]["dispatches"] = len(vals)
     n_bases = int(cfg["genome_bp"])
+    p1 = cfg.get("pass1_kernel", "k_pass1p")
     out = {
         "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, tools/gpu_pmc.sh) of "
                 "`python bench.py --steps 1 --warmup 0 --no-cpu`; values in KB per dispatch (raw counters: "
@@ -35,12 +36,12 @@ def main(bench_json, out_json, *csvs):
         # scan calls in the profiled run: its steps + warmup, plus the visits
         # line's warm call and 3 timed calls (the same scan)
         "steps": int(b["steps"]) + int(b["warmup"]) + (4 if b.get("visits_path") else 0),
-        # packed bases (total / 4 bytes per step) are the only 16-B streaming read of k_pass1p
-        "streaming_read_bytes_per_step": {"k_pass1p": n_bases / 4.0},
+        # packed bases (total / 4 bytes per step) are the only 16-B streaming read of the pass-1 kernel
+        "streaming_read_bytes_per_step": {p1: n_bases / 4.0},
         "kernels": kernels,
     }
     json.dump(out, open(out_json, "w"), indent=1)
-    kp = {k: v for k, v in kernels.items() if k.startswith("k_pass1p")}
+    kp = {k: v for k, v in kernels.items() if k.startswith(p1)}
     print(json.dumps(kp, indent=1))
 
 

@@ -218,6 +218,16 @@ void ks_table_destroy(ks_table *t);
  * pool.  Workspace retained by a context (scan scratch, the table builder's
  * sort scratch of ~20 B x 4^k) is freed by ks_ctx_destroy. */
 void ks_release_cache(void);
+
+/* Fork broker (mclapply after use, test.R:351 then :554-565).  On: right
+ * before this process's first HIP use the library forks a broker process (a
+ * copy that never touched HIP; not started if HIP is already open in the
+ * process, e.g. by torch); children forked later send their host-buffer calls
+ * (ks_kmer_counts, ks_kmer_regions, ks_low_comp_regions, ks_tr_lr_regions,
+ * ks_windowed_dist, ks_kmers_to_file) to it over a Unix socket instead of
+ * being refused.  Off by default (KS_FORK_BROKER=1 turns it on); the R shim's
+ * R_init_kmer_spans turns it on.  Call before the first HIP use. */
+ks_status ks_set_fork_broker(int32_t on);
 /* 1 if the table is stored compressed (uint16 codes + LUT), else 0. */
 int32_t ks_table_is_compressed(const ks_table *t);
 int64_t ks_table_distinct(const ks_table *t);

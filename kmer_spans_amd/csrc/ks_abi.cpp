@@ -12,6 +12,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <mutex>
+#include <new>
 #include <string>
 #include <thread>
 
@@ -55,6 +56,26 @@ static ks_status fork_check(const ks_ctx *ctx) {
 }
 
 bool hip_usable_here() { return g_hip_pid == 0 || g_hip_pid == getpid(); }
+
+bool use_broker() { return broker_wanted(g_hip_pid); }
+
+
+ks_status regions_alloc(ks_regions *out, int64_t n) {
+  const size_t nn = (size_t)std::max<int64_t>(n, 1);
+  const size_t ioff = (3 * nn * 4 + 7) & ~(size_t)7;
+  char *blk = static_cast<char *>(malloc(ioff + 2 * nn * 8));
+  if (!blk) {
+    memset(out, 0, sizeof(*out));
+    return fail(KS_ERR_NOMEM, "out of host memory for %lld regions", (long long)n);
+  }
+  out->n = n;
+  out->seq_id = reinterpret_cast<int32_t *>(blk);
+  out->beg = out->seq_id + nn;
+  out->end = out->beg + nn;
+  out->score = reinterpret_cast<double *>(blk + ioff);
+  if (n == 0) out->score[0] = 0.0;  // (n > 0: the caller fills the second row with zeros)
+  return KS_OK;
+}
 
 ks_status activate(ks_ctx *ctx) {
   KS_TRY(fork_check(ctx));
@@ -130,6 +151,10 @@ std::mutex g_default_mu;
 ks_ctx *g_default = nullptr;
 
 }  // namespace
+
+// In the broker right after fork(): the forking thread held the default
+// context's lock (ks_default_ctx -> ks_ctx_create -> broker_before_hip).
+void broker_reset_locks() { new (&g_default_mu) std::mutex(); }
 }  // namespace ks
 
 using namespace ks;
@@ -145,7 +170,10 @@ extern "C" void ks_regions_free(ks_regions *r) {
 extern "C" ks_status ks_ctx_create(int32_t device, ks_ctx **out) {
   if (!out) return fail(KS_ERR_ARG, "null output");
   KS_TRY(fork_check(nullptr));
-  if (g_hip_pid == 0) g_hip_pid = getpid();
+  if (g_hip_pid == 0) {
+    broker_before_hip();  // (a copy of this process before it touches HIP, when enabled)
+    g_hip_pid = getpid();
+  }
   int ndev = 0;
   KS_HIP(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail(KS_ERR_ARG, "device %d out of range (%d devices)", device, ndev);
@@ -366,6 +394,8 @@ extern "C" ks_status ks_tr_lr_regions(ks_ctx *ctx, const char *const *seqs, cons
   }
   if (bad) fprintf(stderr, "kmer_spans_amd: %lld k-mer strings of tr_lr_regions do not spell %d bases\n",
                    (long long)bad, k);
+  if (use_broker())
+    return broker_tr_lr(seqs, lens, nseq, k, min_length, kmers, kmer_scores, trans_scores, n_scores, spectra, out);
   if (spectra) {
     memcpy(spectra, ks.data(), (size_t)nk * 8);
     memcpy(spectra + nk, tr.data(), (size_t)nk * 8);
@@ -398,6 +428,7 @@ extern "C" ks_status ks_kmer_counts(ks_ctx *ctx, const char *const *seqs, const 
   if (k < 1 || k > KS_MAX_K)                                  // :461-462 (and Q2)
     return fail(KS_ERR_ARG, "k must be a positive integer less than 1+MAX_K");
   if (!counts || !n_words) return fail(KS_ERR_ARG, "null output");
+  if (use_broker()) return broker_kmer_counts(seqs, lens, nseq, k, counts, n_words);
   KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
   Staged st;
@@ -428,6 +459,7 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
                 (long long)want);
   if (!out || !n_bases) return fail(KS_ERR_ARG, "null output");
   memset(out, 0, sizeof(*out));
+  if (use_broker()) return broker_kmer_regions(seqs, lens, nseq, k, w, w_len, min_width, min_score, visits, n_bases, out);
   KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
   double n = 0;
@@ -541,6 +573,7 @@ extern "C" ks_status ks_low_comp_regions(ks_ctx *ctx, const char *const *seqs, c
     return fail(KS_ERR_ARG, "k must be a positive integer less than 1+MAX_K");
   if (!counts || !ranks || !n || !out) return fail(KS_ERR_ARG, "null output");
   memset(out, 0, sizeof(*out));
+  if (use_broker()) return broker_low_comp(seqs, lens, nseq, k, min_width, min_score, thr, counts, ranks, n, out);
   KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
   Staged st;
@@ -618,6 +651,8 @@ extern "C" ks_status ks_windowed_dist(ks_ctx *ctx, const char *const *seqs, cons
     prime_string(kmers[i], k, &c);
     codes[i] = (uint32_t)c;
   }
+  if (use_broker())
+    return broker_windowed(seqs, lens, nseq, kmers, kmer_n, k, window, ret_flag, dist, seq_included, scores);
   KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
   Staged st;

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "ks_internal.h"
 
@@ -285,26 +286,22 @@ __global__ void k_part_sum_last(const unsigned long long *__restrict__ mat, cons
   *last = ex[n - 1] + mat[n - 1];
 }
 
-// Level 1 over the sequence.  shift = 2k - T1: bucket = code >> shift,
-// payload = code & (2^shift - 1) stored as Item.
-template <int kPass, typename Item>
+// Level 1 over the sequence: per block, the LDS histogram of the buckets
+// (code >> shift, shift = 2k - T1) of the k-mers in its tiles, each count
+// rounded up to a multiple of pad (the staged scatter writes whole pieces of
+// pad items), into mat[bucket][block]; the unrounded total is added to
+// *words.
 __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, int64_t total,
                                               const int64_t *__restrict__ offs, int32_t nseq, int k, int shift,
-                                              unsigned long long *__restrict__ mat,
-                                              const unsigned long long *__restrict__ bstart,
-                                              Item *__restrict__ part, int64_t tile0, int64_t ntiles) {
+                                              unsigned long long *__restrict__ mat, int pad,
+                                              unsigned long long *__restrict__ words, int64_t tile0, int64_t ntiles) {
   __shared__ uint32_t lds_b[1 << kT1];
   __shared__ uint32_t bmask[(kPTile + kLook + 32) / 32 + 1];
+  __shared__ unsigned long long wsum[kPT / 64];
   const int nb = 1 << (2 * k - shift);
   const int G = gridDim.x;
-  if (kPass == 1) {
-    for (int i = threadIdx.x; i < nb; i += kPT) lds_b[i] = 0;
-  } else {
-    for (int i = threadIdx.x; i < nb; i += kPT)
-      lds_b[i] = (uint32_t)(mat[(size_t)i * G + blockIdx.x] - bstart[i]);
-  }
+  for (int i = threadIdx.x; i < nb; i += kPT) lds_b[i] = 0;
   const uint32_t mask = (1u << (2 * k)) - 1u;
-  const uint32_t pmask = (1u << shift) - 1u;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
     const int64_t t0 = (tile0 + tile) * kPTile;
     const int64_t base = t0 - kLook;
@@ -345,21 +342,167 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
       if (j >= kLook && q < total && len >= k) {
         const int r1 = r + 1;
         const bool q1 = (len == k) && ((bmask[r1 >> 5] >> (r1 & 31)) & 1u);
-        if (!q1) {
-          const uint32_t bk = code >> shift;
-          if (kPass == 1) {
-            atomicAdd(&lds_b[bk], 1u);
-          } else {
-            const uint32_t slot = atomicAdd(&lds_b[bk], 1u);
-            part[bstart[bk] + slot] = (Item)(code & pmask);
+        if (!q1) atomicAdd(&lds_b[code >> shift], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  unsigned long long t = 0;
+  for (int i = threadIdx.x; i < nb; i += kPT) {
+    const uint32_t c = lds_b[i];
+    t += c;
+    mat[(size_t)i * G + blockIdx.x] = (c + (uint32_t)pad - 1u) / (uint32_t)pad * (uint32_t)pad;
+  }
+  for (int d = 32; d >= 1; d >>= 1) t += __shfl_down(t, d, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long s = 0;
+    for (int w = 0; w < kPT / 64; ++w) s += wsum[w];
+    if (s) atomicAdd(words, s);
+  }
+}
+
+// Single-level scatter through a per-bucket LDS stage of kS items: every
+// (bucket, block) region is a multiple of kS items (k_part with pad = kS)
+// starting 2*kS-byte aligned, and is written only in whole aligned pieces of
+// kS items, so each HBM write request carries 2*kS bytes (the counting-sort
+// scatter below writes ~4 items per bucket and sub-tile: 27.5 GB of partial
+// writes for 6.1 GB of items at the metric genome).  Per sub-tile: a k-mer
+// takes slot = fill[bucket]++ (LDS atomic); slots < kS go to the stage, the
+// rest stay in registers; buckets that reach kS flush the stage's piece
+// (16-B stores), the registers' slots below the last whole piece go straight
+// out (lanes of one wave hold consecutive slots of a hot bucket, so those
+// stores coalesce) and the remainder moves into the stage.  The block's last
+// remainders go out padded with kSentinel (k_bins skips it).
+constexpr uint16_t kSentinel = 0xffffu;  // payloads are < 2^15 on the single level
+template <int kS, int kT>
+__global__ void __launch_bounds__(kT) k_part_scatter_st(const uint8_t *__restrict__ seq, int64_t total,
+                                                         const int64_t *__restrict__ offs, int32_t nseq, int k,
+                                                         int shift, const unsigned long long *__restrict__ ex,
+                                                         uint16_t *__restrict__ part, int64_t tile0, int64_t ntiles) {
+  constexpr int kTile = kT * kPer;  // positions per sub-tile
+  constexpr int kV = kS / 8;        // 16-B vectors per piece
+  static_assert(kPTile % kTile == 0 && kS % 8 == 0, "sub-tiles, pieces");
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+  uint16_t *stage = reinterpret_cast<uint16_t *>(dyn);  // [nb][kS]
+  __shared__ uint32_t fill[1 << kT1], cur[1 << kT1];
+  __shared__ uint32_t bmask[(kTile + kLook + 32) / 32 + 1];
+  const int nb = 1 << (2 * k - shift);
+  const int G = gridDim.x;
+  for (int i = threadIdx.x; i < nb; i += kT) {
+    fill[i] = 0;
+    cur[i] = (uint32_t)ex[(size_t)i * G + blockIdx.x];
+  }
+  const uint32_t mask = (1u << (2 * k)) - 1u;
+  const uint32_t pmask = (1u << shift) - 1u;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
+    for (int sub = 0; sub < kPTile / kTile; ++sub) {
+      const int64_t t0 = (tile0 + tile) * kPTile + (int64_t)sub * kTile;
+      const int64_t base = t0 - kLook;
+      __syncthreads();
+      for (int i = threadIdx.x; i < (kTile + kLook + 32) / 32 + 1; i += kT) bmask[i] = 0;
+      __syncthreads();
+      if (threadIdx.x < 64) mark_seq_starts(offs, nseq, base, t0 + kTile, bmask);
+      __syncthreads();
+      const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
+      uint32_t br[kPer];  // bucket << 16 | slot of the items left in registers, or ~0u
+      uint16_t pay[kPer];
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) br[j] = ~0u;
+      if (p0 < total) {
+        uint8_t b[kLook + kPer];
+        if (p0 >= kLook && p0 + kPer <= total) {
+          const uint4 v0 = *reinterpret_cast<const uint4 *>(seq + p0 - kLook);
+          const uint4 v1 = *reinterpret_cast<const uint4 *>(seq + p0);
+          const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+          for (int j = 0; j < kLook + kPer; ++j) b[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+        } else {
+#pragma unroll
+          for (int j = 0; j < kLook + kPer; ++j) {
+            const int64_t q = p0 - kLook + j;
+            b[j] = (q >= 0 && q < total) ? seq[q] : (uint8_t)'N';
           }
+        }
+        uint32_t code = 0;
+        int len = 0;
+#pragma unroll
+        for (int j = 1; j < kLook + kPer; ++j) {
+          const int64_t q = p0 - kLook + j;
+          const int r = (int)(q - base);
+          if ((bmask[r >> 5] >> (r & 31)) & 1u) len = 0;
+          if (!is_n(b[j])) {
+            code = ((code << 2) | enc(b[j])) & mask;
+            ++len;
+          } else {
+            len = 0;
+          }
+          if (j >= kLook && q < total && len >= k) {
+            const int r1 = r + 1;
+            const bool q1 = (len == k) && ((bmask[r1 >> 5] >> (r1 & 31)) & 1u);
+            if (!q1) {
+              const uint32_t bk = code >> shift;
+              const uint32_t slot = atomicAdd(&fill[bk], 1u);
+              const uint16_t v = (uint16_t)(code & pmask);
+              if (slot < (uint32_t)kS) {
+                stage[bk * kS + slot] = v;
+              } else {
+                br[j - kLook] = (bk << 16) | slot;
+                pay[j - kLook] = v;
+              }
+            }
+          }
+        }
+      }
+      __syncthreads();
+      // whole stage pieces out
+      for (int i = threadIdx.x; i < nb; i += kT) {
+        if (fill[i] >= (uint32_t)kS) {
+          const uint4 *src = reinterpret_cast<const uint4 *>(stage + i * kS);
+          uint4 *dst = reinterpret_cast<uint4 *>(part + cur[i]);
+#pragma unroll
+          for (int v = 0; v < kV; ++v) dst[v] = src[v];
+        }
+      }
+      __syncthreads();
+      // register slots: below the last whole piece straight out, the rest staged
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if (br[j] != ~0u) {
+          const uint32_t bk = br[j] >> 16, slot = br[j] & 0xffffu;
+          const uint32_t F = fill[bk] / kS * kS;
+          if (slot < F) part[cur[bk] + slot] = pay[j];
+          else stage[bk * kS + slot - F] = pay[j];
+        }
+      __syncthreads();
+      for (int i = threadIdx.x; i < nb; i += kT) {
+        const uint32_t f = fill[i];
+        if (f >= (uint32_t)kS) {
+          const uint32_t F = f / kS * kS;
+          cur[i] += F;
+          fill[i] = f - F;
         }
       }
     }
   }
-  if (kPass == 1) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < nb; i += kPT) mat[(size_t)i * G + blockIdx.x] = lds_b[i];
+  __syncthreads();
+  // the block's remainders, padded to a whole piece
+  for (int i = threadIdx.x; i < nb; i += kT) {
+    const uint32_t f = fill[i];
+    if (f == 0) continue;
+    uint4 *dst = reinterpret_cast<uint4 *>(part + cur[i]);
+    for (int v = 0; v < kV; ++v) {
+      uint32_t w[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const uint32_t e0 = v * 8 + 2 * h, e1 = e0 + 1;
+        const uint32_t lo = e0 < f ? stage[i * kS + e0] : kSentinel;
+        const uint32_t hi = e1 < f ? stage[i * kS + e1] : kSentinel;
+        w[h] = lo | (hi << 16);
+      }
+      dst[v] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
   }
 }
 
@@ -649,8 +792,11 @@ __global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
   unsigned long long ah = (a + 7) & ~7ull;
   if (ah > e) ah = e;
   const unsigned long long eb = ah + ((e - ah) & ~7ull);
-  for (unsigned long long i = a + threadIdx.x; i < ah; i += kPT) atomicAdd(&h[part[i]], 1u);
-  for (unsigned long long i = eb + threadIdx.x; i < e; i += kPT) atomicAdd(&h[part[i]], 1u);
+  // (kSentinel: the staged scatter's padding; bins are < 2^15)
+  for (unsigned long long i = a + threadIdx.x; i < ah; i += kPT)
+    if (part[i] != kSentinel) atomicAdd(&h[part[i]], 1u);
+  for (unsigned long long i = eb + threadIdx.x; i < e; i += kPT)
+    if (part[i] != kSentinel) atomicAdd(&h[part[i]], 1u);
   const uint4 *v = reinterpret_cast<const uint4 *>(part + ah);
   const unsigned long long nv = (eb - ah) / 8;
   for (unsigned long long i = threadIdx.x; i < nv; i += kPT) {
@@ -658,8 +804,9 @@ __global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
     const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      atomicAdd(&h[w[j] & 0xffffu], 1u);
-      atomicAdd(&h[w[j] >> 16], 1u);
+      const uint32_t lo = w[j] & 0xffffu, hi = w[j] >> 16;
+      if (lo != kSentinel) atomicAdd(&h[lo], 1u);
+      if (hi != kSentinel) atomicAdd(&h[hi], 1u);
     }
   }
   __syncthreads();
@@ -699,23 +846,32 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   unsigned long long *ex2 = mat2 + m2;
   unsigned long long *s1 = ex2 + m2;            // [nb1 + 1]
   unsigned long long *sf = s1 + nb1 + 1;        // [nbf + 1]
-  unsigned long long *last = sf + nbf + 1;      // [2]
+  unsigned long long *last = sf + nbf + 1;      // [2]: level ends; [2]: the k-mer total
+  // single level: the staged scatter (KS_SCATTER_STAGE = S x lanes, S items
+  // per bucket piece; 0: the counting-sort scatter)
+  int stS = 16, stT = kPT;
+  if (const char *e = getenv("KS_SCATTER_STAGE")) {
+    stS = atoi(e);
+    const char *x = strchr(e, 'x');
+    if (x) stT = atoi(x + 1);
+    if (stS != 16 && stS != 32) stS = 0;
+    if (stT != kPT && stT != kPT / 2) stT = kPT;
+  }
+  const int64_t n_items = total - p_lo;
+  const bool staged = !g.T2 && stS > 0 && n_items + (int64_t)m1 * stS < ((int64_t)1 << 32);
+  const int pad = staged ? stS : 1;
   const size_t item1 = g.T2 ? 4 : 2;
-  KS_TRY(ensure(ctx, SLOT_CHUNK_B, (size_t)(total - p_lo) * item1 + 64, &p1));
-  if (g.T2) KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)(total - p_lo) * 2 + 64, &p2));
+  KS_TRY(ensure(ctx, SLOT_CHUNK_B, (size_t)(n_items + (int64_t)m1 * (pad - 1)) * item1 + 64, &p1));
+  if (g.T2) KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)n_items * 2 + 64, &p2));
   size_t tb = 0, tb2 = 0;
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, mat1, ex1, (int64_t)m1, st));
   if (m2) KS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, mat2, ex2, (int64_t)m2, st));
   tb = std::max(tb, tb2);
   KS_TRY(ensure(ctx, SLOT_SORT_TMP, tb + 16, &tmp));
   // level 1
-  if (g.T2) {
-    hipLaunchKernelGGL((k_part<1, uint32_t>), dim3(G), dim3(kPT), 0, st, s->seq, total, s->offsets_dev, s->nseq, k,
-                       shift, mat1, nullptr, nullptr, tile0, ntiles);
-  } else {
-    hipLaunchKernelGGL((k_part<1, uint16_t>), dim3(G), dim3(kPT), 0, st, s->seq, total, s->offsets_dev, s->nseq, k,
-                       shift, mat1, nullptr, nullptr, tile0, ntiles);
-  }
+  KS_HIP(hipMemsetAsync(last + 2, 0, 8, st));
+  hipLaunchKernelGGL(k_part, dim3(G), dim3(kPT), 0, st, s->seq, total, s->offsets_dev, s->nseq, k, shift, mat1, pad,
+                     last + 2, tile0, ntiles);
   KS_HIP(hipGetLastError());
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, mat1, ex1, (int64_t)m1, st));
   hipLaunchKernelGGL(k_part_sum_last, dim3(1), dim3(1), 0, st, mat1, ex1, m1, last);
@@ -726,6 +882,20 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL((k_part_scatter<uint32_t, kPT>), dim3(G), dim3(kPT), lds, st, s->seq, total, s->offsets_dev, s->nseq,
                        k, shift, ex1, static_cast<uint32_t *>(p1), tile0, ntiles);
+  } else if (staged) {
+    const size_t lds = (size_t)nb1 * stS * 2;
+#define KS_ST(S, T)                                                                                          \
+  do {                                                                                                       \
+    KS_HIP(hipFuncSetAttribute((const void *)k_part_scatter_st<S, T>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                               (int)lds));                                                                   \
+    hipLaunchKernelGGL((k_part_scatter_st<S, T>), dim3(G), dim3(T), lds, st, s->seq, total, s->offsets_dev, s->nseq, \
+                       k, shift, ex1, static_cast<uint16_t *>(p1), tile0, ntiles);                           \
+  } while (0)
+    if (stS == 32 && stT == kPT) KS_ST(32, kPT);
+    else if (stS == 32) KS_ST(32, kPT / 2);
+    else if (stT == kPT) KS_ST(16, kPT);
+    else KS_ST(16, kPT / 2);
+#undef KS_ST
   } else {
     // single level (k <= 13): 512-lane blocks on 8K-position sub-tiles, half
     // the LDS, two blocks per CU (KS_SCATTER_1024: the 1024-lane form)
@@ -779,7 +949,7 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   KS_HIP(hipGetLastError());
   if (!n_words) return KS_OK;
   unsigned long long words = 0;
-  KS_HIP(hipMemcpyAsync(&words, last, 8, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipMemcpyAsync(&words, last + 2, 8, hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
   *n_words = (double)words;
   return KS_OK;

@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <sys/types.h>
 #include <functional>
 #include <string>
 #include <vector>
@@ -183,6 +184,31 @@ ks_status ctx_sub(ks_ctx *ctx, ks_ctx **sub);  // ctx->sub, created on first use
 void pool_release_device(int dev);             // free the device's pooled expanded-table buffer
 ks_status default_ctx(ks_ctx **ctx);  // *ctx or the process default context (fork-checked)
 bool hip_usable_here();  // false in a child forked after HIP was initialised
+// Region output block (ks_regions_free frees it): [seq_id | beg | end] int32,
+// then [score | 0.0] doubles.
+ks_status regions_alloc(ks_regions *out, int64_t n);
+// GPU broker for fork children (ks_broker.cpp): broker_before_hip() forks it
+// right before a process's first HIP use (when enabled); use_broker() is true
+// in a child forked after that, whose host-buffer calls the broker_* forward.
+void broker_before_hip();
+bool broker_wanted(pid_t hip_pid);
+bool use_broker();
+void broker_reset_locks();
+ks_status broker_kmer_counts(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k, int32_t *counts,
+                             double *n_words);
+ks_status broker_kmer_regions(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k, const double *w,
+                              int64_t w_len, int32_t min_width, double min_score, int32_t *visits, double *n_bases,
+                              ks_regions *out);
+ks_status broker_low_comp(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k, int32_t min_width,
+                          double min_score, double thr, int32_t *counts, double *ranks, double *n, ks_regions *out);
+ks_status broker_tr_lr(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k, int32_t min_length,
+                       const char *const *kmers, const double *kmer_scores, const double *trans_scores,
+                       int64_t n_scores, double *spectra, ks_regions *out);
+ks_status broker_windowed(const char *const *seqs, const int64_t *lens, int32_t nseq, const char *const *kmers,
+                          int32_t kmer_n, int32_t k, int32_t window, int32_t ret_flag, int32_t *dist,
+                          int32_t *seq_included, int32_t *const *scores);
+ks_status broker_kmers_to_file(const char *seq_path, const char *out_prefix, const int32_t *ks, int32_t nk,
+                               double min_l, int32_t magic, ks_kmer_file_info *info);
 
 // -------------------------------------------------------------- encoding
 __host__ __device__ __forceinline__ bool is_n(uint8_t c) { return (c | 0x20) == 'n'; }

@@ -378,6 +378,7 @@ extern "C" ks_status ks_kmers_to_file(ks_ctx *ctx, const char *seq_path, const c
   of += ".bin";
   if (of.size() >= sizeof(info->out_path)) return fail(KS_ERR_ARG, "output path too long");
   memcpy(info->out_path, of.c_str(), of.size() + 1);
+  if (use_broker()) return broker_kmers_to_file(seq_path, out_prefix, ks, nk, min_l, magic, info);
   KS_TRY(default_ctx(&ctx));
   // read.count() inside try(): any failure there is the NA result (:145-148)
   auto na = [&](const char *why) {

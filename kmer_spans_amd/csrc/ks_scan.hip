@@ -480,22 +480,7 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
   // 3 x n matrix, the layout of the reference's `pos`), then [score | 0.0]
   // doubles (2 x n, `score`'s layout with the reference's second row, :280)
   // (allocated while the device orders the regions)
-  auto alloc_out = [&]() -> ks_status {
-    const size_t nn = (size_t)std::max<int64_t>(n, 1);
-    const size_t ioff = (3 * nn * 4 + 7) & ~(size_t)7;
-    char *blk = static_cast<char *>(malloc(ioff + 2 * nn * 8));
-    if (!blk) {
-      memset(out, 0, sizeof(*out));
-      return fail(KS_ERR_NOMEM, "out of host memory for %lld regions", (long long)n);
-    }
-    out->n = n;
-    out->seq_id = reinterpret_cast<int32_t *>(blk);
-    out->beg = out->seq_id + nn;
-    out->end = out->beg + nn;
-    out->score = reinterpret_cast<double *>(blk + ioff);
-    if (n == 0) out->score[0] = 0.0;  // (n > 0: zero-filled while the D2H runs)
-    return KS_OK;
-  };
+  auto alloc_out = [&]() -> ks_status { return regions_alloc(out, n); };
   if (n > 0) {
     void *tmpb = nullptr;
     const size_t nn = (size_t)n;

@@ -301,4 +301,9 @@ static const R_CallMethodDef callMethods[] = {
     {"kmers_to_file_r", (DL_FUNC)&kmers_to_file_r, 5},
     {NULL, NULL, 0}};
 
-void R_init_kmer_spans(DllInfo *info) { R_registerRoutines(info, NULL, callMethods, NULL, NULL); }
+void R_init_kmer_spans(DllInfo *info) {
+  R_registerRoutines(info, NULL, callMethods, NULL, NULL);
+  /* mclapply workers forked after a call in the R session (test.R:351 then
+     :554-565) reach the GPU through the broker (ks_broker.cpp) */
+  ks_set_fork_broker(1);
+}

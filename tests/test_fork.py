@@ -2,9 +2,14 @@
 parent may have used the library (test.R:351 then :554-559).  A child that
 inherits a HIP context must get a clear KS_ERR_DEVICE status, never a hang or
 a fault: nothing in the child may touch the parent's HIP state."""
+import json
 import os
+import subprocess
+import sys
 
 import pytest
+
+SCENARIO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fork_broker_scenario.py")
 
 
 def _child_status(call):
@@ -33,6 +38,7 @@ def test_fork_after_use_is_refused_cleanly():
     import numpy as np
     from kmer_spans_amd import _lib
     L = _lib.load()
+    L.ks_set_fork_broker(0)  # (the refusal itself; the broker: test_fork_broker_* below)
     seqs = (C.c_char_p * 1)(b"ACGTACGTAC")
     lens = np.array([10], dtype=np.int64)
     counts = np.zeros(16, dtype=np.int32)
@@ -64,6 +70,7 @@ def test_fork_after_hip_init_is_refused_cpu():
         pytest.skip("covered by the GPU test")
     from kmer_spans_amd import _lib
     L = _lib.load()
+    L.ks_set_fork_broker(0)
     seqs = (C.c_char_p * 1)(b"ACGTACGTAC")
     lens = np.array([10], dtype=np.int64)
     counts = np.zeros(16, dtype=np.int32)
@@ -76,3 +83,37 @@ def test_fork_after_hip_init_is_refused_cpu():
 
     rc, msg = _child_status(call)
     assert rc == 2 and "fork" in msg
+
+
+def _scenario(mode):
+    """tests/fork_broker_scenario.py in a fresh process (the broker is forked
+    by a process that has not touched HIP yet)."""
+    env = dict(os.environ, KS_FORK_BROKER="1")
+    p = subprocess.run([sys.executable, SCENARIO, mode], capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.gpu
+def test_fork_broker_mclapply_pattern():
+    """test.R:351 then :554-565: the parent calls, forked workers call
+    kmer_counts, kmer_regions (with visits), kmer_low_comp_regions,
+    window_kmer_dist (with positions) and lr_regions through the broker; every
+    result equals the parent's own call on the same input."""
+    r = _scenario("gpu")
+    assert r["workers_ok"], r
+    assert r["workers_equal"], r
+    assert sum(r["regions"]) > 0
+
+
+def test_fork_broker_plumbing_cpu():
+    """Without a GPU: a worker's call reaches the broker (its error is the
+    broker's "no device", not the fork refusal); argument errors are still
+    raised in the worker."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("covered by the GPU test")
+    r = _scenario("cpu")
+    assert r["worker_err"] and "fork" not in r["worker_err"], r
+    assert r["worker_err"] == r["parent"], r
+    assert "less than 1+MAX_K" in r["worker_arg_err"], r

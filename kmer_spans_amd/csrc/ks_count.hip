@@ -286,6 +286,114 @@ __global__ void k_part_sum_last(const unsigned long long *__restrict__ mat, cons
   *last = ex[n - 1] + mat[n - 1];
 }
 
+// ---- lane windows of the partitioned counter.  A lane owns kPer
+// consecutive positions and reads them with the kLook bytes before them (two
+// 16-B loads), issued one tile ahead of use (the next tile's loads are in
+// flight while this tile is processed).
+struct LaneWin {
+  uint4 a, b;
+  bool fast;  // both loads in bounds (else the bytes are read one by one)
+};
+
+__device__ __forceinline__ void lane_load(const uint8_t *__restrict__ seq, int64_t total, int64_t p0, LaneWin &w) {
+  w.fast = p0 >= kLook && p0 + kPer <= total;
+  if (w.fast) {
+    w.a = *reinterpret_cast<const uint4 *>(seq + p0 - kLook);
+    w.b = *reinterpret_cast<const uint4 *>(seq + p0);
+  }
+}
+
+// The lane's 32 bytes as 8 little-endian words (byte j = bits 8(j%4) of word j/4).
+__device__ __forceinline__ void lane_bytes(const uint8_t *__restrict__ seq, int64_t total, int64_t p0,
+                                           const LaneWin &w, uint32_t (&x)[8]) {
+  if (w.fast) {
+    x[0] = w.a.x, x[1] = w.a.y, x[2] = w.a.z, x[3] = w.a.w;
+    x[4] = w.b.x, x[5] = w.b.y, x[6] = w.b.z, x[7] = w.b.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = 0;
+#pragma unroll
+    for (int j = 0; j < kLook + kPer; ++j) {
+      const int64_t q = p0 - kLook + j;
+      const uint32_t c = (q >= 0 && q < total) ? seq[q] : (uint32_t)'N';
+      x[j >> 2] |= c << (8 * (j & 3));
+    }
+  }
+}
+
+// The counted k-mers of a lane's positions: emit(i, code) for position
+// p0 + i.  kStarts: some sequence starts inside the tile, marked in bmask
+// (bit r = position base + r): a start resets the run, and the k-mer test
+// drops a run of exactly k bases ending right before a start (Q1).  Without
+// starts the tile needs neither.
+template <bool kStarts, typename F>
+__device__ __forceinline__ void lane_kmers(const uint32_t (&x)[8], int64_t p0, int64_t total, int64_t base,
+                                           const uint32_t *bmask, int k, uint32_t mask, F emit) {
+  // byte j is position p0 - kLook + j: in the sequence while j < jend, bit r0 + j of bmask
+  const int jend = p0 + kPer <= total ? kLook + kPer : (int)(total - (p0 - kLook));
+  const int r0 = (int)(p0 - kLook - base);
+  uint32_t code = 0;
+  int len = 0;
+#pragma unroll
+  for (int j = 1; j < kLook + kPer; ++j) {
+    const int r = r0 + j;
+    if (kStarts && ((bmask[r >> 5] >> (r & 31)) & 1u)) len = 0;
+    const uint8_t c = (uint8_t)(x[j >> 2] >> (8 * (j & 3)));
+    if (!is_n(c)) {
+      code = ((code << 2) | enc(c)) & mask;
+      ++len;
+    } else {
+      len = 0;
+    }
+    if (j >= kLook && j < jend && len >= k) {
+      bool q1 = false;
+      if (kStarts) {
+        const int r1 = r + 1;
+        q1 = (len == k) && ((bmask[r1 >> 5] >> (r1 & 31)) & 1u);
+      }
+      if (!q1) emit(j - kLook, code);
+    }
+  }
+}
+
+// Per block, the sequence starts (offs[0..nseq], ascending) ahead of its
+// tiles, which it visits in ascending order: *ci = the first index with
+// offs >= base (the cursor only moves forward), *nx = that offset.
+__device__ __forceinline__ void starts_seek(const int64_t *__restrict__ offs, int32_t nseq, int64_t base, int32_t *ci,
+                                            int64_t *nx) {
+  while (*nx < base) {
+    ++*ci;
+    *nx = *ci <= nseq ? offs[*ci] : INT64_MAX;
+  }
+}
+
+__device__ __forceinline__ void starts_init(const int64_t *__restrict__ offs, int32_t nseq, int64_t base,
+                                            int32_t *ci, int64_t *nx) {
+  int32_t lo = 0, hi = nseq + 1;  // first index with offs >= base
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (offs[mid] < base) lo = mid + 1;
+    else hi = mid;
+  }
+  *ci = lo;
+  *nx = lo <= nseq ? offs[lo] : INT64_MAX;
+}
+
+// bmask for a tile holding starts (between barriers): bits of offs[ci..] <= lim.
+template <int kWords>
+__device__ __forceinline__ void starts_mark(const int64_t *__restrict__ offs, int32_t nseq, int32_t ci, int64_t base,
+                                            int64_t lim, uint32_t *bmask) {
+  for (int i = threadIdx.x; i < kWords; i += blockDim.x) bmask[i] = 0;
+  __syncthreads();
+  for (int64_t q = ci + (int64_t)threadIdx.x; q <= nseq; q += blockDim.x) {
+    const int64_t v = offs[q];
+    if (v > lim) break;
+    const int r = (int)(v - base);
+    atomicOr(&bmask[r >> 5], 1u << (r & 31));
+  }
+  __syncthreads();
+}
+
 // Level 1 over the sequence: per block, the LDS histogram of the buckets
 // (code >> shift, shift = 2k - T1) of the k-mers in its tiles, each count
 // rounded up to a multiple of pad (the staged scatter writes whole pieces of
@@ -295,56 +403,39 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
                                               const int64_t *__restrict__ offs, int32_t nseq, int k, int shift,
                                               unsigned long long *__restrict__ mat, int pad,
                                               unsigned long long *__restrict__ words, int64_t tile0, int64_t ntiles) {
+  constexpr int kWords = (kPTile + kLook + 32) / 32 + 1;
   __shared__ uint32_t lds_b[1 << kT1];
-  __shared__ uint32_t bmask[(kPTile + kLook + 32) / 32 + 1];
+  __shared__ uint32_t bmask[kWords];
   __shared__ unsigned long long wsum[kPT / 64];
   const int nb = 1 << (2 * k - shift);
   const int G = gridDim.x;
   for (int i = threadIdx.x; i < nb; i += kPT) lds_b[i] = 0;
   const uint32_t mask = (1u << (2 * k)) - 1u;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
+  int32_t ci = 0;
+  int64_t nx = 0;
+  int64_t tile = blockIdx.x;
+  if (tile < ntiles) starts_init(offs, nseq, (tile0 + tile) * kPTile - kLook, &ci, &nx);
+  LaneWin cur;
+  if (tile < ntiles) lane_load(seq, total, (tile0 + tile) * kPTile + (int64_t)threadIdx.x * kPer, cur);
+  __syncthreads();
+  for (; tile < ntiles; tile += G) {
     const int64_t t0 = (tile0 + tile) * kPTile;
-    const int64_t base = t0 - kLook;
-    __syncthreads();
-    for (int i = threadIdx.x; i < (kPTile + kLook + 32) / 32 + 1; i += kPT) bmask[i] = 0;
-    __syncthreads();
-    if (threadIdx.x < 64) mark_seq_starts(offs, nseq, base, t0 + kPTile, bmask);
-    __syncthreads();
+    const int64_t base = t0 - kLook, lim = t0 + kPTile;
     const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
-    if (p0 >= total) continue;
-    uint8_t b[kLook + kPer];
-    if (p0 >= kLook && p0 + kPer <= total) {
-      const uint4 v0 = *reinterpret_cast<const uint4 *>(seq + p0 - kLook);
-      const uint4 v1 = *reinterpret_cast<const uint4 *>(seq + p0);
-      const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-      for (int j = 0; j < kLook + kPer; ++j) b[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
-    } else {
-#pragma unroll
-      for (int j = 0; j < kLook + kPer; ++j) {
-        const int64_t q = p0 - kLook + j;
-        b[j] = (q >= 0 && q < total) ? seq[q] : (uint8_t)'N';
-      }
+    LaneWin nxt;
+    if (tile + G < ntiles) lane_load(seq, total, (tile0 + tile + G) * kPTile + (int64_t)threadIdx.x * kPer, nxt);
+    starts_seek(offs, nseq, base, &ci, &nx);
+    const bool st = nx <= lim;  // (uniform over the block)
+    if (st) starts_mark<kWords>(offs, nseq, ci, base, lim, bmask);
+    if (p0 < total) {
+      uint32_t x[8];
+      lane_bytes(seq, total, p0, cur, x);
+      auto add = [&](int, uint32_t code) { atomicAdd(&lds_b[code >> shift], 1u); };
+      if (st) lane_kmers<true>(x, p0, total, base, bmask, k, mask, add);
+      else lane_kmers<false>(x, p0, total, base, bmask, k, mask, add);
     }
-    uint32_t code = 0;
-    int len = 0;
-#pragma unroll
-    for (int j = 1; j < kLook + kPer; ++j) {
-      const int64_t q = p0 - kLook + j;
-      const int r = (int)(q - base);
-      if ((bmask[r >> 5] >> (r & 31)) & 1u) len = 0;
-      if (!is_n(b[j])) {
-        code = ((code << 2) | enc(b[j])) & mask;
-        ++len;
-      } else {
-        len = 0;
-      }
-      if (j >= kLook && q < total && len >= k) {
-        const int r1 = r + 1;
-        const bool q1 = (len == k) && ((bmask[r1 >> 5] >> (r1 & 31)) & 1u);
-        if (!q1) atomicAdd(&lds_b[code >> shift], 1u);
-      }
-    }
+    if (st) __syncthreads();  // (bmask is rewritten by the next tile holding starts)
+    cur = nxt;
   }
   __syncthreads();
   unsigned long long t = 0;
@@ -373,8 +464,11 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
 // rest stay in registers; buckets that reach kS flush the stage's piece
 // (16-B stores), the registers' slots below the last whole piece go straight
 // out (lanes of one wave hold consecutive slots of a hot bucket, so those
-// stores coalesce) and the remainder moves into the stage.  The block's last
-// remainders go out padded with kSentinel (k_bins skips it).
+// stores coalesce) and the remainder moves into the stage.  The bucket state
+// (fill, cursor) is double-buffered: the flush writes the next sub-tile's
+// state while the register phase still reads this one, two barriers per
+// sub-tile.  The block's last remainders go out padded with kSentinel, which
+// k_bins skips.
 constexpr uint16_t kSentinel = 0xffffu;  // payloads are < 2^15 on the single level
 template <int kS, int kT>
 __global__ void __launch_bounds__(kT) k_part_scatter_st(const uint8_t *__restrict__ seq, int64_t total,
@@ -382,116 +476,103 @@ __global__ void __launch_bounds__(kT) k_part_scatter_st(const uint8_t *__restric
                                                          int shift, const unsigned long long *__restrict__ ex,
                                                          uint16_t *__restrict__ part, int64_t tile0, int64_t ntiles) {
   constexpr int kTile = kT * kPer;  // positions per sub-tile
+  constexpr int kSub = kPTile / kTile;
   constexpr int kV = kS / 8;        // 16-B vectors per piece
+  constexpr int kWords = (kTile + kLook + 32) / 32 + 1;
   static_assert(kPTile % kTile == 0 && kS % 8 == 0, "sub-tiles, pieces");
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
   uint16_t *stage = reinterpret_cast<uint16_t *>(dyn);  // [nb][kS]
-  __shared__ uint32_t fill[1 << kT1], cur[1 << kT1];
-  __shared__ uint32_t bmask[(kTile + kLook + 32) / 32 + 1];
+  __shared__ uint32_t fill[2][1 << kT1], cur[2][1 << kT1];
+  __shared__ uint32_t bmask[kWords];
   const int nb = 1 << (2 * k - shift);
   const int G = gridDim.x;
   for (int i = threadIdx.x; i < nb; i += kT) {
-    fill[i] = 0;
-    cur[i] = (uint32_t)ex[(size_t)i * G + blockIdx.x];
+    fill[0][i] = 0;
+    cur[0][i] = (uint32_t)ex[(size_t)i * G + blockIdx.x];
   }
   const uint32_t mask = (1u << (2 * k)) - 1u;
   const uint32_t pmask = (1u << shift) - 1u;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
-    for (int sub = 0; sub < kPTile / kTile; ++sub) {
-      const int64_t t0 = (tile0 + tile) * kPTile + (int64_t)sub * kTile;
-      const int64_t base = t0 - kLook;
-      __syncthreads();
-      for (int i = threadIdx.x; i < (kTile + kLook + 32) / 32 + 1; i += kT) bmask[i] = 0;
-      __syncthreads();
-      if (threadIdx.x < 64) mark_seq_starts(offs, nseq, base, t0 + kTile, bmask);
-      __syncthreads();
-      const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
-      uint32_t br[kPer];  // bucket << 16 | slot of the items left in registers, or ~0u
-      uint16_t pay[kPer];
+  // the positions k_part's block counted: its kPTile-position tiles, each as
+  // kSub sub-tiles in order; iteration it = (tile index - blockIdx.x) / G * kSub + sub
+  const int64_t nit = blockIdx.x < ntiles ? ((ntiles - 1 - blockIdx.x) / G + 1) * kSub : 0;
+  auto sub_t0 = [&](int64_t it) { return (tile0 + blockIdx.x + (it / kSub) * G) * kPTile + (it % kSub) * kTile; };
+  int32_t ci = 0;
+  int64_t nx = 0;
+  LaneWin win;
+  if (nit) {
+    starts_init(offs, nseq, sub_t0(0) - kLook, &ci, &nx);
+    lane_load(seq, total, sub_t0(0) + (int64_t)threadIdx.x * kPer, win);
+  }
+  int ph = 0;
+  for (int64_t it = 0; it < nit; ++it, ph ^= 1) {
+    const int64_t t0 = sub_t0(it);
+    const int64_t base = t0 - kLook, lim = t0 + kTile;
+    const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
+    LaneWin nxt;
+    if (it + 1 < nit) lane_load(seq, total, sub_t0(it + 1) + (int64_t)threadIdx.x * kPer, nxt);
+    starts_seek(offs, nseq, base, &ci, &nx);
+    const bool st = nx <= lim;  // (uniform over the block)
+    __syncthreads();            // this phase's state is complete (init, or the last flush)
+    if (st) starts_mark<kWords>(offs, nseq, ci, base, lim, bmask);
+    uint32_t *fl = fill[ph], *cu = cur[ph];
+    uint32_t br[kPer];    // bucket << 16 | slot of the items left in registers, or ~0u
+    uint32_t pay[kPer / 2];  // their payloads, two per word
 #pragma unroll
-      for (int j = 0; j < kPer; ++j) br[j] = ~0u;
-      if (p0 < total) {
-        uint8_t b[kLook + kPer];
-        if (p0 >= kLook && p0 + kPer <= total) {
-          const uint4 v0 = *reinterpret_cast<const uint4 *>(seq + p0 - kLook);
-          const uint4 v1 = *reinterpret_cast<const uint4 *>(seq + p0);
-          const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-          for (int j = 0; j < kLook + kPer; ++j) b[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+    for (int j = 0; j < kPer; ++j) br[j] = ~0u;
+    if (p0 < total) {
+      uint32_t x[8];
+      lane_bytes(seq, total, p0, win, x);
+      auto take = [&](int i, uint32_t code) {
+        const uint32_t bk = code >> shift;
+        const uint32_t slot = atomicAdd(&fl[bk], 1u);
+        const uint32_t v = code & pmask;
+        if (slot < (uint32_t)kS) {
+          stage[bk * kS + slot] = (uint16_t)v;
         } else {
+          br[i] = (bk << 16) | slot;
+          pay[i >> 1] = (i & 1) ? ((pay[i >> 1] & 0xffffu) | (v << 16)) : ((pay[i >> 1] & 0xffff0000u) | v);
+        }
+      };
+      if (st) lane_kmers<true>(x, p0, total, base, bmask, k, mask, take);
+      else lane_kmers<false>(x, p0, total, base, bmask, k, mask, take);
+    }
+    __syncthreads();
+    // whole stage pieces out; the next sub-tile's state
+    uint32_t *fl2 = fill[ph ^ 1], *cu2 = cur[ph ^ 1];
+    for (int i = threadIdx.x; i < nb; i += kT) {
+      const uint32_t f = fl[i], c = cu[i];
+      if (f >= (uint32_t)kS) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(stage + i * kS);
+        uint4 *dst = reinterpret_cast<uint4 *>(part + c);
 #pragma unroll
-          for (int j = 0; j < kLook + kPer; ++j) {
-            const int64_t q = p0 - kLook + j;
-            b[j] = (q >= 0 && q < total) ? seq[q] : (uint8_t)'N';
-          }
-        }
-        uint32_t code = 0;
-        int len = 0;
-#pragma unroll
-        for (int j = 1; j < kLook + kPer; ++j) {
-          const int64_t q = p0 - kLook + j;
-          const int r = (int)(q - base);
-          if ((bmask[r >> 5] >> (r & 31)) & 1u) len = 0;
-          if (!is_n(b[j])) {
-            code = ((code << 2) | enc(b[j])) & mask;
-            ++len;
-          } else {
-            len = 0;
-          }
-          if (j >= kLook && q < total && len >= k) {
-            const int r1 = r + 1;
-            const bool q1 = (len == k) && ((bmask[r1 >> 5] >> (r1 & 31)) & 1u);
-            if (!q1) {
-              const uint32_t bk = code >> shift;
-              const uint32_t slot = atomicAdd(&fill[bk], 1u);
-              const uint16_t v = (uint16_t)(code & pmask);
-              if (slot < (uint32_t)kS) {
-                stage[bk * kS + slot] = v;
-              } else {
-                br[j - kLook] = (bk << 16) | slot;
-                pay[j - kLook] = v;
-              }
-            }
-          }
-        }
-      }
-      __syncthreads();
-      // whole stage pieces out
-      for (int i = threadIdx.x; i < nb; i += kT) {
-        if (fill[i] >= (uint32_t)kS) {
-          const uint4 *src = reinterpret_cast<const uint4 *>(stage + i * kS);
-          uint4 *dst = reinterpret_cast<uint4 *>(part + cur[i]);
-#pragma unroll
-          for (int v = 0; v < kV; ++v) dst[v] = src[v];
-        }
-      }
-      __syncthreads();
-      // register slots: below the last whole piece straight out, the rest staged
-#pragma unroll
-      for (int j = 0; j < kPer; ++j)
-        if (br[j] != ~0u) {
-          const uint32_t bk = br[j] >> 16, slot = br[j] & 0xffffu;
-          const uint32_t F = fill[bk] / kS * kS;
-          if (slot < F) part[cur[bk] + slot] = pay[j];
-          else stage[bk * kS + slot - F] = pay[j];
-        }
-      __syncthreads();
-      for (int i = threadIdx.x; i < nb; i += kT) {
-        const uint32_t f = fill[i];
-        if (f >= (uint32_t)kS) {
-          const uint32_t F = f / kS * kS;
-          cur[i] += F;
-          fill[i] = f - F;
-        }
+        for (int v = 0; v < kV; ++v) dst[v] = src[v];
+        const uint32_t F = f / kS * kS;
+        fl2[i] = f - F;
+        cu2[i] = c + F;
+      } else {
+        fl2[i] = f;
+        cu2[i] = c;
       }
     }
+    __syncthreads();
+    // register slots: below the last whole piece straight out, the rest staged
+#pragma unroll
+    for (int j = 0; j < kPer; ++j)
+      if (br[j] != ~0u) {
+        const uint32_t bk = br[j] >> 16, slot = br[j] & 0xffffu;
+        const uint32_t F = fl[bk] / kS * kS;
+        const uint16_t v = (uint16_t)(pay[j >> 1] >> (16 * (j & 1)));
+        if (slot < F) part[cu[bk] + slot] = v;
+        else stage[bk * kS + slot - F] = v;
+      }
+    win = nxt;
   }
   __syncthreads();
   // the block's remainders, padded to a whole piece
   for (int i = threadIdx.x; i < nb; i += kT) {
-    const uint32_t f = fill[i];
+    const uint32_t f = fill[ph][i];
     if (f == 0) continue;
-    uint4 *dst = reinterpret_cast<uint4 *>(part + cur[i]);
+    uint4 *dst = reinterpret_cast<uint4 *>(part + cur[ph][i]);
     for (int v = 0; v < kV; ++v) {
       uint32_t w[4];
 #pragma unroll
@@ -799,8 +880,7 @@ __global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
     if (part[i] != kSentinel) atomicAdd(&h[part[i]], 1u);
   const uint4 *v = reinterpret_cast<const uint4 *>(part + ah);
   const unsigned long long nv = (eb - ah) / 8;
-  for (unsigned long long i = threadIdx.x; i < nv; i += kPT) {
-    const uint4 x = v[i];
+  auto add8 = [&](const uint4 &x) {
     const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -808,7 +888,16 @@ __global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
       if (lo != kSentinel) atomicAdd(&h[lo], 1u);
       if (hi != kSentinel) atomicAdd(&h[hi], 1u);
     }
+  };
+  unsigned long long i = threadIdx.x;
+  for (; i + 3 * kPT < nv; i += 4 * kPT) {  // four loads in flight per lane
+    const uint4 x0 = v[i], x1 = v[i + kPT], x2 = v[i + 2 * kPT], x3 = v[i + 3 * kPT];
+    add8(x0);
+    add8(x1);
+    add8(x2);
+    add8(x3);
   }
+  for (; i < nv; i += kPT) add8(v[i]);
   __syncthreads();
   uint32_t *out = counts + ((size_t)bucket << L);
   for (int i = threadIdx.x; i < nbin; i += kPT) {
@@ -847,15 +936,14 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   unsigned long long *s1 = ex2 + m2;            // [nb1 + 1]
   unsigned long long *sf = s1 + nb1 + 1;        // [nbf + 1]
   unsigned long long *last = sf + nbf + 1;      // [2]: level ends; [2]: the k-mer total
-  // single level: the staged scatter (KS_SCATTER_STAGE = S x lanes, S items
-  // per bucket piece; 0: the counting-sort scatter)
+  // single level: the staged scatter (KS_SCATTER_STAGE: 0 = the counting-sort
+  // scatter; 16x1024 (default) / 16x512 = piece items x lanes.  32-item
+  // pieces do not fit the LDS next to the double-buffered bucket state)
   int stS = 16, stT = kPT;
   if (const char *e = getenv("KS_SCATTER_STAGE")) {
-    stS = atoi(e);
+    stS = atoi(e) == 0 ? 0 : 16;
     const char *x = strchr(e, 'x');
-    if (x) stT = atoi(x + 1);
-    if (stS != 16 && stS != 32) stS = 0;
-    if (stT != kPT && stT != kPT / 2) stT = kPT;
+    if (x && atoi(x + 1) == kPT / 2) stT = kPT / 2;
   }
   const int64_t n_items = total - p_lo;
   const bool staged = !g.T2 && stS > 0 && n_items + (int64_t)m1 * stS < ((int64_t)1 << 32);
@@ -891,9 +979,7 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
     hipLaunchKernelGGL((k_part_scatter_st<S, T>), dim3(G), dim3(T), lds, st, s->seq, total, s->offsets_dev, s->nseq, \
                        k, shift, ex1, static_cast<uint16_t *>(p1), tile0, ntiles);                           \
   } while (0)
-    if (stS == 32 && stT == kPT) KS_ST(32, kPT);
-    else if (stS == 32) KS_ST(32, kPT / 2);
-    else if (stT == kPT) KS_ST(16, kPT);
+    if (stT == kPT) KS_ST(16, kPT);
     else KS_ST(16, kPT / 2);
 #undef KS_ST
   } else {

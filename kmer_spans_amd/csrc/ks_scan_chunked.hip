@@ -2090,7 +2090,7 @@ __global__ void __launch_bounds__(1024) k_summaries(Chunks g, const uint8_t *__r
     for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
     __syncthreads();
   }
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (the part's chunks)
   if (c >= g.nch) return;
   sm.e[c] = INT32_MIN;
   if (o.special[c]) return;
@@ -3649,8 +3649,15 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     int64_t c0, c1, r0, r1, t0, t1;
   };
   const int64_t ctail_all = nch > 1024 ? nch - 1024 : 0;
-  const bool split = p1summ && lay.split_r > 0 && lay.split_r < nruns && lay.split_c >= 1024 &&
-                     lay.split_c + 1024 <= ctail_all;
+  // FP64 line tables (weighted rank) are cut too: the first part's summaries,
+  // carry and heads (~10 ms in all at the metric genome) start while the
+  // second part's pass 1 drains (in-process A/B at config 3: 31.5 vs 32.7 ms
+  // one part; serialising the two pass-1 launches, KS_F64_P1_SERIAL, 31.8-32.0
+  // by split fraction: profiles/r3/rank/split_ab.txt)
+  const bool f64_line = line && !comp;
+  const bool split = (p1summ || f64_line) && (p1summ || getenv("KS_NO_F64_SPLIT") == nullptr) &&
+                     lay.split_r > 0 && lay.split_r < nruns && lay.split_c >= 1024 && lay.split_c + 1024 <= ctail_all;
+  const bool p1_serial = f64_line && getenv("KS_F64_P1_SERIAL") != nullptr;
   Half halves[2];
   int nhalf = 1;
   halves[0] = Half{0, nch, 0, nruns, 0, ntiles};
@@ -3781,6 +3788,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipGetLastError());
       KS_HIP(hipEventRecord(ctx->ev[12], ctx->hi));
       KS_HIP(hipStreamWaitEvent(st, ctx->ev[12], 0));
+      if (p1_serial) KS_HIP(hipStreamWaitEvent(ctx->side, ctx->ev[12], 0));
       p1l(halves[1], ctx->side);
     } else {
       p1l(halves[0], st);
@@ -3889,6 +3897,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     unsigned long long *rep_h = d_replays + 2 * hi;
     unsigned int *err_h = reinterpret_cast<unsigned int *>(d_replays + 2 * hi + 1);
     const unsigned gch_h = (unsigned)((nh + 255) / 256);
+    const unsigned gsum_h = (unsigned)((nh + 1023) / 1024);
     // ---- P2 prediction, segment starts, summaries
     KS_TRY(ascan(p1, xt, h.r0, h.r1, h.t0, h.t1, strm));
     const int64_t wl = (h.c0 > 0 ? h.c0 - 1 : 0) / 64;
@@ -3914,13 +3923,13 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       hipLaunchKernelGGL(k_summ_fixw<false>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
                          d_fix + h.c0, d_nfix + hi, sm, rpb, hi);
     } else if (lds_lut)
-      hipLaunchKernelGGL((k_summaries<true, true>), dim3(gch1k), dim3(1024), 0, strm, g, s->seq, total, k, tv, codes,
+      hipLaunchKernelGGL((k_summaries<true, true>), dim3(gsum_h), dim3(1024), 0, strm, gv, s->seq, total, k, tv, codes,
                          p1, xt, sm);
     else if (comp)
-      hipLaunchKernelGGL((k_summaries<true, false>), dim3(gch1k), dim3(1024), 0, strm, g, s->seq, total, k, tv, codes,
+      hipLaunchKernelGGL((k_summaries<true, false>), dim3(gsum_h), dim3(1024), 0, strm, gv, s->seq, total, k, tv, codes,
                          p1, xt, sm);
     else
-      hipLaunchKernelGGL((k_summaries<false, false>), dim3(gch1k), dim3(1024), 0, strm, g, s->seq, total, k, tv,
+      hipLaunchKernelGGL((k_summaries<false, false>), dim3(gsum_h), dim3(1024), 0, strm, gv, s->seq, total, k, tv,
                          codes, p1, xt, sm);
     KS_HIP(hipGetLastError());
     if (last) KS_HIP(hipEventRecord(ctx->ev[14], strm));

@@ -840,30 +840,92 @@ __global__ void k_part_starts(const unsigned long long *__restrict__ ex, int str
   if (i == nb) bstart[nb] = *last;
 }
 
-// Buckets in descending size (one block, nb <= 4096): order[r] = the bucket
-// of rank r, ties by index.  k_bins' blocks take their bucket through it, so
-// the largest buckets (the all-A / all-T prefixes hold 6.5x the mean at the
-// metric genome) start first instead of ending the kernel alone.
-__global__ void __launch_bounds__(1024) k_bucket_order(const unsigned long long *__restrict__ bstart, int nb,
-                                                       int32_t *__restrict__ order) {
-  __shared__ unsigned long long sz[4096];
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) sz[i] = bstart[i + 1] - bstart[i];
-  __syncthreads();
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
-    const unsigned long long v = sz[i];
-    int r = 0;
-    for (int j = 0; j < nb; ++j) r += (sz[j] > v) || (sz[j] == v && j < i);
-    order[r] = i;
+// Work list of k_bins (one block, nb <= 4096): the non-empty buckets in
+// descending size (bitonic sort of (size, index) keys in LDS), each cut into
+// shares = ceil(size / target) blocks of about target items, target = the
+// mean share of 2048 blocks.  The largest buckets -- the all-A / all-T
+// prefixes hold 6.5x the mean at the metric genome, mostly runs of one
+// k-mer -- no longer end the kernel as one block each.  work[i] = bucket |
+// share << 12 | shares << 22 for block i < *nwork.
+constexpr int kWorkMax = 4096 + 2048;
+__global__ void __launch_bounds__(1024) k_bins_work(const unsigned long long *__restrict__ bstart, int nb,
+                                                    uint32_t *__restrict__ work, uint32_t *__restrict__ nwork) {
+  __shared__ unsigned long long key[4096];
+  __shared__ uint32_t shs[4096];
+  __shared__ uint32_t wsum[16];
+  const unsigned long long tot = bstart[nb] - bstart[0];
+  const unsigned long long target = tot / 2048 + 1;
+  for (int i = threadIdx.x; i < 4096; i += 1024) {
+    const unsigned long long sz = i < nb ? bstart[i + 1] - bstart[i] : 0;
+    key[i] = ((0xffffffffull - (sz > 0xffffffffull ? 0xffffffffull : sz)) << 12) | (unsigned)(i & 4095);
   }
+  __syncthreads();
+  for (int kk = 2; kk <= 4096; kk <<= 1)
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < 4096; i += 1024) {
+        const int l = i ^ j;
+        if (l > i) {
+          const unsigned long long x = key[i], y = key[l];
+          const bool up = (i & kk) == 0;
+          if ((x > y) == up) {
+            key[i] = y;
+            key[l] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  // shares of the r-th largest bucket, then an exclusive scan over r
+  for (int r = threadIdx.x; r < 4096; r += 1024) {
+    const int b = (int)(key[r] & 4095);
+    const unsigned long long sz = b < nb ? bstart[b + 1] - bstart[b] : 0;
+    shs[r] = sz ? (uint32_t)min<unsigned long long>((sz + target - 1) / target, 1023) : 0;
+  }
+  __syncthreads();
+  // block scan of 4096 values: 4 per thread
+  uint32_t v[4], t = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[q] = shs[threadIdx.x * 4 + q];
+    t += v[q];
+  }
+  uint32_t inc = t;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int w = 0; w < wv; ++w) base += wsum[w];
+  uint32_t pos = base + inc - t;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = threadIdx.x * 4 + q;
+    const uint32_t b = (uint32_t)(key[r] & 4095);
+    for (uint32_t j = 0; j < v[q]; ++j) work[pos + j] = b | (j << 12) | (v[q] << 22);
+    pos += v[q];
+  }
+  if (threadIdx.x == 1023) *nwork = pos;
 }
 
-template <bool kOwn>
+// One block per work item (bucket, share of its items): the LDS histogram of
+// the share's bins, added to counts[bucket << L | bin] (a bucket's only share
+// owns those counters; shares of a cut bucket add with atomics).  Runs of
+// equal items (the hot buckets' single-k-mer runs) are added once per run of
+// a lane's 8 items.  kSentinel (the staged scatter's padding) is skipped.
 __global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
-                                              const unsigned long long *__restrict__ bstart, int L, int split,
-                                              uint32_t *__restrict__ counts, const int32_t *__restrict__ order) {
+                                              const unsigned long long *__restrict__ bstart, int L,
+                                              uint32_t *__restrict__ counts, const uint32_t *__restrict__ work,
+                                              const uint32_t *__restrict__ nwork) {
   extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [2^L]
+  // (no work list: block = bucket, one share; the two-level counts' 2^13-2^15 buckets)
+  if (work && blockIdx.x >= *nwork) return;
+  const uint32_t wi = work ? work[blockIdx.x] : (1u << 22);
+  const int bucket = work ? (int)(wi & 4095) : (int)blockIdx.x;
+  const int s = (int)((wi >> 12) & 1023), split = (int)(wi >> 22);
   const int nbin = 1 << L;
-  const int bucket = order ? order[blockIdx.x / split] : blockIdx.x / split, s = blockIdx.x % split;
   for (int i = threadIdx.x; i < nbin; i += kPT) h[i] = 0;
   __syncthreads();
   const unsigned long long a0 = bstart[bucket], a1 = bstart[bucket + 1];
@@ -873,7 +935,6 @@ __global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
   unsigned long long ah = (a + 7) & ~7ull;
   if (ah > e) ah = e;
   const unsigned long long eb = ah + ((e - ah) & ~7ull);
-  // (kSentinel: the staged scatter's padding; bins are < 2^15)
   for (unsigned long long i = a + threadIdx.x; i < ah; i += kPT)
     if (part[i] != kSentinel) atomicAdd(&h[part[i]], 1u);
   for (unsigned long long i = eb + threadIdx.x; i < e; i += kPT)
@@ -882,12 +943,18 @@ __global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
   const unsigned long long nv = (eb - ah) / 8;
   auto add8 = [&](const uint4 &x) {
     const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+    uint32_t cur = w[0] & 0xffffu, run = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t lo = w[j] & 0xffffu, hi = w[j] >> 16;
-      if (lo != kSentinel) atomicAdd(&h[lo], 1u);
-      if (hi != kSentinel) atomicAdd(&h[hi], 1u);
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t y = (w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+      if (y != cur) {
+        if (cur != kSentinel) atomicAdd(&h[cur], run);
+        cur = y;
+        run = 0;
+      }
+      ++run;
     }
+    if (cur != kSentinel) atomicAdd(&h[cur], run);
   };
   unsigned long long i = threadIdx.x;
   for (; i + 3 * kPT < nv; i += 4 * kPT) {  // four loads in flight per lane
@@ -900,12 +967,15 @@ __global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
   for (; i < nv; i += kPT) add8(v[i]);
   __syncthreads();
   uint32_t *out = counts + ((size_t)bucket << L);
-  for (int i = threadIdx.x; i < nbin; i += kPT) {
-    const uint32_t c = h[i];
-    if (kOwn) {
+  if (split == 1) {
+    for (int i = threadIdx.x; i < nbin; i += kPT) {
+      const uint32_t c = h[i];
       if (c) out[i] += c;
-    } else if (c) {
-      atomicAdd(&out[i], c);
+    }
+  } else {
+    for (int i = threadIdx.x; i < nbin; i += kPT) {
+      const uint32_t c = h[i];
+      if (c) atomicAdd(&out[i], c);
     }
   }
 }
@@ -1014,24 +1084,21 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
     bins = static_cast<const uint16_t *>(p2);
     bstart = sf;
   }
+  // k_bins over a device work list (nbf <= 4096 buckets)
   const size_t lds_h = (size_t)4 << g.L;
-  KS_HIP(hipFuncSetAttribute((const void *)k_bins<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_h));
-  KS_HIP(hipFuncSetAttribute((const void *)k_bins<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_h));
-  const int split = nbf >= 2048 ? 1 : (2048 / nbf);
-  int32_t *order = nullptr;
-  if (nbf <= 4096 && !getenv("KS_BINS_INDEX_ORDER")) {
+  KS_HIP(hipFuncSetAttribute((const void *)k_bins, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_h));
+  if (nbf > 4096) {  // two-level counts (k >= 14): a block per final bucket
+    hipLaunchKernelGGL(k_bins, dim3((unsigned)nbf), dim3(kPT), lds_h, st, bins, bstart, g.L, (uint32_t *)counts_dev,
+                       nullptr, nullptr);
+  } else {
     void *ob = nullptr;
-    KS_TRY(ensure(ctx, SLOT_CHUNK_D, (size_t)nbf * 4 + 64, &ob));
-    order = static_cast<int32_t *>(ob);
-    hipLaunchKernelGGL(k_bucket_order, dim3(1), dim3(1024), 0, st, bstart, nbf, order);
+    KS_TRY(ensure(ctx, SLOT_CHUNK_D, (size_t)(kWorkMax + 16) * 4, &ob));
+    uint32_t *work = static_cast<uint32_t *>(ob), *nwork = work + kWorkMax;
+    hipLaunchKernelGGL(k_bins_work, dim3(1), dim3(1024), 0, st, bstart, nbf, work, nwork);
     KS_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_bins, dim3((unsigned)(nbf + 2048)), dim3(kPT), lds_h, st, bins, bstart, g.L,
+                       (uint32_t *)counts_dev, work, nwork);
   }
-  if (split == 1)
-    hipLaunchKernelGGL(k_bins<true>, dim3(nbf), dim3(kPT), lds_h, st, bins, bstart, g.L, 1, (uint32_t *)counts_dev,
-                       order);
-  else
-    hipLaunchKernelGGL(k_bins<false>, dim3(nbf * split), dim3(kPT), lds_h, st, bins, bstart, g.L, split,
-                       (uint32_t *)counts_dev, order);
   KS_HIP(hipGetLastError());
   if (!n_words) return KS_OK;
   unsigned long long words = 0;

@@ -7,6 +7,8 @@ shift
 mkdir -p $O
 export TMPDIR=/tmp
 cd /tmp
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/stats -o run --output-format csv -- python3 $R/tools/ab_count.py --rounds 1 --steps 2 "$@" > $O/stats.log 2>&1 || { tail -20 $O/stats.log; exit 1; }
+find $O/stats -name '*kernel_stats.csv' | head -1 | xargs -I{} sh -c 'grep -E "k_part|k_bins|k_bucket" {} | cut -c1-200'
 i=0
 for P in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS" "WRITE_SIZE GRBM_GUI_ACTIVE" "FETCH_SIZE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES"; do
   i=$((i+1))

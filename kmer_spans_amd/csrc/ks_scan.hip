@@ -42,7 +42,7 @@ namespace {
 // table reads in flight instead of one (the gathers do not depend on S).
 // With an expanded table one read serves J consecutive indices (the
 // (k+J-1)-mer spanning them), as in the chunked gather pass.
-template <int J, bool kCompressed>
+template <int J, bool kCompressed, int GW = 0>
 __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ seq, int64_t total,
                                                   const int64_t *__restrict__ ra,
                                                   const int64_t *__restrict__ rbnd,
@@ -51,7 +51,9 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
                                                   uint32_t *__restrict__ visits, RegionBuf out,
                                                   const unsigned long long *__restrict__ d_cnt, int64_t segcap,
                                                   const uint32_t *__restrict__ packed) {
-  constexpr int G = (J == 1) ? 16 : (J >= 4 ? 4 : (J == 3 ? 6 : 8));  // reads per batch
+  // reads per batch (GW: a wider batch -- FP64 line tables, 8 line reads = 32 indices per round trip:
+  // weighted-rank rescans 3.76 -> 3.61 ms in-process, profiles/r3/rank/lane_ab.txt)
+  constexpr int G = GW ? GW : ((J == 1) ? 16 : (J >= 4 ? 4 : (J == 3 ? 6 : 8)));
   constexpr int PB = G * J;                                           // indices per batch (16, 16, 18, 16, 20)
   using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;  // (k+J-1)-mer code
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -301,6 +303,9 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                      ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed)
   if (tv.compressed) {
     if (J == 6) KS_LANE(6, true); else if (J == 5) KS_LANE(5, true); else if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
+  } else if (J == 4 && tv.line) {
+    hipLaunchKernelGGL((k_scan_lane<4, false, 8>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq,
+                       total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed);
   } else {
     if (J == 5) KS_LANE(5, false); else if (J == 4) KS_LANE(4, false); else if (J == 3) KS_LANE(3, false); else if (J == 2) KS_LANE(2, false); else KS_LANE(1, false);
   }

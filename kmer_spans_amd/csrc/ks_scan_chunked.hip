@@ -3042,7 +3042,7 @@ __global__ void k_fallback_prep(unsigned int *__restrict__ err, unsigned long lo
 // Heads of the R chunks (the carried excursion up to its certain clamp):
 // lane per chunk, from the exact entry.  Uncompressed tables read the
 // expanded table (J indices per read) like P1.
-template <int J, bool kCompressed>
+template <int J, bool kCompressed, bool kWide = false>
 __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
                                                int k, TableView tv, const uint16_t *__restrict__ codes,
                                                Carry cr, unsigned int *__restrict__ err, int gated) {
@@ -3088,11 +3088,14 @@ __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restri
     uint64_t xp = 0;
     uint32_t code = packed_bits(packed, total, start - k, xp) ? (uint32_t)(xp >> (64 - 2 * k))
                                                               : prime_code_guarded(seq, start - k, k, total);
-    for (int b0 = 0; b0 < n && hq < 0; b0 += NB) {
-      double v[NB];
+    // (kWide: two batches' reads in flight per round trip; FP64 line tables)
+    constexpr int NW = kWide ? 2 * NB : NB;
+    for (int b0 = 0; b0 < n && hq < 0; b0 += NW) {
+      double v[NW];
       values16_f64(g, seq, total, k, tv, start, b0, n, code, mask, v);
+      if (kWide) values16_f64(g, seq, total, k, tv, start, b0 + NB, n, code, mask, v + NB);
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
+      for (int j = 0; j < NW; ++j) {
         const int i = b0 + j;
         if (i < n && hq < 0) {
           const double t = T + v[j];
@@ -3959,6 +3962,9 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   hipLaunchKernelGGL((k_heads<J, C>), dim3(gch_h), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes, cr, err_h, \
                      gated)
       if (comp) KS_HEADS(1, true);
+      else if (J == 4 && tv.line)
+        hipLaunchKernelGGL((k_heads<4, false, true>), dim3(gch_h), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes,
+                           cr, err_h, gated);
       else if (J == 4) KS_HEADS(4, false);
       else if (J == 3) KS_HEADS(3, false);
       else if (J == 2) KS_HEADS(2, false);

@@ -167,3 +167,35 @@ def test_genomes_mode(oracle):
         assert np.array_equal(vis.cpu().numpy(), o["counts"]), ("genome visits", g)
         assert st["n_bases"] == sum(lens)
         tab.close()
+
+
+@pytest.mark.parametrize("k", [11, 13, 14])
+def test_count_hot_buckets(oracle, k):
+    """The partitioned counter's hard cases (sequence_kmer_count,
+    kmer_spans.c:135-155): a few buckets holding most of the k-mers (long
+    homopolymer and dinucleotide runs -> the k_bins work list cuts them into
+    shares that add with atomics, and runs of equal items are added once per
+    lane), sequence starts inside tiles (many short sequences, the Q1 quirk at
+    sequence ends), N runs, and the staged scatter's padded regions; counts
+    and the k-mer total equal the oracle's.  k = 14 takes the two-level
+    counter."""
+    import torch
+    from kmer_spans_amd import _lib, device as D
+    ctx = _lib.context(0)
+    D.bind_torch_stream(ctx)
+    rng = np.random.default_rng(k)
+    parts = [b"A" * 3_000_000, b"CA" * 1_000_000, b"T" * 500_000 + b"N" * 77 + b"T" * 700_001]
+    parts.append(rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=2_000_000).tobytes())
+    for _ in range(300):  # short sequences: starts inside the count's tiles
+        L = int(rng.integers(0, 40))
+        parts.append(rng.choice(np.frombuffer(b"ACGTN", dtype=np.uint8), size=L).tobytes())
+    mixed = bytearray(rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=1_500_000).tobytes())
+    for at in rng.integers(0, len(mixed) - 5000, size=200):
+        mixed[at:at + 4000] = b"A" * 4000
+    parts.append(bytes(mixed))
+    ds = D.from_host(parts, "cuda")
+    counts = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+    words = D.count(ctx, ds, k, counts)
+    n, oc = oracle.kmer_counts(parts, k)
+    assert words == n
+    assert np.array_equal(counts.cpu().numpy(), oc)

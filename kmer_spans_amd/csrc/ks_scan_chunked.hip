@@ -2081,15 +2081,31 @@ constexpr bool kParReplay = true;
 // Summary of each chunk for the binade of its predicted trajectory (lane per
 // chunk, full occupancy); chunks predicted to leave the binade or to approach
 // 0 get none.
-template <bool kCompressed, bool kLds>
+// kTab (small k, k_pass1_lds): the base table -- uint16 codes, or FP64
+// values -- staged in LDS too (dynamic, <= 128 KiB) and read through it.
+template <bool kCompressed, bool kLds, bool kTab = false>
 __global__ void __launch_bounds__(1024) k_summaries(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
                                                     int k, TableView tv, const uint16_t *__restrict__ codes, P1 o,
                                                     const double *__restrict__ xt, Summ sm) {
   __shared__ double s_lut[kLds ? kLdsLutMax : 1];
-  if (kLds) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_tab[];
+  if (kLds)
     for (int i = threadIdx.x; i < tv.nlut; i += blockDim.x) s_lut[i] = tv.lut[i];
-    __syncthreads();
+  if (kTab) {
+    const int nk = 1 << (2 * k);
+    if (kCompressed) {
+      uint16_t *sc = reinterpret_cast<uint16_t *>(s_tab);
+      for (int i = threadIdx.x; i < nk; i += blockDim.x) sc[i] = tv.codes[i];
+      tv.codes = sc;
+    } else {
+      double *sv = reinterpret_cast<double *>(s_tab);
+      for (int i = threadIdx.x; i < nk; i += blockDim.x) sv[i] = tv.vals[i];
+      tv.vals = sv;
+    }
+    tv.ext = nullptr;  // (values from the staged base table)
+    tv.line = nullptr;
   }
+  if (kLds || kTab) __syncthreads();
   const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (the part's chunks)
   if (c >= g.nch) return;
   sm.e[c] = INT32_MIN;
@@ -3925,6 +3941,25 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       const unsigned gw = (unsigned)std::max<int64_t>(1, (int64_t)ctx->num_cus * 8);
       hipLaunchKernelGGL(k_summ_fixw<false>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
                          d_fix + h.c0, d_nfix + hi, sm, rpb, hi);
+    } else if (lds_table && getenv("KS_SUMM_GLOBAL_TAB") == nullptr) {
+      // small k: the table staged in LDS as for k_pass1_lds (KS_SUMM_GLOBAL_TAB: read from HBM / L2, A/B)
+      const size_t tb = (size_t)(comp ? 2 : 8) << (2 * k);
+      if (comp && lds_lut) {
+        KS_HIP(hipFuncSetAttribute((const void *)k_summaries<true, true, true>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)tb));
+        hipLaunchKernelGGL((k_summaries<true, true, true>), dim3(gsum_h), dim3(1024), tb, strm, gv, s->seq, total, k,
+                           tv, codes, p1, xt, sm);
+      } else if (comp) {
+        KS_HIP(hipFuncSetAttribute((const void *)k_summaries<true, false, true>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)tb));
+        hipLaunchKernelGGL((k_summaries<true, false, true>), dim3(gsum_h), dim3(1024), tb, strm, gv, s->seq, total, k,
+                           tv, codes, p1, xt, sm);
+      } else {
+        KS_HIP(hipFuncSetAttribute((const void *)k_summaries<false, false, true>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)tb));
+        hipLaunchKernelGGL((k_summaries<false, false, true>), dim3(gsum_h), dim3(1024), tb, strm, gv, s->seq, total,
+                           k, tv, codes, p1, xt, sm);
+      }
     } else if (lds_lut)
       hipLaunchKernelGGL((k_summaries<true, true>), dim3(gsum_h), dim3(1024), 0, strm, gv, s->seq, total, k, tv, codes,
                          p1, xt, sm);

@@ -2081,8 +2081,12 @@ constexpr bool kParReplay = true;
 // Summary of each chunk for the binade of its predicted trajectory (lane per
 // chunk, full occupancy); chunks predicted to leave the binade or to approach
 // 0 get none.
-// kTab (small k, k_pass1_lds): the base table -- uint16 codes, or FP64
-// values -- staged in LDS too (dynamic, <= 128 KiB) and read through it.
+// kTab (small k, k_pass1_lds): the table staged in LDS too (dynamic, <= 128
+// KiB): with a compressed table whose LUT is in LDS (kLds) its uint16 codes,
+// else its 4^k FP64 values (lut[codes[i]] for a compressed one) read as an
+// uncompressed base table (instantiated with kCompressed = false).  At k = 7
+// (`profiles/r3/smallk/`): +-1 (2 values) codes 3.75 ms vs values 4.18;
+// log2 (16 K values, LUT beyond LDS) values 6.4 ms vs codes 9.1.
 template <bool kCompressed, bool kLds, bool kTab = false>
 __global__ void __launch_bounds__(1024) k_summaries(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
                                                     int k, TableView tv, const uint16_t *__restrict__ codes, P1 o,
@@ -2099,8 +2103,10 @@ __global__ void __launch_bounds__(1024) k_summaries(Chunks g, const uint8_t *__r
       tv.codes = sc;
     } else {
       double *sv = reinterpret_cast<double *>(s_tab);
-      for (int i = threadIdx.x; i < nk; i += blockDim.x) sv[i] = tv.vals[i];
+      for (int i = threadIdx.x; i < nk; i += blockDim.x) sv[i] = tv.compressed ? tv.lut[tv.codes[i]] : tv.vals[i];
       tv.vals = sv;
+      tv.compressed = 0;
+      tv.codes = nullptr;
     }
     tv.ext = nullptr;  // (values from the staged base table)
     tv.line = nullptr;
@@ -3943,22 +3949,18 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                          d_fix + h.c0, d_nfix + hi, sm, rpb, hi);
     } else if (lds_table && getenv("KS_SUMM_GLOBAL_TAB") == nullptr) {
       // small k: the table staged in LDS as for k_pass1_lds (KS_SUMM_GLOBAL_TAB: read from HBM / L2, A/B)
-      const size_t tb = (size_t)(comp ? 2 : 8) << (2 * k);
       if (comp && lds_lut) {
+        const size_t tb = (size_t)2 << (2 * k);
         KS_HIP(hipFuncSetAttribute((const void *)k_summaries<true, true, true>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)tb));
         hipLaunchKernelGGL((k_summaries<true, true, true>), dim3(gsum_h), dim3(1024), tb, strm, gv, s->seq, total, k,
-                           tv, codes, p1, xt, sm);
-      } else if (comp) {
-        KS_HIP(hipFuncSetAttribute((const void *)k_summaries<true, false, true>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)tb));
-        hipLaunchKernelGGL((k_summaries<true, false, true>), dim3(gsum_h), dim3(1024), tb, strm, gv, s->seq, total, k,
-                           tv, codes, p1, xt, sm);
+                           tv, nullptr, p1, xt, sm);
       } else {
+        const size_t tb = (size_t)8 << (2 * k);
         KS_HIP(hipFuncSetAttribute((const void *)k_summaries<false, false, true>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)tb));
         hipLaunchKernelGGL((k_summaries<false, false, true>), dim3(gsum_h), dim3(1024), tb, strm, gv, s->seq, total,
-                           k, tv, codes, p1, xt, sm);
+                           k, tv, nullptr, p1, xt, sm);
       }
     } else if (lds_lut)
       hipLaunchKernelGGL((k_summaries<true, true>), dim3(gsum_h), dim3(1024), 0, strm, gv, s->seq, total, k, tv, codes,

@@ -216,7 +216,8 @@ void ks_table_destroy(ks_table *t);
  * host entry points' J = 4 tables).  This returns it to the driver; so does
  * ks_ctx_destroy for its device; environment KS_EXT_POOL=0 disables the
  * pool.  Workspace retained by a context (scan scratch, the table builder's
- * sort scratch of ~20 B x 4^k) is freed by ks_ctx_destroy. */
+ * sort scratch of ~20 B x 4^k) is freed by ks_ctx_destroy.  The last two freed region
+ * output blocks of >= 1 MiB (ks_regions_free) are kept for reuse and freed here too. */
 void ks_release_cache(void);
 
 /* Fork broker (mclapply after use, test.R:351 then :554-565).  On: right

@@ -187,6 +187,7 @@ bool hip_usable_here();  // false in a child forked after HIP was initialised
 // Region output block (ks_regions_free frees it): [seq_id | beg | end] int32,
 // then [score | 0.0] doubles.
 ks_status regions_alloc(ks_regions *out, int64_t n);
+void regions_cache_release();  // the kept output blocks (ks_release_cache)
 // GPU broker for fork children (ks_broker.cpp): broker_before_hip() forks it
 // right before a process's first HIP use (when enabled); use_broker() is true
 // in a child forked after that, whose host-buffer calls the broker_* forward.

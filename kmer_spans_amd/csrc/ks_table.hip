@@ -1209,6 +1209,7 @@ void pool_release_device(int dev) {
 }  // namespace ks
 
 extern "C" void ks_release_cache(void) {
+  regions_cache_release();
   if (!hip_usable_here()) return;
   std::lock_guard<std::mutex> g(g_pool_mu);
   for (PoolBuf &b : g_pool) {

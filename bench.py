@@ -749,6 +749,41 @@ def rank_subline(args, ctx, ds, counts, words, make_table, timed_steps, host, D)
     return out
 
 
+def genome_cpu_baseline(args, ds, host, counts, words, orc, n_genomes):
+    """one genome end to end on one pinned
+    core (the reference's kmer.counts, the log2 table of its counts, and
+    kmer_regions), timed on a sample of contigs for the count and the scan and
+    extrapolated to the whole genome; the 256-genome job time is that times
+    256, stated as an extrapolation."""
+    from oracle import oracle as O
+    k = args.k
+    ids, acc = sample_ids(ds.offsets, args.cpu_sample)
+    old = os.sched_getaffinity(0)
+    os.sched_setaffinity(0, {min(old)})
+    try:
+        t0 = time.perf_counter()
+        O.kmer_counts([host[q] for q in ids], k)
+        t_count = time.perf_counter() - t0
+        hc = counts.cpu().numpy()
+        t0 = time.perf_counter()
+        O.log2_table(hc, k)
+        t_table = time.perf_counter() - t0
+    finally:
+        os.sched_setaffinity(0, old)
+    t_scan = orc.baseline(ids)
+    total = float(ds.total)
+    t_genome = (t_count + t_scan) * total / acc + t_table
+    return {"kind": "port", "cores": 1, "unit": "Gbases/s", "value": round(total / t_genome / 1e9, 5),
+            "seconds_per_genome": round(t_genome, 2), "genomes": 256,
+            "job_seconds_extrapolated": round(t_genome * 256, 1),
+            "phases_s": {"count_sample": round(t_count, 3), "log2_table_full": round(t_table, 3),
+                         "scan_sample": round(t_scan, 3)},
+            "sample": f"count and scan of {len(ids)} contigs ({acc} bp) of one genome, extrapolated to its "
+                      f"{int(total)} bp, plus the log2 table (4^{k} entries) in full; the 256-genome job time "
+                      f"is that x 256 (an extrapolation); oracle/ks_oracle.c, one pinned core "
+                      f"(this run: {n_genomes} genome(s))"}
+
+
 def reduce_parity(ok, dist, tdist):
     """True iff every rank's parity verdict is true (gloo/nccl MIN)."""
     if not dist:
@@ -801,8 +836,10 @@ def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over
     # parity of every genome of this rank after timing (each genome's own
     # table, rebuilt: the timed loop closed it), the oracle on a thread pool
     parity = None
+    cpu = None
     if not args.no_cpu and args.parity != "none":
         ok = True
+        first = True
         for ds, r in zip(dss, results):
             counts.zero_()
             words = D.count(ctx, ds, k, counts)
@@ -810,8 +847,12 @@ def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over
             table.close()
             if init is not None:
                 init.close()
-            orc = Oracle(host_contigs(ds), k, (w_dev.cpu().numpy() - thr) if args.trlr else w_dev.cpu().numpy(), thr,
+            host = host_contigs(ds)
+            orc = Oracle(host, k, (w_dev.cpu().numpy() - thr) if args.trlr else w_dev.cpu().numpy(), thr,
                          args.min_width, args.min_score, args.trlr, args.cpu_threads)
+            if first and rank == 0 and not args.trlr:
+                cpu = genome_cpu_baseline(args, ds, host, counts, words, orc, G * world)
+            first = False
             orc.fill(range(ds.nseq))
             ok &= orc.parity(r[0], r[1], range(ds.nseq))
         parity = bool(reduce_parity(ok, dist, tdist))
@@ -831,6 +872,8 @@ def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over
                        "k": k, "score": args.score, "genomes": G * world, "mode": "genomes",
                        "parallelism": f"genome-per-rank x{world}", "build_id": build_id},
             "regions": n_regions, "parity_sample": parity, "parity_genomes": G * world if parity is not None else 0}
+    if cpu is not None:
+        line["cpu_baseline"] = cpu
     if rank == 0:
         s = json.dumps(line)
         print(s, flush=True)

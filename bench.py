@@ -56,6 +56,13 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 ALGO_BYTES_PER_BASE = 9.0      # 1 B sequence + 8 B FP64 table entry (k >= 8)
+ALGO_BYTES_PER_BASE_LDS = 1.0  # k <= 7, the table LDS-staged (k_pass1_lds): the sequence byte only
+
+
+def algo_bytes_per_base(kernel: str) -> float:
+    """SURVEY 8(d)'s algorithmic bytes per scanned base of the dominant
+    kernel: 1 B when the table lives in LDS (k <= 7, k_pass1_lds), else 9 B."""
+    return ALGO_BYTES_PER_BASE_LDS if kernel.startswith("k_pass1_lds") else ALGO_BYTES_PER_BASE
 RANDOM_WALL_GPS = 50.0         # measured random-request ceiling, contiguous 128 GiB table (profiles/r2/frag_probe.txt)
 METRIC = "Gbases/sec scanned (k=13, log-ratio score) at 1/2/4/8 MI355X; spans bit-exact"
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -262,6 +269,21 @@ class Oracle:
         with ThreadPoolExecutor(self.threads) as ex:
             for q, o in zip(todo, ex.map(lambda q: self._run([self.host[q]]), todo)):
                 self._keep([q], o)
+
+    def visits_sum(self, ids):
+        """The oracle's visit histogram of kmer_regions_r (kmer_spans.c:266-267,
+        every visited index including the restart loop's re-visits) over the
+        given contigs: per-contig histograms on the thread pool, summed as
+        the reference's int32 counts (uint32 wrap-around)."""
+        total = np.zeros(4 ** self.k, dtype=np.uint32)
+        todo = sorted(ids, key=lambda q: -self.host[q].size)
+
+        def one(q):
+            return self.O.scan([self.host[q]], self.k, self.w, self.thr, self.mw, self.ms, visits=True)["counts"]
+        with ThreadPoolExecutor(self.threads) as ex:
+            for v in ex.map(one, todo):
+                total += v.view(np.uint32)
+        return total
 
     def parity(self, pos, score, ids):
         """GPU records restricted to contigs ids equal the oracle's, bitwise."""
@@ -503,12 +525,13 @@ def main():
 
     # ---- dominant kernel roofline (hipEvents on the library stream)
     ms_kernel = float(np.mean([s["ms_scan"] for s in stats]))
-    achieved = ALGO_BYTES_PER_BASE * n_bases / (ms_kernel * 1e-3) / 1e9
     kernel = "k_scan_lane" if stats[-1]["scan_algo"] == 0 else table.pass1_kernel
+    bpb = algo_bytes_per_base(kernel)
+    achieved = bpb * n_bases / (ms_kernel * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": kernel, "kernel_ms": round(ms_kernel, 3), "algo_bytes_per_base": ALGO_BYTES_PER_BASE,
-                "algo_bytes_per_launch": int(ALGO_BYTES_PER_BASE * n_bases)}
+                "kernel": kernel, "kernel_ms": round(ms_kernel, 3), "algo_bytes_per_base": bpb,
+                "algo_bytes_per_launch": int(bpb * n_bases)}
     workload = {"k": k, "score": args.score, "scale": args.scale, "ncontigs": args.ncontigs,
                 "expand": not args.no_expand, "trlr": args.trlr, "mode": args.mode, "world": world,
                 "shard_of": args.shard_of}
@@ -568,12 +591,21 @@ def main():
     # ---- span records to rank 0 (RCCL gather; not on the timed path)
     n_regions_all = int(pos.shape[1])
     if dist:
+        # the span-record gather (the path's only exchange) and the
+        # merge on rank 0, timed beside the step (max over ranks)
         from kmer_spans_amd.dist import gather_regions, merge_shards
+        barrier()
+        tg = time.perf_counter()
         allpos, allscore = gather_regions(pos, score, dev)
+        mpos = None
+        if rank == 0 and args.mode == "shard":
+            mpos, _ = merge_shards(shards, allpos, allscore, one_based=args.trlr, offsets=offsets)
+        gather_ms = max_over_ranks((time.perf_counter() - tg) * 1e3)
+        extra["gather_ms"] = round(gather_ms, 3)
+        extra["step_plus_gather_ms"] = round(ms_step + gather_ms, 3)
         if rank == 0:
             n_regions_all = sum(int(p.shape[1]) for p in allpos)
-            if args.mode == "shard":
-                mpos, _ = merge_shards(shards, allpos, allscore, one_based=args.trlr, offsets=offsets)
+            if mpos is not None:
                 extra["merged_regions"] = int(mpos.shape[1])
                 extra["merged_order_ok"] = bool(np.all(np.diff(mpos[0].astype(np.int64) * (1 << 32) + mpos[1]) > 0))
 
@@ -585,24 +617,39 @@ def main():
     # ---- PCIe-inclusive rate of the drop-in host entry point (never `value`)
     host_path = None
     if world == 1 and not args.no_host_path and not args.trlr and thr == 0.0:
-        api.kmer_regions(host, k, w, args.min_width, args.min_score)  # warm (pinned staging, workspace)
-        th = []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            hr = api.kmer_regions(host, k, w, args.min_width, args.min_score)
-            th.append(time.perf_counter() - t0)
-        t_host = float(np.median(th))
-        host_path = {"seconds": round(t_host, 4), "Gbases_per_s": round(n_bases / t_host / 1e9, 3),
-                     "all_seconds": [round(x, 4) for x in th],
-                     "regions_equal": bool(np.array_equal(hr["pos"], pos)),
-                     "scores_equal": bool(np.array_equal(hr["score"].view(np.uint64), score.view(np.uint64))),
-                     "visits_equal": (bool(np.array_equal(hr["counts"], vis_host)) if vis_host is not None
-                                      else None),
-                     "note": "ks_kmer_regions from host memory with the visit histogram (median of 3): the score "
-                             "table and the bases (2-bit codes + N runs) cross PCIe through pinned buffers, "
-                             "table compress/expand, k-mer count in pieces during staging, scan, visits D2H; "
-                             "visits_equal against the device-resident visits line"}
-        del hr
+        L = _lib.load()
+
+        def host_calls(keep):
+            L.ks_set_host_cache(1 if keep else 0)
+            try:
+                api.kmer_regions(host, k, w, args.min_width, args.min_score)  # warm (pinned staging, contexts)
+                th = []
+                for _ in range(3):
+                    t0 = time.perf_counter()
+                    hr = api.kmer_regions(host, k, w, args.min_width, args.min_score)
+                    th.append(time.perf_counter() - t0)
+            finally:
+                L.ks_set_host_cache(0)
+            t_host = float(np.median(th))
+            out = {"seconds": round(t_host, 4), "Gbases_per_s": round(n_bases / t_host / 1e9, 3),
+                   "all_seconds": [round(x, 4) for x in th],
+                   "regions_equal": bool(np.array_equal(hr["pos"], pos)),
+                   "scores_equal": bool(np.array_equal(hr["score"].view(np.uint64), score.view(np.uint64))),
+                   "visits_equal": (bool(np.array_equal(hr["counts"], vis_host)) if vis_host is not None
+                                    else None)}
+            return out
+        torch.cuda.synchronize()
+        free0 = torch.cuda.mem_get_info(dev)[0]
+        host_path = host_calls(False)
+        host_path["vram_returned"] = bool(torch.cuda.mem_get_info(dev)[0] >= free0 - (64 << 20))
+        host_path["note"] = ("ks_kmer_regions from host memory with the visit histogram (median of 3), default "
+                             "memory policy (ks_set_host_cache(0): each call's workspace and table buffer return "
+                             "to the driver, VRAM back at its pre-call level): the score table and the bases (2-bit "
+                             "codes + N runs) cross PCIe through pinned buffers, table compress/expand, k-mer count "
+                             "in pieces during staging, scan, visits D2H; visits_equal against the device-resident "
+                             "visits line")
+        host_path["cached"] = host_calls(True)
+        host_path["cached"]["note"] = "the same with ks_set_host_cache(1): workspace and table buffer kept between calls"
 
     # ---- CPU baseline (N=1, one pinned core, bounded sample) and the parity
     # verdict (every contig of this rank, oracle on a host thread pool)
@@ -639,6 +686,15 @@ def main():
             parity = bool(reduce_over_ranks(1.0 if ok else 0.0, tdist.ReduceOp.MIN if dist else None) > 0.5)
             extra["parity_bp"] = int(reduce_over_ranks(float(bp), tdist.ReduceOp.SUM if dist else None))
             extra["parity_contigs"] = "all" if args.parity == "all" else check
+            if vis_host is not None and args.parity == "all":
+                # the visit histogram kmer_regions_r returns (kmer_spans.c:266-267, 523-537) over the
+                # whole genome: the oracle's per-contig histograms summed vs the visits line's
+                t0 = time.perf_counter()
+                ov = orc.visits_sum(check)
+                extra["visits_parity"] = bool(np.array_equal(ov, vis_host.view(np.uint32)))
+                extra["visits_parity_bp"] = bp
+                extra["visits_parity_seconds"] = round(time.perf_counter() - t0, 2)
+                del ov
         del orc
 
     # ---- weighted rank (BASELINE config 3) on the same genome and counts
@@ -750,6 +806,42 @@ def rank_subline(args, ctx, ds, counts, words, make_table, timed_steps, host, D)
     out["parity"] = orc.parity(pos, score, range(ds.nseq))
     out["parity_bp"] = int(ds.total)
     out["parity_seconds"] = round(time.perf_counter() - t0, 2)
+    if not args.no_host_path:
+        out["host_low_comp"] = hl = host_low_comp_line(args, host, hc, w, pos, score, int(ds.total), n_bases)
+        hl["parity"] = bool(hl["parity"] and out["parity"] and out["table_equal_oracle"] and hl["n"][0] == words)
+    return out
+
+
+def host_low_comp_line(args, host, counts_host, w_rank, pos, score, total, n_bases):
+    """BASELINE config 3 as the R user calls it: kmer_low_comp_regions
+    (kmer_spans.c:548-621, kmer_spans.R:72-79) from host memory -- the bases
+    cross PCIe, counted in pieces meanwhile, the rank table built on the
+    device, counts + w.rank returned over PCIe while the scan runs -- timed
+    (median of 3, PCIe-inclusive, default memory policy), its outputs checked
+    against the device-resident rank line (regions, scores), the device counts
+    and the device rank table (itself equal to the oracle's, table_equal_oracle)."""
+    from kmer_spans_amd import api
+    k = args.k
+    api.kmer_low_comp_regions(host, k, args.min_width, args.min_score, 0.75)  # warm (pinned buffers)
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        r = api.kmer_low_comp_regions(host, k, args.min_width, args.min_score, 0.75)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    out = {"seconds": round(t, 4), "Gbases_per_s": round(n_bases / t / 1e9, 3),
+           "all_seconds": [round(x, 4) for x in ts],
+           "counts_equal": bool(np.array_equal(r["counts"], counts_host)),
+           "w_rank_equal": bool(np.array_equal(r["w_rank"].view(np.uint64), w_rank.view(np.uint64))),
+           "regions_equal": bool(np.array_equal(r["pos"].T, pos)),
+           "scores_equal": bool(np.array_equal(np.ascontiguousarray(r["score"].T).view(np.uint64),
+                                               np.ascontiguousarray(score).view(np.uint64))),
+           "n": [float(x) for x in r["n"]],
+           "note": f"ks_low_comp_regions from host memory, k={k}, thr 0.75, {total} bp (median of 3, PCIe-inclusive, "
+                   "default memory policy); parity = counts, w.rank, regions and scores equal to the device-resident "
+                   "rank line, whose table equals the oracle's (table_equal_oracle) and whose regions equal the "
+                   "oracle's (parity)"}
+    out["parity"] = out["counts_equal"] and out["w_rank_equal"] and out["regions_equal"] and out["scores_equal"]
     return out
 
 

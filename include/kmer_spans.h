@@ -219,6 +219,15 @@ void ks_table_destroy(ks_table *t);
  * sort scratch of ~20 B x 4^k) is freed by ks_ctx_destroy.  The last two freed region
  * output blocks of >= 1 MiB (ks_regions_free) are kept for reuse and freed here too. */
 void ks_release_cache(void);
+/* Memory policy of the host-buffer entry points (ks_kmer_counts,
+ * ks_kmer_regions, ks_low_comp_regions, ks_tr_lr_regions, ks_windowed_dist):
+ * keep = 0 (the default; what an R session calling kmer_regions_r once
+ * expects) returns the call's device memory when the call ends -- the
+ * context's workspace and the pooled table buffer -- so VRAM is back at its
+ * pre-call level; keep = 1 keeps them for the next call (no re-allocation:
+ * faster repeated calls).  Environment KS_HOST_CACHE=1 sets keep = 1 at load.
+ * The pinned host staging buffer is kept either way. */
+ks_status ks_set_host_cache(int32_t keep);
 
 /* Fork broker (mclapply after use, test.R:351 then :554-565).  On: right
  * before this process's first HIP use the library forks a broker process (a

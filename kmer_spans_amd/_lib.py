@@ -86,7 +86,7 @@ EXPORTS = [
     "ks_fasta_load", "ks_fasta_parse", "ks_fasta_copy_seqs", "ks_fasta_free", "ks_count_multi_dev",
     "ks_count_file_write", "ks_count_file_read", "ks_count_file_free", "ks_kmers_to_file",
     "ks_windowed_dist", "ks_windowed_dev", "ks_table_from_counts",
-    "ks_release_cache", "ks_set_fork_broker",
+    "ks_release_cache", "ks_set_fork_broker", "ks_set_host_cache",
 ]
 
 SCORES = {"log2": 1, "pm1": 2, "rank": 3}  # KS_SCORE_* of ks_table_from_counts
@@ -146,6 +146,7 @@ def load():
         "ks_table_from_counts": ([P, P, I32, I32, D, D, I32, I64, P, P], I32),
         "ks_release_cache": ([], None),
         "ks_set_fork_broker": ([I32], I32),
+        "ks_set_host_cache": ([I32], I32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -165,6 +165,11 @@ ks_status ensure_pinned(ks_ctx *ctx, size_t bytes, void **out) {
 
 namespace {
 
+struct HostEnd {  // host_call_end when a host-buffer entry point returns
+  ks_ctx *c;
+  ~HostEnd() { host_call_end(c); }
+};
+
 ks_status check_seqs(const char *const *seqs, const int64_t *lens, int32_t nseq) {
   if (nseq < 1 || !seqs || !lens)
     return fail(KS_ERR_ARG, "seq_r must be a character vector of length at least one");
@@ -275,7 +280,32 @@ ks_status ctx_sub(ks_ctx *ctx, ks_ctx **sub) {
   *sub = ctx->sub;
   return KS_OK;
 }
+
+static int g_host_cache = -1;  // -1: KS_HOST_CACHE decides on first use
+
+static void free_workspace(ks_ctx *c) {
+  (void)hipSetDevice(c->device);
+  for (hipStream_t x : {c->stream, c->side, c->hi})
+    if (x) (void)hipStreamSynchronize(x);
+  for (auto &b : c->slots) {
+    if (b.ptr) (void)hipFree(b.ptr);
+    b = DevBuf();
+  }
+}
+
+void host_call_end(ks_ctx *ctx) {
+  if (g_host_cache < 0) g_host_cache = getenv("KS_HOST_CACHE") && atoi(getenv("KS_HOST_CACHE")) != 0;
+  if (g_host_cache || !ctx || ctx->pid != getpid()) return;
+  free_workspace(ctx);
+  if (ctx->sub) free_workspace(ctx->sub);
+  pool_release_device(ctx->device);
+}
 }  // namespace ks
+
+extern "C" ks_status ks_set_host_cache(int32_t keep) {
+  ks::g_host_cache = keep ? 1 : 0;
+  return KS_OK;
+}
 
 extern "C" ks_status ks_ctx_set_stream(ks_ctx *c, void *stream) {
   if (!c) return fail(KS_ERR_ARG, "null ctx");
@@ -452,6 +482,7 @@ extern "C" ks_status ks_tr_lr_regions(ks_ctx *ctx, const char *const *seqs, cons
   }
   KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
+  const HostEnd host_end{ctx};  // (ks_set_host_cache)
   Staged st;
   KS_TRY(stage(ctx, seqs, lens, nseq, &st));
   ks_table *t_tr = nullptr, *t_ks = nullptr;
@@ -481,6 +512,7 @@ extern "C" ks_status ks_kmer_counts(ks_ctx *ctx, const char *const *seqs, const 
   if (use_broker()) return broker_kmer_counts(seqs, lens, nseq, k, counts, n_words);
   KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
+  const HostEnd host_end{ctx};  // (ks_set_host_cache)
   Staged st;
   KS_TRY(stage(ctx, seqs, lens, nseq, &st));
   const size_t nb = (size_t)4 << (2 * k);
@@ -491,6 +523,49 @@ extern "C" ks_status ks_kmer_counts(ks_ctx *ctx, const char *const *seqs, const 
   KS_TRY(launch_count(ctx, &st.dev, st.total, none, k, (int32_t *)d_counts, n_words));
   KS_HIP(hipMemcpyAsync(counts, d_counts, nb, hipMemcpyDeviceToHost, ctx->stream));
   KS_HIP(hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+// Stages the host sequences (compact forms, ks_stage.cpp) and counts their
+// k-mers into d_cnt (zeroed here; sequence_kmer_count, kmer_spans.c:135-155).
+// Where the partitioned count takes position ranges, each ~eighth of the
+// staged bases is counted on the side stream while the rest crosses PCIe;
+// otherwise the count follows the staging.  On return ctx->stream is ordered
+// after the count; *words (nullable) = the words counted.
+static ks_status stage_counted(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq, int k,
+                               int32_t *d_cnt, Staged *st, double *words) {
+  const size_t nb = (size_t)4 << (2 * k);
+  int64_t total_in = 0;
+  for (int32_t q = 0; q < nseq; ++q) total_in += std::max<int64_t>(lens[q], 0);
+  KS_HIP(hipMemsetAsync(d_cnt, 0, nb, ctx->stream));
+  const bool piecewise = count_range_ok(k, total_in) && !getenv("KS_HOST_COUNT_AFTER");
+  const int64_t align = std::max<int64_t>(count_range_align(), stage_chunk_bases());
+  const int64_t piece = std::max<int64_t>(align, (total_in / 8 + align - 1) / align * align);
+  int64_t counted = 0;
+  struct Ev {
+    hipEvent_t e = nullptr;
+    ~Ev() {
+      if (e) (void)hipEventDestroy(e);
+    }
+  } ev;
+  if (piecewise) KS_HIP(hipEventCreateWithFlags(&ev.e, hipEventDisableTiming));
+  auto on_bytes = [&](int64_t p1) -> ks_status {
+    if (p1 < total_in && p1 - counted < piece) return KS_OK;
+    KS_TRY(launch_count_range(ctx, ctx->side, &st->dev, counted, p1, k, d_cnt));
+    counted = p1;
+    return KS_OK;
+  };
+  KS_TRY(stage(ctx, seqs, lens, nseq, st, true, piecewise ? std::function<ks_status(int64_t)>(on_bytes) : nullptr));
+  if (piecewise) {  // the main stream waits for the last piece's count
+    KS_HIP(hipEventRecord(ev.e, ctx->side));
+    KS_HIP(hipStreamWaitEvent(ctx->stream, ev.e, 0));
+    if (words) KS_TRY(count_words(ctx, ctx->stream, d_cnt, k, words));
+    return KS_OK;
+  }
+  double w = 0;
+  Runs none;
+  KS_TRY(launch_count(ctx, &st->dev, st->total, none, k, d_cnt, &w));
+  if (words) *words = w;
   return KS_OK;
 }
 
@@ -512,6 +587,7 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
   if (use_broker()) return broker_kmer_regions(seqs, lens, nseq, k, w, w_len, min_width, min_score, visits, n_bases, out);
   KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
+  const HostEnd host_end{ctx};  // (ks_set_host_cache)
   double n = 0;
   for (int32_t q = 0; q < nseq; ++q)
     if (lens[q] >= k) n += (double)lens[q];                   // :535
@@ -538,43 +614,13 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
   // the top-level visits: sequence_kmer_count's histogram (the partitioned
   // count), also the table's position-frequency hint (the binade predictor
   // of the scan's pass-1 summaries is built from it: without it a
-  // metric-size scan spends ~27 ms more on summary fixes).  Where the
-  // partitioned count takes position ranges, each ~eighth of the staged
-  // bases is counted on the side stream while the rest crosses PCIe.
+  // metric-size scan spends ~27 ms more on summary fixes)
   const size_t nb = (size_t)4 << (2 * k);
-  int64_t total_in = 0;
-  for (int32_t q = 0; q < nseq; ++q) total_in += std::max<int64_t>(lens[q], 0);
   void *d_cnt = nullptr;
-  ks_status rc = ensure(ctx, SLOT_COUNTS, nb, &d_cnt);
-  if (rc == KS_OK && hipMemsetAsync(d_cnt, 0, nb, ctx->stream) != hipSuccess)
-    rc = fail(KS_ERR_DEVICE, "hipMemsetAsync failed");
-  const bool piecewise = count_range_ok(k, total_in) && !getenv("KS_HOST_COUNT_AFTER");
-  const int64_t align = std::max<int64_t>(count_range_align(), stage_chunk_bases());
-  const int64_t piece = std::max<int64_t>(align, (total_in / 8 + align - 1) / align * align);
-  int64_t counted = 0;
-  struct Ev {
-    hipEvent_t e = nullptr;
-    ~Ev() {
-      if (e) (void)hipEventDestroy(e);
-    }
-  } ev;
-  if (rc == KS_OK && piecewise && hipEventCreateWithFlags(&ev.e, hipEventDisableTiming) != hipSuccess)
-    rc = fail(KS_ERR_DEVICE, "hipEventCreate failed");
-  hipEvent_t ev_piece = ev.e;
   Staged st;
-  auto on_bytes = [&](int64_t p1) -> ks_status {
-    if (p1 < total_in && p1 - counted < piece) return KS_OK;
-    KS_TRY(launch_count_range(ctx, ctx->side, &st.dev, counted, p1, k, static_cast<int32_t *>(d_cnt)));
-    counted = p1;
-    return KS_OK;
-  };
-  if (rc == KS_OK)
-    rc = stage(ctx, seqs, lens, nseq, &st, true, piecewise ? std::function<ks_status(int64_t)>(on_bytes) : nullptr);
+  ks_status rc = ensure(ctx, SLOT_COUNTS, nb, &d_cnt);
+  if (rc == KS_OK) rc = stage_counted(ctx, seqs, lens, nseq, k, static_cast<int32_t *>(d_cnt), &st, nullptr);
   t_stage = now_ms();
-  if (rc == KS_OK && piecewise) {  // the main stream waits for the last piece's count
-    if (hipEventRecord(ev_piece, ctx->side) != hipSuccess || hipStreamWaitEvent(ctx->stream, ev_piece, 0) != hipSuccess)
-      rc = fail(KS_ERR_DEVICE, "count join failed");
-  }
   if (th.joinable()) th.join();
   if (rc == KS_OK && rc_t != KS_OK) {
     set_error("%s", err_t.c_str());
@@ -585,10 +631,6 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
     return rc;
   }
   const double t1 = now_ms();
-  double words = 0;
-  Runs none;
-  if (rc == KS_OK && !piecewise)
-    rc = launch_count(ctx, &st.dev, st.total, none, k, static_cast<int32_t *>(d_cnt), &words);
   const double t2 = now_ms();
   if (rc == KS_OK) {
     t->ctx = ctx;
@@ -626,31 +668,59 @@ extern "C" ks_status ks_low_comp_regions(ks_ctx *ctx, const char *const *seqs, c
   if (use_broker()) return broker_low_comp(seqs, lens, nseq, k, min_width, min_score, thr, counts, ranks, n, out);
   KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
-  Staged st;
-  KS_TRY(stage(ctx, seqs, lens, nseq, &st));
-  const size_t nb = (size_t)4 << (2 * k);
-  void *d_counts = nullptr;
+  const HostEnd host_end{ctx};  // (ks_set_host_cache)
+  // the pipeline of ks_kmer_regions: the bases cross PCIe as 2-bit codes +
+  // N runs and are counted in pieces meanwhile (:592-601); the weighted
+  // ranks are built on the device (rank_kmers_w :602, closed-form exact
+  // prefix) straight into the scan's FP64 line table; the counts and ranks
+  // (768 MiB at k = 13) return over PCIe from a second host thread, through
+  // the sub-context's pinned buffer, while the scan runs
+  static const bool dbg = getenv("KS_DEBUG_HOST") != nullptr;
+  const double t0 = now_ms();
+  const size_t nb = (size_t)4 << (2 * k), rb = (size_t)8 << (2 * k);
+  void *d_counts = nullptr, *d_rk = nullptr;
   KS_TRY(ensure(ctx, SLOT_COUNTS, nb, &d_counts));
-  KS_HIP(hipMemsetAsync(d_counts, 0, nb, ctx->stream));
+  KS_TRY(ensure(ctx, SLOT_RANKS, rb, &d_rk));
+  double *d_ranks = static_cast<double *>(d_rk);
+  ks_ctx *sub = nullptr;
+  KS_TRY(ctx_sub(ctx, &sub));
+  Staged st;
   double words = 0;
-  Runs none;
-  KS_TRY(launch_count(ctx, &st.dev, st.total, none, k, (int32_t *)d_counts, &words));  // :592-601
+  KS_TRY(stage_counted(ctx, seqs, lens, nseq, k, static_cast<int32_t *>(d_counts), &st, &words));
   n[0] = words;
-  // weighted ranks on the device (rank_kmers_w :602, closed-form exact prefix),
-  // straight into the expanded FP64 table of the scan
-  double *d_ranks = nullptr;
-  if (hipMalloc(&d_ranks, (size_t)8 << (2 * k)) != hipSuccess)
-    return fail(KS_ERR_NOMEM, "hipMalloc of the rank table (k = %d) failed", k);
+  const double t1 = now_ms();
   ks_table *t = nullptr;
   ks_status rc = ks_table_from_counts(ctx, (const int32_t *)d_counts, k, KS_SCORE_RANK, words, thr, KS_TABLE_EXPAND,
                                       host_ext_cap(st.total), d_ranks, &t);
-  if (rc == KS_OK && (hipMemcpyAsync(counts, d_counts, nb, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
-                      hipMemcpyAsync(ranks, d_ranks, (size_t)8 << (2 * k), hipMemcpyDeviceToHost, ctx->stream) !=
-                          hipSuccess))
-    rc = fail(KS_ERR_DEVICE, "count / rank copy failed");
+  const double t2 = now_ms();
+  // the outputs' D2H on the sub-context (ordered after the table build)
+  ks_status rc_o = KS_OK;
+  std::string err_o;
+  double t_out = 0;
+  std::thread th;
+  if (rc == KS_OK) {
+    KS_HIP(hipEventRecord(ctx->ev[23], ctx->stream));
+    th = std::thread([&] {
+      rc_o = activate(sub);
+      if (rc_o == KS_OK && hipStreamWaitEvent(sub->stream, ctx->ev[23], 0) != hipSuccess)
+        rc_o = fail(KS_ERR_DEVICE, "output copy ordering failed");
+      if (rc_o == KS_OK) rc_o = copy_out(sub, counts, d_counts, nb);
+      if (rc_o == KS_OK) rc_o = copy_out(sub, ranks, d_ranks, rb);
+      if (rc_o != KS_OK) err_o = ks_last_error();  // (thread-local)
+      t_out = now_ms();
+    });
+  }
   if (rc == KS_OK) rc = scan_impl(ctx, &st.dev, st.total, k, t, min_width, min_score, nullptr, out, nullptr);
+  const double t3 = now_ms();
+  if (th.joinable()) th.join();
+  if (rc == KS_OK && rc_o != KS_OK) {
+    set_error("%s", err_o.c_str());
+    rc = rc_o;
+  }
+  if (dbg)
+    fprintf(stderr, "[host low_comp] stage+count %.2f rank table %.2f scan %.2f outputs D2H %.2f (from table end) ms\n",
+            t1 - t0, t2 - t1, t3 - t2, t_out - t2);
   ks_table_destroy(t);
-  (void)hipFree(d_ranks);
   n[1] = 0;                                                   // Q8 (:613)
   if (rc != KS_OK) ks_regions_free(out);
   return rc;
@@ -705,6 +775,7 @@ extern "C" ks_status ks_windowed_dist(ks_ctx *ctx, const char *const *seqs, cons
     return broker_windowed(seqs, lens, nseq, kmers, kmer_n, k, window, ret_flag, dist, seq_included, scores);
   KS_TRY(default_ctx(&ctx));
   KS_TRY(activate(ctx));
+  const HostEnd host_end{ctx};  // (ks_set_host_cache)
   Staged st;
   KS_TRY(stage(ctx, seqs, lens, nseq, &st));
   const size_t dn = (size_t)(window + 1) * (size_t)kmer_n;

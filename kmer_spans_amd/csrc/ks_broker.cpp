@@ -9,29 +9,44 @@
 // itself.  A later fork child (an mclapply worker) sends the host-buffer calls
 // the .Call shim makes (kmer_counts, kmer_regions, kmer_low_comp_regions,
 // tr_lr_regions, windowed distributions, kmers_to_file) over a Unix socket to
-// the broker, which runs them on its own HIP context, one request at a time,
-// and sends the outputs back.  Argument validation stays in the caller, so
-// errors read the same either way.  The broker ends with the process that
-// forked it (PR_SET_PDEATHSIG).
+// the broker, which runs them and sends the outputs back.  Argument
+// validation stays in the caller, so errors read the same either way.
+//
+// The broker serves up to KS_BROKER_THREADS (default 4) requests at once,
+// each server thread on its own HIP context (its own streams and workspace,
+// the device shared): test.R:554 runs 20 mclapply workers, whose calls would
+// otherwise queue behind each other.  A connection is served by one thread at
+// a time (its requests stay in order).
+//
+// Only the owner's own processes may use it: a connecting peer must have the
+// broker's uid (SO_PEERCRED) and descend from the process that forked the
+// broker; request lengths are capped per operation.  The broker ends when its
+// parent is gone (getppid() polled every second: PR_SET_PDEATHSIG would fire
+// when the forking *thread* ends, which may be a short-lived one).
 //
 // Wire format: request = u32 magic, u32 op, u64 payload bytes, payload;
 // reply = u64 payload bytes, payload = i32 status, u32 message length,
 // message, outputs.  Payloads are the arguments / outputs in call order,
 // arrays as raw bytes (both ends are the same build on the same host).
+#include <algorithm>
 #include <cerrno>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <dirent.h>
+#include <fcntl.h>
+#include <limits.h>
 #include <poll.h>
 #include <signal.h>
-#include <sys/prctl.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
@@ -45,6 +60,7 @@ constexpr uint32_t kMagic = 0x6b73626bu;  // "kbsk"
 enum Op : uint32_t { OP_COUNTS = 1, OP_REGIONS, OP_LOWCOMP, OP_TRLR, OP_WINDOWED, OP_TOFILE };
 
 std::mutex g_mu;
+std::mutex g_call_mu;     // a worker's connection carries one request at a time
 int g_on = -1;            // -1: KS_FORK_BROKER decides at the first HIP use
 bool g_started = false;   // this process forked its broker
 bool g_is_broker = false;
@@ -216,8 +232,14 @@ ks_status get_regions(Rd &r, ks_regions *out) {
   return KS_OK;
 }
 
-// Runs one request in the broker; returns the reply payload.
-Buf serve(uint32_t op, Rd &r) {
+// Largest request payload of an operation: the sequences and tables of a call
+// (a genome, a 4^15 FP64 table) fit; a file request holds two paths.
+uint64_t max_request(uint32_t op) {
+  return op == OP_TOFILE ? ((uint64_t)1 << 20) : ((uint64_t)1 << 37);
+}
+
+// Runs one request in the broker on ctx; returns the reply payload.
+Buf serve(ks_ctx *ctx, uint32_t op, Rd &r) {
   Buf o;
   ks_status st = KS_OK;
   Buf out;
@@ -232,7 +254,7 @@ Buf serve(uint32_t op, Rd &r) {
       }
       std::vector<int32_t> counts((size_t)1 << (2 * k));
       double w = 0;
-      st = ks_kmer_counts(nullptr, s.ptr.data(), s.lens.data(), s.n, k, counts.data(), &w);
+      st = ks_kmer_counts(ctx, s.ptr.data(), s.lens.data(), s.n, k, counts.data(), &w);
       if (st == KS_OK) {
         out.raw(counts.data(), counts.size() * 4);
         out.put(w);
@@ -260,7 +282,7 @@ Buf serve(uint32_t op, Rd &r) {
       double nb = 0;
       ks_regions g;
       memset(&g, 0, sizeof(g));
-      st = ks_kmer_regions(nullptr, s.ptr.data(), s.lens.data(), s.n, k, w.data(), wl, mw, ms,
+      st = ks_kmer_regions(ctx, s.ptr.data(), s.lens.data(), s.n, k, w.data(), wl, mw, ms,
                            want_vis ? vis.data() : nullptr, &nb, &g);
       if (st == KS_OK) {
         out.put(nb);
@@ -284,7 +306,7 @@ Buf serve(uint32_t op, Rd &r) {
       double n[2] = {0, 0};
       ks_regions g;
       memset(&g, 0, sizeof(g));
-      st = ks_low_comp_regions(nullptr, s.ptr.data(), s.lens.data(), s.n, k, mw, ms, thr, counts.data(), ranks.data(),
+      st = ks_low_comp_regions(ctx, s.ptr.data(), s.lens.data(), s.n, k, mw, ms, thr, counts.data(), ranks.data(),
                                n, &g);
       if (st == KS_OK) {
         out.raw(counts.data(), nk * 4);
@@ -318,7 +340,7 @@ Buf serve(uint32_t op, Rd &r) {
       std::vector<double> sp(want_sp ? (size_t)ns * 2 : 0);
       ks_regions g;
       memset(&g, 0, sizeof(g));
-      st = ks_tr_lr_regions(nullptr, s.ptr.data(), s.lens.data(), s.n, k, ml, kp.data(), ksc.data(), tsc.data(), ns,
+      st = ks_tr_lr_regions(ctx, s.ptr.data(), s.lens.data(), s.n, k, ml, kp.data(), ksc.data(), tsc.data(), ns,
                             want_sp ? sp.data() : nullptr, &g);
       if (st == KS_OK) {
         out.raw(sp.data(), sp.size() * 8);
@@ -354,7 +376,7 @@ Buf serve(uint32_t op, Rd &r) {
           sc[q].resize((size_t)s.lens[q] * (size_t)kn);
           scp[q] = sc[q].data();
         }
-      st = ks_windowed_dist(nullptr, s.ptr.data(), s.lens.data(), s.n, kp.data(), kn, k, win, flag, dist.data(),
+      st = ks_windowed_dist(ctx, s.ptr.data(), s.lens.data(), s.n, kp.data(), kn, k, win, flag, dist.data(),
                             inc.data(), have_sc ? scp.data() : nullptr);
       if (st == KS_OK) {
         out.raw(dist.data(), dist.size() * 4);
@@ -379,7 +401,7 @@ Buf serve(uint32_t op, Rd &r) {
         break;
       }
       ks_kmer_file_info info;
-      st = ks_kmers_to_file(nullptr, path.c_str(), prefix.c_str(), ks.data(), nk, ml, magic, &info);
+      st = ks_kmers_to_file(ctx, path.c_str(), prefix.c_str(), ks.data(), nk, ml, magic, &info);
       if (st == KS_OK) out.raw(&info, sizeof(info));
       break;
     }
@@ -390,6 +412,38 @@ Buf serve(uint32_t op, Rd &r) {
   o.str(st == KS_OK ? "" : ks_last_error());
   if (st == KS_OK) o.raw(out.b.data(), out.b.size());
   return o;
+}
+
+// The parent of pid from /proc (0 if unknown).
+pid_t parent_of(pid_t pid) {
+  char path[64], buf[512];
+  snprintf(path, sizeof(path), "/proc/%d/stat", (int)pid);
+  FILE *f = fopen(path, "r");
+  if (!f) return 0;
+  const size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  const char *p = strrchr(buf, ')');  // comm may hold spaces and parentheses
+  int ppid = 0;
+  char state = 0;
+  if (!p || sscanf(p + 1, " %c %d", &state, &ppid) != 2) return 0;
+  return (pid_t)ppid;
+}
+
+// A connecting peer is served only if it runs as this user and descends from
+// the process that forked the broker (its fork children, e.g. mclapply
+// workers, at any depth).
+bool peer_allowed(int fd, pid_t owner) {
+  ucred cr;
+  socklen_t cl = sizeof(cr);
+  if (getsockopt(fd, SOL_SOCKET, SO_PEERCRED, &cr, &cl) != 0 || cl != sizeof(cr)) return false;
+  if (cr.uid != getuid()) return false;
+  pid_t p = cr.pid;
+  for (int depth = 0; depth < 64 && p > 1; ++depth) {
+    p = parent_of(p);
+    if (p == owner) return true;
+  }
+  return false;
 }
 
 [[noreturn]] void broker_main(int lfd, pid_t owner) {
@@ -404,38 +458,91 @@ Buf serve(uint32_t op, Rd &r) {
     closedir(d);
     for (int fd : fds) close(fd);
   }
-  std::vector<pollfd> pf{{lfd, POLLIN, 0}};
+  int wake[2];  // server threads hand a served connection back to the poll loop
+  if (pipe2(wake, O_CLOEXEC) != 0) _exit(1);
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<int> ready;  // connections with a request waiting, for the server threads
+  int nthreads = 4;
+  if (const char *e = getenv("KS_BROKER_THREADS")) nthreads = std::max(1, std::min(64, atoi(e)));
+  std::mutex ctx_mu;  // (context creation: the process's first HIP use)
+  for (int t = 0; t < nthreads; ++t) {
+    std::thread([&, t] {
+      ks_ctx *ctx = nullptr;
+      for (;;) {
+        int fd;
+        {
+          std::unique_lock<std::mutex> g(mu);
+          cv.wait(g, [&] { return !ready.empty(); });
+          fd = ready.front();
+          ready.pop_front();
+        }
+        uint32_t hdr[2];
+        uint64_t len = 0;
+        bool ok = read_all(fd, hdr, 8) && read_all(fd, &len, 8) && hdr[0] == kMagic && len <= max_request(hdr[1]);
+        std::vector<char> pay;
+        if (ok) {
+          try {
+            pay.resize(len);
+          } catch (const std::bad_alloc &) {
+            ok = false;
+          }
+        }
+        if (ok) ok = read_all(fd, pay.data(), len);
+        if (ok) {
+          if (!ctx) {
+            std::lock_guard<std::mutex> g(ctx_mu);
+            if (ks_ctx_create(0, &ctx) != KS_OK) ctx = nullptr;
+          }
+          Rd r{pay.data(), pay.data() + pay.size()};
+          Buf o;
+          if (ctx) {
+            o = serve(ctx, hdr[1], r);
+          } else {
+            o.put((int32_t)KS_ERR_DEVICE);
+            o.str(ks_last_error());
+          }
+          const uint64_t ol = o.b.size();
+          ok = write_all(fd, &ol, 8) && write_all(fd, o.b.data(), o.b.size());
+        }
+        const int msg[2] = {fd, ok ? 1 : 0};  // back to the poll loop (or dropped: a worker ended / sent garbage)
+        if (write(wake[1], msg, sizeof(msg)) != (ssize_t)sizeof(msg)) _exit(1);
+      }
+      (void)t;
+    }).detach();
+  }
+  std::vector<pollfd> pf{{lfd, POLLIN, 0}, {wake[0], POLLIN, 0}};
   for (;;) {
-    if (getppid() != owner) _exit(0);  // (PR_SET_PDEATHSIG, and the race before it)
+    if (getppid() != owner) _exit(0);  // the owner is gone
     for (auto &p : pf) p.revents = 0;
     const int n = poll(pf.data(), pf.size(), 1000);
     if (n < 0 && errno != EINTR) _exit(1);
     if (n <= 0) continue;
-    for (size_t i = pf.size(); i-- > 1;) {
-      if (!pf[i].revents) continue;
-      const int fd = pf[i].fd;
-      uint32_t hdr[2];
-      uint64_t len = 0;
-      bool ok = read_all(fd, hdr, 8) && read_all(fd, &len, 8) && hdr[0] == kMagic && len < ((uint64_t)1 << 40);
-      std::vector<char> pay;
-      if (ok) {
-        pay.resize(len);
-        ok = read_all(fd, pay.data(), len);
-      }
-      if (ok) {
-        Rd r{pay.data(), pay.data() + pay.size()};
-        Buf o = serve(hdr[1], r);
-        const uint64_t ol = o.b.size();
-        ok = write_all(fd, &ol, 8) && write_all(fd, o.b.data(), o.b.size());
-      }
-      if (!ok) {  // a worker ended (or sent garbage): drop its connection
-        close(fd);
-        pf.erase(pf.begin() + (long)i);
+    std::vector<pollfd> back;
+    if (pf[1].revents & POLLIN) {  // served connections: listen to them again, or close them
+      int msg[2];
+      if (read(wake[0], msg, sizeof(msg)) == (ssize_t)sizeof(msg)) {
+        if (msg[1]) back.push_back({msg[0], POLLIN, 0});
+        else close(msg[0]);
       }
     }
+    for (size_t i = pf.size(); i-- > 2;) {
+      if (!pf[i].revents) continue;
+      const int fd = pf[i].fd;
+      pf.erase(pf.begin() + (long)i);  // (a server thread owns it until it comes back)
+      {
+        std::lock_guard<std::mutex> g(mu);
+        ready.push_back(fd);
+      }
+      cv.notify_one();
+    }
+    for (const pollfd &p : back) pf.push_back(p);
     if (pf[0].revents & POLLIN) {
       const int c = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
-      if (c >= 0) pf.push_back({c, POLLIN, 0});
+      if (c >= 0) {
+        if (peer_allowed(c, owner)) pf.push_back({c, POLLIN, 0});
+        else close(c);
+      }
     }
   }
 }
@@ -468,6 +575,7 @@ ks_status connect_broker(int *out) {
 // already taken: a failure in the broker comes back as that status with the
 // broker's message).
 ks_status call(uint32_t op, const Buf &req, std::vector<char> *rep, Rd *r) {
+  std::lock_guard<std::mutex> g(g_call_mu);  // threads of one worker share its connection
   int fd = -1;
   KS_TRY(connect_broker(&fd));
   const uint32_t hdr[2] = {kMagic, op};
@@ -523,7 +631,6 @@ void broker_before_hip() {
     new (&g_mu) std::mutex();
     broker_reset_locks();
     g_is_broker = true;
-    prctl(PR_SET_PDEATHSIG, SIGKILL);
     broker_main(lfd, owner);
   }
   close(lfd);
@@ -633,9 +740,20 @@ ks_status broker_windowed(const char *const *seqs, const int64_t *lens, int32_t 
 
 ks_status broker_kmers_to_file(const char *seq_path, const char *out_prefix, const int32_t *ks, int32_t nk,
                                double min_l, int32_t magic, ks_kmer_file_info *info) {
+  // relative paths are the worker's: the broker's working directory is the
+  // one the owner had when it first used HIP
+  auto absolute = [](const char *p) {
+    std::string a = p ? p : "";
+    if (!a.empty() && a[0] != '/') {
+      char cwd[PATH_MAX];
+      if (getcwd(cwd, sizeof(cwd))) a = std::string(cwd) + "/" + a;
+    }
+    return a;
+  };
+  const std::string sp = absolute(seq_path), op = absolute(out_prefix);
   Buf q;
-  q.str(seq_path);
-  q.str(out_prefix);
+  q.str(sp.c_str());
+  q.str(op.c_str());
   q.put(nk);
   q.raw(ks, (size_t)nk * 4);
   q.put(min_l);

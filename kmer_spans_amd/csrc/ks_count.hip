@@ -1114,6 +1114,37 @@ bool count_range_ok(int k, int64_t total) {
 
 int64_t count_range_align() { return kPTile; }
 
+namespace {
+// Sum of a histogram's counts read as uint32 (wave sums, one atomic per wave).
+__global__ void __launch_bounds__(256) k_sum_u32(const uint32_t *__restrict__ c, int64_t n,
+                                                 unsigned long long *__restrict__ out) {
+  unsigned long long s = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) s += c[i];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_down(s, d, 64);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, s);
+}
+}  // namespace
+
+// The words counted into a histogram (sequence_kmer_count's return, summed as
+// the callers do, kmer_spans.c:592-601) from the histogram itself: exact when
+// no count can reach 2^32, i.e. for any total < 2^32 (count_range_ok).
+ks_status count_words(ks_ctx *ctx, hipStream_t st, const int32_t *counts_dev, int k, double *n_words) {
+  void *scal = nullptr;
+  KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
+  unsigned long long *d = reinterpret_cast<unsigned long long *>(scal) + 40;
+  KS_HIP(hipMemsetAsync(d, 0, 8, st));
+  const int64_t n = (int64_t)1 << (2 * k);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, (int64_t)ctx->num_cus * 8));
+  hipLaunchKernelGGL(k_sum_u32, dim3(grid), dim3(256), 0, st, reinterpret_cast<const uint32_t *>(counts_dev), n, d);
+  KS_HIP(hipGetLastError());
+  unsigned long long w = 0;
+  KS_HIP(hipMemcpyAsync(&w, d, 8, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipStreamSynchronize(st));
+  *n_words = (double)w;
+  return KS_OK;
+}
+
 ks_status launch_count_range(ks_ctx *ctx, hipStream_t st, const ks_dev_seqs *s, int64_t p_lo, int64_t p_hi, int k,
                              int32_t *counts_dev) {
   if (p_lo % kPTile != 0 || p_hi <= p_lo) return fail(KS_ERR_ARG, "launch_count_range: bad range");

@@ -64,6 +64,7 @@ enum Slot : int {
   SLOT_LAYOUT,      // run layout (chunk / tile bases)
   SLOT_PACKED,      // 2-bit base codes of the whole buffer (find_runs, want_packed)
   SLOT_STAGE_NIB,   // host entry staging: 4-bit base classes as sent over PCIe
+  SLOT_RANKS,       // host low-comp entry: the weighted-rank vector (FP64 [4^k]) on its way out
   SLOT_COUNT
 };
 
@@ -182,6 +183,10 @@ ks_status h2d_pinned(ks_ctx *ctx, void *dst_dev, const void *src, size_t n, int 
 ks_status activate(ks_ctx *ctx);  // fork check + hipSetDevice
 ks_status ctx_sub(ks_ctx *ctx, ks_ctx **sub);  // ctx->sub, created on first use
 void pool_release_device(int dev);             // free the device's pooled expanded-table buffer
+// End of a host-buffer entry point: unless ks_set_host_cache(1), the call's
+// device memory (ctx's and its sub-context's workspace, the pooled table
+// buffer) goes back to the driver.
+void host_call_end(ks_ctx *ctx);
 ks_status default_ctx(ks_ctx **ctx);  // *ctx or the process default context (fork-checked)
 bool hip_usable_here();  // false in a child forked after HIP was initialised
 // Region output block (ks_regions_free frees it): [seq_id | beg | end] int32,
@@ -280,6 +285,9 @@ bool count_range_ok(int k, int64_t total);
 int64_t count_range_align();
 ks_status launch_count_range(ks_ctx *ctx, hipStream_t st, const ks_dev_seqs *s, int64_t p_lo, int64_t p_hi, int k,
                              int32_t *counts_dev);
+// Words counted into a histogram (the sum of its counts as uint32: exact for
+// totals < 2^32, i.e. wherever count_range_ok); synchronises st.
+ks_status count_words(ks_ctx *ctx, hipStream_t st, const int32_t *counts_dev, int k, double *n_words);
 // Which span scan a call performs.  trlr = 0: kmer_regions (kmer_spans.c:
 // 243-307).  trlr = 1: find_kmer_tr_lr_regions (:329-395): the table holds the
 // transition scores, ks the first-k-mer scores, regions need

@@ -380,6 +380,10 @@ extern "C" ks_status ks_kmers_to_file(ks_ctx *ctx, const char *seq_path, const c
   memcpy(info->out_path, of.c_str(), of.size() + 1);
   if (use_broker()) return broker_kmers_to_file(seq_path, out_prefix, ks, nk, min_l, magic, info);
   KS_TRY(default_ctx(&ctx));
+  struct End {  // a host-buffer entry point: ks_set_host_cache policy
+    ks_ctx *c;
+    ~End() { host_call_end(c); }
+  } const host_end{ctx};
   // read.count() inside try(): any failure there is the NA result (:145-148)
   auto na = [&](const char *why) {
     info->written = 0;

@@ -219,7 +219,10 @@ ks_status stage(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32
     const size_t n = (size_t)(hi - lo);
     if (fmt == 2) {
       const size_t pay = two_bit_pay(n);
-      TwoBit tb{cb, reinterpret_cast<uint32_t *>(cb + pay), ((n + 1) / 2 - pay) / 8};
+      // N-run slots after the codes, inside the chunk's nibble-sized share
+      // (a short last chunk may have no room at all: it goes as nibbles)
+      const size_t room = (n + 1) / 2 > pay ? ((n + 1) / 2 - pay) / 8 : 0;
+      TwoBit tb{cb, reinterpret_cast<uint32_t *>(cb + pay), room};
       each([&](int64_t a, int64_t b, const char *src) {
         if (!tb.over) tb.span((uint32_t)(a - lo), src, (size_t)(b - a));
       });

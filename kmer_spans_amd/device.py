@@ -8,6 +8,7 @@ libkmerspans.so (ks_scan_dev / ks_count_dev / ks_table_create).
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -155,12 +156,12 @@ class DeviceTable:
     def pass1_kernel(self) -> str:
         """The pass-1 kernel the chunked scan runs on this table."""
         lk = self.line_kind
+        if self.k <= 7 and not os.environ.get("KS_NO_LDS_TABLE"):  # (scan_chunked: the table staged in LDS first)
+            return "k_pass1_lds"
         if lk == 3:
             return "k_pass1w"
         if lk:
             return "k_pass1l"
-        if self.k <= 7:
-            return "k_pass1_lds"
         if self.positions_per_read > 1:
             return "k_pass1p" if self.compressed else "k_pass1pf"
         return "k_pass1"

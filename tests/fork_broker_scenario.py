@@ -84,6 +84,55 @@ def in_child(fn):
     return json.loads(b"".join(chunks))
 
 
+def start_child(fn):
+    """fn() in a forked child started now; returns a function that waits for
+    it and returns its JSON result (several children run at once)."""
+    r, wfd = os.pipe()
+    pid = os.fork()
+    if pid == 0:
+        os.close(r)
+        code = 0
+        try:
+            try:
+                out = {"ok": fn()}
+            except KmerSpansError as e:
+                out = {"err": str(e)}
+            data = json.dumps(out).encode()
+            while data:
+                data = data[os.write(wfd, data):]
+        except BaseException:  # noqa: BLE001
+            code = 3
+        os._exit(code)
+    os.close(wfd)
+
+    def wait():
+        chunks = []
+        while True:
+            b = os.read(r, 1 << 20)
+            if not b:
+                break
+            chunks.append(b)
+        os.close(r)
+        _, st = os.waitpid(pid, 0)
+        assert os.WEXITSTATUS(st) == 0, st
+        return json.loads(b"".join(chunks))
+    return wait
+
+
+def file_work(tmp, seqs):
+    """kmers.to.file with RELATIVE paths after a chdir (the broker resolves
+    them in the worker's directory), read back."""
+    os.chdir(tmp)
+    with open("g.fa", "w") as f:
+        for i, s in enumerate(seqs):
+            f.write(f">s{i}\n{s}\n")
+    info = api.kmers_to_file("g.fa", "rel_", [3, 5], min_l=10)
+    rk = api.read_kmers(os.path.join(tmp, os.path.basename(info[1]))) if info[1] else False
+    return {"out": os.path.basename(info[1]) if info[1] else None, "in_tmp": bool(info[1]) and
+            os.path.exists(os.path.join(tmp, os.path.basename(info[1]))),
+            "counts": [c.tolist() for c in rk["counts"]] if rk is not False else None}
+
+
 def main(mode):
     res = {"mode": mode}
     seqs = [genome(i) for i in range(3)]
@@ -94,6 +143,19 @@ def main(mode):
         res["workers_ok"] = all("ok" in x for x in kids)
         res["workers_equal"] = res["workers_ok"] and all(x["ok"] == d for x, d in zip(kids, direct))
         res["regions"] = [len(d["reg_pos"][0]) for d in direct]
+        # mclapply(mc.cores = 20) shape: several workers at once (the broker
+        # serves them on its server threads)
+        waits = [start_child(lambda s=s: work(s)) for s in seqs * 2]
+        conc = [w() for w in waits]
+        res["concurrent_ok"] = all("ok" in x for x in conc)
+        res["concurrent_equal"] = res["concurrent_ok"] and all(x["ok"] == d for x, d in zip(conc, direct * 2))
+        import tempfile
+        with tempfile.TemporaryDirectory() as tmp:
+            fk = in_child(lambda: file_work(tmp, seqs[1]))
+            own = [api.kmer_counts(seqs[1], kk, with_f=False)["counts"].tolist() for kk in (3, 5)]
+            res["file_ok"] = "ok" in fk and fk["ok"]["in_tmp"] and fk["ok"]["counts"] == own
+            if not res["file_ok"]:
+                res["file_detail"] = fk.get("err") or {kk: v for kk, v in fk["ok"].items() if kk != "counts"}
     else:
         try:
             api.kmer_counts(seqs[0], 6)
@@ -104,6 +166,29 @@ def main(mode):
         res["worker_err"] = kid.get("err")
         bad = in_child(lambda: api.kmer_counts(seqs[1], 99)["n"])
         res["worker_arg_err"] = bad.get("err")
+        # a process outside the owner's tree (double fork: reparented away)
+        # is refused by the broker's peer check
+        import time
+        r, wfd = os.pipe()
+        pid = os.fork()
+        if pid == 0:
+            if os.fork() == 0:
+                os.close(r)
+                time.sleep(0.5)  # its parent has exited by now
+                try:
+                    api.kmer_counts(seqs[1], 6)
+                    msg = "ran"
+                except KmerSpansError as e:
+                    msg = str(e)
+                except BaseException as e:  # noqa: BLE001
+                    msg = "other: " + repr(e)
+                os.write(wfd, msg.encode())
+                os._exit(0)
+            os._exit(0)
+        os.waitpid(pid, 0)
+        os.close(wfd)
+        res["stranger_err"] = os.read(r, 4096).decode()
+        os.close(r)
     print(json.dumps(res), flush=True)
 
 

@@ -99,11 +99,16 @@ def test_fork_broker_mclapply_pattern():
     """test.R:351 then :554-565: the parent calls, forked workers call
     kmer_counts, kmer_regions (with visits), kmer_low_comp_regions,
     window_kmer_dist (with positions) and lr_regions through the broker; every
-    result equals the parent's own call on the same input."""
+    result equals the parent's own call on the same input; six workers at
+    once (the broker's server threads) give the same results; a worker's
+    kmers_to_file with relative paths after a chdir writes into ITS
+    directory."""
     r = _scenario("gpu")
     assert r["workers_ok"], r
     assert r["workers_equal"], r
     assert sum(r["regions"]) > 0
+    assert r["concurrent_ok"] and r["concurrent_equal"], r
+    assert r["file_ok"], r
 
 
 def test_fork_broker_plumbing_cpu():
@@ -117,3 +122,5 @@ def test_fork_broker_plumbing_cpu():
     assert r["worker_err"] and "fork" not in r["worker_err"], r
     assert r["worker_err"] == r["parent"], r
     assert "less than 1+MAX_K" in r["worker_arg_err"], r
+    # the broker serves only the owner's descendants (SO_PEERCRED + ancestry)
+    assert "went away" in r["stranger_err"] or "not reachable" in r["stranger_err"], r

@@ -175,6 +175,24 @@ def test_host_entry_compact_staging(K, oracle, monkeypatch, alpha, env):
     assert np.array_equal(g["counts"], o["counts"])
 
 
+@pytest.mark.parametrize("tail", [1, 17, 29, 31, 33, 61])
+def test_host_entry_short_last_chunk(K, oracle, tail):
+    """A last staging chunk of a few bases (total = 16 Mi + tail) that
+    alternates N and non-N: a 2-bit chunk shorter than its 16-B code payload
+    has no room for N runs and must go as 4-bit classes (no write past the
+    pinned / device staging buffers), against the oracle."""
+    rng = np.random.default_rng(tail)
+    head = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, size=(1 << 24) - 5)].tobytes().decode()
+    last = ("NA" * tail)[:tail + 5]  # the first sequence's last 5 bases + the tail chunk, alternating
+    seqs = [head, last]
+    k = 5
+    w = rng.normal(size=4 ** k) * 0.5 + 0.05
+    g = K.kmer_regions(seqs, k, w, 20, 3.0)
+    o = oracle.kmer_regions(seqs, k, w, 20, 3.0)
+    _assert_same_regions(g["pos"], g["score"], o["pos"], o["score"], ("short tail", tail))
+    assert np.array_equal(g["counts"], o["counts"])
+
+
 @pytest.mark.parametrize("piecewise,alpha", [(True, b"ACGTACGTACGTACGTacgN"), (False, b"ACGTACGTACGTACGTacgN"),
                                              (True, b"ACGT" * 300 + b"acgN")])
 def test_host_entry_counted_in_pieces(K, oracle, monkeypatch, piecewise, alpha):
@@ -605,3 +623,35 @@ def test_trlr_nonfinite_tables(K, oracle, ctx, nan):
     _assert_same_regions(pos, sc, pos_o, score_o, ("trlr-nonfinite", nan))
     assert st["scan_algo"] == (0 if nan else 1)
     ctx.set_scan_algo(-1)
+
+
+def test_host_entry_returns_vram(K, oracle):
+    """kmer_regions_r from host memory leaves VRAM where it found it (the
+    call's workspace and its table buffer go back to the driver at the end,
+    ks_set_host_cache(0), the default); with ks_set_host_cache(1) they stay
+    for the next call.  Results are the same either way."""
+    import torch
+    from kmer_spans_amd import _lib
+    rng = np.random.default_rng(8)
+    seqs = [np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, size=n)].tobytes().decode()
+            for n in (20_000_000, 3_000_001)]
+    k = 11
+    w = np.round(rng.normal(size=4 ** k) * 4) / 4 + 0.2
+    L = _lib.load()
+    first = K.kmer_regions(seqs, k, w, 40, 8.0)  # warm: contexts, pinned staging
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    again = K.kmer_regions(seqs, k, w, 40, 8.0)
+    free1 = torch.cuda.mem_get_info()[0]
+    assert free1 >= free0 - (16 << 20), (free0, free1)
+    try:
+        assert L.ks_set_host_cache(1) == 0
+        kept = K.kmer_regions(seqs, k, w, 40, 8.0)
+        free2 = torch.cuda.mem_get_info()[0]
+        assert free2 < free0 - (64 << 20), (free0, free2)  # the workspace stayed
+    finally:
+        L.ks_set_host_cache(0)
+    o = oracle.kmer_regions(seqs, k, w, 40, 8.0)
+    for r in (first, again, kept):
+        _assert_same_regions(r["pos"], r["score"], o["pos"], o["score"], "host cache policy")
+        assert np.array_equal(r["counts"], o["counts"])

@@ -257,6 +257,10 @@ extern "C" void ks_ctx_destroy(ks_ctx *c) {
     ks_ctx_destroy(c->sub);
     c->sub = nullptr;
   }
+  if (c->part) {
+    ks_ctx_destroy(c->part);
+    c->part = nullptr;
+  }
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (auto &b : c->slots)
@@ -281,6 +285,12 @@ ks_status ctx_sub(ks_ctx *ctx, ks_ctx **sub) {
   return KS_OK;
 }
 
+ks_status ctx_part(ks_ctx *ctx, ks_ctx **part) {
+  if (!ctx->part) KS_TRY(ks_ctx_create(ctx->device, &ctx->part));
+  *part = ctx->part;
+  return KS_OK;
+}
+
 static int g_host_cache = -1;  // -1: KS_HOST_CACHE decides on first use
 
 static void free_workspace(ks_ctx *c) {
@@ -298,6 +308,7 @@ void host_call_end(ks_ctx *ctx) {
   if (g_host_cache || !ctx || ctx->pid != getpid()) return;
   free_workspace(ctx);
   if (ctx->sub) free_workspace(ctx->sub);
+  if (ctx->part) free_workspace(ctx->part);
   pool_release_device(ctx->device);
 }
 }  // namespace ks

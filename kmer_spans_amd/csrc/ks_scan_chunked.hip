@@ -259,6 +259,7 @@ template <int NV>
 __device__ __forceinline__ void line_values_any(const TableView &tv, uint64_t x, int k, int b0, int n, double v[NV],
                                                 const double *s_lut) {
   switch (tv.line_own) {
+    case 1: line_values<1, NV>(tv, x, k, b0, n, v, s_lut); break;  // (wide lines at k = 15)
     case 2: line_values<2, NV>(tv, x, k, b0, n, v, s_lut); break;
     case 3: line_values<3, NV>(tv, x, k, b0, n, v, s_lut); break;
     case 4: line_values<4, NV>(tv, x, k, b0, n, v, s_lut); break;
@@ -3680,7 +3681,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // one part; serialising the two pass-1 launches, KS_F64_P1_SERIAL, 31.8-32.0
   // by split fraction: profiles/r3/rank/split_ab.txt)
   const bool f64_line = line && !comp;
-  const bool split = (p1summ || f64_line) && (p1summ || getenv("KS_NO_F64_SPLIT") == nullptr) &&
+  const bool split = !ctx->no_split && (p1summ || f64_line) && (p1summ || getenv("KS_NO_F64_SPLIT") == nullptr) &&
                      lay.split_r > 0 && lay.split_r < nruns && lay.split_c >= 1024 && lay.split_c + 1024 <= ctail_all;
   const bool p1_serial = f64_line && getenv("KS_F64_P1_SERIAL") != nullptr;
   Half halves[2];
@@ -3782,7 +3783,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       hipLaunchKernelGGL((k_pass1w<O, false>), dim3(grid), dim3(kWideBlock), 0, strm, gv, total, k, tv, ec, visits, \
                          p1, cand, d_xh, sp1);                                                              \
   } while (0)
-        if (own == 3) KS_P1W(3); else KS_P1W(4);
+        if (own == 1) KS_P1W(1);  // k = 15 (J = 4)
+        else if (own == 2) KS_P1W(2);  // k = 14 (J = 5)
+        else if (own == 3) KS_P1W(3);  // k = 13 (J = 6)
+        else KS_P1W(4);  // k = 12 (J = 7)
 #undef KS_P1W
         return;
       }
@@ -3908,6 +3912,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     KS_HIP(hipEventRecord(ctx->ev[9], ctx->hi));
   } else {
     KS_HIP(hipEventRecord(ctx->ev[9], split ? ctx->side : st));  // end of pass 1 (the last half's stream)
+  }
+  if (ctx->on_pass1) {  // a staggered scan's later part starts now (scan_impl)
+    auto go = std::move(ctx->on_pass1);
+    ctx->on_pass1 = nullptr;
+    go();
   }
 
   // P2-P5 (without the candidates) of one half on stream strm, with its own

@@ -88,8 +88,8 @@ __device__ __forceinline__ void line_entries(const TableView &t, uint64_t key, d
 // (compressed) holds 12-bit codes; 0xFFF escapes to the base table.
 template <int J, bool kCompressed, typename GC>
 __device__ __forceinline__ void gather_group(const TableView &t, GC gcode, uint32_t kmask, double v[J]) {
-  if (J >= 3 && t.line) {  // line table (the dispatch sets J = own + 1): gcode is the (k + own)-mer
-    line_entries<(J >= 3 ? J - 1 : 2)>(t, (uint64_t)gcode, v, nullptr);
+  if (J >= 2 && t.line) {  // line table (the dispatch sets J = own + 1): gcode is the (k + own)-mer
+    line_entries<(J >= 2 ? J - 1 : 1)>(t, (uint64_t)gcode, v, nullptr);
     return;
   }
   if (J == 1) {

@@ -631,17 +631,20 @@ static ks_status build_approx(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev)
   return KS_OK;
 }
 
-// Line table of k in [8, 13] (k <= 7 scans with its table in LDS): the
-// largest own count (m = k + own - 1 <= 15, own <= 5 / 4) whose 4^m x 64 B
-// fit the budget, own >= 2.  Sets *built.
+// Line table of k in [8, 15] (k <= 7 scans with its table in LDS): wide
+// 128-B lines where they apply (below), else the largest own count of 64-B
+// lines (m = k + own - 1 <= 15, own <= 5 / 4, k <= 13) whose 4^m x 64 B fit
+// the budget, own >= 2.  Sets *built.
 static ks_status table_lines(ks_ctx *ctx, ks_table *t, size_t budget, const int32_t *freq_dev, bool *built) {
   *built = false;
   const bool u16 = t->compressed;
-  if (t->k < 8 || t->k > 13 || getenv("KS_NO_LINES")) return KS_OK;
-  // wide 128-B lines (J = own + 3) where they beat the 64-B ones: k = 12, 13
-  // (m = 15), at most kWideLut distinct values (13-bit codes), and an L3
-  // escape share (positions whose value is not among the 2047 heaviest) of
-  // at most 10 %.  KS_NO_WIDE_LINES: the 64-B forms.
+  if (t->k < 8 || t->k > 15 || getenv("KS_NO_LINES")) return KS_OK;
+  // wide 128-B lines (J = own + 3) where they beat the 64-B ones: k = 12 to 15
+  // (m = 15: own = 16 - k, J = 6 at k = 13, 4 at k = 15 against 3 for the
+  // 17-mer expanded table), at most kWideLut distinct values (13-bit codes),
+  // and an L3 escape share (positions whose value is not among the 2047
+  // heaviest) of at most 10 %.  KS_NO_WIDE_LINES: the 64-B forms (k <= 13)
+  // or the expanded table.
   if (u16 && t->k >= 12 && t->distinct <= kWideLut && ((size_t)128 << 30) <= budget &&
       !getenv("KS_NO_WIDE_LINES")) {
     bool use = false;
@@ -667,7 +670,9 @@ static ks_status table_lines(ks_ctx *ctx, ks_table *t, size_t budget, const int3
         KS_HIP(hipEventCreate(&a));
         KS_HIP(hipEventCreate(&b));
         KS_HIP(hipEventRecord(a, st));
-        if (own == 3) launch_build_lines<3, 2>(st, t, 15, ext);
+        if (own == 1) launch_build_lines<1, 2>(st, t, 15, ext);
+        else if (own == 2) launch_build_lines<2, 2>(st, t, 15, ext);
+        else if (own == 3) launch_build_lines<3, 2>(st, t, 15, ext);
         else launch_build_lines<4, 2>(st, t, 15, ext);
         KS_HIP(hipGetLastError());
         KS_HIP(hipEventRecord(b, st));
@@ -689,6 +694,7 @@ static ks_status table_lines(ks_ctx *ctx, ks_table *t, size_t budget, const int3
       }
     }
   }
+  if (t->k > 13) return KS_OK;  // (64-B lines need own >= 2: m <= 15)
   int own = std::min(u16 ? 5 : 4, 16 - t->k);
   for (; own >= 2; --own)
     if (((size_t)64 << (2 * (t->k + own - 1))) <= budget) break;

@@ -53,42 +53,49 @@ def test_chr1_like_50mbp_k11_log2(oracle):
     tab.close()
 
 
-def _k15_table(ndist, seed):
-    """A 4^15-entry table with ndist distinct values, built on the GPU."""
+def _k15_table(ndist, seed, k=15):
+    """A 4^k-entry table with ndist distinct values, built on the GPU."""
     import torch
     g = torch.Generator(device="cuda")
     g.manual_seed(seed)
     vals = torch.randn(ndist, generator=g, device="cuda", dtype=torch.float64) * 0.5 - 0.05
-    idx = torch.randint(0, ndist, (4 ** 15,), generator=g, device="cuda")
+    idx = torch.randint(0, ndist, (4 ** k,), generator=g, device="cuda")
     w = vals[idx].cpu().numpy()
     del idx
     return w
 
 
-@pytest.mark.parametrize("compress", [True, False])
-def test_k15_scan(oracle, compress):
+@pytest.mark.parametrize("k,compress,ndist,J", [(15, True, 3000, 3), (15, True, 2000, 4), (14, True, 2000, 5),
+                                                (15, False, None, 2)])
+def test_k15_scan(oracle, k, compress, ndist, J):
+    """k = 15 / 14 tables in every form the builder picks: wide 128-B lines
+    indexed by the 15-mer (own 1 / 2 + 4 L1 + 16 L2 13-bit codes, 64 L3 11-bit
+    codes: J = 4 / 5) when at most 2047 values carry the positions; the
+    17-mer expanded table (J = 3) when the L3 codes would escape too often
+    (3000 uniform values); FP64 J = 2."""
     import torch
     from kmer_spans_amd import _lib, device as D, genome
     ctx = _lib.context(0)
     D.bind_torch_stream(ctx)
-    k = 15
     parts = [genome.contig(L, 151 + i, device="cuda", repeats=True) for i, L in enumerate((2_000_000, 700_000, 15))]
     ds = D.from_parts(parts, [p.numel() for p in parts], "cuda")
     host = [ds.host_seq(q) for q in range(ds.nseq)]
-    # compressed: 3000 distinct values (uint16 codes, J = 3: (k+2)-mer
-    # indices of 34 bits); uncompressed: every entry its own value (FP64)
+    # compressed: ndist distinct values (uint16 codes); uncompressed: every
+    # entry its own value (FP64)
     if compress:
-        w = _k15_table(3000, 15)
+        w = _k15_table(ndist, 15, k)
     else:
         import torch as T
         g = T.Generator(device="cuda")
         g.manual_seed(16)
-        w = (T.randn(4 ** 15, generator=g, device="cuda", dtype=T.float64) * 0.5 - 0.05).cpu().numpy()
+        w = (T.randn(4 ** k, generator=g, device="cuda", dtype=T.float64) * 0.5 - 0.05).cpu().numpy()
     thr = 0.0
     o = oracle.scan(host, k, w, thr, 30, 3.0, visits=True)
     tab = D.DeviceTable(ctx, w, k, thr, compress=compress, expand=True)
     assert tab.compressed == compress
-    assert tab.positions_per_read == (3 if compress else 2), tab.positions_per_read
+    assert tab.positions_per_read == J, tab.positions_per_read
+    if J >= 4:
+        assert tab.line_kind == 3 and tab.pass1_kernel == "k_pass1w"
     for algo in (0, 1):
         ctx.set_scan_algo(algo)
         vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")

@@ -85,6 +85,8 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--mode", choices=["shard", "genome", "genomes"], default="shard")
     p.add_argument("--genomes-per-rank", type=int, default=2, help="--mode genomes: genomes per rank")
+    p.add_argument("--genomes-serial", action="store_true",
+                   help="--mode genomes: no overlap of genome g+1's count and table with genome g's scan")
     p.add_argument("--scale", type=float, default=1.0, help="genome scale (1.0 = 3.09 Gbp)")
     p.add_argument("--k", type=int, default=13)
     p.add_argument("--score", choices=["log2", "pm1", "rank"], default="log2")
@@ -919,14 +921,62 @@ def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over
             init.close()
         return out
 
-    one(dss[0])  # warm-up (workspace, pinned staging)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    results = [one(ds) for ds in dss]
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
+    # pipelined (default, not with tr_lr): genome g + 1's count and score table
+    # on a second context and stream from a host thread while genome g is
+    # scanned -- independent work (the count is LDS-atomic bound, the table
+    # build write bound, the scan request bound)
+    pipelined = not args.trlr and not args.genomes_serial
+    if pipelined:
+        from kmer_spans_amd import _lib as L_
+        import threading
+        ctx2 = L_.context(torch.cuda.current_device())
+        s_b = torch.cuda.Stream()
+        ctx2.set_stream(s_b.cuda_stream)
+        counts2 = [torch.zeros(4 ** k, dtype=torch.int32, device=dev) for _ in range(2)]
+        cap = int((args.ext_max_gib if args.ext_max_gib else 32.0) * (1 << 30))
+        thr_g = 0.75 if args.score == "rank" else 0.0
+
+        def count_table(ds, cbuf):
+            with torch.cuda.stream(s_b):
+                cbuf.zero_()
+                words = D.count(ctx2, ds, k, cbuf)
+                return D.DeviceTable.from_counts(ctx2, cbuf, k, args.score, total=words, thr=thr_g,
+                                                 expand=not args.no_expand, max_ext_bytes=cap)
+
+        def run_all():
+            out = [None] * G
+            tab = count_table(dss[0], counts2[0])
+            for g in range(G):
+                nxt = {}
+                th = None
+                if g + 1 < G:
+                    th = threading.Thread(target=lambda g=g: nxt.setdefault("t", count_table(dss[g + 1],
+                                                                                             counts2[(g + 1) % 2])))
+                    th.start()
+                out[g] = D.scan(ctx, dss[g], k, tab, args.min_width, args.min_score)
+                tab.close()
+                if th is not None:
+                    th.join()
+                    tab = nxt["t"]
+            return out
+        run_all()  # warm-up (both contexts' workspace, pinned staging)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        results = run_all()
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = max_over_ranks(time.perf_counter() - t0)
+        del counts2
+    else:
+        one(dss[0])  # warm-up (workspace, pinned staging)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        results = [one(ds) for ds in dss]
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = max_over_ranks(time.perf_counter() - t0)
     bases = sum(int(r[2]["n_bases"]) for r in results) * world
     n_regions = sum(int(r[0].shape[1]) for r in results)
     # parity of every genome of this rank after timing (each genome's own

@@ -1006,15 +1006,10 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   unsigned long long *s1 = ex2 + m2;            // [nb1 + 1]
   unsigned long long *sf = s1 + nb1 + 1;        // [nbf + 1]
   unsigned long long *last = sf + nbf + 1;      // [2]: level ends; [2]: the k-mer total
-  // single level: the staged scatter (KS_SCATTER_STAGE: 0 = the counting-sort
-  // scatter; 16x1024 (default) / 16x512 = piece items x lanes.  32-item
+  // single level: the staged scatter, 16-item pieces x 1024 lanes (A/Bs in
+  // the counting-sort scatter below, 512-lane staging; 32-item
   // pieces do not fit the LDS next to the double-buffered bucket state)
-  int stS = 16, stT = kPT;
-  if (const char *e = getenv("KS_SCATTER_STAGE")) {
-    stS = atoi(e) == 0 ? 0 : 16;
-    const char *x = strchr(e, 'x');
-    if (x && atoi(x + 1) == kPT / 2) stT = kPT / 2;
-  }
+  const int stS = 16, stT = kPT;
   const int64_t n_items = total - p_lo;
   const bool staged = !g.T2 && stS > 0 && n_items + (int64_t)m1 * stS < ((int64_t)1 << 32);
   const int pad = staged ? stS : 1;
@@ -1049,23 +1044,17 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
     hipLaunchKernelGGL((k_part_scatter_st<S, T>), dim3(G), dim3(T), lds, st, s->seq, total, s->offsets_dev, s->nseq, \
                        k, shift, ex1, static_cast<uint16_t *>(p1), tile0, ntiles);                           \
   } while (0)
-    if (stT == kPT) KS_ST(16, kPT);
-    else KS_ST(16, kPT / 2);
+    static_assert(stT == kPT, "the staged scatter runs on 1024-lane blocks");
+    KS_ST(16, kPT);
 #undef KS_ST
   } else {
-    // single level (k <= 13): 512-lane blocks on 8K-position sub-tiles, half
-    // the LDS, two blocks per CU (KS_SCATTER_1024: the 1024-lane form)
-    const bool big = getenv("KS_SCATTER_1024") != nullptr;
-    const int kt = big ? kPT : kPT / 2;
-    const size_t lds = (size_t)kt * kPer * (2 + 2);
-    const void *fn = big ? (const void *)k_part_scatter<uint16_t, kPT> : (const void *)k_part_scatter<uint16_t, kPT / 2>;
-    KS_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    if (big)
-      hipLaunchKernelGGL((k_part_scatter<uint16_t, kPT>), dim3(G), dim3(kPT), lds, st, s->seq, total, s->offsets_dev,
-                         s->nseq, k, shift, ex1, static_cast<uint16_t *>(p1), tile0, ntiles);
-    else
-      hipLaunchKernelGGL((k_part_scatter<uint16_t, kPT / 2>), dim3(G), dim3(kPT / 2), lds, st, s->seq, total, s->offsets_dev, s->nseq,
-                       k, shift, ex1, static_cast<uint16_t *>(p1), tile0, ntiles);
+    // single level (k <= 13) past the staged scatter's index range: 512-lane
+    // blocks on 8K-position sub-tiles, half the LDS, two blocks per CU
+    const size_t lds = (size_t)(kPT / 2) * kPer * (2 + 2);
+    KS_HIP(hipFuncSetAttribute((const void *)k_part_scatter<uint16_t, kPT / 2>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((k_part_scatter<uint16_t, kPT / 2>), dim3(G), dim3(kPT / 2), lds, st, s->seq, total,
+                       s->offsets_dev, s->nseq, k, shift, ex1, static_cast<uint16_t *>(p1), tile0, ntiles);
   }
   KS_HIP(hipGetLastError());
   const uint16_t *bins = static_cast<const uint16_t *>(p1);
@@ -1109,7 +1098,7 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
 }
 
 bool count_range_ok(int k, int64_t total) {
-  return k >= kPartMinK && total > 0 && total < ((int64_t)1 << 32) && !getenv("KS_COUNT_ATOMIC");
+  return k >= kPartMinK && total > 0 && total < ((int64_t)1 << 32);
 }
 
 int64_t count_range_align() { return kPTile; }
@@ -1153,8 +1142,7 @@ ks_status launch_count_range(ks_ctx *ctx, hipStream_t st, const ks_dev_seqs *s, 
 
 ks_status launch_count(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const Runs &, int k,
                        int32_t *counts_dev, double *n_words) {
-  if (k >= kPartMinK && total > 0 && total < ((int64_t)1 << 32) && !getenv("KS_COUNT_ATOMIC"))
-    return count_partitioned(ctx, s, total, k, counts_dev, n_words);
+  if (count_range_ok(k, total)) return count_partitioned(ctx, s, total, k, counts_dev, n_words);
   hipStream_t st = ctx->stream;
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
@@ -1186,7 +1174,7 @@ ks_status launch_count_multi(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, c
                              int32_t *const *counts_dev, double *n_words) {
   // k's whose histograms are far beyond L2 take the partitioned counter
   // one by one; the rest share passes of k_count_multi.
-  const bool part_ok = total > 0 && total < ((int64_t)1 << 32) && !getenv("KS_COUNT_ATOMIC");
+  const bool part_ok = total > 0 && total < ((int64_t)1 << 32);
   std::vector<int32_t> rest_k;
   std::vector<int32_t *> rest_c;
   std::vector<int> rest_i;

@@ -1258,7 +1258,7 @@ __global__ void __launch_bounds__(kF64 ? 1024 : 768) k_pass1l(Chunks g, int64_t 
   constexpr int LV = kF64 ? 1 : 2;
   constexpr int J = OWN + LV;
   constexpr int NS = (CH + J - 1) / J;  // steps per chunk (the same for the whole wave)
-  constexpr bool kSumm = !kF64;
+  constexpr bool kSumm = true;  // (xh == nullptr: no predicted binades, no summaries)
   constexpr bool kLut = !kF64 && kLdsLut;
   static_assert(kF64 ? OWN + 4 <= 8 : OWN + 20 <= 32, "line layout");
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[(BS / 64) * 2 * 4096];
@@ -1276,7 +1276,7 @@ __global__ void __launch_bounds__(kF64 ? 1024 : 768) k_pass1l(Chunks g, int64_t 
   const bool first = live && (c == 0 || g.run[c - 1] != g.run[c]);
   const uint32_t kmask = (1u << (2 * k)) - 1u;
   P1Lane<kSumm, kTrlr> L;
-  L.init(start, n, first, live, (kSumm && live) ? xh[c] : 0.0);
+  L.init(start, n, first, live, (kSumm && live && xh) ? xh[c] : 0.0);
   LaneBases B;
   B.load(g.packed, total, start - k);
   const int kx = k + J - 1;  // key length (<= 17)
@@ -1537,18 +1537,48 @@ __global__ void __launch_bounds__(kWideBlock) k_pass1w(Chunks g, int64_t total, 
 constexpr int kLdsTableK = 7;
 template <bool kTrlr>
 __global__ void __launch_bounds__(1024) k_pass1_lds(Chunks g, int64_t total, int k, TableView tv, EmitCfg ec,
-                                                    uint32_t *__restrict__ visits, P1 o, Cand cand) {
+                                                    uint32_t *__restrict__ visits, P1 o, Cand cand,
+                                                    const double *__restrict__ xh, SummP1 sp) {
   __shared__ double s_val[1 << (2 * kLdsTableK)];
   const int nk = 1 << (2 * k);
   for (int i = threadIdx.x; i < nk; i += blockDim.x) s_val[i] = tv_get(tv, (uint32_t)i);
   __syncthreads();
   const uint32_t kmask = (uint32_t)nk - 1u;
   const uint32_t *__restrict__ packed = g.packed;
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < g.nch;
+  for (int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < g.nch;
        c += (int64_t)gridDim.x * blockDim.x) {
     const int64_t start = g.start[c];
     const int n = g.n[c];
     const bool first = c == 0 || g.run[c - 1] != g.run[c];
+    if (xh) {  // pass-1 summaries in the predicted binades (as k_pass1l): the P1Lane form
+      P1Lane<true, kTrlr> L;
+      L.init(start, n, first, true, xh[c]);
+      const int64_t q0 = start - k, last = total >> 4;
+      auto load3 = [&](int64_t q) {
+        const int64_t w = q >> 4;
+        return make_uint3(packed[min(w, last)], packed[min(w + 1, last)], packed[min(w + 2, last)]);
+      };
+      uint3 cur = load3(q0);
+      for (int b0 = 0; b0 < n; b0 += 16) {
+        const uint3 nxt = load3(q0 + b0 + 16);
+        const uint32_t bp = 2u * (uint32_t)((q0 + b0) & 15);
+        const uint64_t x = ((((uint64_t)cur.x << 32) | cur.y) << bp) | (((uint64_t)cur.z << bp) >> 32);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int i = b0 + j;
+          if (i < n) {
+            const uint32_t code = (uint32_t)(x >> (64 - 2 * (j + k))) & kmask;  // k-mer ending at start + i - 1
+            double s = s_val[code];
+            if (kTrlr && first && i == 0) s = ec.ks[code];
+            if (visits) atomicAdd(&visits[code], 1u);
+            L.step(s, i, ec, cand);
+          }
+        }
+        cur = nxt;
+      }
+      L.finish(c, o, sp);
+      continue;
+    }
     // 16 indices per batch: their k-mers from one 64-bit window of packed
     // bases (three words, loaded one batch ahead, uniform across the wave)
     const int64_t q0 = start - k, last = total >> 4;
@@ -3654,7 +3684,14 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // tables on the pipelined pass with a binade predictor (a table without
   // one, a failed allocation of the predictor, is scanned unexpanded)
   const bool line = tv.line != nullptr && !lds_table && runs.packed != nullptr;  // line table: k_pass1l
-  const bool p1summ = comp && (Jt >= 2 || line) && !lds_table && runs.packed != nullptr && tv.approx != nullptr;
+  // (FP64 line tables, weighted rank, too: KS_F64_P1SUMM=0 leaves their
+  // summaries to k_summaries after the prescan, the former path, for A/B runs)
+  const bool f64_summ = !comp && line && !(getenv("KS_F64_P1SUMM") && atoi(getenv("KS_F64_P1SUMM")) == 0);
+  // (small k, the table in LDS: KS_LDS_P1SUMM=0 leaves the summaries to
+  // k_summaries with the LDS-staged table, the former path)
+  const bool lds_summ = lds_table && !(getenv("KS_LDS_P1SUMM") && atoi(getenv("KS_LDS_P1SUMM")) == 0);
+  const bool p1summ = (lds_table ? lds_summ : (comp ? (Jt >= 2 || line) : f64_summ)) && runs.packed != nullptr &&
+                      tv.approx != nullptr;
   // (the carry reads no replay slots unless k_marks_select wrote them)
   if (!p1summ) rpb.slot = nullptr;
   // per-index code store (uint16 per scan index, 2 B x 256 per chunk):
@@ -3678,12 +3715,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // FP64 line tables (weighted rank) are cut too: the first part's summaries,
   // carry and heads (~10 ms in all at the metric genome) start while the
   // second part's pass 1 drains (in-process A/B at config 3: 31.5 vs 32.7 ms
-  // one part; serialising the two pass-1 launches, KS_F64_P1_SERIAL, 31.8-32.0
-  // by split fraction: profiles/r3/rank/split_ab.txt)
+  // one part; serialising the two pass-1 launches 31.8-32.0 by split
+  // fraction: profiles/r3/rank/split_ab.txt)
   const bool f64_line = line && !comp;
-  const bool split = !ctx->no_split && (p1summ || f64_line) && (p1summ || getenv("KS_NO_F64_SPLIT") == nullptr) &&
-                     lay.split_r > 0 && lay.split_r < nruns && lay.split_c >= 1024 && lay.split_c + 1024 <= ctail_all;
-  const bool p1_serial = f64_line && getenv("KS_F64_P1_SERIAL") != nullptr;
+  const bool split = !ctx->no_split && (p1summ || f64_line) && lay.split_r > 0 && lay.split_r < nruns &&
+                     lay.split_c >= 1024 && lay.split_c + 1024 <= ctail_all;
   Half halves[2];
   int nhalf = 1;
   halves[0] = Half{0, nch, 0, nruns, 0, ntiles};
@@ -3718,12 +3754,20 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     // the first half's predictor and prescan first (they gate its pass 1;
     // the predictor holds whole CUs: 128 KiB of LDS per block), then the
     // second half's on the side stream, under the first half's pass 1
+    // Below ~1 Gbp (4 M chunks) both halves' predictors run first, on the main
+    // stream: the second half's, queued beside the first half's pass 1, took
+    // 1.02 ms there against 0.09 ms alone and held back its own pass 1 (8-way
+    // shard timeline, profiles/r3/timelines/shard8_step_timeline.txt).
+    // KS_PREDICT_BOTH_FIRST=0/1 overrides (A/B).
+    const char *bf = getenv("KS_PREDICT_BOTH_FIRST");
+    const bool both_first = split && (bf ? atoi(bf) != 0 : nch <= ((int64_t)4 << 20));
     KS_TRY(predict(halves[0], st));
     if (split) {
       side_forked = true;
+      if (both_first) KS_TRY(predict(halves[1], st));
       KS_HIP(hipEventRecord(ctx->ev[16], st));
       KS_HIP(hipStreamWaitEvent(ctx->side, ctx->ev[16], 0));
-      KS_TRY(predict(halves[1], ctx->side));
+      if (!both_first) KS_TRY(predict(halves[1], ctx->side));
     }
   }
   KS_HIP(hipEventRecord(ctx->ev[8], st));
@@ -3752,10 +3796,31 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                          ec, visits, p1, cand, runs.packed, d_xh, sp1);                                      \
   } while (0)
   if (lds_table) {
-    // small k: the whole table in LDS, persistent blocks (one per CU), no code store
-    const unsigned gl = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nch + 1023) / 1024, ctx->num_cus));
-    if (ec.trlr) hipLaunchKernelGGL(k_pass1_lds<true>, dim3(gl), dim3(1024), 0, st, g, total, k, tv, ec, visits, p1, cand);
-    else hipLaunchKernelGGL(k_pass1_lds<false>, dim3(gl), dim3(1024), 0, st, g, total, k, tv, ec, visits, p1, cand);
+    // small k: the whole table in LDS, persistent blocks (one per CU), no
+    // code store; with pass-1 summaries the halves as for line tables
+    auto p1lds = [&](const Half &h, hipStream_t strm) {
+      const Chunks gv = view(h);
+      const unsigned gl = (unsigned)std::max<int64_t>(1, std::min<int64_t>((h.c1 - h.c0 + 1023) / 1024, ctx->num_cus));
+      const double *xh = p1summ ? d_xh : nullptr;
+      if (ec.trlr)
+        hipLaunchKernelGGL(k_pass1_lds<true>, dim3(gl), dim3(1024), 0, strm, gv, total, k, tv, ec, visits, p1, cand, xh,
+                           sp1);
+      else
+        hipLaunchKernelGGL(k_pass1_lds<false>, dim3(gl), dim3(1024), 0, strm, gv, total, k, tv, ec, visits, p1, cand, xh,
+                           sp1);
+    };
+    if (split) {
+      KS_HIP(hipEventRecord(ctx->ev[17], st));
+      KS_HIP(hipStreamWaitEvent(ctx->hi, ctx->ev[17], 0));
+      if (!side_forked) KS_HIP(hipStreamWaitEvent(ctx->side, ctx->ev[17], 0));
+      p1lds(halves[0], ctx->hi);
+      KS_HIP(hipGetLastError());
+      KS_HIP(hipEventRecord(ctx->ev[12], ctx->hi));
+      KS_HIP(hipStreamWaitEvent(st, ctx->ev[12], 0));
+      p1lds(halves[1], ctx->side);
+    } else {
+      p1lds(halves[0], st);
+    }
     codes = nullptr;
   } else if (line && (p1summ || !comp)) {
     // line tables: every chunk (no tail: a lane's bases come from guarded loads)
@@ -3764,10 +3829,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   do {                                                                                                       \
     if (ec.trlr)                                                                                             \
       hipLaunchKernelGGL((k_pass1l<O, F, L, true>), dim3(GRID), dim3(F ? 1024 : 768), 0, STRM, GV, total, k, tv, ec, \
-                         visits, p1, cand, d_xh, sp1);                                                       \
+                         visits, p1, cand, p1summ ? d_xh : nullptr, sp1);                                    \
     else                                                                                                     \
       hipLaunchKernelGGL((k_pass1l<O, F, L, false>), dim3(GRID), dim3(F ? 1024 : 768), 0, STRM, GV, total, k, tv, \
-                         ec, visits, p1, cand, d_xh, sp1);                                                   \
+                         ec, visits, p1, cand, p1summ ? d_xh : nullptr, sp1);                                \
   } while (0)
     auto p1l = [&](const Half &h, hipStream_t strm) {
       const Chunks gv = view(h);
@@ -3817,7 +3882,6 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipGetLastError());
       KS_HIP(hipEventRecord(ctx->ev[12], ctx->hi));
       KS_HIP(hipStreamWaitEvent(st, ctx->ev[12], 0));
-      if (p1_serial) KS_HIP(hipStreamWaitEvent(ctx->side, ctx->ev[12], 0));
       p1l(halves[1], ctx->side);
     } else {
       p1l(halves[0], st);
@@ -3956,8 +4020,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       const unsigned gw = (unsigned)std::max<int64_t>(1, (int64_t)ctx->num_cus * 8);
       hipLaunchKernelGGL(k_summ_fixw<false>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
                          d_fix + h.c0, d_nfix + hi, sm, rpb, hi);
-    } else if (lds_table && getenv("KS_SUMM_GLOBAL_TAB") == nullptr) {
-      // small k: the table staged in LDS as for k_pass1_lds (KS_SUMM_GLOBAL_TAB: read from HBM / L2, A/B)
+    } else if (lds_table) {
+      // small k: the table staged in LDS as for k_pass1_lds (from HBM / L2: 12.8 / 18.7 vs 3.8 / 6.4 ms)
       if (comp && lds_lut) {
         const size_t tb = (size_t)2 << (2 * k);
         KS_HIP(hipFuncSetAttribute((const void *)k_summaries<true, true, true>,

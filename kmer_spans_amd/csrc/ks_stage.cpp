@@ -30,12 +30,7 @@ namespace {
 
 // Bases per chunk: the unit of host packing, H2D and device unpacking
 // (16 Mi bases = 4 MiB as 2-bit codes; the first copy starts ~2 ms in).
-constexpr size_t kStageChunkDefault = (size_t)16 << 20;
-const size_t kStageChunk = [] {
-  const char *e = getenv("KS_STAGE_CHUNK_MB");  // (experiments: Mi bases per chunk, a power of two)
-  const size_t v = e ? (size_t)atol(e) : 0;
-  return (v >= 1 && v <= 1024 && (v & (v - 1)) == 0) ? v << 20 : kStageChunkDefault;
-}();
+constexpr size_t kStageChunk = (size_t)16 << 20;
 
 inline uint8_t code2(uint8_t c) { return (c >> 1) & 3; }
 inline uint8_t nib_class(uint8_t c) { return is_n(c) ? 4 : code2(c); }

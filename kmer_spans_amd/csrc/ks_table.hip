@@ -436,32 +436,45 @@ __global__ void k_build_approx(const uint16_t *__restrict__ codes, const double 
 
 }  // namespace
 
-// Process-wide pool of ONE expanded-table buffer per device.  A fresh
-// hipMalloc of 32-128 GiB takes 0.3 ms to 6 s on the box (the driver clears
-// new VRAM; tools/alloc_probe.py), while a buffer freed by this process is
-// handed back at once; tables built per call (host entry points, one table
-// per genome) would pay that on every table.  A destroyed table's buffer is
-// kept here and reused by the next expansion that fits in it;
-// ks_release_cache() returns it to the driver; KS_EXT_POOL=0 disables it.
+// Process-wide pool of expanded-table buffers, per device ONE, or TWO whose
+// sum stays within kPoolPairMax (two tables alive at once, e.g. genome g + 1's
+// table built while genome g is scanned).  A fresh hipMalloc of 32-128 GiB
+// takes 0.3 ms to 6 s on the box (the driver clears new VRAM;
+// tools/alloc_probe.py), while a buffer freed by this process is handed back
+// at once; tables built per call (one table per genome) would pay that on
+// every table.  A destroyed table's buffer is kept here and reused by the
+// next expansion that fits in it; ks_release_cache() returns them to the
+// driver (the host entry points do at the end of each call unless
+// ks_set_host_cache(1)); KS_EXT_POOL=0 disables the pool.
 namespace {
 std::mutex g_pool_mu;
 struct PoolBuf {
   void *p = nullptr;
   size_t bytes = 0;
 };
-PoolBuf g_pool[64];
+constexpr size_t kPoolPairMax = (size_t)80 << 30;
+PoolBuf g_pool[64][2];
 bool pool_on() {
   static const bool on = !(getenv("KS_EXT_POOL") && atoi(getenv("KS_EXT_POOL")) == 0);
   return on;
 }
+size_t pool_bytes(int dev) { return g_pool[dev][0].bytes + g_pool[dev][1].bytes; }  // (under g_pool_mu)
+void pool_free_all(int dev) {  // (under g_pool_mu)
+  for (PoolBuf &b : g_pool[dev]) {
+    if (b.p) (void)hipFree(b.p);
+    b = PoolBuf();
+  }
+}
 void *pool_take(int dev, size_t bytes, size_t *cap) {
   if (!pool_on() || dev < 0 || dev >= 64) return nullptr;
   std::lock_guard<std::mutex> g(g_pool_mu);
-  PoolBuf &b = g_pool[dev];
-  if (!b.p || b.bytes < bytes) return nullptr;
-  void *p = b.p;
-  *cap = b.bytes;
-  b = PoolBuf();
+  PoolBuf *best = nullptr;  // the smallest that fits
+  for (PoolBuf &b : g_pool[dev])
+    if (b.p && b.bytes >= bytes && (!best || b.bytes < best->bytes)) best = &b;
+  if (!best) return nullptr;
+  void *p = best->p;
+  *cap = best->bytes;
+  *best = PoolBuf();
   return p;
 }
 void pool_give(int dev, void *p, size_t bytes) {
@@ -475,10 +488,20 @@ void pool_give(int dev, void *p, size_t bytes) {
     (void)hipDeviceSynchronize();
     if (cur >= 0) (void)hipSetDevice(cur);
     std::lock_guard<std::mutex> g(g_pool_mu);
-    PoolBuf &b = g_pool[dev];
-    if (!b.p || b.bytes < bytes) {
-      std::swap(b.p, p);
-      std::swap(b.bytes, bytes);
+    PoolBuf *s = g_pool[dev];
+    PoolBuf *slot = nullptr;
+    if (!s[0].p && !s[1].p) slot = &s[0];
+    else if ((!s[0].p || !s[1].p) && pool_bytes(dev) + bytes <= kPoolPairMax) slot = s[0].p ? &s[1] : &s[0];
+    if (slot) {
+      slot->p = p;
+      slot->bytes = bytes;
+      p = nullptr;
+    } else {  // the smaller kept buffer goes if this one is larger
+      PoolBuf *small = !s[0].p ? &s[1] : !s[1].p ? &s[0] : (s[0].bytes <= s[1].bytes ? &s[0] : &s[1]);
+      if (small->bytes < bytes) {
+        std::swap(small->p, p);
+        std::swap(small->bytes, bytes);
+      }
     }
   }
   if (p) (void)hipFree(p);
@@ -490,11 +513,9 @@ void pool_give(int dev, void *p, size_t bytes) {
 // gathers over 128 GiB run at 49.3-50.6 G/s from a contiguous buffer and
 // 47.5-48.7 G/s from a plain one on the same box (tools/frag_probe.hip,
 // profiles/r2/frag_probe.txt): fewer, larger translation fragments.
-// KS_NO_CONTIG_EXT=1 keeps the plain allocation.
 static hipError_t ext_malloc(void **p, size_t bytes) {
-  static const bool contig = !getenv("KS_NO_CONTIG_EXT");
   static const bool dbg = getenv("KS_DEBUG_ALLOC") != nullptr;
-  if (contig && bytes >= ((size_t)1 << 30)) {
+  if (bytes >= ((size_t)1 << 30)) {
     if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) {
       if (dbg) fprintf(stderr, "[ext alloc] contiguous %zu bytes at %p\n", bytes, *p);
       return hipSuccess;
@@ -507,8 +528,10 @@ static hipError_t ext_malloc(void **p, size_t bytes) {
 }
 
 // Tables whose chunked scan predicts carry binades before pass 1: compressed
-// tables scanned by the pipelined pass (k > 7: small k stages the table in LDS).
-static bool k_approx_ok(const ks_table *t) { return t->compressed && t->k > 7; }
+// tables scanned by the pipelined pass, FP64 line tables (weighted rank), and
+// small k (k <= 7, the table staged in LDS by pass 1; there the prefix table
+// holds the values themselves).
+static bool k_approx_ok(const ks_table *t) { return t->k >= 1; }
 
 // Entry bytes of an expanded table with J values per entry.
 static size_t ext_entry_bytes(bool u16, int J) {
@@ -585,12 +608,9 @@ static void *ext_alloc(ks_ctx *ctx, size_t bytes, size_t *cap) {
   *cap = bytes;
   if (ext_malloc(&ext, bytes) == hipSuccess) return ext;
   (void)hipGetLastError();
-  {  // a pooled buffer too small for this table may be what is in the way
+  {  // pooled buffers too small for this table may be what is in the way
     std::lock_guard<std::mutex> g(g_pool_mu);
-    if (ctx->device >= 0 && ctx->device < 64 && g_pool[ctx->device].p) {
-      (void)hipFree(g_pool[ctx->device].p);
-      g_pool[ctx->device] = PoolBuf();
-    }
+    if (ctx->device >= 0 && ctx->device < 64) pool_free_all(ctx->device);
   }
   if (ext_malloc(&ext, bytes) == hipSuccess) return ext;
   (void)hipGetLastError();
@@ -749,7 +769,7 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   KS_HIP(hipMemGetInfo(&free_b, &total_b));
   {  // the pooled buffer of a destroyed table is free memory for this purpose
     std::lock_guard<std::mutex> g(g_pool_mu);
-    if (ctx->device >= 0 && ctx->device < 64) free_b += g_pool[ctx->device].bytes;
+    if (ctx->device >= 0 && ctx->device < 64) free_b += pool_bytes(ctx->device);
   }
   // leave room for the sequences and the scan workspace
   const size_t reserve = std::max<size_t>((size_t)32 << 30, total_b / 4);
@@ -779,7 +799,6 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
     const size_t bytes = ((size_t)1 << (2 * kx)) * ext_entry_bytes(u16, c.J);
     if (bytes > budget) continue;
     if (c.bits == 12) {
-      if (getenv("KS_NO_CODE12")) continue;
       bool use = false;
       const double t0 = now_ms();
       KS_TRY(choose_code12(ctx, t, freq_dev, max_escape, &use));
@@ -1209,8 +1228,7 @@ namespace ks {
 void pool_release_device(int dev) {
   if (dev < 0 || dev >= 64) return;
   std::lock_guard<std::mutex> g(g_pool_mu);
-  if (g_pool[dev].p) (void)hipFree(g_pool[dev].p);
-  g_pool[dev] = PoolBuf();
+  pool_free_all(dev);
 }
 }  // namespace ks
 
@@ -1218,10 +1236,7 @@ extern "C" void ks_release_cache(void) {
   regions_cache_release();
   if (!hip_usable_here()) return;
   std::lock_guard<std::mutex> g(g_pool_mu);
-  for (PoolBuf &b : g_pool) {
-    if (b.p) (void)hipFree(b.p);
-    b = PoolBuf();
-  }
+  for (int d = 0; d < 64; ++d) pool_free_all(d);
 }
 
 extern "C" int32_t ks_table_is_compressed(const ks_table *t) { return t && t->compressed ? 1 : 0; }

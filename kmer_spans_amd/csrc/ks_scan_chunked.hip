@@ -283,9 +283,10 @@ __device__ __forceinline__ void values16_nostore(const Chunks &g, const uint8_t 
     line_values_any<NV>(tv, x, k, b0, n, v, s_lut);
     return;
   }
-  if (pk && tv.ext && tv.ext_J >= 2 && k + tv.ext_J - 1 + 15 <= 32) {
+  if (pk && tv.compressed && tv.ext && tv.ext_J >= 2 && k + tv.ext_J - 1 + 15 <= 32) {
     // one expanded-table read per J indices (the gathers of k_summ_fixw and
-    // the heads: 4 random requests per 16 indices at J = 5 instead of 32)
+    // the heads: 4 random requests per 16 indices at J = 5 instead of 32;
+    // uint16 / 12-bit code entries: FP64 tables take the base table below)
     const int J = tv.ext_J, kx = k + J - 1;
     const uint64_t xmask = (kx >= 32) ? ~0ull : ((1ull << (2 * kx)) - 1ull);
     const bool c12 = tv.ext_bits == 12;
@@ -322,6 +323,10 @@ __device__ __forceinline__ void values16_nostore(const Chunks &g, const uint8_t 
   for (int j = 0; j < NV; ++j) {
     if (pk) code = (uint32_t)(x >> (64 - 2 * (j + k))) & kmask;
     else if (j > 0 && b0 + j < n) code = ((code << 2) | enc(seq[p + k - 1 + j])) & kmask;
+    if (!tv.compressed) {  // FP64 base table (small k with the table in LDS for pass 1)
+      v[j] = b0 + j < n ? tv.vals[code] : 0.0;
+      continue;
+    }
     const uint32_t q = b0 + j < n ? tv.codes[code] : 0u;
     v[j] = b0 + j < n ? (s_lut ? s_lut[q] : tv.lut[q]) : 0.0;
   }
@@ -429,6 +434,120 @@ constexpr int kP1TailMargin = kP1WinReach > kP1StageReach ? (kP1WinReach > 352 ?
                                                           : (kP1StageReach > 352 ? kP1StageReach : 352);
 static_assert(16 * kP1StageWords + 4 <= kP1TailMargin + 16 + 1, "staged packed words stay inside the buffer");
 static_assert(kP1WinReach <= kP1TailMargin + 1, "pipelined windows stay inside the buffer");
+
+// Wave-uniform broadcast of lane j's value (v_readlane: a VALU op, unlike a
+// variable-lane __shfl which goes through ds_bpermute).
+__device__ __forceinline__ int rl32(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
+__device__ __forceinline__ long long rl64(long long v, int j) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(v & 0xffffffff), j);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(v >> 32), j);
+  return (long long)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double rld(double v, int j) { return __longlong_as_double(rl64(__double_as_longlong(v), j)); }
+
+// Wave64 scans on DPP lane moves (GFX9 DPP, a VALU operand modifier: no LDS
+// round trip, unlike the ds_bpermute behind a variable __shfl): lane i reads
+// lane i - d of its 16-lane row (row_shr:d), lane 15 of the row before
+// (row_bcast:15, rows 1 and 3), lane 31 (row_bcast:31, rows 2 and 3), or
+// lane i - 1 across the wave (wave_shr:1).  Lanes without a source read 0,
+// the identity of every scan below.  The whole wave must be active.
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, RM, 0xf, true);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ long long dpp_i64(long long v) {
+  const int lo = dpp_i32<CTRL, RM>((int)(v & 0xffffffff)), hi = dpp_i32<CTRL, RM>((int)(v >> 32));
+  return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_f64(double v) {
+  return __longlong_as_double(dpp_i64<CTRL, RM>(__double_as_longlong(v)));
+}
+constexpr int kDppShr1 = 0x111, kDppShr2 = 0x112, kDppShr4 = 0x114, kDppShr8 = 0x118, kDppBc15 = 0x142,
+              kDppBc31 = 0x143, kDppWaveShr1 = 0x138;
+// Inclusive wave scan of an associative op(left, right) whose identity is
+// all-zero bits, on a value type V moved by Mov<CTRL, RM>(V).
+#define KS_DPP_SCAN(V, x, MOV, OP)                     \
+  do {                                                 \
+    x = OP(MOV<kDppShr1, 0xf>(x), x);                  \
+    x = OP(MOV<kDppShr2, 0xf>(x), x);                  \
+    x = OP(MOV<kDppShr4, 0xf>(x), x);                  \
+    x = OP(MOV<kDppShr8, 0xf>(x), x);                  \
+    x = OP(MOV<kDppBc15, 0xa>(x), x);                  \
+    x = OP(MOV<kDppBc31, 0xc>(x), x);                  \
+  } while (0)
+
+__device__ __forceinline__ double wave_sum_incl(double x) {
+  auto add = [](double a, double b) { return a + b; };
+  KS_DPP_SCAN(double, x, dpp_f64, add);
+  return x;
+}
+// previous lane's value (0 in lane 0)
+__device__ __forceinline__ long long wave_prev_i64(long long v) { return dpp_i64<kDppWaveShr1, 0xf>(v); }
+__device__ __forceinline__ int wave_prev_i32(int v) { return dpp_i32<kDppWaveShr1, 0xf>(v); }
+
+// Parity-pair integer maps (d0, d1): entry parity p -> increment d_p;
+// (a then b)_p = a_p + b_{(p + a_p) & 1}.  Identity (0, 0).
+struct PPair {
+  long long d0, d1;
+};
+__device__ __forceinline__ PPair pp_compose(const PPair &a, const PPair &b) {
+  return PPair{a.d0 + ((a.d0 & 1) ? b.d1 : b.d0), a.d1 + (((1 + a.d1) & 1) ? b.d1 : b.d0)};
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ PPair dpp_pp(const PPair &v) {
+  return PPair{dpp_i64<CTRL, RM>(v.d0), dpp_i64<CTRL, RM>(v.d1)};
+}
+__device__ __forceinline__ PPair pp_scan_incl(PPair x) {
+  KS_DPP_SCAN(PPair, x, dpp_pp, pp_compose);
+  return x;
+}
+__device__ __forceinline__ PPair pp_prev(const PPair &v) { return PPair{wave_prev_i64(v.d0), wave_prev_i64(v.d1)}; }
+
+// segmented parity-pair scan element (f: a segment starts in this lane's part)
+struct SegPP {
+  PPair s;
+  int f;
+};
+template <int CTRL, int RM>
+__device__ __forceinline__ SegPP dpp_seg(const SegPP &v) {
+  return SegPP{dpp_pp<CTRL, RM>(v.s), dpp_i32<CTRL, RM>(v.f)};
+}
+__device__ __forceinline__ SegPP seg_op(const SegPP &l, const SegPP &r) {
+  return SegPP{r.f ? r.s : pp_compose(l.s, r.s), l.f | r.f};
+}
+// forward fill of a flagged value
+struct FillM {
+  long long m;
+  int f;
+};
+template <int CTRL, int RM>
+__device__ __forceinline__ FillM dpp_fill(const FillM &v) {
+  return FillM{dpp_i64<CTRL, RM>(v.m), dpp_i32<CTRL, RM>(v.f)};
+}
+__device__ __forceinline__ FillM fill_op(const FillM &l, const FillM &r) { return FillM{r.f ? r.m : l.m, l.f | r.f}; }
+
+// DPP moves whose lanes without a source keep `old` (bound_ctrl off): scans
+// whose identity is not all-zero bits.
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_f64_or(double v, double old) {
+  const long long x = __double_as_longlong(v), o = __double_as_longlong(old);
+  const int lo = __builtin_amdgcn_update_dpp((int)(o & 0xffffffff), (int)(x & 0xffffffff), CTRL, RM, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(x >> 32), CTRL, RM, 0xf, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+// The predictor's max-plus pairs: (a1, b1) then (a2, b2) = (a1 + a2,
+// max(b1 + a2, b2)); identity (0, -inf).
+struct APair {
+  double a, b;
+};
+template <int CTRL, int RM>
+__device__ __forceinline__ APair dpp_ap(const APair &v) {
+  return APair{dpp_f64_or<CTRL, RM>(v.a, 0.0), dpp_f64_or<CTRL, RM>(v.b, -INFINITY)};
+}
+__device__ __forceinline__ APair ap_op(const APair &l, const APair &r) { return APair{l.a + r.a, fmax(l.b + r.a, r.b)}; }
+__device__ __forceinline__ APair ap_prev(const APair &v) { return dpp_ap<kDppWaveShr1, 0xf>(v); }
 
 // ------------------------------------------------------------------- P0
 
@@ -1966,23 +2085,16 @@ __global__ void __launch_bounds__(64) k_approx_scan(const int64_t *__restrict__ 
   double carry = 0.0;
   for (int64_t cb = c0; cb < c1; cb += 64) {
     const int64_t c = cb + lane;
-    double a = 0.0, b = -INFINITY;  // identity
+    APair p{0.0, -INFINITY};  // identity
     if (c < c1) {
-      a = o.special[c] ? -INFINITY : o.asum[c];
-      b = o.cexit[c];
+      p.a = o.special[c] ? -INFINITY : o.asum[c];
+      p.b = o.cexit[c];
     }
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {  // (a1,b1) then (a2,b2) = (a1+a2, max(b1+a2, b2))
-      const double pa = __shfl_up(a, d, 64), pb = __shfl_up(b, d, 64);
-      if (lane >= d) {
-        b = fmax(pb + a, b);
-        a = pa + a;
-      }
-    }
-    double ea = __shfl_up(a, 1, 64), eb = __shfl_up(b, 1, 64);
-    if (lane == 0) { ea = 0.0; eb = -INFINITY; }
+    KS_DPP_SCAN(APair, p, dpp_ap, ap_op);
+    const APair ex = ap_prev(p);
+    const double ea = ex.a, eb = ex.b;
     if (c < c1) xt[c] = fmax(carry + ea, eb);
-    const double la = __shfl(a, 63, 64), lb = __shfl(b, 63, 64);
+    const double la = rld(p.a, 63), lb = rld(p.b, 63);
     carry = fmax(carry + la, lb);
     if (!(carry == carry)) carry = 0.0;
   }
@@ -2024,14 +2136,17 @@ __device__ __forceinline__ void tile_of(const int64_t *__restrict__ tbase, const
 // composition order differs from k_approx_scan, so the FP64 results may
 // differ in the last bits: only a prediction, never a result.
 __device__ __forceinline__ void ascan_pair(double &a, double &b, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {  // (a1,b1) then (a2,b2) = (a1+a2, max(b1+a2, b2))
-    const double pa = __shfl_up(a, d, 64), pb = __shfl_up(b, d, 64);
-    if (lane >= d) {
-      b = fmax(pb + a, b);
-      a = pa + a;
-    }
-  }
+  APair p{a, b};  // (a1,b1) then (a2,b2) = (a1+a2, max(b1+a2, b2))
+  KS_DPP_SCAN(APair, p, dpp_ap, ap_op);
+  a = p.a;
+  b = p.b;
+  (void)lane;
+}
+// the exclusive pair (the previous lane's inclusive one; identity in lane 0)
+__device__ __forceinline__ void ascan_prev(double a, double b, double &ea, double &eb) {
+  const APair ex = ap_prev(APair{a, b});
+  ea = ex.a;
+  eb = ex.b;
 }
 __global__ void __launch_bounds__(256) k_ascan_tiles(const int64_t *__restrict__ tbase, const int64_t *__restrict__ cbase,
                                                     int64_t nruns, const int32_t *__restrict__ trun, P1 o, double2 *__restrict__ tagg, int64_t t_lo,
@@ -2067,12 +2182,12 @@ __global__ void __launch_bounds__(64) k_ascan_runs(const int64_t *__restrict__ t
       b = v.y;
     }
     ascan_pair(a, b, lane);
-    double ea = __shfl_up(a, 1, 64), eb = __shfl_up(b, 1, 64);
-    if (lane == 0) { ea = 0.0; eb = -INFINITY; }
+    double ea, eb;
+    ascan_prev(a, b, ea, eb);
     double xin = fmax(carry + ea, eb);
     if (!(xin == xin)) xin = 0.0;
     if (t < t1) tin[t] = xin;
-    const double la = __shfl(a, 63, 64), lb = __shfl(b, 63, 64);
+    const double la = rld(a, 63), lb = rld(b, 63);
     carry = fmax(carry + la, lb);
     if (!(carry == carry)) carry = 0.0;
   }
@@ -2092,8 +2207,8 @@ __global__ void __launch_bounds__(256) k_ascan_apply(const int64_t *__restrict__
     b = o.cexit[c];
   }
   ascan_pair(a, b, lane);
-  double ea = __shfl_up(a, 1, 64), eb = __shfl_up(b, 1, 64);
-  if (lane == 0) { ea = 0.0; eb = -INFINITY; }
+  double ea, eb;
+  ascan_prev(a, b, ea, eb);
   if (c < c1) xt[c] = fmax(tin[t] + ea, eb);
 }
 
@@ -2333,15 +2448,10 @@ __global__ void __launch_bounds__(256) k_summ_fixw(Chunks g, const uint8_t *__re
       }
       pre[q] = lm;
     }
-    PMap inc = lm;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const PMap o{__shfl_up(inc.d0, d, 64), __shfl_up(inc.d1, d, 64)};
-      if (lane >= d) inc = pm_compose(o, inc);
-    }
-    PMap exc{__shfl_up(inc.d0, 1, 64), __shfl_up(inc.d1, 1, 64)};
-    if (lane == 0) exc = PMap{0, 0};
-    const PMap tot{__shfl(inc.d0, 63, 64), __shfl(inc.d1, 63, 64)};
+    const PPair incp = pp_scan_incl(PPair{lm.d0, lm.d1});
+    const PPair excp = pp_prev(incp);
+    const PMap exc{excp.d0, excp.d1};
+    const PMap tot{rl64(incp.d0, 63), rl64(incp.d1, 63)};
     ok = __all(ok);
     long long M[2], N[2];
     int A[2];
@@ -2418,15 +2528,6 @@ __global__ void __launch_bounds__(256) k_seg_marks(Chunks g, P1 o, const double 
 // tile's lanes are computed wave-parallel, once per binade); a certain clamp
 // (x + minprefix < -margin) -> clean exit (R); else exact replay (U).  The
 // chain is wave-uniform; L chunks also get their head (max/argmax) here.
-// Wave-uniform broadcast of lane j's value (v_readlane: a VALU op, unlike a
-// variable-lane __shfl which goes through ds_bpermute).
-__device__ __forceinline__ int rl32(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
-__device__ __forceinline__ long long rl64(long long v, int j) {
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(v & 0xffffffff), j);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(v >> 32), j);
-  return (long long)(((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ double rld(double v, int j) { return __longlong_as_double(rl64(__double_as_longlong(v), j)); }
 
 // Exact carry, one wave per run, walking 64-chunk tiles (lane j <-> chunk
 // cb + j, its inputs in registers, broadcast with v_readlane).  Per chunk, in
@@ -2472,13 +2573,8 @@ __device__ bool replay_par(const double v[4], int n, double x, double &T, double
     labs += fabs(vq);
     a[q] = loc;
   }
-  double incl = loc, sab = labs;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const double o = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += o;
-    sab += __shfl_xor(sab, d, 64);
-  }
+  const double incl = wave_sum_incl(loc);
+  const double sab = rld(wave_sum_incl(labs), 63);
   if (!(sab < 1.0e300)) return false;  // non-finite values: serial
   const double excl = incl - loc;
   const double err = ldexp(x + sab, -42);  // >> 2 * 256 * 2^-53 * (x + sum |s|)
@@ -2498,7 +2594,7 @@ __device__ bool replay_par(const double v[4], int n, double x, double &T, double
   // (d0, d1) = increment for an even / odd m, and pairs compose
   // associatively: (f then g)_b = f_b + g_{(b + f_b) & 1}.
   const int ex = binade_of(x);
-  const int eprev_lane = __shfl_up(e[3], 1, 64);
+  const int eprev_lane = wave_prev_i32(e[3]);
   bool cr[4];
   long long d0[4], d1[4];
 #pragma unroll
@@ -2539,23 +2635,12 @@ __device__ bool replay_par(const double v[4], int n, double x, double &T, double
     Q0[q] = r0;
     Q1[q] = r1;
   }
-  long long s0 = r0, s1 = r1;  // lane aggregate after its last crossing
-  bool fc = lflag;
-#pragma unroll
-  for (int dd = 1; dd < 64; dd <<= 1) {
-    const long long o0 = __shfl_up(s0, dd, 64), o1 = __shfl_up(s1, dd, 64);
-    const int fo = __shfl_up((int)fc, dd, 64);
-    if (lane >= dd) {
-      if (!fc) {
-        long long n0, n1;
-        comp(o0, o1, s0, s1, n0, n1);
-        s0 = n0; s1 = n1;
-      }
-      fc = fc || fo;
-    }
-  }
-  long long c0 = __shfl_up(s0, 1, 64), c1 = __shfl_up(s1, 1, 64);  // exclusive carry-in
-  if (lane == 0) { c0 = 0; c1 = 0; }
+  // segmented scan of the lane aggregates after their last crossing:
+  // (L, R) -> R.f ? R : (L.s then R.s, L.f | R.f); identity ((0, 0), 0)
+  SegPP sg{PPair{r0, r1}, lflag ? 1 : 0};
+  KS_DPP_SCAN(SegPP, sg, dpp_seg, seg_op);
+  const PPair cin = pp_prev(sg.s);  // exclusive carry-in (lane 0: identity)
+  long long c0 = cin.d0, c1 = cin.d1;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     if (cr[q]) break;
@@ -2607,16 +2692,11 @@ __device__ bool replay_par(const double v[4], int n, double x, double &T, double
 #pragma unroll
   for (int q = 0; q < 4; ++q)
     if (cr[q]) { lastm = Mc[q]; has = true; }
-  long long fm = lastm;
-  bool ff = has;
-#pragma unroll
-  for (int dd = 1; dd < 64; dd <<= 1) {
-    const long long mo = __shfl_up(fm, dd, 64);
-    const int fo = __shfl_up((int)ff, dd, 64);
-    if (lane >= dd && !ff && fo) { fm = mo; ff = true; }
-  }
-  long long start_m = __shfl_up(fm, 1, 64);
-  const int start_f = __shfl_up((int)ff, 1, 64);
+  // forward fill: (L, R) -> (R.f ? R.m : L.m, L.f | R.f); identity (0, 0)
+  FillM fw{lastm, has ? 1 : 0};
+  KS_DPP_SCAN(FillM, fw, dpp_fill, fill_op);
+  long long start_m = wave_prev_i64(fw.m);
+  const int start_f = wave_prev_i32(fw.f);
   if (lane == 0 || !start_f) start_m = mant_of(x);
   double S[4];
   bool inb = true;
@@ -2637,9 +2717,11 @@ __device__ bool replay_par(const double v[4], int n, double x, double &T, double
 #pragma unroll
   for (int q = 0; q < 4; ++q)
     if (live[q] && S[q] > bm) { bm = S[q]; bi = 4 * lane + q; }
+  // wave max (the DPP identity 0.0 is below no result: every S is >= 0)
   double wm = bm;
-#pragma unroll
-  for (int dd = 1; dd < 64; dd <<= 1) wm = fmax(wm, __shfl_xor(wm, dd, 64));
+  auto dmax = [](double a, double b) { return fmax(a, b); };
+  KS_DPP_SCAN(double, wm, dpp_f64, dmax);
+  wm = rld(wm, 63);
   const unsigned long long bl = __ballot(bm == wm && bm >= 0.0);
   const int fl = __ffsll((long long)bl) - 1;
   hmax = wm;
@@ -2719,19 +2801,9 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
           hi1 = tc.HI[2 * t + 1];
         }
         if (!in || te != e) d0 = d1 = 0;  // identity beyond the first rejected tile (never used)
-        long long i0 = d0, i1 = d1;  // inclusive composed increments
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const long long p0 = __shfl_up(i0, d, 64), p1 = __shfl_up(i1, d, 64);
-          if (lane >= d) {
-            const long long n0 = p0 + ((p0 & 1) ? i1 : i0);
-            const long long n1 = p1 + (((1 + p1) & 1) ? i1 : i0);
-            i0 = n0;
-            i1 = n1;
-          }
-        }
-        long long x0 = __shfl_up(i0, 1, 64), x1 = __shfl_up(i1, 1, 64);
-        if (lane == 0) { x0 = 0; x1 = 0; }
+        const PPair ip = pp_scan_incl(PPair{d0, d1});  // inclusive composed increments
+        const PPair xp = pp_prev(ip);
+        const long long i0 = ip.d0, i1 = ip.d1, x0 = xp.d0, x1 = xp.d1;
         const long long m0 = mant_of(x);
         const long long mt = m0 + ((m0 & 1) ? x1 : x0);  // entry mantissa of tile t
         const int pt = (int)(mt & 1);
@@ -2793,19 +2865,9 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
       if (x >= kLMin && x < 1.0e18 && rl32(se, j) == binade_of(x)) {
         const int e = binade_of(x);
         const bool in = live && lane >= j;
-        long long i0 = in ? D[0] : 0, i1 = in ? D[1] : 0;  // inclusive composed map
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const long long p0 = __shfl_up(i0, d, 64), p1 = __shfl_up(i1, d, 64);
-          if (lane >= d) {
-            const long long n0 = p0 + ((p0 & 1) ? i1 : i0);          // entry parity 0
-            const long long n1 = p1 + (((1 + p1) & 1) ? i1 : i0);    // entry parity 1
-            i0 = n0;
-            i1 = n1;
-          }
-        }
-        long long x0 = __shfl_up(i0, 1, 64), x1 = __shfl_up(i1, 1, 64);
-        if (lane == 0) { x0 = 0; x1 = 0; }
+        const PPair ip = pp_scan_incl(PPair{in ? D[0] : 0, in ? D[1] : 0});  // inclusive composed map
+        const PPair xp = pp_prev(ip);
+        const long long x0 = xp.d0, x1 = xp.d1;
         const long long m0 = mant_of(x);
         const long long mj = m0 + ((m0 & 1) ? x1 : x0);  // exact entry of this lane's chunk
         const int pj = (int)(mj & 1);
@@ -2952,19 +3014,9 @@ __global__ void __launch_bounds__(256) k_tile_comp(Chunks g, Summ sm, TileComp t
   const long long D0 = sm.D[2 * c], D1 = sm.D[2 * c + 1];
   const long long M0 = sm.M[2 * c], M1 = sm.M[2 * c + 1];
   const long long N0 = sm.N[2 * c], N1 = sm.N[2 * c + 1];
-  long long i0 = D0, i1 = D1;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const long long p0 = __shfl_up(i0, d, 64), p1 = __shfl_up(i1, d, 64);
-    if (lane >= d) {
-      const long long n0 = p0 + ((p0 & 1) ? i1 : i0);
-      const long long n1 = p1 + (((1 + p1) & 1) ? i1 : i0);
-      i0 = n0;
-      i1 = n1;
-    }
-  }
-  long long x0 = __shfl_up(i0, 1, 64), x1 = __shfl_up(i1, 1, 64);
-  if (lane == 0) { x0 = 0; x1 = 0; }
+  const PPair ip = pp_scan_incl(PPair{D0, D1});
+  const PPair xp = pp_prev(ip);
+  const long long i0 = ip.d0, i1 = ip.d1, x0 = xp.d0, x1 = xp.d1;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     // entry mantissa m (parity p): chunk lane enters at m + inc with parity pj
@@ -3005,19 +3057,8 @@ __global__ void __launch_bounds__(256) k_tile_apply(Chunks g, Summ sm, TileComp 
   const bool live = c < g.nch;
   const int64_t cc = live ? c : 64 * t;
   const long long D0 = sm.D[2 * cc], D1 = sm.D[2 * cc + 1];
-  long long i0 = live ? D0 : 0, i1 = live ? D1 : 0;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const long long p0 = __shfl_up(i0, d, 64), p1 = __shfl_up(i1, d, 64);
-    if (lane >= d) {
-      const long long n0 = p0 + ((p0 & 1) ? i1 : i0);
-      const long long n1 = p1 + (((1 + p1) & 1) ? i1 : i0);
-      i0 = n0;
-      i1 = n1;
-    }
-  }
-  long long x0 = __shfl_up(i0, 1, 64), x1 = __shfl_up(i1, 1, 64);
-  if (lane == 0) { x0 = 0; x1 = 0; }
+  const PPair xp = pp_prev(pp_scan_incl(PPair{live ? D0 : 0, live ? D1 : 0}));
+  const long long x0 = xp.d0, x1 = xp.d1;
   if (!live) return;
   const long long mj = m + ((m & 1) ? x1 : x0);
   const int pj = (int)(mj & 1);
@@ -3302,16 +3343,6 @@ __device__ __forceinline__ XState x_compose(const XState &f1, const XState &f2) 
   return r;
 }
 
-__device__ __forceinline__ XState x_shfl_up(const XState &a, int d) {
-  XState r;
-  r.reset = __shfl_up(a.reset, d, 64);
-  r.open = __shfl_up(a.open, d, 64);
-  r.xb = __shfl_up(a.xb, d, 64);
-  r.xa = __shfl_up(a.xa, d, 64);
-  r.xm = __shfl_up(a.xm, d, 64);
-  return r;
-}
-
 __device__ __forceinline__ XState x_shfl(const XState &a, int l) {
   XState r;
   r.reset = __shfl(a.reset, l, 64);
@@ -3368,12 +3399,17 @@ __device__ __forceinline__ ChunkOp chunk_op(const Chunks &g, const P1 &o, const 
   return r;
 }
 
+// DPP move of a state; lanes without a source read the identity (EXTEND by
+// nothing: xm = -inf)
+template <int CTRL, int RM>
+__device__ __forceinline__ XState dpp_x(const XState &a) {
+  return XState{dpp_i32<CTRL, RM>(a.reset), dpp_i32<CTRL, RM>(a.open), dpp_i64<CTRL, RM>(a.xb),
+                dpp_i64<CTRL, RM>(a.xa), dpp_f64_or<CTRL, RM>(a.xm, -INFINITY)};
+}
+
 __device__ __forceinline__ XState wave_inclusive(XState inc, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const XState p = x_shfl_up(inc, d);
-    if (lane >= d) inc = x_compose(p, inc);
-  }
+  KS_DPP_SCAN(XState, inc, dpp_x, x_compose);
+  (void)lane;
   return inc;
 }
 
@@ -3434,8 +3470,7 @@ __global__ void __launch_bounds__(64) k_stitch_runs(const int64_t *__restrict__ 
     XState f{0, 0, 0, 0, -INFINITY};
     if (t < t1) f = xt_load(agg, t);
     const XState inc = wave_inclusive(f, lane);
-    XState exc = x_shfl_up(inc, 1);
-    if (lane == 0) exc = XState{0, 0, 0, 0, -INFINITY};
+    const XState exc = dpp_x<kDppWaveShr1, 0xf>(inc);  // (lane 0: the identity)
     if (t < t1) xt_store(tin, t, x_compose(carry, exc));
     carry = x_compose(carry, x_shfl(inc, 63));
   }
@@ -3463,8 +3498,7 @@ __global__ void __launch_bounds__(256) k_stitch_emit(Chunks g, const int64_t *__
   op.closes = false;
   if (live) op = chunk_op(g, o, cr, c);
   const XState inc = wave_inclusive(op.f, lane);
-  XState exc = x_shfl_up(inc, 1);
-  if (lane == 0) exc = XState{0, 0, 0, 0, -INFINITY};
+  const XState exc = dpp_x<kDppWaveShr1, 0xf>(inc);  // (lane 0: the identity)
   const XState in = x_compose(xt_load(tin, t), exc);  // state entering chunk c
   double xm = in.xm;
   long long xa = in.xa;

@@ -563,7 +563,7 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
 
 
 // Staggered two-part scan.  The input is cut at the sequence boundary nearest
-// a fraction f of its bases (KS_PARTS_FRAC, default 0.45; 0: one part).  The
+// a fraction f of its bases (KS_PARTS_FRAC; default 0 = one part).  The
 // first part [0, m) runs here; the second [m, nseq) on the part context from
 // a second host thread, which starts only once the first part has queued its
 // pass 1 and whose stream waits for the first part's pre-pass-1 work (ev[8]):
@@ -579,7 +579,7 @@ static ks_status scan_parts(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, in
                             int32_t min_width, double min_score, ks_regions *out, ks_scan_stats *stats,
                             const ScanMode &mode) {
   // (read per call: in-process A/B runs switch them)
-  const double frac = getenv("KS_PARTS_FRAC") ? atof(getenv("KS_PARTS_FRAC")) : 0.45;
+  const double frac = getenv("KS_PARTS_FRAC") ? atof(getenv("KS_PARTS_FRAC")) : 0.0;  // (opt-in: DESIGN.md §6)
   const int64_t min_total = getenv("KS_PARTS_MIN") ? atoll(getenv("KS_PARTS_MIN")) : ((int64_t)1 << 28);
   if (!(frac > 0.0 && frac < 1.0) || mode.trlr || ctx->scan_algo == 0 || total < min_total || s->nseq < 2)
     return KS_INTERNAL_PART_ABORT;

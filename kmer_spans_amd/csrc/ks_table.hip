@@ -452,7 +452,7 @@ struct PoolBuf {
   void *p = nullptr;
   size_t bytes = 0;
 };
-constexpr size_t kPoolPairMax = (size_t)80 << 30;
+constexpr size_t kPoolPairMax = (size_t)130 << 30;  // (two 64 GiB tables; one 128 GiB table alone)
 PoolBuf g_pool[64][2];
 bool pool_on() {
   static const bool on = !(getenv("KS_EXT_POOL") && atoi(getenv("KS_EXT_POOL")) == 0);

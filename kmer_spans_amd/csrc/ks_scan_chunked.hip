@@ -1773,15 +1773,18 @@ __global__ void __launch_bounds__(1024) k_pass1_lds(Chunks g, int64_t total, int
 // 16-B (J = 2) or 32-B (J = 3, 4) entry per J scan indices, the next batch's
 // entries in flight while the current batch runs the clean trajectory, bases
 // rolled from the packed codes.  Same outputs as k_pass1<J, false, false>
-// (no code store: later passes re-read the table).
+// (no code store: later passes re-read the table), plus (xh != nullptr) the
+// binade-integer summaries in the predicted binades (P1Lane, as k_pass1l):
+// at k = 15 a separate k_summaries pass re-read the 64 GiB table.
 template <int J, bool kTrlr>
 __global__ void __launch_bounds__(1024) k_pass1pf(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
                                                   TableView tv, EmitCfg ec, uint32_t *__restrict__ visits, P1 o,
-                                                  Cand cand, const uint32_t *__restrict__ packed) {
+                                                  Cand cand, const uint32_t *__restrict__ packed,
+                                                  const double *__restrict__ xh, SummP1 sp) {
   constexpr int G = (J == 2) ? 8 : 4;  // table reads per batch
   constexpr int PB = G * J;            // scan indices per batch (16, 12, 16)
   using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.nch) return;
   const double2 *__restrict__ E = reinterpret_cast<const double2 *>(tv.ext);
   const int kx = k + J - 1;
@@ -1791,7 +1794,12 @@ __global__ void __launch_bounds__(1024) k_pass1pf(Chunks g, const uint8_t *__res
   const int n = g.n[c];
   const bool first = c == 0 || g.run[c - 1] != g.run[c];
   // tail lanes (reads could pass the end of the buffer) are left to k_pass1
-  if (start + n + kP1TailMargin > total) return;
+  if (start + n + kP1TailMargin > total) {
+    sp.e[2 * c] = sp.e[2 * c + 1] = INT32_MIN;  // no pass-1 summary (the workspace is reused)
+    return;
+  }
+  P1Lane<true, kTrlr> L;
+  L.init(start, n, first, true, xh ? xh[c] : 0.0);
   GC gcode = (GC)prime_code_guarded64(seq, start - k, kx, total);
   const double first_val = (kTrlr && first) ? ec.ks[(uint32_t)(gcode >> (2 * (J - 1))) & kmask] : 0.0;
   const int64_t q0 = start + J - 1;
@@ -1823,10 +1831,6 @@ __global__ void __launch_bounds__(1024) k_pass1pf(Chunks g, const uint8_t *__res
   roll(win, q0, gc);
   fetch(gc, 0, e0, e1);
   win = *reinterpret_cast<const u32x3a4 *>(packed + ((q0 + PB) >> 4));
-  double prev = 0.0, best = 0.0;
-  int beg = -1, arg = 0;
-  double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
-  bool special = false;
   for (int b0 = 0; b0 < n; b0 += PB) {
     GC gn[G];
     double2 n0[G], n1[G];
@@ -1844,37 +1848,7 @@ __global__ void __launch_bounds__(1024) k_pass1pf(Chunks g, const uint8_t *__res
         const int i = b0 + j;
         if (i < n) {
           if (visits) atomicAdd(&visits[(uint32_t)(gc[gi] >> (2 * (J - 1 - t))) & kmask], 1u);
-          asum += s;
-          pmin = asum < pmin ? asum : pmin;
-          pmax = asum > pmax ? asum : pmax;
-          sabs += fabs(s);
-          special |= !isfinite(s);
-          const double tt = prev + s;
-          const double S = tt > 0 ? tt : 0.0;
-          const bool open = (prev == 0) & (S > 0);
-          const bool close = (prev > 0) & (S == 0);
-          const int f0 = first ? 0 : -1;
-          const long long ml = kTrlr ? ec.min_len : 0;
-          const bool want =
-              kTrlr ? (close & (((long long)((arg != f0 ? arg - 1 : arg) - (beg != f0 ? beg - 1 : beg)) >= ml) |
-                                ((long long)((i != f0 ? i - 1 : i) - (arg != f0 ? arg - 1 : arg) - 1) >=
-                                 (ml > 1 ? ml : 1LL))))
-                    : (close & ((uint64_t)(int64_t)(arg - beg) >= ec.mw) & (best >= ec.min_score));
-          if (want) {
-            const int64_t slot = append_one(cand.count, cand.segcap);
-            if (slot >= 0) {
-              cand.beg[slot] = start + beg;
-              cand.arg[slot] = start + arg;
-              cand.rst[slot] = start + i;
-              cand.best[slot] = best;
-            }
-            __builtin_amdgcn_s_waitcnt(0x0F70);
-          }
-          const bool up = open | (S > best);
-          best = up ? S : best;
-          arg = up ? i : arg;
-          beg = open ? i : (close ? -1 : beg);
-          prev = S;
+          L.step(s, i, ec, cand);
         }
       }
     }
@@ -1885,17 +1859,7 @@ __global__ void __launch_bounds__(1024) k_pass1pf(Chunks g, const uint8_t *__res
       e1[gi] = n1[gi];
     }
   }
-  o.cexit[c] = prev;
-  o.asum[c] = asum;
-  o.pmin[c] = pmin;
-  o.pmax[c] = pmax;
-  o.sabs[c] = sabs;
-  o.special[c] = special ? 1 : 0;
-  if (prev > 0) {
-    o.tbeg[c] = beg; o.tmax[c] = best; o.targ[c] = arg;
-  } else {
-    o.tbeg[c] = -1; o.tmax[c] = 0.0; o.targ[c] = 0;
-  }
+  L.finish(c, o, sp);
 }
 
 // ------------------------------------------------------------------- P3
@@ -3720,7 +3684,9 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const bool line = tv.line != nullptr && !lds_table && runs.packed != nullptr;  // line table: k_pass1l
   // (FP64 line tables, weighted rank, too: KS_F64_P1SUMM=0 leaves their
   // summaries to k_summaries after the prescan, the former path, for A/B runs)
-  const bool f64_summ = !comp && line && !(getenv("KS_F64_P1SUMM") && atoi(getenv("KS_F64_P1SUMM")) == 0);
+  // (and FP64 expanded tables, k_pass1pf: weighted rank at k = 14, 15)
+  const bool f64_summ = !comp && (line || (!lds_table && Jt >= 2 && Jt <= 4)) &&
+                        !(getenv("KS_F64_P1SUMM") && atoi(getenv("KS_F64_P1SUMM")) == 0);
   // (small k, the table in LDS: KS_LDS_P1SUMM=0 leaves the summaries to
   // k_summaries with the LDS-staged table, the former path)
   const bool lds_summ = lds_table && !(getenv("KS_LDS_P1SUMM") && atoi(getenv("KS_LDS_P1SUMM")) == 0);
@@ -3921,6 +3887,52 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       p1l(halves[0], st);
     }
     KS_HIP(hipGetLastError());
+  } else if (!comp && J >= 2 && J <= 4 && pipelined) {  // FP64 expanded table (weighted rank)
+    hipStream_t side = ctx->side;
+    const bool tail = nch > ctail;
+    const double *xh = p1summ ? d_xh : nullptr;
+#define KS_P1PF(J, GV, GRID, STRM)                                                                             \
+    do {                                                                                                       \
+      if (ec.trlr) hipLaunchKernelGGL((k_pass1pf<J, true>), dim3(GRID), dim3(1024), 0, STRM, GV, s->seq, total, k, \
+                                      tv, ec, visits, p1, cand, runs.packed, xh, sp1);                         \
+      else hipLaunchKernelGGL((k_pass1pf<J, false>), dim3(GRID), dim3(1024), 0, STRM, GV, s->seq, total, k, tv, \
+                              ec, visits, p1, cand, runs.packed, xh, sp1);                                     \
+    } while (0)
+    auto p1f = [&](const Half &h, hipStream_t strm) {
+      const Chunks gv = view(h);
+      const unsigned grid = (unsigned)((h.c1 - h.c0 + 1023) / 1024);
+      if (J == 4) KS_P1PF(4, gv, grid, strm); else if (J == 3) KS_P1PF(3, gv, grid, strm); else KS_P1PF(2, gv, grid, strm);
+    };
+#undef KS_P1PF
+    auto p1tail = [&]() {
+      if (J == 4) KS_P1TC(4, false, false); else if (J == 3) KS_P1TC(3, false, false); else KS_P1TC(2, false, false);
+    };
+    if (split) {  // the halves at once, as the compressed pass below
+      KS_HIP(hipEventRecord(ctx->ev[17], st));
+      KS_HIP(hipStreamWaitEvent(ctx->hi, ctx->ev[17], 0));
+      if (!side_forked) KS_HIP(hipStreamWaitEvent(side, ctx->ev[17], 0));
+      p1f(halves[0], ctx->hi);
+      KS_HIP(hipGetLastError());
+      KS_HIP(hipEventRecord(ctx->ev[12], ctx->hi));
+      KS_HIP(hipStreamWaitEvent(st, ctx->ev[12], 0));
+      if (tail) {
+        p1tail();
+        KS_HIP(hipGetLastError());
+      }
+      p1f(halves[1], side);
+    } else {
+      if (tail) {
+        KS_HIP(hipEventRecord(ctx->ev[12], st));
+        KS_HIP(hipStreamWaitEvent(side, ctx->ev[12], 0));
+        p1tail();
+        KS_HIP(hipGetLastError());
+        KS_HIP(hipEventRecord(ctx->ev[13], side));
+      }
+      p1f(halves[0], st);
+      KS_HIP(hipGetLastError());
+      if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
+    }
+    KS_HIP(hipGetLastError());
   } else if (p1summ) {
     // the tail chunks (a latency-bound serial walk each) run on the side
     // stream, overlapped with the pipelined pass (of the last half)
@@ -3972,27 +3984,6 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipGetLastError());
       if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
     }
-  } else if (!comp && J >= 2 && J <= 4 && pipelined) {  // FP64 expanded table (weighted rank)
-    hipStream_t side = ctx->side;
-    const bool tail = nch > ctail;
-    if (tail) {
-      KS_HIP(hipEventRecord(ctx->ev[12], st));
-      KS_HIP(hipStreamWaitEvent(side, ctx->ev[12], 0));
-      if (J == 4) KS_P1TC(4, false, false); else if (J == 3) KS_P1TC(3, false, false); else KS_P1TC(2, false, false);
-      KS_HIP(hipGetLastError());
-      KS_HIP(hipEventRecord(ctx->ev[13], side));
-    }
-#define KS_P1PF(J)                                                                                             \
-    do {                                                                                                       \
-      if (ec.trlr) hipLaunchKernelGGL((k_pass1pf<J, true>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, \
-                                      tv, ec, visits, p1, cand, runs.packed);                                  \
-      else hipLaunchKernelGGL((k_pass1pf<J, false>), dim3(gch1k), dim3(1024), 0, st, g, s->seq, total, k, tv,  \
-                              ec, visits, p1, cand, runs.packed);                                              \
-    } while (0)
-    if (J == 4) KS_P1PF(4); else if (J == 3) KS_P1PF(3); else KS_P1PF(2);
-#undef KS_P1PF
-    KS_HIP(hipGetLastError());
-    if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
   } else if (comp) {
     KS_P1(1, true, false);  // unexpanded compressed table (with the code store)
   } else {

@@ -145,6 +145,39 @@ def test_rank_k15(oracle):
     tab.close()
 
 
+@pytest.mark.parametrize("k,jmax", [(10, 2), (11, 3), (9, 4)])
+def test_rank_expanded_pass1_summaries(oracle, monkeypatch, k, jmax):
+    """The FP64 expanded form of the k = 14 / 15 weighted-rank tables
+    (k_pass1pf, forced at small k by KS_EXT_MAX_J) with its pass-1 binade
+    summaries and halves, and without them (KS_F64_P1SUMM=0): regions,
+    scores and visits equal to the oracle on a multi-contig genome."""
+    import torch
+    from kmer_spans_amd import _lib, device as D, genome
+    monkeypatch.setenv("KS_EXT_MAX_J", str(jmax))
+    ctx = _lib.context(0)
+    D.bind_torch_stream(ctx)
+    parts = [genome.contig(L, 40 + i, device="cuda", repeats=True)
+             for i, L in enumerate((1_500_000, 1_100_000, 800_000, 60_000))]
+    ds = D.from_parts(parts, [p.numel() for p in parts], "cuda")
+    host = [ds.host_seq(i) for i in range(len(parts))]
+    counts = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+    words = D.count(ctx, ds, k, counts)
+    w = torch.empty(4 ** k, dtype=torch.float64, device="cuda")
+    tab = D.DeviceTable.from_counts(ctx, counts, k, "rank", total=words, thr=0.6, expand=True, w_out=w)
+    assert not tab.compressed and tab.positions_per_read == jmax
+    o = oracle.scan(host, k, w.cpu().numpy(), 0.6, 50, 5.0, visits=True)
+    ctx.set_scan_algo(1)
+    for summ in ("1", "0"):
+        monkeypatch.setenv("KS_F64_P1SUMM", summ)
+        vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+        pos, sc, st = D.scan(ctx, ds, k, tab, 50, 5.0, vis)
+        _same(pos, sc, o, ("rank expanded", k, jmax, summ))
+        assert np.array_equal(vis.cpu().numpy(), o["counts"]), ("rank expanded visits", k, jmax, summ)
+    ctx.set_scan_algo(-1)
+    assert o["pos"].shape[1] > 0
+    tab.close()
+
+
 def test_genomes_mode(oracle):
     """Config 5 logic (bench.py --mode genomes, test.R:550-567's per-scaffold
     pattern at genome scale): several genomes scanned one after another on

@@ -575,32 +575,17 @@ __global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__r
 // bases; a max-plus scan of them (k_approx_scan) predicts each chunk's entry,
 // i.e. the binade pass 1 summarises in.  Only a prediction: a wrong binade
 // costs one gathered summary (k_summ_fixw), never a result.
-template <int PS>
-__global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k, const uint16_t *__restrict__ approx, int kp,
-                                                  double *__restrict__ pa, double *__restrict__ pb) {
-  __shared__ __half s_ap[1 << 16];
-  const int np = 1 << (2 * kp);
-  for (int i = threadIdx.x; i < np; i += blockDim.x) s_ap[i] = __ushort_as_half(approx[i]);
-  __syncthreads();
-  const uint32_t pmask = (uint32_t)np - 1u;
-  const uint32_t *__restrict__ packed = g.packed;
-  for (int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < g.nch;
-       c += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t start = g.start[c];
-    const int n = g.n[c];
-    const int64_t q0 = start - k;  // index i's k-mer prefix: bases [q0 + i, q0 + i + kp)
-    // the chunk's 18 packed words (bases q0 .. q0 + 287) are loaded up front,
-    // all in flight at once; batch t (indices 16 t .. 16 t + 15) reads its
-    // 32-base window from words t .. t + 2 at the chunk's fixed bit offset,
-    // with the batches unrolled so the words stay in registers
+// The chunk's 18 packed words (bases q0 .. q0 + 287, q0 = start - k) in
+// registers: five aligned 16-B loads (a quarter of the requests of 18 word
+// loads: the lanes of a wave read 64 different lines per instruction), then
+// the 18 words at offset w0 - wa selected in registers.
+struct PredWords {
+  uint32_t a[20];
+  int o;
+  __device__ __forceinline__ void load(const uint32_t *__restrict__ packed, int64_t total, int64_t q0) {
     const int64_t w0 = q0 >> 4, last = total >> 4;
-    uint32_t wd[18];
     const int64_t wa = w0 & ~(int64_t)3;
     if (wa + 20 <= last + 1) {
-      // five aligned 16-B loads (a quarter of the requests of 18 word loads:
-      // the lanes of a wave read 64 different lines per instruction), then
-      // the 18 words at offset w0 - wa selected in registers
-      uint32_t a[20];
       const uint4 *P4 = reinterpret_cast<const uint4 *>(packed + wa);
 #pragma unroll
       for (int t = 0; t < 5; ++t) {
@@ -610,19 +595,44 @@ __global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k
         a[4 * t + 2] = v.z;
         a[4 * t + 3] = v.w;
       }
-      const int o = (int)(w0 - wa);
-#pragma unroll
-      for (int t = 0; t < 18; ++t) wd[t] = o == 0 ? a[t] : (o == 1 ? a[t + 1] : (o == 2 ? a[t + 2] : a[t + 3]));
+      o = (int)(w0 - wa);
     } else {
 #pragma unroll
-      for (int t = 0; t < 18; ++t) wd[t] = packed[min(w0 + t, last)];
+      for (int t = 0; t < 18; ++t) a[t] = packed[min(w0 + t, last)];
+      o = 0;
     }
+  }
+  __device__ __forceinline__ uint32_t w(int t) const {
+    return o == 0 ? a[t] : (o == 1 ? a[t + 1] : (o == 2 ? a[t + 2] : a[t + 3]));
+  }
+};
+
+// P0 binade predictor (pass-1 summaries): the approximate sum and clean
+// exit of every chunk from the fp16 prefix means of the table (ks_table::
+// d_approx, <= 128 KiB in LDS, one block per CU), rolled from the packed
+// bases; a max-plus scan of them (k_approx_scan) predicts each chunk's entry,
+// i.e. the binade pass 1 summarises in.  Only a prediction: a wrong binade
+// costs one gathered summary (k_summ_fixw), never a result.  One block per
+// CU (4 waves per SIMD) hides little latency, so kPf software-pipelines the
+// grid-stride loop: the next chunk's packed words and the start / length of
+// the one after it are in flight while a chunk is summed.
+template <int PS, bool kPf = false>
+__global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k, const uint16_t *__restrict__ approx, int kp,
+                                                  double *__restrict__ pa, double *__restrict__ pb) {
+  __shared__ __half s_ap[1 << 16];
+  const int np = 1 << (2 * kp);
+  for (int i = threadIdx.x; i < np; i += blockDim.x) s_ap[i] = __ushort_as_half(approx[i]);
+  __syncthreads();
+  const uint32_t pmask = (uint32_t)np - 1u;
+  const uint32_t *__restrict__ packed = g.packed;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  auto sum_chunk = [&](const PredWords &W, int64_t q0, int n, int64_t c) {
     const uint32_t bp = 2u * (uint32_t)(q0 & 15);
     float tsum = 0.f, tex = 0.f;
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
       if (16 * t < n) {
-        const uint64_t x = ((((uint64_t)wd[t] << 32) | wd[t + 1]) << bp) | (((uint64_t)wd[t + 2] << bp) >> 32);
+        const uint64_t x = ((((uint64_t)W.w(t) << 32) | W.w(t + 1)) << bp) | (((uint64_t)W.w(t + 2) << bp) >> 32);
         // every PS-th index, weighted PS (A/B: PS = 2 cuts the predictor 1.11 -> 0.80 ms with the
         // same 16.2 K gathered summaries at the metric config)
         float a[16 / PS];
@@ -639,6 +649,43 @@ __global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k
     }
     pa[c] = tsum;
     pb[c] = tex;
+  };
+  int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (!kPf) {
+    for (; c < g.nch; c += stride) {
+      PredWords W;
+      const int64_t q0 = g.start[c] - k;  // index i's k-mer prefix: bases [q0 + i, q0 + i + kp)
+      W.load(packed, total, q0);
+      sum_chunk(W, q0, g.n[c], c);
+    }
+    return;
+  }
+  if (c >= g.nch) return;
+  int64_t q0 = g.start[c] - k;
+  int n = g.n[c];
+  PredWords W;
+  W.load(packed, total, q0);
+  int64_t c1 = c + stride;
+  int64_t q1 = 0;
+  int n1 = 0;
+  if (c1 < g.nch) {
+    q1 = g.start[c1] - k;
+    n1 = g.n[c1];
+  }
+  for (;;) {
+    PredWords W1;
+    const int64_t c2 = c1 + stride;
+    int64_t q2 = 0;
+    int n2 = 0;
+    if (c1 < g.nch) W1.load(packed, total, q1);
+    if (c2 < g.nch) {
+      q2 = g.start[c2] - k;
+      n2 = g.n[c2];
+    }
+    sum_chunk(W, q0, n, c);
+    if (c1 >= g.nch) break;
+    c = c1; q0 = q1; n = n1; W = W1;
+    c1 = c2; q1 = q2; n1 = n2;
   }
 }
 
@@ -3741,13 +3788,19 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     pp.asum = reinterpret_cast<double *>(W + o_pa);
     pp.cexit = reinterpret_cast<double *>(W + o_pb);
     pp.special = reinterpret_cast<uint8_t *>(W + o_pz);
+    // KS_PREDICT_PF=1 (A/B): the software-pipelined predictor loop
+    const bool pred_pf = getenv("KS_PREDICT_PF") && atoi(getenv("KS_PREDICT_PF")) != 0;
     auto predict = [&](const Half &h, hipStream_t strm) -> ks_status {
       KS_HIP(hipMemsetAsync(W + o_pz + h.c0, 0, (size_t)(h.c1 - h.c0), strm));
       const unsigned gl =
           (unsigned)std::max<int64_t>(1, std::min<int64_t>((h.c1 - h.c0 + 1023) / 1024, ctx->num_cus));
       // every second index sampled (A/B: every 4th / 8th changed nothing)
-      hipLaunchKernelGGL(k_predict<2>, dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx, tv.approx_k,
-                         pp.asum, pp.cexit);
+      if (pred_pf)
+        hipLaunchKernelGGL((k_predict<2, true>), dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx,
+                           tv.approx_k, pp.asum, pp.cexit);
+      else
+        hipLaunchKernelGGL((k_predict<2, false>), dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx,
+                           tv.approx_k, pp.asum, pp.cexit);
       KS_HIP(hipGetLastError());
       return ascan(pp, d_xh, h.r0, h.r1, h.t0, h.t1, strm);
     };

@@ -12,9 +12,9 @@ $AB --rounds 3 --steps 3 nev0: nev1:KS_NEV_VARIANT=1 nev2:KS_NEV_VARIANT=2 nev3:
 tail -5 $O/ab_nev.txt
 $AB --rounds 3 --steps 2 --score rank one: nosumm:KS_F64_P1SUMM=0 p55:KS_PARTS_FRAC=0.55 --out $O/ab_rank.json > $O/ab_rank.txt 2>&1 || { tail -30 $O/ab_rank.txt; exit 1; }
 tail -4 $O/ab_rank.txt
-$AB --rounds 3 --steps 3 one: p55:KS_PARTS_FRAC=0.55 p65:KS_PARTS_FRAC=0.65 --out $O/ab_log2.json > $O/ab_log2.txt 2>&1 || { tail -30 $O/ab_log2.txt; exit 1; }
+$AB --rounds 3 --steps 3 one: pf:KS_PREDICT_PF=1 p55:KS_PARTS_FRAC=0.55 --out $O/ab_log2.json > $O/ab_log2.txt 2>&1 || { tail -30 $O/ab_log2.txt; exit 1; }
 tail -4 $O/ab_log2.txt
-$AB --rounds 3 --steps 3 --shard-of 8 one:KS_PREDICT_BOTH_FIRST=0 bf: p55bf:KS_PARTS_FRAC=0.55 --out $O/ab_shard8.json > $O/ab_shard8.txt 2>&1 || { tail -30 $O/ab_shard8.txt; exit 1; }
+$AB --rounds 3 --steps 3 --shard-of 8 one:KS_PREDICT_BOTH_FIRST=0 bf: bfpf:KS_PREDICT_PF=1 --out $O/ab_shard8.json > $O/ab_shard8.txt 2>&1 || { tail -30 $O/ab_shard8.txt; exit 1; }
 tail -4 $O/ab_shard8.txt
 fi
 if [[ $P == *b* ]]; then

@@ -43,8 +43,12 @@ namespace {
 // sequential state machine consumes them, so a lane keeps several random
 // table reads in flight instead of one (the gathers do not depend on S).
 // With an expanded table one read serves J consecutive indices (the
-// (k+J-1)-mer spanning them), as in the chunked gather pass.
-template <int J, bool kCompressed, int GW = 0>
+// (k+J-1)-mer spanning them), as in the chunked gather pass.  kPf: the next
+// batch's reads are issued before the current batch is consumed (a restart
+// drops them), so a long rescan -- one lane alone in its wave for most of
+// the kernel, the weighted-rank tail -- waits for one table round trip per
+// two batches instead of one per batch.
+template <int J, bool kCompressed, int GW = 0, bool kPf = false>
 __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ seq, int64_t total,
                                                   const int64_t *__restrict__ ra,
                                                   const int64_t *__restrict__ rbnd,
@@ -67,35 +71,45 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
   const int kx = k + J - 1;
   const GC xmask = (2 * kx >= 8 * (int)sizeof(GC)) ? ~(GC)0 : (((GC)1 << (2 * kx)) - 1);
   const uint32_t kmask = (1u << (2 * k)) - 1u;
-  int64_t i = a;  // priming point
-  for (;;) {
-    // (k+J-1)-mer of the group starting at scan index i + k
-    GC gcode = (GC)prime_code_guarded64(seq, i, kx, total);
-    double S = 0.0, prev = 0.0, best = 0.0;
-    int64_t beg = 0, arg = 0;
-    bool restart = false;
-    for (int64_t p0 = i + k; p0 < b && !restart; p0 += PB) {
-      const int n = (int)((b - p0) < PB ? (b - p0) : PB);
-      double v[PB];
-      GC gc[G];
-      uint64_t xb = 0;  // the batch's PB <= 20 rolled-in bases from the packed codes (2 * PB <= 64 bits)
-      const bool pk = packed_bits(packed, total, p0 + J - 1, xb);
+  GC gcode = 0;
+  // values and group keys of the batch at p0 (gcode rolls on to the next batch)
+  auto gather = [&](int64_t p0, double vv[PB], GC gg[G]) {
+    const int n = (int)((b - p0) < PB ? (b - p0) : PB);
+    uint64_t xb = 0;  // the batch's PB <= 20 rolled-in bases from the packed codes (2 * PB <= 64 bits)
+    const bool pk = packed_bits(packed, total, p0 + J - 1, xb);
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        gc[g] = gcode;
-        if (g * J < n) {
-          gather_group<J, kCompressed>(tv, gcode, kmask, v + g * J);
-          if (pk) {
-            gcode = ((gcode << (2 * J)) | (GC)((xb >> (64 - 2 * J * (g + 1))) & ((1ull << (2 * J)) - 1))) & xmask;
-          } else {
+    for (int g = 0; g < G; ++g) {
+      gg[g] = gcode;
+      if (g * J < n) {
+        gather_group<J, kCompressed>(tv, gcode, kmask, vv + g * J);
+        if (pk) {
+          gcode = ((gcode << (2 * J)) | (GC)((xb >> (64 - 2 * J * (g + 1))) & ((1ull << (2 * J)) - 1))) & xmask;
+        } else {
 #pragma unroll
-            for (int t = 0; t < J; ++t) {
-              const int64_t q = p0 + g * J + J - 1 + t;
-              gcode = ((gcode << 2) | enc(q < total ? seq[q] : (uint8_t)'N')) & xmask;
-            }
+          for (int t = 0; t < J; ++t) {
+            const int64_t q = p0 + g * J + J - 1 + t;
+            gcode = ((gcode << 2) | enc(q < total ? seq[q] : (uint8_t)'N')) & xmask;
           }
         }
       }
+    }
+  };
+  int64_t i = a;  // priming point
+  for (;;) {
+    // (k+J-1)-mer of the group starting at scan index i + k
+    gcode = (GC)prime_code_guarded64(seq, i, kx, total);
+    double S = 0.0, prev = 0.0, best = 0.0;
+    int64_t beg = 0, arg = 0;
+    bool restart = false;
+    double v[PB];
+    GC gc[G];
+    if (kPf && i + k < b) gather(i + k, v, gc);
+    for (int64_t p0 = i + k; p0 < b && !restart; p0 += PB) {
+      const int n = (int)((b - p0) < PB ? (b - p0) : PB);
+      double vn[PB];
+      GC gn[G];
+      if (!kPf) gather(p0, v, gc);
+      else if (p0 + PB < b) gather(p0 + PB, vn, gn);
 #pragma unroll
       for (int j = 0; j < PB; ++j) {  // fully unrolled: v[]/gc[] stay in registers
         if (j < n && !restart) {
@@ -119,6 +133,12 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
             prev = S;
           }
         }
+      }
+      if (kPf) {
+#pragma unroll
+        for (int j = 0; j < PB; ++j) v[j] = vn[j];
+#pragma unroll
+        for (int g = 0; g < G; ++g) gc[g] = gn[g];
       }
     }
     if (restart) continue;
@@ -306,8 +326,23 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
   if (tv.compressed) {
     if (J == 6) KS_LANE(6, true); else if (J == 5) KS_LANE(5, true); else if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
   } else if (J == 4 && tv.line) {
-    hipLaunchKernelGGL((k_scan_lane<4, false, 8>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq,
-                       total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed);
+    // (KS_LANE_PF=1, A/B: the next batch's line reads in flight while a batch is consumed)
+    if (getenv("KS_LANE_PF") && atoi(getenv("KS_LANE_PF")) != 0)
+      hipLaunchKernelGGL((k_scan_lane<4, false, 8, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream,
+                         seq, total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed);
+    else
+      hipLaunchKernelGGL((k_scan_lane<4, false, 8>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq,
+                         total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed);
+  } else if (!tv.compressed && J >= 2 && getenv("KS_LANE_PF") && atoi(getenv("KS_LANE_PF")) != 0) {
+    if (J == 4) hipLaunchKernelGGL((k_scan_lane<4, false, 0, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
+                                   ctx->stream, seq, total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt,
+                                   segcap, packed);
+    else if (J == 3) hipLaunchKernelGGL((k_scan_lane<3, false, 0, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
+                                        ctx->stream, seq, total, ra, rb, rs, n, k, tv, mw, min_score, visits, out,
+                                        d_cnt, segcap, packed);
+    else hipLaunchKernelGGL((k_scan_lane<2, false, 0, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
+                            ctx->stream, seq, total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap,
+                            packed);
   } else {
     if (J == 5) KS_LANE(5, false); else if (J == 4) KS_LANE(4, false); else if (J == 3) KS_LANE(3, false); else if (J == 2) KS_LANE(2, false); else KS_LANE(1, false);
   }

@@ -49,9 +49,13 @@ def test_line_forms(oracle, setup, monkeypatch, k, cap, own_u16, own_f64, score)
     wh = w.cpu().numpy()
     o = oracle.scan(host, k, wh, thr, 100 if score != "pm1" else 20, 20.0 if score != "pm1" else 5.0, visits=True)
     mw, ms = (100, 20.0) if score != "pm1" else (20, 5.0)
-    for route in ("count", "atomic"):
+    for route in ("count", "atomic", "lane_pf"):
         if route == "atomic":
             monkeypatch.setenv("KS_VISITS_ATOMIC", "1")
+        if route == "lane_pf":  # the prefetching rescan lane kernel
+            if score != "rank":
+                continue
+            monkeypatch.setenv("KS_LANE_PF", "1")
         ctx.set_scan_algo(1)
         vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
         pos, sc, st = D.scan(ctx, ds, k, tab, mw, ms, vis)
@@ -59,6 +63,7 @@ def test_line_forms(oracle, setup, monkeypatch, k, cap, own_u16, own_f64, score)
         _same(pos, sc, o["pos"], o["score"], (score, k, cap, route))
         assert np.array_equal(vis.cpu().numpy(), o["counts"]), (score, k, cap, route, "visits")
         monkeypatch.delenv("KS_VISITS_ATOMIC", raising=False)
+        monkeypatch.delenv("KS_LANE_PF", raising=False)
     ctx.set_scan_algo(-1)
     tab.close()
 

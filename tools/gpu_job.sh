@@ -10,7 +10,7 @@ AB="timeout -k 10 600 python -u tools/ab_inproc.py"
 if [[ $P == *a* ]]; then
 $AB --rounds 3 --steps 3 nev0: nev1:KS_NEV_VARIANT=1 nev2:KS_NEV_VARIANT=2 nev3:KS_NEV_VARIANT=3 --out $O/ab_nev.json > $O/ab_nev.txt 2>&1 || { tail -30 $O/ab_nev.txt; exit 1; }
 tail -5 $O/ab_nev.txt
-$AB --rounds 3 --steps 2 --score rank one: nosumm:KS_F64_P1SUMM=0 p55:KS_PARTS_FRAC=0.55 --out $O/ab_rank.json > $O/ab_rank.txt 2>&1 || { tail -30 $O/ab_rank.txt; exit 1; }
+$AB --rounds 3 --steps 2 --score rank one: nosumm:KS_F64_P1SUMM=0 lanepf:KS_LANE_PF=1 --out $O/ab_rank.json > $O/ab_rank.txt 2>&1 || { tail -30 $O/ab_rank.txt; exit 1; }
 tail -4 $O/ab_rank.txt
 $AB --rounds 3 --steps 3 one: pf:KS_PREDICT_PF=1 p55:KS_PARTS_FRAC=0.55 --out $O/ab_log2.json > $O/ab_log2.txt 2>&1 || { tail -30 $O/ab_log2.txt; exit 1; }
 tail -4 $O/ab_log2.txt

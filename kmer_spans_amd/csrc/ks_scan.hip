@@ -333,16 +333,19 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
     else
       hipLaunchKernelGGL((k_scan_lane<4, false, 8>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq,
                          total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed);
-  } else if (!tv.compressed && J >= 2 && getenv("KS_LANE_PF") && atoi(getenv("KS_LANE_PF")) != 0) {
+  } else if (!tv.compressed && J >= 2 && J <= 5 && getenv("KS_LANE_PF") && atoi(getenv("KS_LANE_PF")) != 0) {
     if (J == 4) hipLaunchKernelGGL((k_scan_lane<4, false, 0, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
                                    ctx->stream, seq, total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt,
                                    segcap, packed);
     else if (J == 3) hipLaunchKernelGGL((k_scan_lane<3, false, 0, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
                                         ctx->stream, seq, total, ra, rb, rs, n, k, tv, mw, min_score, visits, out,
                                         d_cnt, segcap, packed);
-    else hipLaunchKernelGGL((k_scan_lane<2, false, 0, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
+    else if (J == 2) hipLaunchKernelGGL((k_scan_lane<2, false, 0, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
+                                        ctx->stream, seq, total, ra, rb, rs, n, k, tv, mw, min_score, visits, out,
+                                        d_cnt, segcap, packed);
+    else hipLaunchKernelGGL((k_scan_lane<5, false, 0, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
                             ctx->stream, seq, total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap,
-                            packed);
+                            packed);  // (J = 5: FP64 lines of own 4)
   } else {
     if (J == 5) KS_LANE(5, false); else if (J == 4) KS_LANE(4, false); else if (J == 3) KS_LANE(3, false); else if (J == 2) KS_LANE(2, false); else KS_LANE(1, false);
   }

@@ -929,7 +929,9 @@ def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over
     if pipelined:
         from kmer_spans_amd import _lib as L_
         import threading
-        ctx2 = L_.context(torch.cuda.current_device())
+        # its own context (workspace, streams): _lib.context(dev) is the cached
+        # per-device context that ctx already is
+        ctx2 = L_.Context(torch.cuda.current_device())
         s_b = torch.cuda.Stream()
         ctx2.set_stream(s_b.cuda_stream)
         counts2 = [torch.zeros(4 ** k, dtype=torch.int32, device=dev) for _ in range(2)]
@@ -940,8 +942,10 @@ def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over
             with torch.cuda.stream(s_b):
                 cbuf.zero_()
                 words = D.count(ctx2, ds, k, cbuf)
-                return D.DeviceTable.from_counts(ctx2, cbuf, k, args.score, total=words, thr=thr_g,
+                tab_ = D.DeviceTable.from_counts(ctx2, cbuf, k, args.score, total=words, thr=thr_g,
                                                  expand=not args.no_expand, max_ext_bytes=cap)
+                s_b.synchronize()  # complete before ctx's stream scans with it
+                return tab_
 
         def run_all():
             out = [None] * G
@@ -968,6 +972,7 @@ def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over
         barrier()
         elapsed = max_over_ranks(time.perf_counter() - t0)
         del counts2
+        ctx2.close()
     else:
         one(dss[0])  # warm-up (workspace, pinned staging)
         barrier()

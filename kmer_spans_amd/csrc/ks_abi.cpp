@@ -121,6 +121,11 @@ ks_status activate(ks_ctx *ctx) {
   return KS_OK;
 }
 
+ks_status ctx_busy() {
+  return fail(KS_ERR_ARG, "this ks_ctx is in use by another thread: a context takes one call at a time "
+                          "(create one context per thread)");
+}
+
 ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out) {
   DevBuf &b = ctx->slots[s];
   if (b.bytes < bytes) {
@@ -400,7 +405,7 @@ extern "C" ks_status ks_count_dev(ks_ctx *ctx, const ks_dev_seqs *s, int32_t k, 
   KS_TRY(check_dev_seqs(s));
   if (k < 1 || k > KS_MAX_K) return fail(KS_ERR_ARG, "k must be a positive integer less than 1+MAX_K");
   if (!counts_dev || !n_words) return fail(KS_ERR_ARG, "null argument");
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   Runs none;
   return launch_count(ctx, s, s->offsets_host[s->nseq], none, k, counts_dev, n_words);
 }
@@ -414,7 +419,7 @@ extern "C" ks_status ks_scan_dev(ks_ctx *ctx, const ks_dev_seqs *s, int32_t k, c
     return fail(KS_ERR_ARG, "kmer sizes larger than or equal to %d not currently supported", KS_MAX_K + 1);
   if (t->k != k) return fail(KS_ERR_ARG, "table built for k=%d used with k=%d", t->k, k);
   memset(out, 0, sizeof(*out));
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   return scan_impl(ctx, s, s->offsets_host[s->nseq], k, t, min_width, min_score, visits_dev, out, stats);
 }
 
@@ -428,7 +433,7 @@ extern "C" ks_status ks_tr_lr_dev(ks_ctx *ctx, const ks_dev_seqs *s, int32_t k, 
   if (!init->d_vals || init->thr != 0.0 || trans->thr != 0.0)
     return fail(KS_ERR_ARG, "tr_lr tables need threshold 0 and an uncompressed init table");
   memset(out, 0, sizeof(*out));
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   ScanMode mode;
   mode.trlr = 1;
   mode.ks = init->d_vals;
@@ -492,7 +497,7 @@ extern "C" ks_status ks_tr_lr_regions(ks_ctx *ctx, const char *const *seqs, cons
     memcpy(spectra + nk, tr.data(), (size_t)nk * 8);
   }
   KS_TRY(default_ctx(&ctx));
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   const HostEnd host_end{ctx};  // (ks_set_host_cache)
   Staged st;
   KS_TRY(stage(ctx, seqs, lens, nseq, &st));
@@ -522,7 +527,7 @@ extern "C" ks_status ks_kmer_counts(ks_ctx *ctx, const char *const *seqs, const 
   if (!counts || !n_words) return fail(KS_ERR_ARG, "null output");
   if (use_broker()) return broker_kmer_counts(seqs, lens, nseq, k, counts, n_words);
   KS_TRY(default_ctx(&ctx));
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   const HostEnd host_end{ctx};  // (ks_set_host_cache)
   Staged st;
   KS_TRY(stage(ctx, seqs, lens, nseq, &st));
@@ -597,7 +602,7 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
   memset(out, 0, sizeof(*out));
   if (use_broker()) return broker_kmer_regions(seqs, lens, nseq, k, w, w_len, min_width, min_score, visits, n_bases, out);
   KS_TRY(default_ctx(&ctx));
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   const HostEnd host_end{ctx};  // (ks_set_host_cache)
   double n = 0;
   for (int32_t q = 0; q < nseq; ++q)
@@ -678,7 +683,7 @@ extern "C" ks_status ks_low_comp_regions(ks_ctx *ctx, const char *const *seqs, c
   memset(out, 0, sizeof(*out));
   if (use_broker()) return broker_low_comp(seqs, lens, nseq, k, min_width, min_score, thr, counts, ranks, n, out);
   KS_TRY(default_ctx(&ctx));
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   const HostEnd host_end{ctx};  // (ks_set_host_cache)
   // the pipeline of ks_kmer_regions: the bases cross PCIe as 2-bit codes +
   // N runs and are counted in pieces meanwhile (:592-601); the weighted
@@ -756,7 +761,7 @@ extern "C" ks_status ks_windowed_dev(ks_ctx *ctx, const ks_dev_seqs *s, const ui
   KS_TRY(check_windowed(kmer_n, k, window));
   for (int32_t i = 0; i < kmer_n; ++i)
     if (kmer_codes[i] >> (2 * k)) return fail(KS_ERR_ARG, "k-mer code %u out of range for k=%d", kmer_codes[i], k);
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   return windowed_impl(ctx, s, s->offsets_host[s->nseq], kmer_codes, kmer_n, k, window, dist_dev, included_dev,
                        scores_dev);
 }
@@ -785,7 +790,7 @@ extern "C" ks_status ks_windowed_dist(ks_ctx *ctx, const char *const *seqs, cons
   if (use_broker())
     return broker_windowed(seqs, lens, nseq, kmers, kmer_n, k, window, ret_flag, dist, seq_included, scores);
   KS_TRY(default_ctx(&ctx));
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   const HostEnd host_end{ctx};  // (ks_set_host_cache)
   Staged st;
   KS_TRY(stage(ctx, seqs, lens, nseq, &st));

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdarg>
 #include <cstdint>
@@ -11,6 +12,7 @@
 #include <sys/types.h>
 #include <functional>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/kmer_spans.h"
@@ -76,6 +78,7 @@ struct DevBuf {
 }  // namespace ks
 
 struct ks_ctx {
+  std::atomic<std::thread::id> user{};  // the thread inside an entry point (CtxUse)
   int device = 0;
   int pid = 0;  // creating process (fork check)
   hipStream_t stream = nullptr;
@@ -186,6 +189,31 @@ ks_status copy_out(ks_ctx *ctx, void *dst, const void *src_dev, size_t n);
 // (synchronises ctx->stream)
 ks_status h2d_pinned(ks_ctx *ctx, void *dst_dev, const void *src, size_t n, int nthr);
 ks_status activate(ks_ctx *ctx);  // fork check + hipSetDevice
+// A context is used by one thread at a time (include/kmer_spans.h): an entry
+// point marks its context as in use for its duration (nested entry points
+// of the same thread pass), and a call from a second thread meanwhile fails
+// with KS_ERR_ARG instead of racing on the workspace.
+struct CtxUse {
+  ks_ctx *c = nullptr;
+  bool owner = false, busy = false;
+  explicit CtxUse(ks_ctx *ctx) : c(ctx) {
+    if (!c) return;
+    std::thread::id none{};
+    const std::thread::id me = std::this_thread::get_id();
+    if (c->user.compare_exchange_strong(none, me)) owner = true;
+    else busy = none != me;
+  }
+  ~CtxUse() {
+    if (owner) c->user.store(std::thread::id());
+  }
+  CtxUse(const CtxUse &) = delete;
+  CtxUse &operator=(const CtxUse &) = delete;
+};
+ks_status ctx_busy();  // the KS_ERR_ARG of a context used by another thread
+#define KS_ENTER(ctx)                        \
+  CtxUse ks_use_(ctx);                       \
+  if (ks_use_.busy) return ks::ctx_busy();   \
+  KS_TRY(activate(ctx))
 ks_status ctx_sub(ks_ctx *ctx, ks_ctx **sub);  // ctx->sub, created on first use
 ks_status ctx_part(ks_ctx *ctx, ks_ctx **part);  // ctx->part, created on first use
 void pool_release_device(int dev);             // free the device's pooled expanded-table buffer

@@ -257,7 +257,7 @@ extern "C" ks_status ks_fasta_load(ks_ctx *ctx, const char *path, int64_t min_le
   KS_TRY(default_ctx(&ctx));
   HostView v;
   KS_TRY(open_view(path, &v));
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   return fasta_from_view(ctx, v, path, min_len, out);
 }
 
@@ -268,7 +268,7 @@ extern "C" ks_status ks_fasta_parse(ks_ctx *ctx, const char *buf, int64_t n, int
   HostView v;
   v.p = reinterpret_cast<const uint8_t *>(buf);
   v.n = (size_t)n;
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   return fasta_from_view(ctx, v, "buffer", min_len, out);
 }
 
@@ -291,7 +291,7 @@ extern "C" ks_status ks_count_multi_dev(ks_ctx *ctx, const ks_dev_seqs *s, const
     if (ks[i] < 1 || ks[i] > KS_MAX_K) return fail(KS_ERR_ARG, "k must be a positive integer less than 1+MAX_K");
     if (!counts_dev[i]) return fail(KS_ERR_ARG, "null count buffer");
   }
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   return launch_count_multi(ctx, s, s->offsets_host[s->nseq], ks, nk, counts_dev, n_words);
 }
 
@@ -392,7 +392,7 @@ extern "C" ks_status ks_kmers_to_file(ks_ctx *ctx, const char *seq_path, const c
   };
   HostView v;
   if (open_view(seq_path, &v) != KS_OK) return na(ks_last_error());
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   ks_fasta fa;
   fasta_reset(&fa);
   const int64_t ml = std::isfinite(min_l) ? (int64_t)std::ceil(min_l) : (min_l > 0 ? INT64_MAX : INT64_MIN);

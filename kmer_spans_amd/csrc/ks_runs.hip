@@ -88,15 +88,15 @@ __device__ __forceinline__ void append_events(uint32_t starts, uint32_t ends, in
 // words -- pure functions of the bytes -- the part's later passes may read).
 // kPre: lane 0's byte before its unit is loaded with the unit loads (one
 // memory round trip per step) instead of after them (A/B: KS_NEV_LATE_PREV=1).
-// U: units per lane and step (U loads in flight); kNT: nontemporal byte loads
-// (the step reads the bytes once: they need not displace the packed words
-// and table lines from L2 / MALL).
-template <bool kMul, bool kPre, int U = 4, bool kNT = false>  // multiply-based byte packing, lane 0's preceding byte loaded early (both A/B winners)
+// Four units per lane and step (eight, and nontemporal byte loads, measured
+// the same: 0.89-0.95 ms, profiles/r4/ab/ab_nev.txt).
+template <bool kMul, bool kPre>  // multiply-based byte packing, lane 0's preceding byte loaded early (both A/B winners)
 __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ seq, int64_t total,
                                                   unsigned long long *__restrict__ ev,
                                                   unsigned long long *__restrict__ ev_count, int64_t cap,
                                                   uint32_t *__restrict__ packed, int64_t p_lo, int64_t p_hi,
                                                   int64_t u0, int64_t u1) {
+  constexpr int U = 4;  // units per lane and step (U loads in flight)
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
   const int lane = threadIdx.x & 63;
   for (int64_t ub = u0 + (int64_t)blockIdx.x * blockDim.x * U; ub < u1; ub += stride) {
@@ -106,15 +106,7 @@ __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ se
     for (int j = 0; j < U; ++j) {
       const int64_t p0 = (ub + j * blockDim.x + threadIdx.x) * 16;
       v[j] = make_uint4(0, 0, 0, 0);
-      if (p0 + 16 <= total) {
-        if (kNT) {
-          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-          const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(seq + p0));
-          v[j] = make_uint4(q.x, q.y, q.z, q.w);
-        } else {
-          v[j] = *reinterpret_cast<const uint4 *>(seq + p0);
-        }
-      }
+      if (p0 + 16 <= total) v[j] = *reinterpret_cast<const uint4 *>(seq + p0);
       pb[j] = 'N';
       if (kPre && lane == 0 && p0 > 0 && p0 - 1 < total) pb[j] = seq[p0 - 1];
     }
@@ -337,21 +329,8 @@ ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs
     const int64_t u1 = std::min<int64_t>(nunits, p_hi / 16 + 1 + kMargin);
     const unsigned grid = (unsigned)std::max<int64_t>(
         1, std::min<int64_t>((u1 - u0 + 1023) / 1024, (int64_t)ctx->num_cus * 16));
-    // KS_NEV_VARIANT (A/B): 0 four units per lane and step, 1 eight, 2 eight with nontemporal loads
-    const char *nv = getenv("KS_NEV_VARIANT");
-    const int var = nv ? atoi(nv) : 0;
-    if (var == 1)
-      hipLaunchKernelGGL((k_n_events<true, true, 8, false>), dim3(grid), dim3(256), 0, st, s->seq, total,
-                         (unsigned long long *)evp, d_count, cap, packed, p_lo, p_hi, u0, u1);
-    else if (var == 2)
-      hipLaunchKernelGGL((k_n_events<true, true, 8, true>), dim3(grid), dim3(256), 0, st, s->seq, total,
-                         (unsigned long long *)evp, d_count, cap, packed, p_lo, p_hi, u0, u1);
-    else if (var == 3)
-      hipLaunchKernelGGL((k_n_events<true, true, 4, true>), dim3(grid), dim3(256), 0, st, s->seq, total,
-                         (unsigned long long *)evp, d_count, cap, packed, p_lo, p_hi, u0, u1);
-    else
-      hipLaunchKernelGGL((k_n_events<true, true>), dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp,
-                         d_count, cap, packed, p_lo, p_hi, u0, u1);
+    hipLaunchKernelGGL((k_n_events<true, true>), dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp,
+                       d_count, cap, packed, p_lo, p_hi, u0, u1);
     KS_HIP(hipGetLastError());
     if (s->nseq > 1) {
       hipLaunchKernelGGL(k_seq_events, dim3((unsigned)((s->nseq + 255) / 256)), dim3(256), 0, st, s->seq, total,

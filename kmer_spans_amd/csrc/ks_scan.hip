@@ -35,7 +35,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                            double min_score, uint32_t *visits, const RegionBuf &out,
                            const unsigned long long *d_cnt = nullptr, int64_t segcap = 0,
                            const ScanMode &mode = ScanMode(), int init_step = 1, const int64_t *offs = nullptr,
-                           const uint32_t *packed = nullptr);
+                           const uint32_t *packed = nullptr, const uint32_t *perm = nullptr);
 
 namespace {
 
@@ -43,12 +43,10 @@ namespace {
 // sequential state machine consumes them, so a lane keeps several random
 // table reads in flight instead of one (the gathers do not depend on S).
 // With an expanded table one read serves J consecutive indices (the
-// (k+J-1)-mer spanning them), as in the chunked gather pass.  kPf: the next
-// batch's reads are issued before the current batch is consumed (a restart
-// drops them), so a long rescan -- one lane alone in its wave for most of
-// the kernel, the weighted-rank tail -- waits for one table round trip per
-// two batches instead of one per batch.
-template <int J, bool kCompressed, int GW = 0, bool kPf = false>
+// (k+J-1)-mer spanning them), as in the chunked gather pass.  (Issuing the
+// next batch's reads before a batch is consumed measured no faster on the
+// weighted-rank rescans: 3.94 vs 3.64 ms, profiles/r4/ab/ab_rank.txt.)
+template <int J, bool kCompressed, int GW = 0>
 __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ seq, int64_t total,
                                                   const int64_t *__restrict__ ra,
                                                   const int64_t *__restrict__ rbnd,
@@ -56,14 +54,16 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
                                                   int k, TableView tv, uint64_t mw, double min_score,
                                                   uint32_t *__restrict__ visits, RegionBuf out,
                                                   const unsigned long long *__restrict__ d_cnt, int64_t segcap,
-                                                  const uint32_t *__restrict__ packed) {
+                                                  const uint32_t *__restrict__ packed,
+                                                  const uint32_t *__restrict__ perm) {
   // reads per batch (GW: a wider batch -- FP64 line tables, 8 line reads = 32 indices per round trip:
   // weighted-rank rescans 3.76 -> 3.61 ms in-process, profiles/r3/rank/lane_ab.txt)
   constexpr int G = GW ? GW : ((J == 1) ? 16 : (J >= 4 ? 4 : (J == 3 ? 6 : 8)));
   constexpr int PB = G * J;                                           // indices per batch (16, 16, 18, 16, 20)
   using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;  // (k+J-1)-mer code
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nruns) return;
+  const int64_t r0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r0 >= nruns) return;
+  const int64_t r = perm ? (int64_t)perm[r0] : r0;  // (perm: the slots in length order)
   if (d_cnt && (r % segcap) >= (int64_t)d_cnt[r / segcap]) return;  // segmented list: unused slot
   const int64_t a = ra[r], b = rbnd[r];
   if (b - a <= k) return;
@@ -103,13 +103,9 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
     bool restart = false;
     double v[PB];
     GC gc[G];
-    if (kPf && i + k < b) gather(i + k, v, gc);
     for (int64_t p0 = i + k; p0 < b && !restart; p0 += PB) {
       const int n = (int)((b - p0) < PB ? (b - p0) : PB);
-      double vn[PB];
-      GC gn[G];
-      if (!kPf) gather(p0, v, gc);
-      else if (p0 + PB < b) gather(p0 + PB, vn, gn);
+      gather(p0, v, gc);
 #pragma unroll
       for (int j = 0; j < PB; ++j) {  // fully unrolled: v[]/gc[] stay in registers
         if (j < n && !restart) {
@@ -133,12 +129,6 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
             prev = S;
           }
         }
-      }
-      if (kPf) {
-#pragma unroll
-        for (int j = 0; j < PB; ++j) v[j] = vn[j];
-#pragma unroll
-        for (int g = 0; g < G; ++g) gc[g] = gn[g];
       }
     }
     if (restart) continue;
@@ -303,7 +293,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
                            const unsigned long long *d_cnt, int64_t segcap, const ScanMode &mode, int init_step,
-                           const int64_t *offs, const uint32_t *packed) {
+                           const int64_t *offs, const uint32_t *packed, const uint32_t *perm) {
   if (n <= 0) return KS_OK;
   // line tables: own + 1 indices per read (gather_group's line form)
   const int J = tv.line ? tv.line_own + 1 : (tv.ext ? tv.ext_J : 1);
@@ -322,30 +312,12 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
   }
 #define KS_LANE(J, C)                                                                                   \
   hipLaunchKernelGGL((k_scan_lane<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, total, \
-                     ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed)
+                     ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed, perm)
   if (tv.compressed) {
     if (J == 6) KS_LANE(6, true); else if (J == 5) KS_LANE(5, true); else if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
   } else if (J == 4 && tv.line) {
-    // (KS_LANE_PF=1, A/B: the next batch's line reads in flight while a batch is consumed)
-    if (getenv("KS_LANE_PF") && atoi(getenv("KS_LANE_PF")) != 0)
-      hipLaunchKernelGGL((k_scan_lane<4, false, 8, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream,
-                         seq, total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed);
-    else
-      hipLaunchKernelGGL((k_scan_lane<4, false, 8>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq,
-                         total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed);
-  } else if (!tv.compressed && J >= 2 && J <= 5 && getenv("KS_LANE_PF") && atoi(getenv("KS_LANE_PF")) != 0) {
-    if (J == 4) hipLaunchKernelGGL((k_scan_lane<4, false, 0, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
-                                   ctx->stream, seq, total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt,
-                                   segcap, packed);
-    else if (J == 3) hipLaunchKernelGGL((k_scan_lane<3, false, 0, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
-                                        ctx->stream, seq, total, ra, rb, rs, n, k, tv, mw, min_score, visits, out,
-                                        d_cnt, segcap, packed);
-    else if (J == 2) hipLaunchKernelGGL((k_scan_lane<2, false, 0, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
-                                        ctx->stream, seq, total, ra, rb, rs, n, k, tv, mw, min_score, visits, out,
-                                        d_cnt, segcap, packed);
-    else hipLaunchKernelGGL((k_scan_lane<5, false, 0, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
-                            ctx->stream, seq, total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap,
-                            packed);  // (J = 5: FP64 lines of own 4)
+    hipLaunchKernelGGL((k_scan_lane<4, false, 8>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq,
+                       total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed, perm);
   } else {
     if (J == 5) KS_LANE(5, false); else if (J == 4) KS_LANE(4, false); else if (J == 3) KS_LANE(3, false); else if (J == 2) KS_LANE(2, false); else KS_LANE(1, false);
   }

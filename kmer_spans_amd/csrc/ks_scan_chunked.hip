@@ -44,7 +44,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                            double min_score, uint32_t *visits, const RegionBuf &out,
                            const unsigned long long *d_cnt = nullptr, int64_t segcap = 0,
                            const ScanMode &mode = ScanMode(), int init_step = 1, const int64_t *offs = nullptr,
-                           const uint32_t *packed = nullptr);
+                           const uint32_t *packed = nullptr, const uint32_t *perm = nullptr);
 
 namespace {
 
@@ -612,11 +612,10 @@ struct PredWords {
 // d_approx, <= 128 KiB in LDS, one block per CU), rolled from the packed
 // bases; a max-plus scan of them (k_approx_scan) predicts each chunk's entry,
 // i.e. the binade pass 1 summarises in.  Only a prediction: a wrong binade
-// costs one gathered summary (k_summ_fixw), never a result.  One block per
-// CU (4 waves per SIMD) hides little latency, so kPf software-pipelines the
-// grid-stride loop: the next chunk's packed words and the start / length of
-// the one after it are in flight while a chunk is summed.
-template <int PS, bool kPf = false>
+// costs one gathered summary (k_summ_fixw), never a result.  (A
+// software-pipelined loop -- the next chunk's words in flight while one is
+// summed -- measured the same: profiles/r4/ab/ab_log2.txt.)
+template <int PS>
 __global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k, const uint16_t *__restrict__ approx, int kp,
                                                   double *__restrict__ pa, double *__restrict__ pb) {
   __shared__ __half s_ap[1 << 16];
@@ -650,42 +649,11 @@ __global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k
     pa[c] = tsum;
     pb[c] = tex;
   };
-  int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (!kPf) {
-    for (; c < g.nch; c += stride) {
-      PredWords W;
-      const int64_t q0 = g.start[c] - k;  // index i's k-mer prefix: bases [q0 + i, q0 + i + kp)
-      W.load(packed, total, q0);
-      sum_chunk(W, q0, g.n[c], c);
-    }
-    return;
-  }
-  if (c >= g.nch) return;
-  int64_t q0 = g.start[c] - k;
-  int n = g.n[c];
-  PredWords W;
-  W.load(packed, total, q0);
-  int64_t c1 = c + stride;
-  int64_t q1 = 0;
-  int n1 = 0;
-  if (c1 < g.nch) {
-    q1 = g.start[c1] - k;
-    n1 = g.n[c1];
-  }
-  for (;;) {
-    PredWords W1;
-    const int64_t c2 = c1 + stride;
-    int64_t q2 = 0;
-    int n2 = 0;
-    if (c1 < g.nch) W1.load(packed, total, q1);
-    if (c2 < g.nch) {
-      q2 = g.start[c2] - k;
-      n2 = g.n[c2];
-    }
-    sum_chunk(W, q0, n, c);
-    if (c1 >= g.nch) break;
-    c = c1; q0 = q1; n = n1; W = W1;
-    c1 = c2; q1 = q2; n1 = n2;
+  for (int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < g.nch; c += stride) {
+    PredWords W;
+    const int64_t q0 = g.start[c] - k;  // index i's k-mer prefix: bases [q0 + i, q0 + i + kp)
+    W.load(packed, total, q0);
+    sum_chunk(W, q0, g.n[c], c);
   }
 }
 
@@ -3528,6 +3496,22 @@ __global__ void __launch_bounds__(256) k_stitch_emit(Chunks g, const int64_t *__
 
 // Candidates (closed emittable excursions of the clean trajectories) are
 // valid when they begin at or after their chunk's valid_from.
+// Rescan order: the slots of the segmented rescan list keyed by length,
+// longest first (unused slots last), so that the lanes of a wave walk about
+// as far as each other and the longest walks start first.  Weighted rank at
+// the metric genome: 1.09 M rescans of 32-4520 indices (182 M in all) in
+// list order left most lanes of a wave idle behind its longest one.
+__global__ void k_rescan_keys(const int64_t *__restrict__ ra, const int64_t *__restrict__ rb,
+                              const unsigned long long *__restrict__ cnt, int64_t segcap, int64_t n,
+                              uint16_t *__restrict__ key, uint32_t *__restrict__ idx) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const bool used = (r % segcap) < (int64_t)cnt[r / segcap];
+  const int64_t len = used ? rb[r] - ra[r] : 0;
+  key[r] = (uint16_t)(0xffff - (len < 0xffff ? len : 0xffff));
+  idx[r] = (uint32_t)r;
+}
+
 __global__ void k_candidates(Chunks g, const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase,
                              int64_t nruns, const int32_t *__restrict__ rseq, EmitCfg ec, Cand cand,
                              Carry cr, RegionBuf out, Rescan rs) {
@@ -3729,11 +3713,13 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // tables on the pipelined pass with a binade predictor (a table without
   // one, a failed allocation of the predictor, is scanned unexpanded)
   const bool line = tv.line != nullptr && !lds_table && runs.packed != nullptr;  // line table: k_pass1l
-  // (FP64 line tables, weighted rank, too: KS_F64_P1SUMM=0 leaves their
-  // summaries to k_summaries after the prescan, the former path, for A/B runs)
-  // (and FP64 expanded tables, k_pass1pf: weighted rank at k = 14, 15)
-  const bool f64_summ = !comp && (line || (!lds_table && Jt >= 2 && Jt <= 4)) &&
-                        !(getenv("KS_F64_P1SUMM") && atoi(getenv("KS_F64_P1SUMM")) == 0);
+  // (FP64 expanded tables, k_pass1pf: weighted rank at k = 14, 15 -- 57.4 vs
+  // 63.2 ms at k = 15; FP64 line tables (k <= 13) measured slower with them,
+  // 32.3 vs 30.3 ms at config 3, so they keep k_summaries unless
+  // KS_F64_P1SUMM=1; KS_F64_P1SUMM=0 turns both off: profiles/r4/ab/)
+  const char *f64e = getenv("KS_F64_P1SUMM");
+  const bool f64_summ = !comp && !lds_table &&
+                        (f64e ? atoi(f64e) != 0 && (line || (Jt >= 2 && Jt <= 4)) : (!line && Jt >= 2 && Jt <= 4));
   // (small k, the table in LDS: KS_LDS_P1SUMM=0 leaves the summaries to
   // k_summaries with the LDS-staged table, the former path)
   const bool lds_summ = lds_table && !(getenv("KS_LDS_P1SUMM") && atoi(getenv("KS_LDS_P1SUMM")) == 0);
@@ -3788,39 +3774,27 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     pp.asum = reinterpret_cast<double *>(W + o_pa);
     pp.cexit = reinterpret_cast<double *>(W + o_pb);
     pp.special = reinterpret_cast<uint8_t *>(W + o_pz);
-    // KS_PREDICT_PF=1 (A/B): the software-pipelined predictor loop
-    const bool pred_pf = getenv("KS_PREDICT_PF") && atoi(getenv("KS_PREDICT_PF")) != 0;
     auto predict = [&](const Half &h, hipStream_t strm) -> ks_status {
       KS_HIP(hipMemsetAsync(W + o_pz + h.c0, 0, (size_t)(h.c1 - h.c0), strm));
       const unsigned gl =
           (unsigned)std::max<int64_t>(1, std::min<int64_t>((h.c1 - h.c0 + 1023) / 1024, ctx->num_cus));
       // every second index sampled (A/B: every 4th / 8th changed nothing)
-      if (pred_pf)
-        hipLaunchKernelGGL((k_predict<2, true>), dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx,
-                           tv.approx_k, pp.asum, pp.cexit);
-      else
-        hipLaunchKernelGGL((k_predict<2, false>), dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx,
-                           tv.approx_k, pp.asum, pp.cexit);
+      hipLaunchKernelGGL(k_predict<2>, dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx, tv.approx_k,
+                         pp.asum, pp.cexit);
       KS_HIP(hipGetLastError());
       return ascan(pp, d_xh, h.r0, h.r1, h.t0, h.t1, strm);
     };
     // the first half's predictor and prescan first (they gate its pass 1;
     // the predictor holds whole CUs: 128 KiB of LDS per block), then the
-    // second half's on the side stream, under the first half's pass 1
-    // Below ~1 Gbp (4 M chunks) both halves' predictors run first, on the main
-    // stream: the second half's, queued beside the first half's pass 1, took
-    // 1.02 ms there against 0.09 ms alone and held back its own pass 1 (8-way
-    // shard timeline, profiles/r3/timelines/shard8_step_timeline.txt).
-    // KS_PREDICT_BOTH_FIRST=0/1 overrides (A/B).
-    const char *bf = getenv("KS_PREDICT_BOTH_FIRST");
-    const bool both_first = split && (bf ? atoi(bf) != 0 : nch <= ((int64_t)4 << 20));
+    // second half's on the side stream, under the first half's pass 1 (also
+    // at shard sizes: both first on the main stream measured 2.48 vs 2.38 ms
+    // at the 8-way shard, profiles/r4/ab/ab_shard8.txt)
     KS_TRY(predict(halves[0], st));
     if (split) {
       side_forked = true;
-      if (both_first) KS_TRY(predict(halves[1], st));
       KS_HIP(hipEventRecord(ctx->ev[16], st));
       KS_HIP(hipStreamWaitEvent(ctx->side, ctx->ev[16], 0));
-      if (!both_first) KS_TRY(predict(halves[1], ctx->side));
+      KS_TRY(predict(halves[1], ctx->side));
     }
   }
   KS_HIP(hipEventRecord(ctx->ev[8], st));
@@ -4207,8 +4181,31 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                      nruns, runs.seq, ec, cand, cr, rb, rs);
   KS_HIP(hipGetLastError());
   KS_HIP(hipEventRecord(ctx->ev[10], st));
+  // FP64 tables (weighted rank: many rescans, 3.6 ms of lane walks at config
+  // 3) take their rescans longest first; KS_RESCAN_SORT=0/1 overrides (A/B)
+  const uint32_t *perm = nullptr;
+  {
+    const char *rse = getenv("KS_RESCAN_SORT");
+    const bool sort_res = (rse ? atoi(rse) != 0 : !comp) && !mode.trlr && rcap < ((int64_t)1 << 31);
+    if (sort_res) {
+      void *kb = nullptr, *tmp = nullptr;
+      KS_TRY(ensure(ctx, SLOT_WORK_B, (size_t)rcap * 12 + 1024, &kb));
+      uint16_t *k_in = static_cast<uint16_t *>(kb);
+      uint16_t *k_out = k_in + ((rcap + 127) & ~(int64_t)127);
+      uint32_t *i_in = reinterpret_cast<uint32_t *>(k_out + ((rcap + 127) & ~(int64_t)127));
+      uint32_t *i_out = i_in + rcap;
+      size_t tb = 0;
+      KS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k_in, k_out, i_in, i_out, (int)rcap, 0, 16, st));
+      KS_TRY(ensure(ctx, SLOT_SORT_TMP, tb + 16, &tmp));
+      hipLaunchKernelGGL(k_rescan_keys, dim3((unsigned)((rcap + 255) / 256)), dim3(256), 0, st, rs.a, rs.b, rs.count,
+                         rs.segcap, rcap, k_in, i_in);
+      KS_HIP(hipGetLastError());
+      KS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k_in, k_out, i_in, i_out, (int)rcap, 0, 16, st));
+      perm = i_out;
+    }
+  }
   KS_TRY(launch_scan_lane(ctx, s->seq, total, rs.a, rs.b, rs.seq, rcap, k, tv, mw, min_score, visits_rescan, rb,
-                          rs.count, rs.segcap, mode, 0, nullptr, runs.packed));
+                          rs.count, rs.segcap, mode, 0, nullptr, runs.packed, perm));
   KS_HIP(hipEventRecord(ctx->ev[11], st));
   // the region counters too (final: the rescans above append the last
   // regions), copied next to the scan's counters: one readback for both, and

@@ -778,6 +778,10 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
   if (!jmax_env) {  // line tables first (k_pass1l); KS_NO_LINES: the (k+J-1)-mer forms below
     bool built = false;
     KS_TRY(table_lines(ctx, t, budget, freq_dev, &built));
+    // (complete on return, the predictor included: a table may be scanned
+    // from another context's stream, e.g. genome g + 1's table built while
+    // genome g is scanned)
+    if (built) KS_HIP(hipStreamSynchronize(ctx->stream));
     if (built) return KS_OK;
   }
   // candidates, best first: (J, code bits); (k+J-1)-mer indices up to 34 bits
@@ -856,6 +860,7 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
     t->d_lut12 = nullptr;
   }
   KS_TRY(build_approx(ctx, t, freq_dev));
+  KS_HIP(hipStreamSynchronize(ctx->stream));  // (complete on return, as above)
   t->d_ext = ext;
   t->ext_J = J;
   t->ext_bits = bits;
@@ -883,7 +888,7 @@ ks_status ks::table_create(ks_ctx *ctx, const double *w_host, int32_t k, double 
   const int32_t allow_compress = flags & KS_TABLE_COMPRESS;
   if (!ctx || !w_host || !out) return fail(KS_ERR_ARG, "ks_table_create: null argument");
   if (k < 1 || k > KS_MAX_K) return fail(KS_ERR_ARG, "k must be between 1 and %d", KS_MAX_K);
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   const double t_start = now_ms();
   const int64_t n = (int64_t)1 << (2 * k);
   hipStream_t st = ctx->stream;
@@ -990,7 +995,7 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
   if (k < 1 || k > KS_MAX_K) return fail(KS_ERR_ARG, "k must be between 1 and %d", KS_MAX_K);
   if (score != KS_SCORE_LOG2 && score != KS_SCORE_PM1 && score != KS_SCORE_RANK)
     return fail(KS_ERR_ARG, "ks_table_from_counts: unknown score %d", score);
-  KS_TRY(activate(ctx));
+  KS_ENTER(ctx);
   const double t_start = now_ms();
   const int64_t n = (int64_t)1 << (2 * k);
   hipStream_t st = ctx->stream;

@@ -167,13 +167,12 @@ def test_rank_expanded_pass1_summaries(oracle, monkeypatch, k, jmax):
     assert not tab.compressed and tab.positions_per_read == jmax
     o = oracle.scan(host, k, w.cpu().numpy(), 0.6, 50, 5.0, visits=True)
     ctx.set_scan_algo(1)
-    for summ, lane_pf in (("1", "0"), ("0", "0"), ("1", "1")):
+    for summ in ("1", "0"):
         monkeypatch.setenv("KS_F64_P1SUMM", summ)
-        monkeypatch.setenv("KS_LANE_PF", lane_pf)  # the prefetching rescan lane kernel
         vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
         pos, sc, st = D.scan(ctx, ds, k, tab, 50, 5.0, vis)
-        _same(pos, sc, o, ("rank expanded", k, jmax, summ, lane_pf))
-        assert np.array_equal(vis.cpu().numpy(), o["counts"]), ("rank expanded visits", k, jmax, summ, lane_pf)
+        _same(pos, sc, o, ("rank expanded", k, jmax, summ))
+        assert np.array_equal(vis.cpu().numpy(), o["counts"]), ("rank expanded visits", k, jmax, summ)
     ctx.set_scan_algo(-1)
     assert o["pos"].shape[1] > 0
     tab.close()

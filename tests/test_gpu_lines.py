@@ -49,13 +49,14 @@ def test_line_forms(oracle, setup, monkeypatch, k, cap, own_u16, own_f64, score)
     wh = w.cpu().numpy()
     o = oracle.scan(host, k, wh, thr, 100 if score != "pm1" else 20, 20.0 if score != "pm1" else 5.0, visits=True)
     mw, ms = (100, 20.0) if score != "pm1" else (20, 5.0)
-    for route in ("count", "atomic", "lane_pf"):
-        if route == "atomic":
+    for route in ("count", "atomic", "f64summ"):
+        if route == "atomic":  # (and the rescans in length order on every table)
             monkeypatch.setenv("KS_VISITS_ATOMIC", "1")
-        if route == "lane_pf":  # the prefetching rescan lane kernel
+            monkeypatch.setenv("KS_RESCAN_SORT", "1")
+        if route == "f64summ":  # FP64 lines with pass-1 summaries (off by default)
             if score != "rank":
                 continue
-            monkeypatch.setenv("KS_LANE_PF", "1")
+            monkeypatch.setenv("KS_F64_P1SUMM", "1")
         ctx.set_scan_algo(1)
         vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
         pos, sc, st = D.scan(ctx, ds, k, tab, mw, ms, vis)
@@ -63,7 +64,8 @@ def test_line_forms(oracle, setup, monkeypatch, k, cap, own_u16, own_f64, score)
         _same(pos, sc, o["pos"], o["score"], (score, k, cap, route))
         assert np.array_equal(vis.cpu().numpy(), o["counts"]), (score, k, cap, route, "visits")
         monkeypatch.delenv("KS_VISITS_ATOMIC", raising=False)
-        monkeypatch.delenv("KS_LANE_PF", raising=False)
+        monkeypatch.delenv("KS_F64_P1SUMM", raising=False)
+        monkeypatch.delenv("KS_RESCAN_SORT", raising=False)
     ctx.set_scan_algo(-1)
     tab.close()
 

@@ -8,24 +8,28 @@ cd $R
 P=${2:-ab}
 AB="timeout -k 10 600 python -u tools/ab_inproc.py"
 if [[ $P == *a* ]]; then
-$AB --rounds 3 --steps 3 nev0: nev1:KS_NEV_VARIANT=1 nev2:KS_NEV_VARIANT=2 nev3:KS_NEV_VARIANT=3 --out $O/ab_nev.json > $O/ab_nev.txt 2>&1 || { tail -30 $O/ab_nev.txt; exit 1; }
-tail -5 $O/ab_nev.txt
-$AB --rounds 3 --steps 2 --score rank one: nosumm:KS_F64_P1SUMM=0 lanepf:KS_LANE_PF=1 --out $O/ab_rank.json > $O/ab_rank.txt 2>&1 || { tail -30 $O/ab_rank.txt; exit 1; }
+$AB --rounds 3 --steps 2 --score rank one: nosort:KS_RESCAN_SORT=0 summ:KS_F64_P1SUMM=1 --out $O/ab_rank.json > $O/ab_rank.txt 2>&1 || { tail -30 $O/ab_rank.txt; exit 1; }
 tail -4 $O/ab_rank.txt
-$AB --rounds 3 --steps 3 one: pf:KS_PREDICT_PF=1 p55:KS_PARTS_FRAC=0.55 --out $O/ab_log2.json > $O/ab_log2.txt 2>&1 || { tail -30 $O/ab_log2.txt; exit 1; }
+$AB --rounds 3 --steps 3 one: sort:KS_RESCAN_SORT=1 --out $O/ab_log2.json > $O/ab_log2.txt 2>&1 || { tail -30 $O/ab_log2.txt; exit 1; }
 tail -4 $O/ab_log2.txt
-$AB --rounds 3 --steps 3 --shard-of 8 one:KS_PREDICT_BOTH_FIRST=0 bf: bfpf:KS_PREDICT_PF=1 --out $O/ab_shard8.json > $O/ab_shard8.txt 2>&1 || { tail -30 $O/ab_shard8.txt; exit 1; }
+$AB --rounds 3 --steps 3 --shard-of 8 one: --out $O/ab_shard8.json > $O/ab_shard8.txt 2>&1 || { tail -30 $O/ab_shard8.txt; exit 1; }
 tail -4 $O/ab_shard8.txt
 fi
 if [[ $P == *b* ]]; then
+$AB --rounds 2 --steps 2 --k 15 --score rank one: nosumm:KS_F64_P1SUMM=0 --out $O/ab_k15rank.json > $O/ab_k15rank.txt 2>&1 || { tail -30 $O/ab_k15rank.txt; exit 1; }
+tail -3 $O/ab_k15rank.txt
+$AB --rounds 2 --steps 3 --k 15 --score log2 one: --out $O/ab_k15log2.json > $O/ab_k15log2.txt 2>&1 || { tail -30 $O/ab_k15log2.txt; exit 1; }
+tail -2 $O/ab_k15log2.txt
 $AB --rounds 3 --steps 3 --k 7 --score pm1 summ: old:KS_LDS_P1SUMM=0 --out $O/ab_k7pm1.json > $O/ab_k7pm1.txt 2>&1 || { tail -30 $O/ab_k7pm1.txt; exit 1; }
 tail -3 $O/ab_k7pm1.txt
 $AB --rounds 3 --steps 3 --k 7 --score log2 summ: old:KS_LDS_P1SUMM=0 --out $O/ab_k7log2.json > $O/ab_k7log2.txt 2>&1 || { tail -30 $O/ab_k7log2.txt; exit 1; }
 tail -3 $O/ab_k7log2.txt
 KS_DEBUG_CARRY=1 timeout -k 10 300 python -u tools/ab_inproc.py --rounds 1 --steps 1 --score rank dbg: > $O/rank_debug.txt 2>&1 || { tail -30 $O/rank_debug.txt; exit 1; }
 grep -E "^\[(carry|rescan|p1summ|replay)" $O/rank_debug.txt | head -12
+fi
+if [[ $P == *g* ]]; then
 B="timeout -k 10 600 python -u bench.py --mode genomes --genomes-per-rank 4"
-$B --out $O/genomes_pipe32.json > $O/genomes_pipe32.log 2>&1 || { tail -30 $O/genomes_pipe32.log; exit 1; }
+$B --no-cpu --out $O/genomes_pipe32.json > $O/genomes_pipe32.log 2>&1 || { tail -30 $O/genomes_pipe32.log; exit 1; }
 $B --no-cpu --ext-max-gib 64 --out $O/genomes_pipe64.json > $O/genomes_pipe64.log 2>&1 || { tail -30 $O/genomes_pipe64.log; exit 1; }
 $B --no-cpu --genomes-serial --out $O/genomes_serial32.json > $O/genomes_serial32.log 2>&1 || { tail -30 $O/genomes_serial32.log; exit 1; }
 python3 -c "

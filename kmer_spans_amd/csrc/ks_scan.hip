@@ -35,7 +35,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                            double min_score, uint32_t *visits, const RegionBuf &out,
                            const unsigned long long *d_cnt = nullptr, int64_t segcap = 0,
                            const ScanMode &mode = ScanMode(), int init_step = 1, const int64_t *offs = nullptr,
-                           const uint32_t *packed = nullptr, const uint32_t *perm = nullptr);
+                           const uint32_t *packed = nullptr);
 
 namespace {
 
@@ -54,16 +54,14 @@ __global__ void __launch_bounds__(64) k_scan_lane(const uint8_t *__restrict__ se
                                                   int k, TableView tv, uint64_t mw, double min_score,
                                                   uint32_t *__restrict__ visits, RegionBuf out,
                                                   const unsigned long long *__restrict__ d_cnt, int64_t segcap,
-                                                  const uint32_t *__restrict__ packed,
-                                                  const uint32_t *__restrict__ perm) {
+                                                  const uint32_t *__restrict__ packed) {
   // reads per batch (GW: a wider batch -- FP64 line tables, 8 line reads = 32 indices per round trip:
   // weighted-rank rescans 3.76 -> 3.61 ms in-process, profiles/r3/rank/lane_ab.txt)
   constexpr int G = GW ? GW : ((J == 1) ? 16 : (J >= 4 ? 4 : (J == 3 ? 6 : 8)));
   constexpr int PB = G * J;                                           // indices per batch (16, 16, 18, 16, 20)
   using GC = typename std::conditional<(J >= 3), uint64_t, uint32_t>::type;  // (k+J-1)-mer code
-  const int64_t r0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r0 >= nruns) return;
-  const int64_t r = perm ? (int64_t)perm[r0] : r0;  // (perm: the slots in length order)
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nruns) return;
   if (d_cnt && (r % segcap) >= (int64_t)d_cnt[r / segcap]) return;  // segmented list: unused slot
   const int64_t a = ra[r], b = rbnd[r];
   if (b - a <= k) return;
@@ -293,7 +291,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
                            const unsigned long long *d_cnt, int64_t segcap, const ScanMode &mode, int init_step,
-                           const int64_t *offs, const uint32_t *packed, const uint32_t *perm) {
+                           const int64_t *offs, const uint32_t *packed) {
   if (n <= 0) return KS_OK;
   // line tables: own + 1 indices per read (gather_group's line form)
   const int J = tv.line ? tv.line_own + 1 : (tv.ext ? tv.ext_J : 1);
@@ -312,12 +310,12 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
   }
 #define KS_LANE(J, C)                                                                                   \
   hipLaunchKernelGGL((k_scan_lane<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, total, \
-                     ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed, perm)
+                     ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed)
   if (tv.compressed) {
     if (J == 6) KS_LANE(6, true); else if (J == 5) KS_LANE(5, true); else if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
   } else if (J == 4 && tv.line) {
     hipLaunchKernelGGL((k_scan_lane<4, false, 8>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq,
-                       total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed, perm);
+                       total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed);
   } else {
     if (J == 5) KS_LANE(5, false); else if (J == 4) KS_LANE(4, false); else if (J == 3) KS_LANE(3, false); else if (J == 2) KS_LANE(2, false); else KS_LANE(1, false);
   }

@@ -44,7 +44,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                            double min_score, uint32_t *visits, const RegionBuf &out,
                            const unsigned long long *d_cnt = nullptr, int64_t segcap = 0,
                            const ScanMode &mode = ScanMode(), int init_step = 1, const int64_t *offs = nullptr,
-                           const uint32_t *packed = nullptr, const uint32_t *perm = nullptr);
+                           const uint32_t *packed = nullptr);
 
 namespace {
 
@@ -355,10 +355,13 @@ __device__ __forceinline__ void values16_f64(const Chunks &g, const uint8_t *__r
 }
 
 // Values of scan indices i0 .. i0+3 of chunk c (0 past n): one 8-byte code
-// load (compressed) or one k-mer prime plus three rolls.
+// load (compressed) or one k-mer prime plus three rolls.  start: the chunk's
+// first scan index (g.start[c]), loaded by the caller ahead of time; xin
+// (have_x): the 64 packed bits from base start + i0 - k, prefetched.
 __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
                                         const TableView &tv, const uint16_t *__restrict__ codes, int64_t c,
-                                        int i0, int n, double v[4]) {
+                                        int64_t start, int i0, int n, double v[4], bool have_x = false,
+                                        uint64_t xin = 0) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) v[q] = 0.0;
   if (i0 >= n) return;
@@ -370,18 +373,19 @@ __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restri
       if (i0 + q < n) v[q] = tv.lut[(cw[q >> 1] >> (16 * (q & 1))) & 0xffffu];
     return;
   }
-  const int64_t p = g.start[c] + i0;
+  const int64_t p = start + i0;
   if (tv.line) {  // line table: OWN + 1 indices per read
-    uint64_t xp = 0;
-    if (packed_bits(g.packed, total, p - k, xp)) {
+    uint64_t xp = xin;
+    if (have_x || packed_bits(g.packed, total, p - k, xp)) {
       line_values_any<4>(tv, xp, k, i0, n, v, nullptr);
       return;
     }
   }
   if (!tv.compressed && tv.ext && tv.ext_J == 4) {  // FP64 expanded table: the 4 values in one 32-B entry
-    uint64_t xp = 0;
-    const uint64_t gcode = packed_bits(g.packed, total, p - k, xp) ? (xp >> (64 - 2 * (k + 3)))
-                                                                    : prime_code_guarded64(seq, p - k, k + 3, total);
+    uint64_t xp = xin;
+    const uint64_t gcode = (have_x || packed_bits(g.packed, total, p - k, xp))
+                               ? (xp >> (64 - 2 * (k + 3)))
+                               : prime_code_guarded64(seq, p - k, k + 3, total);
     const double2 *E = reinterpret_cast<const double2 *>(tv.ext);
     const double2 e0 = E[2 * gcode], e1 = E[2 * gcode + 1];
     const double ev[4] = {e0.x, e0.y, e1.x, e1.y};
@@ -2724,8 +2728,11 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
   // per-lane inputs of one 64-chunk tile; the next tile's are loaded before
   // the current one is processed (all loads independent: hides their latency
   // behind the tile's scan)
+  // (start: a replay's first memory round trip -- chunk start, then its
+  // packed bases, then the table -- is taken here, with the tile's loads)
   struct TileIn {
     double exit, pmin, sabs;
+    int64_t start;
     int spec, n, se, rs;
     long long D[2], M[2], N[2];
     int A[2];
@@ -2739,6 +2746,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
     t.sabs = o.sabs[cc];
     t.spec = live ? o.special[cc] : 1;
     t.n = live ? g.n[cc] : 0;
+    t.start = g.start[cc];
     t.rs = (live && rp.slot) ? rp.slot[cc] : -1;
     const int se = sm.e[cc];
     t.se = live ? se : INT32_MIN;
@@ -2756,6 +2764,12 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
   load_tile(c0, tile_end(c0), cur);
   long long t_fast = 0, t_rep = 0;  // diagnostics: cycles in fast tiles, in replays
   bool try_batch = true;
+  // the packed bases of the chunk after a replayed one, loaded under that
+  // replay's table reads (replays come in runs where the carry crosses
+  // binades): pf_c = the chunk they belong to, pf_ok = packed_bits' result
+  int64_t pf_c = -1;
+  bool pf_ok = false;
+  uint64_t pf_x = 0;
   for (int64_t cb = c0; cb < c1;) {
     const long long tt0 = dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
     // Tile batch: up to 64 whole tiles at once from their composites (the
@@ -2913,7 +2927,14 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
           v[2] = b.x;
           v[3] = b.y;
         } else {
-          values4(g, seq, total, k, tv, kCompressed ? codes : nullptr, cj, 4 * lane, n, v);
+          const bool hx = !kCompressed && pf_c == cj && pf_ok;
+          values4(g, seq, total, k, tv, kCompressed ? codes : nullptr, cj, rl64(cur.start, j), 4 * lane, n, v, hx,
+                  pf_x);
+        }
+        if (!kCompressed && cj + 1 < c1) {  // the next chunk's packed bases, under this replay's reads
+          const int64_t stn = (j + 1 < nb) ? rl64(cur.start, j + 1) : rl64(nxt.start, 0);
+          pf_ok = packed_bits(g.packed, total, stn + 4 * lane - k, pf_x);
+          pf_c = cj + 1;
         }
         double T = x, hmax = -1.0;
         int hq = -1, harg = 0;
@@ -3496,22 +3517,6 @@ __global__ void __launch_bounds__(256) k_stitch_emit(Chunks g, const int64_t *__
 
 // Candidates (closed emittable excursions of the clean trajectories) are
 // valid when they begin at or after their chunk's valid_from.
-// Rescan order: the slots of the segmented rescan list keyed by length,
-// longest first (unused slots last), so that the lanes of a wave walk about
-// as far as each other and the longest walks start first.  Weighted rank at
-// the metric genome: 1.09 M rescans of 32-4520 indices (182 M in all) in
-// list order left most lanes of a wave idle behind its longest one.
-__global__ void k_rescan_keys(const int64_t *__restrict__ ra, const int64_t *__restrict__ rb,
-                              const unsigned long long *__restrict__ cnt, int64_t segcap, int64_t n,
-                              uint16_t *__restrict__ key, uint32_t *__restrict__ idx) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  const bool used = (r % segcap) < (int64_t)cnt[r / segcap];
-  const int64_t len = used ? rb[r] - ra[r] : 0;
-  key[r] = (uint16_t)(0xffff - (len < 0xffff ? len : 0xffff));
-  idx[r] = (uint32_t)r;
-}
-
 __global__ void k_candidates(Chunks g, const int64_t *__restrict__ ra, const int64_t *__restrict__ cbase,
                              int64_t nruns, const int32_t *__restrict__ rseq, EmitCfg ec, Cand cand,
                              Carry cr, RegionBuf out, Rescan rs) {
@@ -4181,31 +4186,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                      nruns, runs.seq, ec, cand, cr, rb, rs);
   KS_HIP(hipGetLastError());
   KS_HIP(hipEventRecord(ctx->ev[10], st));
-  // FP64 tables (weighted rank: many rescans, 3.6 ms of lane walks at config
-  // 3) take their rescans longest first; KS_RESCAN_SORT=0/1 overrides (A/B)
-  const uint32_t *perm = nullptr;
-  {
-    const char *rse = getenv("KS_RESCAN_SORT");
-    const bool sort_res = (rse ? atoi(rse) != 0 : !comp) && !mode.trlr && rcap < ((int64_t)1 << 31);
-    if (sort_res) {
-      void *kb = nullptr, *tmp = nullptr;
-      KS_TRY(ensure(ctx, SLOT_WORK_B, (size_t)rcap * 12 + 1024, &kb));
-      uint16_t *k_in = static_cast<uint16_t *>(kb);
-      uint16_t *k_out = k_in + ((rcap + 127) & ~(int64_t)127);
-      uint32_t *i_in = reinterpret_cast<uint32_t *>(k_out + ((rcap + 127) & ~(int64_t)127));
-      uint32_t *i_out = i_in + rcap;
-      size_t tb = 0;
-      KS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k_in, k_out, i_in, i_out, (int)rcap, 0, 16, st));
-      KS_TRY(ensure(ctx, SLOT_SORT_TMP, tb + 16, &tmp));
-      hipLaunchKernelGGL(k_rescan_keys, dim3((unsigned)((rcap + 255) / 256)), dim3(256), 0, st, rs.a, rs.b, rs.count,
-                         rs.segcap, rcap, k_in, i_in);
-      KS_HIP(hipGetLastError());
-      KS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k_in, k_out, i_in, i_out, (int)rcap, 0, 16, st));
-      perm = i_out;
-    }
-  }
+  // (the rescan slots in list order: sorted longest first they took 5.23 vs
+  // 3.56 ms at config 3, profiles/r4/ab2/ab_rank.txt)
   KS_TRY(launch_scan_lane(ctx, s->seq, total, rs.a, rs.b, rs.seq, rcap, k, tv, mw, min_score, visits_rescan, rb,
-                          rs.count, rs.segcap, mode, 0, nullptr, runs.packed, perm));
+                          rs.count, rs.segcap, mode, 0, nullptr, runs.packed));
   KS_HIP(hipEventRecord(ctx->ev[11], st));
   // the region counters too (final: the rescans above append the last
   // regions), copied next to the scan's counters: one readback for both, and

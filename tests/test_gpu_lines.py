@@ -50,9 +50,8 @@ def test_line_forms(oracle, setup, monkeypatch, k, cap, own_u16, own_f64, score)
     o = oracle.scan(host, k, wh, thr, 100 if score != "pm1" else 20, 20.0 if score != "pm1" else 5.0, visits=True)
     mw, ms = (100, 20.0) if score != "pm1" else (20, 5.0)
     for route in ("count", "atomic", "f64summ"):
-        if route == "atomic":  # (and the rescans in length order on every table)
+        if route == "atomic":
             monkeypatch.setenv("KS_VISITS_ATOMIC", "1")
-            monkeypatch.setenv("KS_RESCAN_SORT", "1")
         if route == "f64summ":  # FP64 lines with pass-1 summaries (off by default)
             if score != "rank":
                 continue
@@ -65,7 +64,6 @@ def test_line_forms(oracle, setup, monkeypatch, k, cap, own_u16, own_f64, score)
         assert np.array_equal(vis.cpu().numpy(), o["counts"]), (score, k, cap, route, "visits")
         monkeypatch.delenv("KS_VISITS_ATOMIC", raising=False)
         monkeypatch.delenv("KS_F64_P1SUMM", raising=False)
-        monkeypatch.delenv("KS_RESCAN_SORT", raising=False)
     ctx.set_scan_algo(-1)
     tab.close()
 

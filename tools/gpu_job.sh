@@ -8,9 +8,9 @@ cd $R
 P=${2:-ab}
 AB="timeout -k 10 600 python -u tools/ab_inproc.py"
 if [[ $P == *a* ]]; then
-$AB --rounds 3 --steps 2 --score rank one: nosort:KS_RESCAN_SORT=0 summ:KS_F64_P1SUMM=1 --out $O/ab_rank.json > $O/ab_rank.txt 2>&1 || { tail -30 $O/ab_rank.txt; exit 1; }
+$AB --rounds 3 --steps 2 --score rank one: --out $O/ab_rank.json > $O/ab_rank.txt 2>&1 || { tail -30 $O/ab_rank.txt; exit 1; }
 tail -4 $O/ab_rank.txt
-$AB --rounds 3 --steps 3 one: sort:KS_RESCAN_SORT=1 --out $O/ab_log2.json > $O/ab_log2.txt 2>&1 || { tail -30 $O/ab_log2.txt; exit 1; }
+$AB --rounds 3 --steps 3 one: --out $O/ab_log2.json > $O/ab_log2.txt 2>&1 || { tail -30 $O/ab_log2.txt; exit 1; }
 tail -4 $O/ab_log2.txt
 $AB --rounds 3 --steps 3 --shard-of 8 one: --out $O/ab_shard8.json > $O/ab_shard8.txt 2>&1 || { tail -30 $O/ab_shard8.txt; exit 1; }
 tail -4 $O/ab_shard8.txt
@@ -37,4 +37,12 @@ import json
 for n in ('genomes_pipe32','genomes_pipe64','genomes_serial32'):
     b=json.load(open('$O/'+n+'.json')); print(n, b['value'], b['ms_per_step'], b.get('parity_sample'))
 "
+fi
+if [[ $P == *p* ]]; then
+timeout -k 10 300 python -u tools/genome_phases.py --ext-gib 32 > $O/phases32.txt 2>&1 || { tail -30 $O/phases32.txt; exit 1; }
+tail -1 $O/phases32.txt
+timeout -k 10 300 python -u tools/genome_phases.py --ext-gib 140 > $O/phases140.txt 2>&1 || { tail -30 $O/phases140.txt; exit 1; }
+tail -1 $O/phases140.txt
+$AB --rounds 2 --steps 2 --k 15 --score rank one: --out $O/ab_k15rank.json > $O/ab_k15rank.txt 2>&1 || { tail -30 $O/ab_k15rank.txt; exit 1; }
+tail -2 $O/ab_k15rank.txt
 fi

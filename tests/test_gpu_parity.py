@@ -14,8 +14,15 @@ def _regions_from(pos, score):
     return [(int(pos[0][i]), int(pos[1][i]), int(pos[2][i]), float(score[0][i])) for i in range(pos.shape[1])]
 
 
+def _diff(a_pos, a_score, b_pos, b_score):
+    """Records only in a / only in b (for the failure message)."""
+    ra = {tuple(c) + (float(s),) for c, s in zip(a_pos.T.tolist(), a_score[0].tolist())}
+    rb = {tuple(c) + (float(s),) for c, s in zip(b_pos.T.tolist(), b_score[0].tolist())}
+    return {"only_gpu": sorted(ra - rb)[:6], "only_ref": sorted(rb - ra)[:6]}
+
+
 def _assert_same_regions(a_pos, a_score, b_pos, b_score, what=""):
-    assert a_pos.shape == b_pos.shape, (what, a_pos.shape, b_pos.shape)
+    assert a_pos.shape == b_pos.shape, (what, a_pos.shape, b_pos.shape, _diff(a_pos, a_score, b_pos, b_score))
     assert np.array_equal(a_pos, b_pos), what
     # bitwise FP64 equality of the scores
     assert np.array_equal(a_score.view(np.uint64), b_score.view(np.uint64)), what
@@ -94,6 +101,10 @@ def test_random_regions_vs_oracle(K, oracle, ctx, algo):
             k, seqs, w, mw, ms = _random_inputs(rng)
             g = K.kmer_regions(seqs, k, w, mw, ms)
             o = oracle.kmer_regions(seqs, k, w, mw, ms)
+            if g["pos"].shape != o["pos"].shape or not np.array_equal(g["pos"], o["pos"]):
+                # a failure that does not repeat: the same call again, 3 times
+                again = [K.kmer_regions(seqs, k, w, mw, ms)["pos"].shape for _ in range(3)]
+                print("random case mismatch", (k, mw, ms, [len(s) for s in seqs]), "again", again)
             _assert_same_regions(g["pos"], g["score"], o["pos"], o["score"], (seqs, k, mw, ms))
             assert np.array_equal(g["counts"], o["counts"])
             assert g["n"] == o["n"]

@@ -6,9 +6,13 @@ each bracketed by a device sync, on one human-shaped genome, repeated.
 """
 import argparse
 import json
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():

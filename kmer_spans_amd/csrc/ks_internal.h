@@ -141,6 +141,10 @@ struct ks_table {
   double ms_total = 0;
   bool no_nan_posinf = true;    // no s is NaN or +Inf (-Inf allowed: it clamps to 0)
   double max_abs = 0.0;         // max |s| over the finite values
+  // every s is a finite integer of magnitude <= 2^20 (+-1 tables, integer
+  // scores): FP64 sums of up to 2^32 of them are exact, so the chunked scan's
+  // max-plus prescan is the exact carry (no binade summaries, no replays)
+  bool int_exact = false;
   // Narrow codes (ext_bits = 12, J = 5): the uint16 codes are numbered by
   // position weight, so the 4095 values covering most positions have codes
   // 0..4094, which are also their 12-bit codes (d_map12 is the identity,

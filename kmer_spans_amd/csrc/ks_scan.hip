@@ -362,7 +362,8 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
   const bool line = t->line_kind != 0;
   TableView tv{t->d_vals,  t->d_codes,   t->d_lut,     t->compressed ? 1 : 0, line ? nullptr : t->d_ext,
                line ? 1 : t->ext_J, (int)t->distinct, t->ext_bits, t->d_lut12, t->d_map12, t->d_approx, t->approx_k,
-               line ? static_cast<const uint8_t *>(t->d_ext) : nullptr, t->line_kind, t->line_own};
+               line ? static_cast<const uint8_t *>(t->d_ext) : nullptr, t->line_kind, t->line_own,
+               t->int_exact ? 1 : 0};
   const uint64_t mw = (uint64_t)(int64_t)min_width;
   int algo = ctx->scan_algo;
   if (algo < 0) algo = (longest > (1 << 15)) ? 1 : 0;

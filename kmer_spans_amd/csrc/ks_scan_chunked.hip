@@ -65,6 +65,7 @@ struct P1 {  // per-chunk results of the gather pass
   double *cexit, *asum, *pmin, *pmax, *sabs, *tmax;
   int32_t *tbeg, *targ;  // trailing open excursion (relative), tbeg = -1: none
   uint8_t *special;      // a non-finite value occurred
+  int32_t *parg;         // first index of the prefix maximum pmax
 };
 
 struct Summ {  // binade-integer summaries for the predicted binade (P2)
@@ -717,6 +718,7 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
   double prev = 0.0, best = 0.0;
   int beg = -1, arg = 0;
   double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
+  int parg = 0;
   bool special = false;
   for (int b0 = 0; b0 < n; b0 += PB) {
     uint8_t by[32];  // bytes rolled in by groups 1..G: start + b0 + J - 1 + [0, PB)
@@ -796,6 +798,7 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
         const double s = v[j];
         asum += s;
         pmin = fmin(pmin, asum);
+        parg = asum > pmax ? i : parg;
         pmax = fmax(pmax, asum);
         sabs += fabs(s);
         special |= !isfinite(s);
@@ -825,6 +828,7 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
   o.asum[c] = asum;
   o.pmin[c] = pmin;
   o.pmax[c] = pmax;
+  o.parg[c] = parg;
   o.sabs[c] = sabs;
   o.special[c] = special ? 1 : 0;
   if (prev > 0) {
@@ -957,6 +961,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
   double prev = 0.0, best = 0.0;
   int beg = -1, arg = 0;
   double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
+  int parg = 0;
   bool special = false;
   // The binade-integer summary of this chunk for the binade of its
   // predicted entry xh (k_predict), single trajectory: s rounded to the binade's
@@ -973,7 +978,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
   int sarg = 0, sarg2 = 0;
   bool sbad = false, sbad2 = false;
   {
-    const double x = xh[c];
+    const double x = xh ? xh[c] : 0.0;  // (no predictor: no summaries)
     if (x >= kP1SumMin && x < 1.0e15) {
       se = binade_of(x);
       sC = 1.5 * ldexp(1.0, se);
@@ -1069,6 +1074,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
           // signalling NaN and a NaN asum never replaces the extreme)
           asum += s;
           pmin = asum < pmin ? asum : pmin;
+          parg = asum > pmax ? i : parg;
           pmax = asum > pmax ? asum : pmax;
           sabs += fabs(s);
           special |= !isfinite(s);
@@ -1155,6 +1161,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
   o.asum[c] = asum;
   o.pmin[c] = pmin;
   o.pmax[c] = pmax;
+  o.parg[c] = parg;
   o.sabs[c] = sabs;
   o.special[c] = special ? 1 : 0;
   if (prev > 0) {
@@ -1214,6 +1221,7 @@ struct P1Lane {
   double prev = 0.0, best = 0.0;
   int beg = -1, arg = 0;
   double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
+  int parg = 0;
   bool special = false;
   int se = INT32_MIN, se2 = INT32_MIN;
   double sC = 0.0, sH = 0.0, scur = 0.0, smx = -INFINITY;
@@ -1243,6 +1251,7 @@ struct P1Lane {
   __device__ __forceinline__ void step(double s, int i, const EmitCfg &ec, const Cand &cand) {
     asum += s;
     pmin = asum < pmin ? asum : pmin;
+    parg = asum > pmax ? i : parg;
     pmax = asum > pmax ? asum : pmax;
     sabs += fabs(s);
     special |= !isfinite(s);
@@ -1310,6 +1319,7 @@ struct P1Lane {
     o.asum[c] = asum;
     o.pmin[c] = pmin;
     o.pmax[c] = pmax;
+    o.parg[c] = parg;
     o.sabs[c] = sabs;
     o.special[c] = special ? 1 : 0;
     if (prev > 0) {
@@ -1546,7 +1556,7 @@ __global__ void __launch_bounds__(kWideBlock) k_pass1w(Chunks g, int64_t total, 
   const bool first = live && (c == 0 || g.run[c - 1] != g.run[c]);
   const uint32_t kmask = (1u << (2 * k)) - 1u;
   P1Lane<true, kTrlr> L;
-  L.init(start, n, first, live, live ? xh[c] : 0.0);
+  L.init(start, n, first, live, (live && xh) ? xh[c] : 0.0);
   LaneBases B;
   B.load(g.packed, total, start - k);
   const int kx = k + J - 1;  // key length (<= 18)
@@ -1728,6 +1738,7 @@ __global__ void __launch_bounds__(1024) k_pass1_lds(Chunks g, int64_t total, int
     double prev = 0.0, best = 0.0;
     int beg = -1, arg = 0;
     double asum = 0.0, pmin = INFINITY, pmax = -INFINITY, sabs = 0.0;
+    int parg = 0;
     bool special = false;
     for (int b0 = 0; b0 < n; b0 += 16) {
       const uint3 nxt = load3(q0 + b0 + 16);
@@ -1742,6 +1753,7 @@ __global__ void __launch_bounds__(1024) k_pass1_lds(Chunks g, int64_t total, int
         if (visits) atomicAdd(&visits[code], 1u);
         asum += s;
         pmin = asum < pmin ? asum : pmin;
+        parg = asum > pmax ? i : parg;
         pmax = asum > pmax ? asum : pmax;
         sabs += fabs(s);
         special |= !isfinite(s);
@@ -1777,6 +1789,7 @@ __global__ void __launch_bounds__(1024) k_pass1_lds(Chunks g, int64_t total, int
     o.asum[c] = asum;
     o.pmin[c] = pmin;
     o.pmax[c] = pmax;
+    o.parg[c] = parg;
     o.sabs[c] = sabs;
     o.special[c] = special ? 1 : 0;
     if (prev > 0) {
@@ -2995,6 +3008,31 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
   }
 }
 
+// Exact carry (tables of small integers, ks_table::int_exact): every partial
+// sum is exact in FP64, so the max-plus prescan xt (k_ascan_*) is the exact
+// entry of every chunk -- max(x + sum, clean exit) composes exactly -- and a
+// chunk's carried head follows from its pass-1 aggregates: entered at 0, the
+// clean trajectory; no clamp (x + prefix min > 0), the trajectory x + prefix
+// with its maximum x + pmax first reached at parg (mode L); else mode R (the
+// head up to the clamp: k_heads).  Replaces the predictor, the binade
+// summaries and the replays.
+__global__ void __launch_bounds__(256) k_carry_exact(Chunks g, P1 o, const double *__restrict__ xt, Carry cr) {
+  const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= g.nch) return;
+  const double x = xt[c];
+  cr.x[c] = x;
+  if (x == 0.0) {
+    cr.mode[c] = (uint8_t)kModeClean;
+  } else if (x + o.pmin[c] > 0.0) {
+    cr.mode[c] = (uint8_t)kModeL;
+    cr.hq[c] = -1;
+    cr.hmax[c] = x + o.pmax[c];
+    cr.harg[c] = o.parg[c];
+  } else {
+    cr.mode[c] = (uint8_t)kModeR;
+  }
+}
+
 // Tile composites (TileComp) of the global tiles of chunks [g.c0, g.nch):
 // one wave per tile, from the final summaries (after k_summ_fixw).  Also
 // clears the batch marks (ee) of the range.
@@ -3570,7 +3608,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const size_t o_n = off; off += al(nch * 4);
   const size_t o_run = off; off += al(nch * 4);
   const size_t o_p1d = off; off += al(nch * 8 * 6);
-  const size_t o_p1i = off; off += al(nch * 4 * 2);
+  const size_t o_p1i = off; off += al(nch * 4 * 3);
   const size_t o_spec = off; off += al(nch);
   const size_t o_xt = off; off += al(nch * 8);
   const size_t o_se = off; off += al(nch * 4);
@@ -3615,7 +3653,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   double *p1d = reinterpret_cast<double *>(W + o_p1d);
   int32_t *p1i = reinterpret_cast<int32_t *>(W + o_p1i);
   P1 p1{p1d, p1d + nch, p1d + 2 * nch, p1d + 3 * nch, p1d + 4 * nch, p1d + 5 * nch, p1i, p1i + nch,
-        reinterpret_cast<uint8_t *>(W + o_spec)};
+        reinterpret_cast<uint8_t *>(W + o_spec), p1i + 2 * nch};
   double *xt = reinterpret_cast<double *>(W + o_xt);
   long long *sD = reinterpret_cast<long long *>(W + o_sD);
   Summ sm{reinterpret_cast<int32_t *>(W + o_se), sD, sD + 2 * nch, sD + 4 * nch,
@@ -3728,15 +3766,18 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // (small k, the table in LDS: KS_LDS_P1SUMM=0 leaves the summaries to
   // k_summaries with the LDS-staged table, the former path)
   const bool lds_summ = lds_table && !(getenv("KS_LDS_P1SUMM") && atoi(getenv("KS_LDS_P1SUMM")) == 0);
-  const bool p1summ = (lds_table ? lds_summ : (comp ? (Jt >= 2 || line) : f64_summ)) && runs.packed != nullptr &&
-                      tv.approx != nullptr;
+  // integer tables: the exact carry (k_carry_exact) needs no predictor and
+  // no summaries (KS_NO_EXACT: the general path, for A/B runs and tests)
+  const bool exact = tv.exact && !mode.trlr && runs.packed != nullptr && getenv("KS_NO_EXACT") == nullptr;
+  const bool p1summ = !exact && (lds_table ? lds_summ : (comp ? (Jt >= 2 || line) : f64_summ)) &&
+                      runs.packed != nullptr && tv.approx != nullptr;
   // (the carry reads no replay slots unless k_marks_select wrote them)
   if (!p1summ) rpb.slot = nullptr;
   // per-index code store (uint16 per scan index, 2 B x 256 per chunk):
   // written by the compressed unexpanded pass 1 (k_pass1<1, ...>) for the
   // binade summaries (k_summaries)
   uint16_t *codes = nullptr;
-  if (comp && !p1summ && !lds_table) {
+  if (comp && !p1summ && !exact && !lds_table) {
     void *cp = nullptr;
     const int64_t ctiles = (nch + 63) / 64;  // code store tiles (global chunk index / 64)
     KS_TRY(ensure(ctx, SLOT_CHUNK_B, (size_t)ctiles * 64 * CH * 2, &cp));
@@ -3756,7 +3797,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // one part; serialising the two pass-1 launches 31.8-32.0 by split
   // fraction: profiles/r3/rank/split_ab.txt)
   const bool f64_line = line && !comp;
-  const bool split = !ctx->no_split && (p1summ || f64_line) && lay.split_r > 0 && lay.split_r < nruns &&
+  const bool split = !ctx->no_split && (p1summ || exact || f64_line) && lay.split_r > 0 && lay.split_r < nruns &&
                      lay.split_c >= 1024 && lay.split_c + 1024 <= ctail_all;
   Half halves[2];
   int nhalf = 1;
@@ -3816,16 +3857,16 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   hipLaunchKernelGGL((k_pass1<J, C, L>), dim3((unsigned)((nch - ctail + 1023) / 1024)), dim3(1024), 0, side, g, \
                      s->seq, total, k, tv, p1summ ? nullptr : codes, ec, visits, p1, cand, ctail, 1)
   // compressed tables are scanned expanded only on the summarising pass
-  const int J = (tv.ext != nullptr && (p1summ || !comp)) ? tv.ext_J : 1;
+  const int J = (tv.ext != nullptr && (p1summ || exact || !comp)) ? tv.ext_J : 1;
   const bool pipelined = runs.packed != nullptr;
 #define KS_P1P(J, L, GV, GRID, STRM)                                                                           \
   do {                                                                                                       \
     if (ec.trlr)                                                                                             \
       hipLaunchKernelGGL((k_pass1p<J, L, true>), dim3(GRID), dim3(kP1Block), 0, STRM, GV, s->seq, total, k, tv, \
-                         ec, visits, p1, cand, runs.packed, d_xh, sp1);                                      \
+                         ec, visits, p1, cand, runs.packed, p1summ ? d_xh : nullptr, sp1);                   \
     else                                                                                                     \
       hipLaunchKernelGGL((k_pass1p<J, L, false>), dim3(GRID), dim3(kP1Block), 0, STRM, GV, s->seq, total, k, tv, \
-                         ec, visits, p1, cand, runs.packed, d_xh, sp1);                                      \
+                         ec, visits, p1, cand, runs.packed, p1summ ? d_xh : nullptr, sp1);                   \
   } while (0)
   if (lds_table) {
     // small k: the whole table in LDS, persistent blocks (one per CU), no
@@ -3854,7 +3895,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       p1lds(halves[0], st);
     }
     codes = nullptr;
-  } else if (line && (p1summ || !comp)) {
+  } else if (line && (p1summ || exact || !comp)) {
     // line tables: every chunk (no tail: a lane's bases come from guarded loads)
     const bool lut = tv.nlut <= kLineLutMax;
 #define KS_P1L(O, F, L, GV, GRID, STRM)                                                                        \
@@ -3875,10 +3916,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   do {                                                                                                      \
     if (ec.trlr)                                                                                            \
       hipLaunchKernelGGL((k_pass1w<O, true>), dim3(grid), dim3(kWideBlock), 0, strm, gv, total, k, tv, ec, visits, \
-                         p1, cand, d_xh, sp1);                                                              \
+                         p1, cand, p1summ ? d_xh : nullptr, sp1);                                           \
     else                                                                                                    \
       hipLaunchKernelGGL((k_pass1w<O, false>), dim3(grid), dim3(kWideBlock), 0, strm, gv, total, k, tv, ec, visits, \
-                         p1, cand, d_xh, sp1);                                                              \
+                         p1, cand, p1summ ? d_xh : nullptr, sp1);                                           \
   } while (0)
         if (own == 1) KS_P1W(1);  // k = 15 (J = 4)
         else if (own == 2) KS_P1W(2);  // k = 14 (J = 5)
@@ -3965,7 +4006,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
     }
     KS_HIP(hipGetLastError());
-  } else if (p1summ) {
+  } else if (p1summ || exact) {
     // the tail chunks (a latency-bound serial walk each) run on the side
     // stream, overlapped with the pipelined pass (of the last half)
     hipStream_t side = ctx->side;
@@ -4058,12 +4099,14 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     const int64_t wl = (h.c0 > 0 ? h.c0 - 1 : 0) / 64;
     const int64_t nwm = (h.c1 + 63) / 64 - wl;
     // segment marks and summary selection in one pass over the chunks
-    if (!p1summ) {
+    if (!p1summ && !exact) {
       hipLaunchKernelGGL(k_seg_marks, dim3((unsigned)((nwm + wpb - 1) / wpb)), dim3(64 * wpb), 0, strm, gv, p1, xt,
                          d_flag, nwm);
       KS_HIP(hipGetLastError());
     }
-    if (p1summ) {
+    if (exact) {  // the prescan is the carry (k_carry_exact)
+      hipLaunchKernelGGL(k_carry_exact, dim3(gch_h), dim3(256), 0, strm, gv, p1, xt, cr);
+    } else if (p1summ) {
       KS_HIP(hipMemsetAsync(d_nfix + hi, 0, 8, strm));
       KS_HIP(hipMemsetAsync(rpb.count + hi, 0, 8, strm));
       hipLaunchKernelGGL(k_marks_select, dim3((unsigned)((nwm + 3) / 4)), dim3(256), 0, strm, gv, p1, xt, d_flag, nwm,
@@ -4109,18 +4152,19 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     const unsigned nwc = (unsigned)((h.c1 - 1) / 64 - wc + 1);
     const TileComp tch = tcomp;
     const unsigned gtc = (unsigned)(((h.c1 - 1) / 64 - wc + 1 + 3) / 4);  // 4 tiles per block
-    {
+    if (!exact) {
       hipLaunchKernelGGL(k_tile_comp, dim3(gtc), dim3(256), 0, strm, gv, sm, tch);
       KS_HIP(hipGetLastError());
     }
-    if (comp)
+    if (exact) {
+    } else if (comp)
       hipLaunchKernelGGL(k_carry_win<true>, dim3((nwc + wpb - 1) / wpb), dim3(64 * wpb), 0, strm, gv, d_flag, s->seq, total, k, tv, codes, p1,
                          sm, cr, tch, rpb, rep_h, err_h, dbg);
     else
       hipLaunchKernelGGL(k_carry_win<false>, dim3((nwc + wpb - 1) / wpb), dim3(64 * wpb), 0, strm, gv, d_flag, s->seq, total, k, tv, codes,
                          p1, sm, cr, tch, rpb, rep_h, err_h, dbg);
     KS_HIP(hipGetLastError());
-    {
+    if (!exact) {
       hipLaunchKernelGGL(k_tile_apply, dim3(gtc), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 0);
       KS_HIP(hipGetLastError());
     }
@@ -4140,8 +4184,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     };
     heads(0);
     KS_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_fallback_prep, dim3(1), dim3(1), 0, strm, err_h, rep_h, force_fb);
-    if (nr > 0) {
+    if (!exact) hipLaunchKernelGGL(k_fallback_prep, dim3(1), dim3(1), 0, strm, err_h, rep_h, force_fb);
+    if (nr > 0 && !exact) {
       if (comp)
         hipLaunchKernelGGL(k_carry_run<true>, dim3((unsigned)nr), dim3(64), 0, strm, gv, d_cbase, h.r1, s->seq, total,
                            k, tv, codes, p1, sm, cr, tch, rpb, rep_h, err_h, nullptr, h.r0);
@@ -4150,7 +4194,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                            total, k, tv, codes, p1, sm, cr, tch, rpb, rep_h, err_h, nullptr, h.r0);
       hipLaunchKernelGGL(k_tile_apply, dim3(gtc), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 1);
     }
-    heads(1);
+    if (!exact) heads(1);
     KS_HIP(hipGetLastError());
     if (last) KS_HIP(hipEventRecord(ctx->ev[15], strm));
 

@@ -23,6 +23,7 @@ struct TableView {
   const uint8_t *line;     // line table (ks_table line_kind), nullptr if absent; ext is then nullptr
   int line_kind;           // 1: uint16 codes, 2: FP64 values
   int line_own;
+  int exact;               // ks_table::int_exact
 };
 
 // LUT entries that fit the LDS copy used by the streaming passes (64 KiB).

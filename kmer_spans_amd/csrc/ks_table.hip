@@ -32,22 +32,26 @@ __global__ void k_sub_thr(const double *__restrict__ w, double thr, double *__re
   }
 }
 
-// max |s| over the finite values (as the bits of a non-negative double) and
-// a flag for NaN or +Inf (-Inf only ever clamps to 0).
+// max |s| over the finite values (as the bits of a non-negative double), a
+// flag for NaN or +Inf (-Inf only ever clamps to 0) and a flag for any s
+// that is not a finite integer of magnitude <= 2^20 (ks_table::int_exact).
 __global__ void k_absmax(const double *__restrict__ s, int64_t n, unsigned long long *__restrict__ out) {
-  unsigned long long m = 0, bad = 0;
+  unsigned long long m = 0, bad = 0, nonint = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const double v = s[i];
     if (isfinite(v)) m = max(m, (unsigned long long)__double_as_longlong(fabs(v)));
     else if (!(v < 0)) bad = 1;  // NaN or +Inf
+    if (!(isfinite(v) && v == rint(v) && fabs(v) <= 0x1p20)) nonint = 1;
   }
   for (int d = 32; d >= 1; d >>= 1) {
     m = max(m, (unsigned long long)__shfl_down(m, d, 64));
     bad |= __shfl_down(bad, d, 64);
+    nonint |= __shfl_down(nonint, d, 64);
   }
   if ((threadIdx.x & 63) == 0) {
     atomicMax(&out[0], m);
     if (bad) atomicOr(&out[1], 1ull);
+    if (nonint) atomicOr(&out[2], 1ull);
   }
 }
 
@@ -934,14 +938,15 @@ ks_status ks::table_create(ks_ctx *ctx, const double *w_host, int32_t k, double 
   hipLaunchKernelGGL(k_sub_thr, dim3(grid), dim3(256), 0, st, d_w, thr, t->d_vals, d_bits, n);
   KS_TBL_HIP(hipGetLastError());
   {  // finiteness and magnitude (tr_lr decides between the chunked and the literal path)
-    unsigned long long *d_am = nullptr, h_am[2] = {0, 0};
-    KS_TBL_HIP(hipMalloc(&d_am, 16));
-    KS_TBL_HIP(hipMemsetAsync(d_am, 0, 16, st));
+    unsigned long long *d_am = nullptr, h_am[3] = {0, 0, 0};
+    KS_TBL_HIP(hipMalloc(&d_am, 24));
+    KS_TBL_HIP(hipMemsetAsync(d_am, 0, 24, st));
     hipLaunchKernelGGL(k_absmax, dim3(grid), dim3(256), 0, st, t->d_vals, n, d_am);
-    KS_TBL_HIP(hipMemcpyAsync(h_am, d_am, 16, hipMemcpyDeviceToHost, st));
+    KS_TBL_HIP(hipMemcpyAsync(h_am, d_am, 24, hipMemcpyDeviceToHost, st));
     KS_TBL_HIP(hipStreamSynchronize(st));
     KS_TBL_HIP(hipFree(d_am));
     t->no_nan_posinf = h_am[1] == 0;
+    t->int_exact = h_am[2] == 0;
     double ma = 0;
     memcpy(&ma, &h_am[0], 8);
     t->max_abs = ma;
@@ -1112,17 +1117,18 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
     KS_TFC(hipMalloc(&t->d_vals, n * sizeof(double)));
     hipLaunchKernelGGL(k_sub_thr, dim3(grid), dim3(256), 0, st, d_w, thr, t->d_vals, nullptr, n);
     KS_TFC(hipGetLastError());
-    unsigned long long *d_am = static_cast<unsigned long long *>(dalloc(16)), h_am[2] = {0, 0};
+    unsigned long long *d_am = static_cast<unsigned long long *>(dalloc(24)), h_am[3] = {0, 0, 0};
     if (!d_am) {
       cleanup();
       ks_table_destroy(t);
       return fail(KS_ERR_NOMEM, "ks_table_from_counts: device allocation failed");
     }
-    KS_TFC(hipMemsetAsync(d_am, 0, 16, st));
+    KS_TFC(hipMemsetAsync(d_am, 0, 24, st));
     hipLaunchKernelGGL(k_absmax, dim3(grid), dim3(256), 0, st, t->d_vals, n, d_am);
-    KS_TFC(hipMemcpyAsync(h_am, d_am, 16, hipMemcpyDeviceToHost, st));
+    KS_TFC(hipMemcpyAsync(h_am, d_am, 24, hipMemcpyDeviceToHost, st));
     KS_TFC(hipStreamSynchronize(st));
     t->no_nan_posinf = h_am[1] == 0;
+    t->int_exact = h_am[2] == 0;
     memcpy(&t->max_abs, &h_am[0], 8);
     t->ms_upload = now_ms() - t_start;
   } else {
@@ -1132,14 +1138,16 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
     score_of_counts(score == KS_SCORE_LOG2 ? 1 : 2, dv.data(), dm.data(), nu, wv.data());
     std::vector<uint64_t> sb(nu);
     double ma = 0.0;
-    bool bad = false;
+    bool bad = false, nonint = false;
     for (int i = 0; i < nu; ++i) {
       sv[i] = wv[i] - thr;
       memcpy(&sb[i], &sv[i], 8);
       if (std::isfinite(sv[i])) ma = std::max(ma, std::fabs(sv[i]));
       else if (!(sv[i] < 0)) bad = true;
+      if (!(std::isfinite(sv[i]) && sv[i] == std::rint(sv[i]) && std::fabs(sv[i]) <= 0x1p20)) nonint = true;
     }
     t->no_nan_posinf = !bad;
+    t->int_exact = !nonint;
     t->max_abs = ma;
     std::vector<uint64_t> ub(sb);
     std::sort(ub.begin(), ub.end());

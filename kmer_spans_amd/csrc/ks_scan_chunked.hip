@@ -3768,7 +3768,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const bool lds_summ = lds_table && !(getenv("KS_LDS_P1SUMM") && atoi(getenv("KS_LDS_P1SUMM")) == 0);
   // integer tables: the exact carry (k_carry_exact) needs no predictor and
   // no summaries (KS_NO_EXACT: the general path, for A/B runs and tests)
-  const bool exact = tv.exact && !mode.trlr && runs.packed != nullptr && getenv("KS_NO_EXACT") == nullptr;
+  // (on the table forms of the pipelined passes -- LDS, line, expanded; an
+  // unexpanded table of another size takes the code-store pass and k_summaries)
+  const bool exact = tv.exact && !mode.trlr && runs.packed != nullptr && (lds_table || line || Jt >= 2) &&
+                     getenv("KS_NO_EXACT") == nullptr;
   const bool p1summ = !exact && (lds_table ? lds_summ : (comp ? (Jt >= 2 || line) : f64_summ)) &&
                       runs.packed != nullptr && tv.approx != nullptr;
   // (the carry reads no replay slots unless k_marks_select wrote them)

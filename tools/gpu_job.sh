@@ -47,10 +47,10 @@ $AB --rounds 2 --steps 2 --k 15 --score rank one: --out $O/ab_k15rank.json > $O/
 tail -2 $O/ab_k15rank.txt
 fi
 if [[ $P == *x* ]]; then
-$AB --rounds 3 --steps 3 --k 7 --score pm1 exact: gen:KS_NO_EXACT=1 --out $O/ab_k7pm1_exact.json > $O/ab_k7pm1_exact.txt 2>&1 || { tail -30 $O/ab_k7pm1_exact.txt; exit 1; }
+$AB --rounds 3 --steps 3 --k 7 --score pm1 one: split:KS_EXACT_SPLIT=1 --out $O/ab_k7pm1_exact.json > $O/ab_k7pm1_exact.txt 2>&1 || { tail -30 $O/ab_k7pm1_exact.txt; exit 1; }
 tail -2 $O/ab_k7pm1_exact.txt
-$AB --rounds 3 --steps 3 --score pm1 exact: gen:KS_NO_EXACT=1 --out $O/ab_pm1_exact.json > $O/ab_pm1_exact.txt 2>&1 || { tail -30 $O/ab_pm1_exact.txt; exit 1; }
+$AB --rounds 3 --steps 3 --score pm1 one: split:KS_EXACT_SPLIT=1 --out $O/ab_pm1_exact.json > $O/ab_pm1_exact.txt 2>&1 || { tail -30 $O/ab_pm1_exact.txt; exit 1; }
 tail -2 $O/ab_pm1_exact.txt
-$AB --rounds 3 --steps 3 one: --out $O/ab_log2.json > $O/ab_log2.txt 2>&1 || { tail -30 $O/ab_log2.txt; exit 1; }
-tail -1 $O/ab_log2.txt
+$AB --rounds 4 --steps 3 one: shfl:KS_NEV_SHFL=1 --out $O/ab_log2.json > $O/ab_log2.txt 2>&1 || { tail -30 $O/ab_log2.txt; exit 1; }
+tail -2 $O/ab_log2.txt
 fi

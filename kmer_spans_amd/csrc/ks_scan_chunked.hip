@@ -3618,7 +3618,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const size_t o_mode = off; off += al(nch);
   const size_t o_hq = off; off += al(nch * 4 * 2);
   const size_t o_hmax = off; off += al(nch * 8);
-  const size_t o_cnt = off; off += al(8 * (3 * kSegs + 8));  // + the region counters' copy
+  const size_t o_cnt = off; off += al(8 * (5 * kSegs + 8));  // + the region counters' copy, half 1's lists
   const size_t o_flag = off; off += al(nch + 64);
   const size_t o_xagg = off; off += al(ntiles * 32) * 2;
   // pass-1 summaries: predictor sums / exits / zero flags, predicted entries,
@@ -3707,29 +3707,43 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   unsigned long long *d_nfix = reinterpret_cast<unsigned long long *>(W + o_fix);  // [2]: one per half
   int64_t *d_fix = reinterpret_cast<int64_t *>(W + o_fix + 16);
   // cnts: [0, kSegs) candidate counters, [kSegs, 2 kSegs) rescan counters,
-  // [2 kSegs + 2h] replays, [2 kSegs + 2h + 1] error bits (u32) of half h
+  // [2 kSegs + 2h] replays, [2 kSegs + 2h + 1] error bits (u32) of half h,
+  // [2 kSegs + 8, 3 kSegs + 8) the region counters' copy, [3 kSegs + 8,
+  // 5 kSegs + 8) the second half's candidate and rescan counters
   KS_HIP(hipMemsetAsync(cnts, 0, 8 * (2 * kSegs + 8), st));
+  KS_HIP(hipMemsetAsync(cnts + 3 * kSegs + 8, 0, 8 * (2 * kSegs), st));
   unsigned long long *d_replays = cnts + 2 * kSegs;
 
-  int64_t ccap = std::max<int64_t>(1 << 16, nch / 4);
+  // Candidates and rescans in one list per half: the first half's are
+  // emitted and rescanned while the second half is post-processed (a list
+  // cannot be read while the other half's pass 1 still appends to it).
+  int64_t ccap = std::max<int64_t>(1 << 16, nch / 4);  // per list
   const size_t cand_bytes = ctx->slots[SLOT_CHUNK_C].bytes;  // use what the grow-only slot holds
-  if (cand_bytes > 1024 && (cand_bytes - 1024) / 40 > (size_t)ccap) ccap = (int64_t)((cand_bytes - 1024) / 40);
+  if (cand_bytes > 2048 && (cand_bytes - 2048) / 80 > (size_t)ccap) ccap = (int64_t)((cand_bytes - 2048) / 80);
   const int64_t csegcap = ccap / kSegs;
   ccap = csegcap * kSegs;
   void *cbuf = nullptr;
-  KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)ccap * 40 + 1024, &cbuf));
-  Cand cand{reinterpret_cast<long long *>(cbuf), reinterpret_cast<long long *>(cbuf) + ccap,
-            reinterpret_cast<long long *>(cbuf) + 2 * ccap, reinterpret_cast<double *>(cbuf) + 3 * ccap,
-            cnts, ccap, csegcap};
+  KS_TRY(ensure(ctx, SLOT_CHUNK_C, (size_t)ccap * 80 + 2048, &cbuf));
+  auto cand_list = [&](int h) {
+    long long *b = reinterpret_cast<long long *>(cbuf) + (size_t)h * 5 * ccap;
+    return Cand{b, b + ccap, b + 2 * ccap, reinterpret_cast<double *>(b + 3 * ccap),
+                h ? cnts + 3 * kSegs + 8 : cnts, ccap, csegcap};
+  };
+  const Cand cands[2] = {cand_list(0), cand_list(1)};
+  Cand cand = cands[0];  // (the list the pass-1 launches below append to: the second half's switches it)
   // kmer_regions: a rescan accompanies a region in the same segment; tr_lr
   // rescans every closed excursion, so its capacity grows on its own
   const int64_t rsegcap = std::max<int64_t>(rb.segcap, ctx->rescan_segcap);
-  const int64_t rcap = rsegcap * kSegs;
+  const int64_t rcap = rsegcap * kSegs;  // per list
   void *rsb = nullptr;
-  KS_TRY(ensure(ctx, SLOT_WORK_A, (size_t)rcap * 20 + 1024, &rsb));
-  Rescan rs{reinterpret_cast<int64_t *>(rsb), reinterpret_cast<int64_t *>(rsb) + rcap,
-            reinterpret_cast<int32_t *>(reinterpret_cast<int64_t *>(rsb) + 2 * rcap), cnts + kSegs, rcap,
-            rsegcap};
+  KS_TRY(ensure(ctx, SLOT_WORK_A, (size_t)rcap * 40 + 2048, &rsb));
+  auto rescan_list = [&](int h) {
+    int64_t *b = reinterpret_cast<int64_t *>(static_cast<char *>(rsb) + (size_t)h * ((size_t)rcap * 20 + 256));
+    return Rescan{b, b + rcap, reinterpret_cast<int32_t *>(b + 2 * rcap), h ? cnts + 4 * kSegs + 8 : cnts + kSegs,
+                  rcap, rsegcap};
+  };
+  const Rescan rss[2] = {rescan_list(0), rescan_list(1)};
+  const Rescan &rs = rss[0];
   // KS_DEBUG_CARRY=1: per-window carry statistics to stderr (diagnostics only)
   static const bool dbg_on = getenv("KS_DEBUG_CARRY") != nullptr;
   long long *dbg = nullptr;
@@ -3895,6 +3909,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipGetLastError());
       KS_HIP(hipEventRecord(ctx->ev[12], ctx->hi));
       KS_HIP(hipStreamWaitEvent(st, ctx->ev[12], 0));
+      cand = cands[1];
       p1lds(halves[1], ctx->side);
     } else {
       p1lds(halves[0], st);
@@ -3960,6 +3975,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipGetLastError());
       KS_HIP(hipEventRecord(ctx->ev[12], ctx->hi));
       KS_HIP(hipStreamWaitEvent(st, ctx->ev[12], 0));
+      cand = cands[1];
       p1l(halves[1], ctx->side);
     } else {
       p1l(halves[0], st);
@@ -3993,6 +4009,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipGetLastError());
       KS_HIP(hipEventRecord(ctx->ev[12], ctx->hi));
       KS_HIP(hipStreamWaitEvent(st, ctx->ev[12], 0));
+      cand = cands[1];  // (the tail chunks are the second half's)
       if (tail) {
         p1tail();
         KS_HIP(hipGetLastError());
@@ -4040,6 +4057,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipGetLastError());
       KS_HIP(hipEventRecord(ctx->ev[12], ctx->hi));
       KS_HIP(hipStreamWaitEvent(st, ctx->ev[12], 0));
+      cand = cands[1];  // (the tail chunks are the second half's)
       if (tail) {
         if (J == 5) KS_P1T(5, false);
         else if (lds_lut) { if (J == 4) KS_P1T(4, true); else if (J == 3) KS_P1T(3, true); else KS_P1T(2, true); }
@@ -4211,50 +4229,60 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     }
     if (nr > 0) {
       hipLaunchKernelGGL(k_stitch_runs, dim3((unsigned)nr), dim3(64), 0, strm, d_tbase, h.r1, runs.a, runs.b, runs.seq,
-                         ec, xagg, xtin, rb, rs, h.r0);
+                         ec, xagg, xtin, rb, rss[hi], h.r0);
       KS_HIP(hipGetLastError());
     }
     if (nt > 0) {
       hipLaunchKernelGGL(k_stitch_emit, dim3((unsigned)((nt + wpb - 1) / wpb)), dim3(64 * wpb), 0, strm, g, d_tbase, d_cbase,
-                         nruns, d_trun, runs.a, runs.seq, p1, cr, ec, xtin, rb, rs, err_h, h.t0, h.t1);
+                         nruns, d_trun, runs.a, runs.seq, p1, cr, ec, xtin, rb, rss[hi], err_h, h.t0, h.t1);
       KS_HIP(hipGetLastError());
     }
     return KS_OK;
   };
+  // ---- candidates (count read on the device), rescans: of each half's
+  // list on the stream of its post-processing (the first half's under the
+  // second half's, weighted rank: ~3.8 ms of lane walks), on st
+  // (the rescan slots in list order: sorted longest first they took 5.23 vs
+  // 3.56 ms at config 3, profiles/r4/ab2/ab_rank.txt)
+  auto emit_rescan = [&](int h) -> ks_status {
+    hipLaunchKernelGGL(k_candidates, dim3((unsigned)((ccap + 255) / 256)), dim3(256), 0, st, g, runs.a, d_cbase,
+                       nruns, runs.seq, ec, cands[h], cr, rb, rss[h]);
+    KS_HIP(hipGetLastError());
+    if (h == nhalf - 1) KS_HIP(hipEventRecord(ctx->ev[10], st));
+    KS_TRY(launch_scan_lane(ctx, s->seq, total, rss[h].a, rss[h].b, rss[h].seq, rcap, k, tv, mw, min_score,
+                            visits_rescan, rb, rss[h].count, rss[h].segcap, mode, 0, nullptr, runs.packed));
+    return KS_OK;
+  };
   if (split) {
     KS_TRY(post(0, halves[0], st));         // under the second half's pass 1
+    KS_TRY(emit_rescan(0));                 // under the second half's post-processing
     KS_TRY(post(1, halves[1], ctx->side));
     KS_HIP(hipEventRecord(ctx->ev[13], ctx->side));
     KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
+    KS_TRY(emit_rescan(1));
   } else {
     KS_TRY(post(0, halves[0], st));
+    KS_TRY(emit_rescan(0));
   }
-
-  // ---- candidates (count read on the device), rescans
-  hipLaunchKernelGGL(k_candidates, dim3((unsigned)((ccap + 255) / 256)), dim3(256), 0, st, g, runs.a, d_cbase,
-                     nruns, runs.seq, ec, cand, cr, rb, rs);
-  KS_HIP(hipGetLastError());
-  KS_HIP(hipEventRecord(ctx->ev[10], st));
-  // (the rescan slots in list order: sorted longest first they took 5.23 vs
-  // 3.56 ms at config 3, profiles/r4/ab2/ab_rank.txt)
-  KS_TRY(launch_scan_lane(ctx, s->seq, total, rs.a, rs.b, rs.seq, rcap, k, tv, mw, min_score, visits_rescan, rb,
-                          rs.count, rs.segcap, mode, 0, nullptr, runs.packed));
   KS_HIP(hipEventRecord(ctx->ev[11], st));
   // the region counters too (final: the rescans above append the last
   // regions), copied next to the scan's counters: one readback for both, and
   // scan_impl needs no round trip of its own
   hipLaunchKernelGGL(k_copy_u64, dim3(1), dim3(64), 0, st, rb.count, cnts + 2 * kSegs + 8, kSegs);
   KS_HIP(hipGetLastError());
-  std::vector<unsigned long long> hcv(3 * kSegs + 8);
-  KS_HIP(hipMemcpyAsync(hcv.data(), cnts, 8 * (3 * kSegs + 8), hipMemcpyDeviceToHost, st));
+  std::vector<unsigned long long> hcv(5 * kSegs + 8);
+  KS_HIP(hipMemcpyAsync(hcv.data(), cnts, 8 * (5 * kSegs + 8), hipMemcpyDeviceToHost, st));
   KS_HIP(hipStreamSynchronize(st));
   std::copy(hcv.begin() + 2 * kSegs + 8, hcv.begin() + 3 * kSegs + 8, ctx->hreg);
   ctx->hreg_ok = true;
   unsigned long long cand_max = 0, res_max = 0, res_tot = 0;
   for (int q = 0; q < kSegs; ++q) {
-    cand_max = std::max(cand_max, hcv[q]);
-    res_max = std::max(res_max, hcv[kSegs + q]);
-    res_tot += std::min<unsigned long long>(hcv[kSegs + q], (unsigned long long)rs.segcap);
+    const unsigned long long c0 = hcv[q], c1 = hcv[3 * kSegs + 8 + q];
+    const unsigned long long r0 = hcv[kSegs + q], r1 = hcv[4 * kSegs + 8 + q];
+    cand_max = std::max(cand_max, std::max(c0, c1));
+    res_max = std::max(res_max, std::max(r0, r1));
+    res_tot += std::min<unsigned long long>(r0, (unsigned long long)rs.segcap) +
+               std::min<unsigned long long>(r1, (unsigned long long)rs.segcap);
   }
   // hc: [0] largest candidate segment, [1] rescans, [2] replays, [3] error bits
   const unsigned long long hc[4] = {cand_max, res_tot, hcv[2 * kSegs] + hcv[2 * kSegs + 2],
@@ -4299,10 +4327,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     }
   }
   if (errbits & ~16u) return fail(KS_ERR_INTERNAL, "chunked scan consistency check failed (bits %u)", errbits);
-  if ((int64_t)cand_max > csegcap) {  // grow the candidate buffer and rerun the pass
+  if ((int64_t)cand_max > csegcap) {  // grow the candidate buffers and rerun the pass
     void *grown = nullptr;
     const size_t seg = (size_t)(cand_max + cand_max / 4 + 64);
-    KS_TRY(ensure(ctx, SLOT_CHUNK_C, seg * kSegs * 40 + 1024, &grown));
+    KS_TRY(ensure(ctx, SLOT_CHUNK_C, seg * kSegs * 80 + 2048, &grown));
     return KS_INTERNAL_RETRY;
   }
   if ((int64_t)res_max > rs.segcap) {  // grow the rescan buffer (regions may have overflowed too) and rerun

@@ -90,9 +90,9 @@ __device__ __forceinline__ void append_events(uint32_t starts, uint32_t ends, in
 // memory round trip per step) instead of after them (A/B: KS_NEV_LATE_PREV=1).
 // Four units per lane and step (eight, and nontemporal byte loads, measured
 // the same: 0.89-0.95 ms, profiles/r4/ab/ab_nev.txt).
-// kDpp: lane - 1's last byte by a DPP wave_shr:1 move (a VALU operand, no
-// LDS round trip) instead of __shfl_up (ds_bpermute).
-template <bool kMul, bool kPre, bool kDpp = true>  // multiply-based byte packing, lane 0's preceding byte loaded early (both A/B winners)
+// Lane - 1's last byte comes by a DPP wave_shr:1 move (a VALU operand, no
+// LDS round trip; 0.849 vs 0.875 ms with __shfl_up, profiles/r4/ab3/ab_log2.txt).
+template <bool kMul, bool kPre>  // multiply-based byte packing, lane 0's preceding byte loaded early (both A/B winners)
 __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ seq, int64_t total,
                                                   unsigned long long *__restrict__ ev,
                                                   unsigned long long *__restrict__ ev_count, int64_t cap,
@@ -119,8 +119,7 @@ __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ se
       uint32_t starts = 0, ends = 0;
       // the byte before the unit: lane - 1's last byte (the same step's
       // previous unit), loaded by lane 0
-      uint32_t prev_b = kDpp ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v[j].w >> 24), 0x138, 0xf, 0xf, true)
-                             : __shfl_up(v[j].w >> 24, 1, 64);
+      uint32_t prev_b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v[j].w >> 24), 0x138, 0xf, 0xf, true);
       if (kPre && lane == 0)
         prev_b = pb[j];
       else if (lane == 0 || p0 + 16 > total)
@@ -332,12 +331,8 @@ ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs
     const int64_t u1 = std::min<int64_t>(nunits, p_hi / 16 + 1 + kMargin);
     const unsigned grid = (unsigned)std::max<int64_t>(
         1, std::min<int64_t>((u1 - u0 + 1023) / 1024, (int64_t)ctx->num_cus * 16));
-    if (getenv("KS_NEV_SHFL"))  // (A/B: the former __shfl_up)
-      hipLaunchKernelGGL((k_n_events<true, true, false>), dim3(grid), dim3(256), 0, st, s->seq, total,
-                         (unsigned long long *)evp, d_count, cap, packed, p_lo, p_hi, u0, u1);
-    else
-      hipLaunchKernelGGL((k_n_events<true, true>), dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp,
-                         d_count, cap, packed, p_lo, p_hi, u0, u1);
+    hipLaunchKernelGGL((k_n_events<true, true>), dim3(grid), dim3(256), 0, st, s->seq, total, (unsigned long long *)evp,
+                       d_count, cap, packed, p_lo, p_hi, u0, u1);
     KS_HIP(hipGetLastError());
     if (s->nseq > 1) {
       hipLaunchKernelGGL(k_seq_events, dim3((unsigned)((s->nseq + 255) / 256)), dim3(256), 0, st, s->seq, total,

@@ -3814,9 +3814,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // one part; serialising the two pass-1 launches 31.8-32.0 by split
   // fraction: profiles/r3/rank/split_ab.txt)
   const bool f64_line = line && !comp;
-  // (the exact carry's post-processing is short: one part unless KS_EXACT_SPLIT=1, A/B)
-  const bool exact_split = exact && getenv("KS_EXACT_SPLIT") && atoi(getenv("KS_EXACT_SPLIT")) != 0;
-  const bool split = !ctx->no_split && (p1summ || exact_split || f64_line) && lay.split_r > 0 && lay.split_r < nruns &&
+  // (the exact carry's post-processing is short: one part -- two measured the
+  // same at lower run-to-run spread, 6.44 vs 6.55 ms median at k = 7,
+  // profiles/r4/ab3/ab_k7pm1_exact_split.txt)
+  const bool split = !ctx->no_split && (p1summ || (f64_line && !exact)) && lay.split_r > 0 && lay.split_r < nruns &&
                      lay.split_c >= 1024 && lay.split_c + 1024 <= ctail_all;
   Half halves[2];
   int nhalf = 1;

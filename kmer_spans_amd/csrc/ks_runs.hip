@@ -45,6 +45,11 @@ __device__ __forceinline__ uint32_t n_mask4m(uint32_t w) {
   const uint32_t z = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
   return ((z >> 7) * 0x10204080u) >> 28;
 }
+// 0x80 in each N / n byte of w (n_mask4m before the bit gather)
+__device__ __forceinline__ uint32_t n_flags4(uint32_t w) {
+  const uint32_t x = (w | 0x20202020u) ^ 0x6e6e6e6eu;
+  return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+}
 
 // Appends the events of `cnt` set bits of starts/ends (bit i <-> p0 + i).
 __device__ __forceinline__ void append_events(uint32_t starts, uint32_t ends, int64_t p0,
@@ -128,7 +133,13 @@ __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ se
         uint32_t nm = 0xffffu;
         if (p0 + 16 <= total) {
           if (kMul) {
-            nm = n_mask4m(v[j].x) | (n_mask4m(v[j].y) << 4) | (n_mask4m(v[j].z) << 8) | (n_mask4m(v[j].w) << 12);
+            // byte flags first; the bit gather only for a unit holding an N
+            // (most units hold none)
+            const uint32_t f0 = n_flags4(v[j].x), f1 = n_flags4(v[j].y), f2 = n_flags4(v[j].z), f3 = n_flags4(v[j].w);
+            nm = 0;
+            if (f0 | f1 | f2 | f3)
+              nm = (((f0 >> 7) * 0x10204080u) >> 28) | ((((f1 >> 7) * 0x10204080u) >> 28) << 4) |
+                   ((((f2 >> 7) * 0x10204080u) >> 28) << 8) | ((((f3 >> 7) * 0x10204080u) >> 28) << 12);
             if (packed)
               packed[u] = (enc_pack4m(v[j].x) << 24) | (enc_pack4m(v[j].y) << 16) | (enc_pack4m(v[j].z) << 8) |
                           enc_pack4m(v[j].w);

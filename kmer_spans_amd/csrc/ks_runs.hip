@@ -13,6 +13,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "ks_internal.h"
 
@@ -117,64 +118,77 @@ __global__ void __launch_bounds__(256) k_n_events(const uint8_t *__restrict__ se
       pb[j] = 'N';
       if (kPre && lane == 0 && p0 > 0 && p0 - 1 < total) pb[j] = seq[p0 - 1];
     }
+    // a step whose units all lie inside the range, before total, with a byte
+    // before them (block-uniform, nearly every step): no range or end tests
+    const int64_t step_end = ub + (int64_t)U * blockDim.x;  // one past its last unit
+    const bool inner = ub * 16 > p_lo && step_end * 16 <= (p_hi < total ? p_hi : total) && step_end <= u1;
+    auto units = [&](auto inner_tag) {
+      constexpr bool kIn = decltype(inner_tag)::value;
 #pragma unroll
-    for (int j = 0; j < U; ++j) {
-      const int64_t u = ub + j * blockDim.x + threadIdx.x;
-      const int64_t p0 = u * 16;
-      uint32_t starts = 0, ends = 0;
-      // the byte before the unit: lane - 1's last byte (the same step's
-      // previous unit), loaded by lane 0
-      uint32_t prev_b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v[j].w >> 24), 0x138, 0xf, 0xf, true);
-      if (kPre && lane == 0)
-        prev_b = pb[j];
-      else if (lane == 0 || p0 + 16 > total)
-        prev_b = p0 == 0 ? (uint32_t)'N' : (p0 - 1 < total ? seq[p0 - 1] : 'N');
-      if (u < u1) {
-        uint32_t nm = 0xffffu;
-        if (p0 + 16 <= total) {
-          if (kMul) {
-            // byte flags first; the bit gather only for a unit holding an N
-            // (most units hold none)
-            const uint32_t f0 = n_flags4(v[j].x), f1 = n_flags4(v[j].y), f2 = n_flags4(v[j].z), f3 = n_flags4(v[j].w);
-            nm = 0;
-            if (f0 | f1 | f2 | f3)
-              nm = (((f0 >> 7) * 0x10204080u) >> 28) | ((((f1 >> 7) * 0x10204080u) >> 28) << 4) |
-                   ((((f2 >> 7) * 0x10204080u) >> 28) << 8) | ((((f3 >> 7) * 0x10204080u) >> 28) << 12);
-            if (packed)
-              packed[u] = (enc_pack4m(v[j].x) << 24) | (enc_pack4m(v[j].y) << 16) | (enc_pack4m(v[j].z) << 8) |
-                          enc_pack4m(v[j].w);
+      for (int j = 0; j < U; ++j) {
+        const int64_t u = ub + j * blockDim.x + threadIdx.x;
+        const int64_t p0 = u * 16;
+        uint32_t starts = 0, ends = 0;
+        // the byte before the unit: lane - 1's last byte (the same step's
+        // previous unit), loaded by lane 0
+        uint32_t prev_b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v[j].w >> 24), 0x138, 0xf, 0xf, true);
+        if (kPre && lane == 0)
+          prev_b = pb[j];
+        else if (lane == 0 || (!kIn && p0 + 16 > total))
+          prev_b = p0 == 0 ? (uint32_t)'N' : (p0 - 1 < total ? seq[p0 - 1] : 'N');
+        if (kIn || u < u1) {
+          uint32_t nm = 0xffffu;
+          if (kIn || p0 + 16 <= total) {
+            if (kMul) {
+              // byte flags first; the bit gather only for a unit holding an N
+              // (most units hold none)
+              const uint32_t f0 = n_flags4(v[j].x), f1 = n_flags4(v[j].y), f2 = n_flags4(v[j].z),
+                             f3 = n_flags4(v[j].w);
+              nm = 0;
+              if (f0 | f1 | f2 | f3)
+                nm = (((f0 >> 7) * 0x10204080u) >> 28) | ((((f1 >> 7) * 0x10204080u) >> 28) << 4) |
+                     ((((f2 >> 7) * 0x10204080u) >> 28) << 8) | ((((f3 >> 7) * 0x10204080u) >> 28) << 12);
+              if (packed)
+                packed[u] = (enc_pack4m(v[j].x) << 24) | (enc_pack4m(v[j].y) << 16) | (enc_pack4m(v[j].z) << 8) |
+                            enc_pack4m(v[j].w);
+            } else {
+              nm = n_mask4(v[j].x) | (n_mask4(v[j].y) << 4) | (n_mask4(v[j].z) << 8) | (n_mask4(v[j].w) << 12);
+              if (packed)
+                packed[u] = (enc_pack4(v[j].x) << 24) | (enc_pack4(v[j].y) << 16) | (enc_pack4(v[j].z) << 8) |
+                            enc_pack4(v[j].w);
+            }
           } else {
-            nm = n_mask4(v[j].x) | (n_mask4(v[j].y) << 4) | (n_mask4(v[j].z) << 8) | (n_mask4(v[j].w) << 12);
-            if (packed)
-              packed[u] = (enc_pack4(v[j].x) << 24) | (enc_pack4(v[j].y) << 16) | (enc_pack4(v[j].z) << 8) |
-                          enc_pack4(v[j].w);
+            uint32_t pw = 0;
+            for (int q = 0; q < 16; ++q) {
+              const uint8_t c = p0 + q < total ? seq[p0 + q] : (uint8_t)'N';
+              if (p0 + q < total && !is_n(c)) nm &= ~(1u << q);
+              pw |= enc(c) << (30 - 2 * q);
+            }
+            if (packed) packed[u] = pw;
           }
-        } else {
-          uint32_t pw = 0;
-          for (int q = 0; q < 16; ++q) {
-            const uint8_t c = p0 + q < total ? seq[p0 + q] : (uint8_t)'N';
-            if (p0 + q < total && !is_n(c)) nm &= ~(1u << q);
-            pw |= enc(c) << (30 - 2 * q);
+          if (!kIn && (p0 < p_lo || p0 + 16 > p_hi)) {  // a unit at an end of the range: outside reads as N
+            for (int q = 0; q < 16; ++q)
+              if (p0 + q < p_lo || p0 + q >= p_hi) nm |= 1u << q;
           }
-          if (packed) packed[u] = pw;
+          const uint32_t prev_n =
+              (is_n((uint8_t)prev_b) || (!kIn && (p0 <= p_lo || p0 - 1 >= p_hi))) ? 1u : 0u;
+          const uint32_t non = ~nm & 0xffffu;
+          starts = non & ((nm << 1) | prev_n);
+          ends = nm & ((non << 1) | (prev_n ^ 1u)) & 0xffffu;
+          if (!kIn && p0 + 16 > p_hi) {  // no events past position p_hi
+            const int keep = (int)(p_hi - p0) + 1;
+            const uint32_t km = keep <= 0 ? 0u : keep >= 16 ? 0xffffu : ((1u << keep) - 1u);
+            starts &= km;
+            ends &= km;
+          }
         }
-        if (p0 < p_lo || p0 + 16 > p_hi) {  // a unit at an end of the range: outside reads as N
-          for (int q = 0; q < 16; ++q)
-            if (p0 + q < p_lo || p0 + q >= p_hi) nm |= 1u << q;
-        }
-        const uint32_t prev_n = (is_n((uint8_t)prev_b) || p0 <= p_lo || p0 - 1 >= p_hi) ? 1u : 0u;
-        const uint32_t non = ~nm & 0xffffu;
-        starts = non & ((nm << 1) | prev_n);
-        ends = nm & ((non << 1) | (prev_n ^ 1u)) & 0xffffu;
-        if (p0 + 16 > p_hi) {  // no events past position p_hi
-          const int keep = (int)(p_hi - p0) + 1;
-          const uint32_t km = keep <= 0 ? 0u : keep >= 16 ? 0xffffu : ((1u << keep) - 1u);
-          starts &= km;
-          ends &= km;
-        }
+        append_events(starts, ends, p0, ev, ev_count, cap);
       }
-      append_events(starts, ends, p0, ev, ev_count, cap);
-    }
+    };
+    if (inner)
+      units(std::integral_constant<bool, true>());
+    else
+      units(std::integral_constant<bool, false>());
   }
 }
 

@@ -623,7 +623,7 @@ struct PredWords {
 template <int PS>
 __global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k, const uint16_t *__restrict__ approx, int kp,
                                                   double *__restrict__ pa, double *__restrict__ pb) {
-  __shared__ __half s_ap[1 << 16];
+  extern __shared__ __half s_ap[];  // 4^kp entries (dynamic: 32 KiB at kp = 7 lets 4 blocks share a CU)
   const int np = 1 << (2 * kp);
   for (int i = threadIdx.x; i < np; i += blockDim.x) s_ap[i] = __ushort_as_half(approx[i]);
   __syncthreads();
@@ -3842,10 +3842,13 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     pp.special = reinterpret_cast<uint8_t *>(W + o_pz);
     auto predict = [&](const Half &h, hipStream_t strm) -> ks_status {
       KS_HIP(hipMemsetAsync(W + o_pz + h.c0, 0, (size_t)(h.c1 - h.c0), strm));
-      const unsigned gl =
-          (unsigned)std::max<int64_t>(1, std::min<int64_t>((h.c1 - h.c0 + 1023) / 1024, ctx->num_cus));
+      const size_t lds = (size_t)2 << (2 * tv.approx_k);  // the fp16 prefix table
+      const int per_cu = lds <= ((size_t)32 << 10) ? 4 : 1;
+      const unsigned gl = (unsigned)std::max<int64_t>(
+          1, std::min<int64_t>((h.c1 - h.c0 + 1023) / 1024, (int64_t)ctx->num_cus * per_cu));
+      KS_HIP(hipFuncSetAttribute((const void *)k_predict<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       // every second index sampled (A/B: every 4th / 8th changed nothing)
-      hipLaunchKernelGGL(k_predict<2>, dim3(gl), dim3(1024), 0, strm, view(h), total, k, tv.approx, tv.approx_k,
+      hipLaunchKernelGGL(k_predict<2>, dim3(gl), dim3(1024), lds, strm, view(h), total, k, tv.approx, tv.approx_k,
                          pp.asum, pp.cexit);
       KS_HIP(hipGetLastError());
       return ascan(pp, d_xh, h.r0, h.r1, h.t0, h.t1, strm);

@@ -62,3 +62,11 @@ tail -1 $O/ab_k15rank.txt
 $AB --rounds 3 --steps 3 --k 7 --score pm1 one: --out $O/ab_k7pm1.json > $O/ab_k7pm1.txt 2>&1 || { tail -30 $O/ab_k7pm1.txt; exit 1; }
 tail -1 $O/ab_k7pm1.txt
 fi
+if [[ $P == *k* ]]; then
+M="timeout -k 10 300 python -u bench.py --no-cpu --no-rank --no-host-path --no-visits --steps 20"
+for i in 1 2; do
+$M --out $O/k8_$i.json > $O/k8_$i.log 2>&1 || { tail -20 $O/k8_$i.log; exit 1; }
+KS_APPROX_K=7 $M --out $O/k7_$i.json > $O/k7_$i.log 2>&1 || { tail -20 $O/k7_$i.log; exit 1; }
+done
+for f in k8_1 k7_1 k8_2 k7_2; do python3 -c "import json;b=json.load(open('$O/$f.json'));print('$f', b['value'], b['ms_per_step'], b['phase_ms'])"; done
+fi

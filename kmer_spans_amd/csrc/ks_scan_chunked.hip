@@ -1683,7 +1683,10 @@ __global__ void __launch_bounds__(kWideBlock) k_pass1w(Chunks g, int64_t total, 
 // the packed bases and the base table (values16_nostore / values4).  Same
 // outputs as k_pass1.
 constexpr int kLdsTableK = 7;
-template <bool kTrlr>
+// kExact (integer tables, k_carry_exact): no |s| sum and no non-finite flag
+// (neither is read on that path; two of the ~30 VALU ops per index of this
+// ALU-bound pass)
+template <bool kTrlr, bool kExact = false>
 __global__ void __launch_bounds__(1024) k_pass1_lds(Chunks g, int64_t total, int k, TableView tv, EmitCfg ec,
                                                     uint32_t *__restrict__ visits, P1 o, Cand cand,
                                                     const double *__restrict__ xh, SummP1 sp) {
@@ -1755,8 +1758,10 @@ __global__ void __launch_bounds__(1024) k_pass1_lds(Chunks g, int64_t total, int
         pmin = asum < pmin ? asum : pmin;
         parg = asum > pmax ? i : parg;
         pmax = asum > pmax ? asum : pmax;
-        sabs += fabs(s);
-        special |= !isfinite(s);
+        if (!kExact) {
+          sabs += fabs(s);
+          special |= !isfinite(s);
+        }
         const double tt = prev + s;
         const double S = tt > 0 ? tt : 0.0;
         const bool open = (prev == 0) & (S > 0);
@@ -3901,6 +3906,9 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       if (ec.trlr)
         hipLaunchKernelGGL(k_pass1_lds<true>, dim3(gl), dim3(1024), 0, strm, gv, total, k, tv, ec, visits, p1, cand, xh,
                            sp1);
+      else if (exact)
+        hipLaunchKernelGGL((k_pass1_lds<false, true>), dim3(gl), dim3(1024), 0, strm, gv, total, k, tv, ec, visits, p1,
+                           cand, xh, sp1);
       else
         hipLaunchKernelGGL(k_pass1_lds<false>, dim3(gl), dim3(1024), 0, strm, gv, total, k, tv, ec, visits, p1, cand, xh,
                            sp1);

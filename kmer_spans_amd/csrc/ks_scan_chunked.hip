@@ -1683,6 +1683,85 @@ __global__ void __launch_bounds__(kWideBlock) k_pass1w(Chunks g, int64_t total, 
 // the packed bases and the base table (values16_nostore / values4).  Same
 // outputs as k_pass1.
 constexpr int kLdsTableK = 7;
+// Pass 1 of small-k integer tables (k <= 7, ks_table::int_exact): the
+// clean trajectory of a chunk starts at 0 and moves by at most 2^20 per
+// index, so it and the chunk aggregates fit int32 (|S| <= 2^28) and equal the
+// FP64 chain exactly; 32-bit integer compares and selects instead of FP64
+// ones (half the VALU work of this ALU-bound pass), the table as int32 in
+// LDS (64 KiB at k = 7: two blocks per CU).  Outputs as k_pass1_lds<false,
+// true> (FP64 aggregates, no |s| sum, no non-finite flag).
+__global__ void __launch_bounds__(1024) k_pass1_lds_int(Chunks g, int64_t total, int k, TableView tv, EmitCfg ec,
+                                                        uint32_t *__restrict__ visits, P1 o, Cand cand) {
+  __shared__ int32_t s_val[1 << (2 * kLdsTableK)];
+  const int nk = 1 << (2 * k);
+  for (int i = threadIdx.x; i < nk; i += blockDim.x) s_val[i] = (int32_t)tv_get(tv, (uint32_t)i);
+  __syncthreads();
+  const uint32_t kmask = (uint32_t)nk - 1u;
+  const uint32_t *__restrict__ packed = g.packed;
+  const int64_t last = total >> 4;
+  for (int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < g.nch;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t start = g.start[c];
+    const int n = g.n[c];
+    const int64_t q0 = start - k;
+    auto load3 = [&](int64_t q) {
+      const int64_t w = q >> 4;
+      return make_uint3(packed[min(w, last)], packed[min(w + 1, last)], packed[min(w + 2, last)]);
+    };
+    uint3 cur = load3(q0);
+    int32_t prev = 0, best = 0, asum = 0, pmin = INT32_MAX, pmax = INT32_MIN;
+    int beg = -1, arg = 0, parg = 0;
+    for (int b0 = 0; b0 < n; b0 += 16) {
+      const uint3 nxt = load3(q0 + b0 + 16);
+      const uint32_t bp = 2u * (uint32_t)((q0 + b0) & 15);
+      const uint64_t x = ((((uint64_t)cur.x << 32) | cur.y) << bp) | (((uint64_t)cur.z << bp) >> 32);
+      for (int j = 0; j < 16; ++j) {
+        const int i = b0 + j;
+        if (i >= n) break;
+        const uint32_t code = (uint32_t)(x >> (64 - 2 * (j + k))) & kmask;  // k-mer ending at start + i - 1
+        const int32_t sv = s_val[code];
+        if (visits) atomicAdd(&visits[code], 1u);
+        asum += sv;
+        pmin = asum < pmin ? asum : pmin;
+        parg = asum > pmax ? i : parg;
+        pmax = asum > pmax ? asum : pmax;
+        const int32_t tt = prev + sv;
+        const int32_t S = tt > 0 ? tt : 0;
+        const bool open = (prev == 0) & (S > 0);
+        const bool close = (prev > 0) & (S == 0);
+        const bool want = close & ((uint64_t)(int64_t)(arg - beg) >= ec.mw) & ((double)best >= ec.min_score);
+        if (want) {
+          const int64_t slot = append_one(cand.count, cand.segcap);
+          if (slot >= 0) {
+            cand.beg[slot] = start + beg;
+            cand.arg[slot] = start + arg;
+            cand.rst[slot] = start + i;
+            cand.best[slot] = (double)best;
+          }
+        }
+        const bool up = open | (S > best);
+        best = up ? S : best;
+        arg = up ? i : arg;
+        beg = open ? i : (close ? -1 : beg);
+        prev = S;
+      }
+      cur = nxt;
+    }
+    o.cexit[c] = (double)prev;
+    o.asum[c] = (double)asum;
+    o.pmin[c] = n > 0 ? (double)pmin : INFINITY;
+    o.pmax[c] = n > 0 ? (double)pmax : -INFINITY;
+    o.parg[c] = parg;
+    o.sabs[c] = 0.0;
+    o.special[c] = 0;
+    if (prev > 0) {
+      o.tbeg[c] = beg; o.tmax[c] = (double)best; o.targ[c] = arg;
+    } else {
+      o.tbeg[c] = -1; o.tmax[c] = 0.0; o.targ[c] = 0;
+    }
+  }
+}
+
 // kExact (integer tables, k_carry_exact): no |s| sum and no non-finite flag
 // (neither is read on that path; two of the ~30 VALU ops per index of this
 // ALU-bound pass)
@@ -3899,6 +3978,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   if (lds_table) {
     // small k: the whole table in LDS, persistent blocks (one per CU), no
     // code store; with pass-1 summaries the halves as for line tables
+    // integer small-k tables: the int32 pass (KS_NO_LDS_INT: the FP64 one, A/B)
+    const bool lds_int = getenv("KS_NO_LDS_INT") == nullptr;
     auto p1lds = [&](const Half &h, hipStream_t strm) {
       const Chunks gv = view(h);
       const unsigned gl = (unsigned)std::max<int64_t>(1, std::min<int64_t>((h.c1 - h.c0 + 1023) / 1024, ctx->num_cus));
@@ -3906,6 +3987,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       if (ec.trlr)
         hipLaunchKernelGGL(k_pass1_lds<true>, dim3(gl), dim3(1024), 0, strm, gv, total, k, tv, ec, visits, p1, cand, xh,
                            sp1);
+      else if (exact && lds_int)  // (two blocks per CU)
+        hipLaunchKernelGGL(k_pass1_lds_int, dim3((unsigned)std::max<int64_t>(
+                                                 1, std::min<int64_t>((h.c1 - h.c0 + 1023) / 1024, 2 * ctx->num_cus))),
+                           dim3(1024), 0, strm, gv, total, k, tv, ec, visits, p1, cand);
       else if (exact)
         hipLaunchKernelGGL((k_pass1_lds<false, true>), dim3(gl), dim3(1024), 0, strm, gv, total, k, tv, ec, visits, p1,
                            cand, xh, sp1);

@@ -59,7 +59,7 @@ $AB --rounds 3 --steps 2 --score rank one: --out $O/ab_rank.json > $O/ab_rank.tx
 tail -1 $O/ab_rank.txt
 $AB --rounds 2 --steps 2 --k 15 --score rank one: --out $O/ab_k15rank.json > $O/ab_k15rank.txt 2>&1 || { tail -30 $O/ab_k15rank.txt; exit 1; }
 tail -1 $O/ab_k15rank.txt
-$AB --rounds 3 --steps 3 --k 7 --score pm1 one: --out $O/ab_k7pm1.json > $O/ab_k7pm1.txt 2>&1 || { tail -30 $O/ab_k7pm1.txt; exit 1; }
+$AB --rounds 3 --steps 3 --k 7 --score pm1 one: fp64:KS_NO_LDS_INT=1 --out $O/ab_k7pm1.json > $O/ab_k7pm1.txt 2>&1 || { tail -30 $O/ab_k7pm1.txt; exit 1; }
 tail -1 $O/ab_k7pm1.txt
 fi
 if [[ $P == *k* ]]; then

@@ -70,8 +70,10 @@ void ks_regions_free(ks_regions *r);
 
 /* Execution context: one GPU, one HIP stream, a grow-only device workspace.
  * Created lazily per process (fork-safe: never touches HIP until first use,
- * test.R:550-567 forks with mclapply).  Not thread-safe; one call at a time,
- * like the reference on R's main thread. */
+ * test.R:550-567 forks with mclapply).  One call at a time per context, like
+ * the reference on R's main thread: a call entered from a second thread while
+ * another is inside one on the same context returns KS_ERR_ARG ("in use by
+ * another thread"); use one context per thread. */
 typedef struct ks_ctx ks_ctx;
 ks_status ks_ctx_create(int32_t device, ks_ctx **out);
 void ks_ctx_destroy(ks_ctx *ctx);

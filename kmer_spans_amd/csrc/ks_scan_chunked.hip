@@ -4351,11 +4351,14 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     return KS_OK;
   };
   if (split) {
+    // KS_RESCAN_EARLY=0 (A/B): both halves' lists after the join
+    const bool early = !(getenv("KS_RESCAN_EARLY") && atoi(getenv("KS_RESCAN_EARLY")) == 0);
     KS_TRY(post(0, halves[0], st));         // under the second half's pass 1
-    KS_TRY(emit_rescan(0));                 // under the second half's post-processing
+    if (early) KS_TRY(emit_rescan(0));      // under the second half's post-processing
     KS_TRY(post(1, halves[1], ctx->side));
     KS_HIP(hipEventRecord(ctx->ev[13], ctx->side));
     KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
+    if (!early) KS_TRY(emit_rescan(0));
     KS_TRY(emit_rescan(1));
   } else {
     KS_TRY(post(0, halves[0], st));

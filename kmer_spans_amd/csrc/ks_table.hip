@@ -642,9 +642,12 @@ static void launch_build_lines(hipStream_t st, const ks_table *t, int m, void *o
 // expanded / line table of a compressed table.
 static ks_status build_approx(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev) {
   if (!k_approx_ok(t)) return KS_OK;
-  // prefix length of the binade predictor: 8 bases (128 KiB of fp16 means,
-  // one predictor block per CU); KS_APPROX_K=7 (A/B): 32 KiB, four blocks
-  const int kp_max = getenv("KS_APPROX_K") ? std::max(1, std::min(8, atoi(getenv("KS_APPROX_K")))) : 8;
+  // prefix length of the binade predictor: 7 bases, 32 KiB of fp16 means --
+  // four predictor blocks per CU, and the second half's predictor no longer
+  // holds whole CUs beside the first half's pass 1: metric step 14.37 vs
+  // 14.89-15.18 ms with 8 bases (128 KiB, one block per CU), the summary
+  // fixes unchanged (profiles/r4/ab3/approx_k*.json); KS_APPROX_K overrides
+  const int kp_max = getenv("KS_APPROX_K") ? std::max(1, std::min(8, atoi(getenv("KS_APPROX_K")))) : 7;
   const int kp = std::min(t->k, kp_max);
   if (hipMalloc(&t->d_approx, ((size_t)2 << (2 * kp)) + 16) != hipSuccess) {
     (void)hipGetLastError();

@@ -8,7 +8,7 @@ cd $R
 P=${2:-ab}
 AB="timeout -k 10 600 python -u tools/ab_inproc.py"
 if [[ $P == *a* ]]; then
-$AB --rounds 3 --steps 2 --score rank one: --out $O/ab_rank.json > $O/ab_rank.txt 2>&1 || { tail -30 $O/ab_rank.txt; exit 1; }
+$AB --rounds 3 --steps 2 --score rank one: late:KS_RESCAN_EARLY=0 --out $O/ab_rank.json > $O/ab_rank.txt 2>&1 || { tail -30 $O/ab_rank.txt; exit 1; }
 tail -4 $O/ab_rank.txt
 $AB --rounds 3 --steps 3 one: --out $O/ab_log2.json > $O/ab_log2.txt 2>&1 || { tail -30 $O/ab_log2.txt; exit 1; }
 tail -4 $O/ab_log2.txt
@@ -55,10 +55,10 @@ $AB --rounds 4 --steps 3 one: shfl:KS_NEV_SHFL=1 --out $O/ab_log2.json > $O/ab_l
 tail -2 $O/ab_log2.txt
 fi
 if [[ $P == *r* ]]; then
-$AB --rounds 3 --steps 2 --score rank one: --out $O/ab_rank.json > $O/ab_rank.txt 2>&1 || { tail -30 $O/ab_rank.txt; exit 1; }
-tail -1 $O/ab_rank.txt
-$AB --rounds 2 --steps 2 --k 15 --score rank one: --out $O/ab_k15rank.json > $O/ab_k15rank.txt 2>&1 || { tail -30 $O/ab_k15rank.txt; exit 1; }
-tail -1 $O/ab_k15rank.txt
+$AB --rounds 3 --steps 2 --score rank one: late:KS_RESCAN_EARLY=0 --out $O/ab_rank.json > $O/ab_rank.txt 2>&1 || { tail -30 $O/ab_rank.txt; exit 1; }
+tail -2 $O/ab_rank.txt
+$AB --rounds 2 --steps 2 --k 15 --score rank one: late:KS_RESCAN_EARLY=0 --out $O/ab_k15rank.json > $O/ab_k15rank.txt 2>&1 || { tail -30 $O/ab_k15rank.txt; exit 1; }
+tail -2 $O/ab_k15rank.txt
 $AB --rounds 3 --steps 3 --k 7 --score pm1 one: fp64:KS_NO_LDS_INT=1 --out $O/ab_k7pm1.json > $O/ab_k7pm1.txt 2>&1 || { tail -30 $O/ab_k7pm1.txt; exit 1; }
 tail -1 $O/ab_k7pm1.txt
 fi

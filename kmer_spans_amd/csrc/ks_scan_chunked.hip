@@ -585,7 +585,7 @@ __global__ void k_make_chunks(const int64_t *__restrict__ ra, const int64_t *__r
 // loads: the lanes of a wave read 64 different lines per instruction), then
 // the 18 words at offset w0 - wa selected in registers.
 struct PredWords {
-  uint32_t a[20];
+  uint32_t a[21];  // a[20]: the third word of the last 16 indices at o = 3 (past the loads: 0)
   int o;
   __device__ __forceinline__ void load(const uint32_t *__restrict__ packed, int64_t total, int64_t q0) {
     const int64_t w0 = q0 >> 4, last = total >> 4;
@@ -600,6 +600,7 @@ struct PredWords {
         a[4 * t + 2] = v.z;
         a[4 * t + 3] = v.w;
       }
+      a[20] = 0;
       o = (int)(w0 - wa);
     } else {
 #pragma unroll
@@ -637,8 +638,8 @@ __global__ void __launch_bounds__(1024) k_predict(Chunks g, int64_t total, int k
     for (int t = 0; t < 16; ++t) {
       if (16 * t < n) {
         const uint64_t x = ((((uint64_t)W.w(t) << 32) | W.w(t + 1)) << bp) | (((uint64_t)W.w(t + 2) << bp) >> 32);
-        // every PS-th index, weighted PS (A/B: PS = 2 cuts the predictor 1.11 -> 0.80 ms with the
-        // same 16.2 K gathered summaries at the metric config)
+        // every PS-th index, weighted PS (A/B: PS = 2 cut the predictor 1.11 -> 0.80 ms with the
+        // same 16.2 K gathered summaries at the metric config; PS = 4 is the default since round 4)
         float a[16 / PS];
 #pragma unroll
         for (int j = 0; j < 16; j += PS)
@@ -3930,10 +3931,23 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       const int per_cu = lds <= ((size_t)32 << 10) ? 4 : 1;
       const unsigned gl = (unsigned)std::max<int64_t>(
           1, std::min<int64_t>((h.c1 - h.c0 + 1023) / 1024, (int64_t)ctx->num_cus * per_cu));
-      KS_HIP(hipFuncSetAttribute((const void *)k_predict<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      // every second index sampled (A/B: every 4th / 8th changed nothing)
-      hipLaunchKernelGGL(k_predict<2>, dim3(gl), dim3(1024), lds, strm, view(h), total, k, tv.approx, tv.approx_k,
-                         pp.asum, pp.cexit);
+      // every fourth index sampled, weighted 4 (at four 32-KiB blocks per CU:
+      // metric step 14.48 vs 14.62 ms median with every second, predictor 0.56 vs
+      // 0.64 ms; every eighth: predictor 0.21 ms but more mispredicted binades,
+      // carry + stitch 1.18 vs 0.85 ms; profiles/r4/ab4/ab_pred_log2.txt).
+      // KS_PRED_PS=2 / 8 for A/B.
+      const int ps = getenv("KS_PRED_PS") ? atoi(getenv("KS_PRED_PS")) : 4;
+      const void *kf = ps == 8 ? (const void *)k_predict<8> : ps == 4 ? (const void *)k_predict<4> : (const void *)k_predict<2>;
+      KS_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      if (ps == 8)
+        hipLaunchKernelGGL(k_predict<8>, dim3(gl), dim3(1024), lds, strm, view(h), total, k, tv.approx, tv.approx_k,
+                           pp.asum, pp.cexit);
+      else if (ps == 4)
+        hipLaunchKernelGGL(k_predict<4>, dim3(gl), dim3(1024), lds, strm, view(h), total, k, tv.approx, tv.approx_k,
+                           pp.asum, pp.cexit);
+      else
+        hipLaunchKernelGGL(k_predict<2>, dim3(gl), dim3(1024), lds, strm, view(h), total, k, tv.approx, tv.approx_k,
+                           pp.asum, pp.cexit);
       KS_HIP(hipGetLastError());
       return ascan(pp, d_xh, h.r0, h.r1, h.t0, h.t1, strm);
     };

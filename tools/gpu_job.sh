@@ -3,6 +3,7 @@
 # variants on the same allocations).  Usage: tools/gpu_job.sh TAG [PARTS]
 #   m: metric (log2 k = 13)   r: weighted rank k = 13 / 15   x: +-1 k = 7 / 13
 #   p: per-genome phases (config 5)   d: rank carry / rescan diagnostics
+#   s: shard-of-8 and config 2 (fixed cost at small sizes)   q: predictor sampling stride
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${1:-job}
@@ -21,6 +22,14 @@ fi
 if [[ $P == *x* ]]; then
 ab ab_k7pm1 --rounds 3 --steps 3 --k 7 --score pm1 one: fp64:KS_NO_LDS_INT=1 gen:KS_NO_EXACT=1
 ab ab_pm1 --rounds 3 --steps 3 --score pm1 one: gen:KS_NO_EXACT=1
+fi
+if [[ $P == *s* ]]; then
+ab ab_shard8 --rounds 4 --steps 10 --shard-of 8 one: late:KS_RESCAN_EARLY=0 f60:KS_SPLIT_FRAC=0.6 f80:KS_SPLIT_FRAC=0.8
+ab ab_cfg2 --rounds 4 --steps 10 --k 11 --ncontigs 1 one: late:KS_RESCAN_EARLY=0 f80:KS_SPLIT_FRAC=0.8
+fi
+if [[ $P == *q* ]]; then
+ab ab_pred_log2 --rounds 3 --steps 3 one: ps4:KS_PRED_PS=4 ps8:KS_PRED_PS=8
+ab ab_pred_shard8 --rounds 4 --steps 10 --shard-of 8 one: ps4:KS_PRED_PS=4
 fi
 if [[ $P == *p* ]]; then
 timeout -k 10 300 python -u tools/genome_phases.py --ext-gib 32 > $O/phases32.txt 2>&1 || { tail -30 $O/phases32.txt; exit 1; }

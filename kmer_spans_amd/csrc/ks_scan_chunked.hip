@@ -72,7 +72,28 @@ struct Summ {  // binade-integer summaries for the predicted binade (P2)
   int32_t *e;             // binade, INT32_MIN: none
   long long *D, *M, *N;   // [2 * nch] by entry parity
   int32_t *A;             // [2 * nch]
+  // pass-1 summaries (p1summ): sel[c] < 2 = the chunk's summary is pass 1's
+  // slot 2c + sel[c] of pD..pA for both entry parities (k_marks_select keeps
+  // it in place instead of copying it into D..A); 2 = D..A.  sel null: D..A.
+  uint8_t *sel = nullptr;
+  const long long *pD = nullptr, *pM = nullptr, *pN = nullptr;
+  const int32_t *pA = nullptr;
 };
+
+// Where chunk c's summary fields are: index i0 (entry parity 0) and i1
+// (parity 1) into D / M / N / A.
+struct SummAt {
+  const long long *D, *M, *N;
+  const int32_t *A;
+  int64_t i0, i1;
+};
+__device__ __forceinline__ SummAt summ_at(const Summ &sm, int64_t c) {
+  if (sm.sel) {
+    const int s = sm.sel[c];
+    if (s < 2) return SummAt{sm.pD, sm.pM, sm.pN, sm.pA, 2 * c + s, 2 * c + s};
+  }
+  return SummAt{sm.D, sm.M, sm.N, sm.A, 2 * c, 2 * c + 1};
+}
 
 struct SummP1 {  // binade summaries computed by pass 1 for the predicted binade (single trajectory)
   int32_t *e;             // [2 * nch] binade, INT32_MIN: none (no prediction, a tie, out of range)
@@ -2375,6 +2396,7 @@ __device__ __forceinline__ void select_one(const Chunks &g, const P1 &o, const d
                                            bool &want, bool &rwant) {
   want = rwant = false;
   sm.e[c] = INT32_MIN;
+  uint8_t sel = 2;
   const double x = xt[c];
   if (rp.slot) rp.slot[c] = -1;
   if (!o.special[c] && x >= kLMin && x < 1.0e18) {
@@ -2385,14 +2407,18 @@ __device__ __forceinline__ void select_one(const Chunks &g, const P1 &o, const d
       const int t = sp.e[2 * c] == e ? 0 : (sp.e[2 * c + 1] == e ? 1 : -1);
       if (t >= 0) {
         sm.e[c] = e;
-        const long long D = sp.D[2 * c + t], M = sp.M[2 * c + t], N = sp.N[2 * c + t];
-        const int A = sp.A[2 * c + t];
+        if (sm.sel) {
+          sel = (uint8_t)t;  // read in place (summ_at)
+        } else {
+          const long long D = sp.D[2 * c + t], M = sp.M[2 * c + t], N = sp.N[2 * c + t];
+          const int A = sp.A[2 * c + t];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          sm.D[2 * c + q] = D;
-          sm.M[2 * c + q] = M;
-          sm.N[2 * c + q] = N;
-          sm.A[2 * c + q] = A;
+          for (int q = 0; q < 2; ++q) {
+            sm.D[2 * c + q] = D;
+            sm.M[2 * c + q] = M;
+            sm.N[2 * c + q] = N;
+            sm.A[2 * c + q] = A;
+          }
         }
       } else {
         want = true;
@@ -2401,9 +2427,10 @@ __device__ __forceinline__ void select_one(const Chunks &g, const P1 &o, const d
       }
     }
   }
+  if (sm.sel) sm.sel[c] = sel;
   // no summary will serve it: a likely replay unless it enters at 0 or
   // clamps for certain (with a wide margin: a needless prefetch is cheap)
-  rwant = rp.slot && !want && sm.e[c] == INT32_MIN && !o.special[c] && x > 0.0 &&
+  rwant = rp.slot && !want && sel == 2 && sm.e[c] == INT32_MIN && !o.special[c] && x > 0.0 &&
           !(x + o.pmin[c] < -ldexp(fabs(x) + o.sabs[c], -8));
 }
 
@@ -2848,13 +2875,15 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
     t.rs = (live && rp.slot) ? rp.slot[cc] : -1;
     const int se = sm.e[cc];
     t.se = live ? se : INT32_MIN;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      t.D[q] = sm.D[2 * cc + q];
-      t.M[q] = sm.M[2 * cc + q];
-      t.N[q] = sm.N[2 * cc + q];
-      t.A[q] = sm.A[2 * cc + q];
-    }
+    const SummAt r = summ_at(sm, cc);
+    t.D[0] = r.D[r.i0];
+    t.D[1] = r.D[r.i1];
+    t.M[0] = r.M[r.i0];
+    t.M[1] = r.M[r.i1];
+    t.N[0] = r.N[r.i0];
+    t.N[1] = r.N[r.i1];
+    t.A[0] = r.A[r.i0];
+    t.A[1] = r.A[r.i1];
   };
   // tiles are the global 64-chunk tiles (partial at the segment's ends)
   auto tile_end = [&](int64_t cb) { return min(c1, (cb & ~(int64_t)63) + 64); };
@@ -3134,9 +3163,10 @@ __global__ void __launch_bounds__(256) k_tile_comp(Chunks g, Summ sm, TileComp t
     if (lane == 0) tc.e[t] = INT32_MIN;
     return;
   }
-  const long long D0 = sm.D[2 * c], D1 = sm.D[2 * c + 1];
-  const long long M0 = sm.M[2 * c], M1 = sm.M[2 * c + 1];
-  const long long N0 = sm.N[2 * c], N1 = sm.N[2 * c + 1];
+  const SummAt r = summ_at(sm, c);
+  const long long D0 = r.D[r.i0], D1 = r.D[r.i1];
+  const long long M0 = r.M[r.i0], M1 = r.M[r.i1];
+  const long long N0 = r.N[r.i0], N1 = r.N[r.i1];
   const PPair ip = pp_scan_incl(PPair{D0, D1});
   const PPair xp = pp_prev(ip);
   const long long i0 = ip.d0, i1 = ip.d1, x0 = xp.d0, x1 = xp.d1;
@@ -3179,7 +3209,8 @@ __global__ void __launch_bounds__(256) k_tile_apply(Chunks g, Summ sm, TileComp 
   const int64_t c = 64 * t + lane;
   const bool live = c < g.nch;
   const int64_t cc = live ? c : 64 * t;
-  const long long D0 = sm.D[2 * cc], D1 = sm.D[2 * cc + 1];
+  const SummAt r = summ_at(sm, cc);
+  const long long D0 = r.D[r.i0], D1 = r.D[r.i1];
   const PPair xp = pp_prev(pp_scan_incl(PPair{live ? D0 : 0, live ? D1 : 0}));
   const long long x0 = xp.d0, x1 = xp.d1;
   if (!live) return;
@@ -3188,8 +3219,8 @@ __global__ void __launch_bounds__(256) k_tile_apply(Chunks g, Summ sm, TileComp 
   cr.x[c] = from_mant(mj, e);
   cr.mode[c] = (uint8_t)kModeL;
   cr.hq[c] = -1;
-  cr.hmax[c] = from_mant(mj + (pj ? sm.M[2 * c + 1] : sm.M[2 * c]), e);
-  cr.harg[c] = pj ? sm.A[2 * c + 1] : sm.A[2 * c];
+  cr.hmax[c] = from_mant(mj + r.M[pj ? r.i1 : r.i0], e);
+  cr.harg[c] = r.A[pj ? r.i1 : r.i0];
 }
 
 // Carry by window: block w runs the segments that start in chunks
@@ -3716,6 +3747,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const size_t o_spd = off; off += al(nch * 8 * 6);
   const size_t o_spa = off; off += al(nch * 4 * 2);
   const size_t o_fix = off; off += al(nch * 8 + 16);
+  const size_t o_ssel = off; off += al(nch);  // Summ::sel
   const size_t o_tagg = off; off += al(ntiles * 16);  // parallel approximate scan: tile maps, tile entries
   const size_t o_tin = off; off += al(ntiles * 8);
   const size_t o_trun = off; off += al(ntiles * 4 + 4);  // stitch tile -> run (k_tile_runs)
@@ -3875,6 +3907,16 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
                       runs.packed != nullptr && tv.approx != nullptr;
   // (the carry reads no replay slots unless k_marks_select wrote them)
   if (!p1summ) rpb.slot = nullptr;
+  // pass-1 summaries are read where pass 1 wrote them (summ_at): the selection
+  // writes a byte per chunk instead of copying 56 (metric step 14.47 vs 14.61 ms
+  // median in-process, profiles/r4/ab4/ab_copy_log2.txt; KS_SUMM_COPY=1: the copy)
+  if (p1summ && getenv("KS_SUMM_COPY") == nullptr) {
+    sm.sel = reinterpret_cast<uint8_t *>(W + o_ssel);
+    sm.pD = sp1.D;
+    sm.pM = sp1.M;
+    sm.pN = sp1.N;
+    sm.pA = sp1.A;
+  }
   // per-index code store (uint16 per scan index, 2 B x 256 per chunk):
   // written by the compressed unexpanded pass 1 (k_pass1<1, ...>) for the
   // binade summaries (k_summaries)

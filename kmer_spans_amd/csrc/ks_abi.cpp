@@ -143,6 +143,13 @@ ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out) {
       return fail(KS_ERR_NOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
     }
     b.bytes = want;
+    // KS_DEBUG_POISON=<byte> (tests): a fresh slot holds that byte everywhere,
+    // so a read of workspace the call did not write shows up reproducibly
+    static const int poison = getenv("KS_DEBUG_POISON") ? (int)strtol(getenv("KS_DEBUG_POISON"), nullptr, 0) : -1;
+    if (poison >= 0) {
+      KS_HIP(hipMemset(b.ptr, poison & 0xff, want));
+      KS_HIP(hipDeviceSynchronize());
+    }
   }
   *out = b.ptr;
   return KS_OK;

@@ -264,12 +264,15 @@ __global__ void k_run_counts(const int64_t *__restrict__ ra, const int64_t *__re
 // cbase[r] >= frac * cbase[n] (out: r, cbase[r], tbase[r]).
 __global__ void k_split(const int64_t *__restrict__ cbase, const int64_t *__restrict__ tbase, int64_t n,
                         double frac, unsigned long long *__restrict__ out) {
-  // frac < 0: by size -- 0.7 for a genome (the second part's pass 1 covers
-  // the first part's post-processing), 0.8 at shard sizes (<= 2 M chunks,
-  // ~500 Mbp), where that post-processing is short and the second part's
-  // own tail dominates (in-process A/B at the 8-way shard: 2.47 vs 2.58 ms;
-  // 4-way equal; 2-way and the whole genome 0.7)
-  if (frac < 0) frac = cbase[n] <= (2ll << 20) ? 0.8 : 0.7;
+  // frac < 0: by size -- 0.65 for a genome (a shorter predictor before the
+  // first part's pass 1; in process on two boxes: 0.6 13.91-14.00 vs 0.7
+  // 14.09-14.22 ms, then 0.65 14.07-14.11 vs 0.6 14.19-14.29 vs 0.7
+  // 14.24-14.29 ms, rank and k = 15 unchanged: profiles/r4/ab4/ab_frac_*.txt;
+  // 0.7 until round 4), 0.8 at
+  // shard sizes (<= 2 M chunks, ~500 Mbp), where the post-processing is short
+  // and the second part's own tail dominates (in-process A/B at the 8-way
+  // shard: 2.47 vs 2.58 ms; 4-way equal)
+  if (frac < 0) frac = cbase[n] <= (2ll << 20) ? 0.8 : 0.65;
   const int64_t half = (int64_t)((double)cbase[n] * frac);
   int64_t lo = 0, hi = n;
   while (lo < hi) {

@@ -4,7 +4,7 @@
 #   m: metric (log2 k = 13)   r: weighted rank k = 13 / 15   x: +-1 k = 7 / 13
 #   p: per-genome phases (config 5)   d: rank carry / rescan diagnostics
 #   s: shard-of-8 and config 2 (fixed cost at small sizes)   q: predictor sampling stride
-#   c: GPU tests, then pass-1 summaries read in place vs copied
+#   c: GPU tests, then pass-1 summaries read in place vs copied   f: split fraction (metric)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${1:-job}
@@ -38,6 +38,14 @@ tail -1 $O/pytest_gpu.txt
 ab ab_sel_log2 --rounds 3 --steps 3 one: copy:KS_SUMM_COPY=1
 ab ab_sel_shard8 --rounds 4 --steps 10 --shard-of 8 one: copy:KS_SUMM_COPY=1
 ab ab_sel_k15 --rounds 2 --steps 2 --k 15 one: copy:KS_SUMM_COPY=1
+fi
+if [[ $P == *f* ]]; then
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 || { tail -30 $O/pytest_gpu.txt; exit 1; }
+tail -1 $O/pytest_gpu.txt
+ab ab_frac_log2 --rounds 3 --steps 3 one: f70:KS_SPLIT_FRAC=0.7 f55:KS_SPLIT_FRAC=0.55 f65:KS_SPLIT_FRAC=0.65
+ab ab_frac_rank --rounds 3 --steps 2 --score rank one: f70:KS_SPLIT_FRAC=0.7
+ab ab_frac_k15 --rounds 2 --steps 2 --k 15 one: f70:KS_SPLIT_FRAC=0.7
+ab ab_frac_k15rank --rounds 2 --steps 2 --k 15 --score rank one: f70:KS_SPLIT_FRAC=0.7
 fi
 if [[ $P == *p* ]]; then
 timeout -k 10 300 python -u tools/genome_phases.py --ext-gib 32 > $O/phases32.txt 2>&1 || { tail -30 $O/phases32.txt; exit 1; }

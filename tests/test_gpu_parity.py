@@ -23,7 +23,8 @@ def _diff(a_pos, a_score, b_pos, b_score):
 
 def _assert_same_regions(a_pos, a_score, b_pos, b_score, what=""):
     assert a_pos.shape == b_pos.shape, (what, a_pos.shape, b_pos.shape, _diff(a_pos, a_score, b_pos, b_score))
-    assert np.array_equal(a_pos, b_pos), what
+    assert np.array_equal(a_pos, b_pos), (what, a_pos.T.tolist()[:8], b_pos.T.tolist()[:8],
+                                          _diff(a_pos, a_score, b_pos, b_score))
     # bitwise FP64 equality of the scores
     assert np.array_equal(a_score.view(np.uint64), b_score.view(np.uint64)), what
 
@@ -103,8 +104,10 @@ def test_random_regions_vs_oracle(K, oracle, ctx, algo):
             o = oracle.kmer_regions(seqs, k, w, mw, ms)
             if g["pos"].shape != o["pos"].shape or not np.array_equal(g["pos"], o["pos"]):
                 # a failure that does not repeat: the same call again, 3 times
-                again = [K.kmer_regions(seqs, k, w, mw, ms)["pos"].shape for _ in range(3)]
-                print("random case mismatch", (k, mw, ms, [len(s) for s in seqs]), "again", again)
+                again = [K.kmer_regions(seqs, k, w, mw, ms)["pos"] for _ in range(3)]
+                print("random case mismatch", (k, mw, ms, [len(s) for s in seqs]), "again",
+                      [(a.shape, bool(np.array_equal(a, o["pos"]))) for a in again],
+                      "first", g["pos"].T.tolist()[:8], "oracle", o["pos"].T.tolist()[:8])
             _assert_same_regions(g["pos"], g["score"], o["pos"], o["score"], (seqs, k, mw, ms))
             assert np.array_equal(g["counts"], o["counts"])
             assert g["n"] == o["n"]

@@ -127,6 +127,39 @@ ks_status ks_tr_lr_regions(ks_ctx *ctx, const char *const *seqs, const int64_t *
                            const double *kmer_scores, const double *trans_scores, int64_t n_scores,
                            double *spectra, ks_regions *out);
 
+/* ---------------------------------------------------------------------
+ * Several GPUs of one node behind the same entry points.  With a device list
+ * of two or more entries, ks_kmer_counts, ks_kmer_regions and
+ * ks_low_comp_regions called with ctx == NULL (what the .Call shim does)
+ * spread the call: the sequences -- a sequence longer than half a fair share
+ * cut in the middle of its N gaps of >= 1000 bases when whole sequences do
+ * not balance -- are dealt to the devices by LPT on length, each device
+ * stages, counts and scans its share on a context of its own from a host
+ * thread of its own, counts and visit histograms are added exactly (uint32
+ * wrap-around), kmer_low_comp_regions builds every device's weighted-rank
+ * table from the summed counts, and the regions come back in the caller's
+ * coordinates and (seq_id, beg) order: the results equal the one-device
+ * call's.  The list may repeat a device (two contexts on one card).  A call
+ * with an explicit ctx runs on that ctx's device only.  The reference runs
+ * these routines on R's main thread (kmer_spans.c:452-621); this replaces the
+ * mclapply-over-sequences pattern of test.R:550-567 inside one call. */
+/* devices: n device ordinals (n = 0: device 0 alone, the default).  Read from
+ * KS_DEVICES ("0,1,2,3") at first use unless set here. */
+ks_status ks_set_devices(const int32_t *devices, int32_t n);
+/* The list's length; its first cap entries into devices. */
+int32_t ks_get_devices(int32_t *devices, int32_t cap);
+/* The shard plan (host only, no device): the pieces nparts devices take, rows
+ * (part, sequence, lo, hi) of int64 in out[4 * cap], each part's rows ordered
+ * by (sequence, lo); returns the number of pieces (> cap: only cap written),
+ * -1 on a bad argument. */
+int64_t ks_shard_plan(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t nparts,
+                      int64_t *out, int64_t cap);
+/* Merge of the parts' regions (parts[p] in the coordinates of part p's pieces
+ * passed as sequences in plan order, as a call on them returns them) into the
+ * caller's coordinates and (seq_id, beg) order (host only). */
+ks_status ks_merge_parts(const int64_t *plan, int64_t npieces, int32_t nparts, const ks_regions *parts,
+                         ks_regions *out);
+
 /* kmer_seq_r(k_r) -- replaces kmer_spans.c:623-639.  out: 4^k * (k+1) bytes,
  * NUL-terminated k-char strings in internal code order. Host only. */
 ks_status ks_kmer_seq(int32_t k, char *out, size_t out_len);

@@ -51,6 +51,23 @@ class _HostSeqs:
         self.lens = np.array([b.size for b in self.bufs] or [0], dtype=np.int64)
 
 
+def set_devices(devices) -> None:
+    """Devices the host entry points (kmer_counts, kmer_regions,
+    kmer_low_comp_regions on device 0, i.e. the library's default) spread a
+    call over (ks_set_devices: LPT shards, one context and host thread per
+    entry, counts added, regions merged into the caller's order).  [] or one
+    device: device 0 alone.  The list may repeat a device."""
+    d = np.ascontiguousarray(np.asarray(list(devices), dtype=np.int32))
+    check(load().ks_set_devices(d.ctypes.data if d.size else None, int(d.size)))
+
+
+def get_devices() -> list:
+    n = int(load().ks_get_devices(None, 0))
+    d = np.zeros(max(n, 1), dtype=np.int32)
+    load().ks_get_devices(d.ctypes.data, n)
+    return d[:n].tolist()
+
+
 def _ctx(device):
     """Device 0 uses the library's lazily created default context, so that
     argument errors surface before any HIP call (kmer_spans.c validates before

@@ -533,7 +533,14 @@ extern "C" ks_status ks_kmer_counts(ks_ctx *ctx, const char *const *seqs, const 
     return fail(KS_ERR_ARG, "k must be a positive integer less than 1+MAX_K");
   if (!counts || !n_words) return fail(KS_ERR_ARG, "null output");
   if (use_broker()) return broker_kmer_counts(seqs, lens, nseq, k, counts, n_words);
+  if (!ctx && multi_devices() > 1) return multi_kmer_counts(seqs, lens, nseq, k, counts, n_words);
   KS_TRY(default_ctx(&ctx));
+  return kmer_counts_on(ctx, seqs, lens, nseq, k, counts, n_words);
+}
+
+// The body of ks_kmer_counts on one context (validated arguments).
+ks_status ks::kmer_counts_on(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k,
+                             int32_t *counts, double *n_words) {
   KS_ENTER(ctx);
   const HostEnd host_end{ctx};  // (ks_set_host_cache)
   Staged st;
@@ -555,8 +562,8 @@ extern "C" ks_status ks_kmer_counts(ks_ctx *ctx, const char *const *seqs, const 
 // staged bases is counted on the side stream while the rest crosses PCIe;
 // otherwise the count follows the staging.  On return ctx->stream is ordered
 // after the count; *words (nullable) = the words counted.
-static ks_status stage_counted(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq, int k,
-                               int32_t *d_cnt, Staged *st, double *words) {
+ks_status ks::stage_counted(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq, int k,
+                           int32_t *d_cnt, Staged *st, double *words) {
   const size_t nb = (size_t)4 << (2 * k);
   int64_t total_in = 0;
   for (int32_t q = 0; q < nseq; ++q) total_in += std::max<int64_t>(lens[q], 0);
@@ -608,13 +615,22 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
   if (!out || !n_bases) return fail(KS_ERR_ARG, "null output");
   memset(out, 0, sizeof(*out));
   if (use_broker()) return broker_kmer_regions(seqs, lens, nseq, k, w, w_len, min_width, min_score, visits, n_bases, out);
-  KS_TRY(default_ctx(&ctx));
-  KS_ENTER(ctx);
-  const HostEnd host_end{ctx};  // (ks_set_host_cache)
   double n = 0;
   for (int32_t q = 0; q < nseq; ++q)
     if (lens[q] >= k) n += (double)lens[q];                   // :535
   *n_bases = n;
+  if (!ctx && multi_devices() > 1) return multi_kmer_regions(seqs, lens, nseq, k, w, min_width, min_score, visits, out);
+  KS_TRY(default_ctx(&ctx));
+  return kmer_regions_on(ctx, seqs, lens, nseq, k, w, min_width, min_score, visits, out);
+}
+
+// The body of ks_kmer_regions on one context (validated arguments).
+ks_status ks::kmer_regions_on(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k,
+                              const double *w, int32_t min_width, double min_score, int32_t *visits,
+                              ks_regions *out) {
+  KS_ENTER(ctx);
+  const HostEnd host_end{ctx};  // (ks_set_host_cache)
+  const int64_t want = (int64_t)1 << (2 * k);
   static const bool dbg = getenv("KS_DEBUG_HOST") != nullptr;  // phase times to stderr
   const double t0 = now_ms();
   // The score table's upload and compression (host w, independent of the
@@ -655,6 +671,24 @@ extern "C" ks_status ks_kmer_regions(ks_ctx *ctx, const char *const *seqs, const
   }
   const double t1 = now_ms();
   const double t2 = now_ms();
+  static const bool verify = getenv("KS_DEBUG_VERIFY") != nullptr;  // (diagnostics, ks_scan_chunked.hip)
+  if (verify && k <= 11) {  // the device table against the caller's w
+    std::vector<double> dv((size_t)want);
+    if (t->compressed) {
+      std::vector<uint16_t> cd((size_t)want);
+      std::vector<double> lut((size_t)t->distinct);
+      KS_HIP(hipMemcpy(cd.data(), t->d_codes, cd.size() * 2, hipMemcpyDeviceToHost));
+      KS_HIP(hipMemcpy(lut.data(), t->d_lut, lut.size() * 8, hipMemcpyDeviceToHost));
+      for (int64_t i = 0; i < want; ++i) dv[i] = lut[cd[i]];
+    } else {
+      KS_HIP(hipMemcpy(dv.data(), t->d_vals, dv.size() * 8, hipMemcpyDeviceToHost));
+    }
+    long long bad = 0;
+    for (int64_t i = 0; i < want; ++i)
+      if (memcmp(&dv[i], &w[i], 8) != 0 && !(dv[i] != dv[i] && w[i] != w[i]) && ++bad <= 8)
+        fprintf(stderr, "[verify] table entry %lld = %.17g, host %.17g\n", (long long)i, dv[i], w[i]);
+    if (bad) fprintf(stderr, "[verify] %lld table entries differ\n", bad);
+  }
   if (rc == KS_OK) {
     t->ctx = ctx;
     rc = table_expand(ctx, t, (size_t)host_ext_cap(st.total), static_cast<const int32_t *>(d_cnt));
@@ -689,6 +723,8 @@ extern "C" ks_status ks_low_comp_regions(ks_ctx *ctx, const char *const *seqs, c
   if (!counts || !ranks || !n || !out) return fail(KS_ERR_ARG, "null output");
   memset(out, 0, sizeof(*out));
   if (use_broker()) return broker_low_comp(seqs, lens, nseq, k, min_width, min_score, thr, counts, ranks, n, out);
+  if (!ctx && multi_devices() > 1)
+    return multi_low_comp_regions(seqs, lens, nseq, k, min_width, min_score, thr, counts, ranks, n, out);
   KS_TRY(default_ctx(&ctx));
   KS_ENTER(ctx);
   const HostEnd host_end{ctx};  // (ks_set_host_cache)

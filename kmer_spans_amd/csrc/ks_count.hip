@@ -1121,7 +1121,7 @@ __global__ void __launch_bounds__(256) k_sum_u32(const uint32_t *__restrict__ c,
 ks_status count_words(ks_ctx *ctx, hipStream_t st, const int32_t *counts_dev, int k, double *n_words) {
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
-  unsigned long long *d = reinterpret_cast<unsigned long long *>(scal) + 40;
+  unsigned long long *d = reinterpret_cast<unsigned long long *>(scal) + kScSumWords;
   KS_HIP(hipMemsetAsync(d, 0, 8, st));
   const int64_t n = (int64_t)1 << (2 * k);
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, (int64_t)ctx->num_cus * 8));
@@ -1146,7 +1146,7 @@ ks_status launch_count(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, const R
   hipStream_t st = ctx->stream;
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
-  unsigned long long *d_words = reinterpret_cast<unsigned long long *>(scal) + 1;
+  unsigned long long *d_words = reinterpret_cast<unsigned long long *>(scal) + kScWords;
   KS_HIP(hipMemsetAsync(d_words, 0, 8, st));
   const int64_t ntiles = (total + kTile - 1) / kTile;
   if (ntiles > 0) {
@@ -1197,7 +1197,7 @@ ks_status launch_count_multi(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, c
   hipStream_t st = ctx->stream;
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
-  unsigned long long *d_words = reinterpret_cast<unsigned long long *>(scal) + 8;
+  unsigned long long *d_words = reinterpret_cast<unsigned long long *>(scal) + kScMultiWords;
   for (int b0 = 0; b0 < nk; b0 += kMaxBatch) {
     const int nb = std::min(kMaxBatch, nk - b0);
     KBatch kb{};

@@ -70,6 +70,17 @@ enum Slot : int {
   SLOT_COUNT
 };
 
+// SLOT_SCALARS (4 KiB = 512 u64 words): every user's offset, in one place.
+// Users on one context run in order on its streams; none of these ranges
+// overlap, so a count and a scan may share a context's slot.
+constexpr int kScEvents = 0;       // find_runs: run-event count
+constexpr int kScWords = 1;        // launch_count: words counted
+constexpr int kScLayout = 8;       // run_layout: 8 aggregates [8, 16)
+constexpr int kScRegions = 16;     // scan_core: region counters [16, 16 + kSegs)
+constexpr int kScSumWords = 96;    // count_words: sum of a histogram
+constexpr int kScMultiWords = 104; // launch_count_multi: words per k of a batch [104, 112)
+constexpr int kScEnd = 112;
+
 struct DevBuf {
   void *ptr = nullptr;
   size_t bytes = 0;
@@ -231,6 +242,28 @@ bool hip_usable_here();  // false in a child forked after HIP was initialised
 // then [score | 0.0] doubles.
 ks_status regions_alloc(ks_regions *out, int64_t n);
 void regions_cache_release();  // the kept output blocks (ks_release_cache)
+struct Staged;
+// Host entry bodies on one context, arguments validated (ks_abi.cpp); the
+// multi-device forms (ks_multi.cpp) run them on a shard of the input each.
+ks_status kmer_counts_on(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k,
+                         int32_t *counts, double *n_words);
+ks_status kmer_regions_on(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k,
+                          const double *w, int32_t min_width, double min_score, int32_t *visits, ks_regions *out);
+// Stage host sequences and count their k-mers into d_cnt (zeroed here), the
+// count overlapping the PCIe transfer where it can; ctx->stream is ordered
+// after the count on return; *words (nullable) = the words counted.
+ks_status stage_counted(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32_t nseq, int k,
+                        int32_t *d_cnt, Staged *st, double *words);
+// Devices of the NULL-context host entry points (ks_set_devices, KS_DEVICES);
+// > 1: the multi-device forms below take the call.
+int multi_devices();
+ks_status multi_kmer_counts(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k, int32_t *counts,
+                            double *n_words);
+ks_status multi_kmer_regions(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k, const double *w,
+                             int32_t min_width, double min_score, int32_t *visits, ks_regions *out);
+ks_status multi_low_comp_regions(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k,
+                                 int32_t min_width, double min_score, double thr, int32_t *counts, double *ranks,
+                                 double *n, ks_regions *out);
 // GPU broker for fork children (ks_broker.cpp): broker_before_hip() forks it
 // right before a process's first HIP use (when enabled); use_broker() is true
 // in a child forked after that, whose host-buffer calls the broker_* forward.
@@ -298,6 +331,7 @@ ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int t
 // segments of segcap slots, each with its own counter, so that appends from
 // thousands of waves do not serialise on one address; slot s*segcap + i.
 constexpr int kSegs = 64;
+static_assert(kScRegions + kSegs <= kScSumWords && kScEnd * 8 <= 4096, "SLOT_SCALARS layout");
 static_assert(kSegs <= 64, "ks_ctx::hreg holds kSegs counters");
 
 struct RegionBuf {

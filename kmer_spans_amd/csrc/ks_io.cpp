@@ -380,6 +380,9 @@ extern "C" ks_status ks_kmers_to_file(ks_ctx *ctx, const char *seq_path, const c
   memcpy(info->out_path, of.c_str(), of.size() + 1);
   if (use_broker()) return broker_kmers_to_file(seq_path, out_prefix, ks, nk, min_l, magic, info);
   KS_TRY(default_ctx(&ctx));
+  // (the context is this thread's before the end-of-call guard exists: a
+  // refused call must not release another thread's workspace)
+  KS_ENTER(ctx);
   struct End {  // a host-buffer entry point: ks_set_host_cache policy
     ks_ctx *c;
     ~End() { host_call_end(c); }
@@ -392,7 +395,6 @@ extern "C" ks_status ks_kmers_to_file(ks_ctx *ctx, const char *seq_path, const c
   };
   HostView v;
   if (open_view(seq_path, &v) != KS_OK) return na(ks_last_error());
-  KS_ENTER(ctx);
   ks_fasta fa;
   fasta_reset(&fa);
   const int64_t ml = std::isfinite(min_l) ? (int64_t)std::ceil(min_l) : (min_l > 0 ? INT64_MAX : INT64_MIN);

@@ -300,7 +300,7 @@ ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int t
   lay->tbase = lay->cbase + (n + 1);
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
-  unsigned long long *agg = reinterpret_cast<unsigned long long *>(scal) + 8;
+  unsigned long long *agg = reinterpret_cast<unsigned long long *>(scal) + kScLayout;
   KS_HIP(hipMemsetAsync(agg, 0, 24, st));
   if (trlr && !offs_dev) return fail(KS_ERR_INTERNAL, "run_layout: tr_lr needs sequence offsets");
   hipLaunchKernelGGL(k_run_counts, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st, runs.a, runs.b,
@@ -345,7 +345,7 @@ ks_status find_runs(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, Runs *runs
   runs->packed = nullptr;
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
-  unsigned long long *d_count = reinterpret_cast<unsigned long long *>(scal);
+  unsigned long long *d_count = reinterpret_cast<unsigned long long *>(scal) + kScEvents;
   int64_t cap = 1 << 20;
   if (ctx->slots[SLOT_EVENTS].bytes / 8 > (size_t)cap) cap = ctx->slots[SLOT_EVENTS].bytes / 8;
   unsigned long long n_ev = 0;

@@ -378,7 +378,7 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
                                      reg_bytes > 64 ? (int64_t)((reg_bytes - 64) / 28) : 0) / kSegs;
   void *scal = nullptr;
   KS_TRY(ensure(ctx, SLOT_SCALARS, 4096, &scal));
-  unsigned long long *d_rcount = reinterpret_cast<unsigned long long *>(scal) + 16;  // [kSegs]
+  unsigned long long *d_rcount = reinterpret_cast<unsigned long long *>(scal) + kScRegions;  // [kSegs]
   std::vector<unsigned long long> hcnt(kSegs, 0);
   auto read_counts = [&]() -> ks_status {  // -> hcnt (sync), or the copy the chunked scan made
     if (ctx->hreg_ok) {

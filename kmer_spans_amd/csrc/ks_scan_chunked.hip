@@ -3703,6 +3703,101 @@ __global__ void k_candidates(Chunks g, const int64_t *__restrict__ ra, const int
 
 }  // namespace
 
+// KS_DEBUG_VERIFY=1 (diagnostics): after a chunked scan of a small input
+// (<= 64 Mi bases, k <= 11, kmer_regions mode), the device's packed codes,
+// chunk layout, pass-1 results and carry modes are copied back and checked
+// against a host recomputation from the sequence bytes and the base table;
+// every mismatch goes to stderr with its chunk and both values.  Reads the
+// buffers after the call's last kernel, so a value that is right here but was
+// wrong when a kernel read it points at an ordering edge, one that is wrong
+// here at the kernel that wrote it.
+static void debug_verify(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, const TableView &tv,
+                         const Chunks &g, const P1 &p1, const Carry &cr, bool exact, int trlr) {
+  const int64_t nch = g.nch;
+  if (trlr || k > 11 || total > ((int64_t)64 << 20) || nch <= 0) return;
+  (void)hipDeviceSynchronize();
+  auto get = [&](auto *dst, const void *src, size_t n) {
+    if (n) (void)hipMemcpy(dst, src, n * sizeof(*dst), hipMemcpyDeviceToHost);
+  };
+  std::vector<uint8_t> seq((size_t)total);
+  get(seq.data(), s->seq, (size_t)total);
+  const int64_t nk = (int64_t)1 << (2 * k);
+  std::vector<double> val((size_t)nk);
+  if (tv.compressed) {
+    std::vector<uint16_t> codes((size_t)nk);
+    get(codes.data(), tv.codes, (size_t)nk);
+    std::vector<double> lut((size_t)std::max(tv.nlut, 1));
+    get(lut.data(), tv.lut, (size_t)tv.nlut);
+    for (int64_t i = 0; i < nk; ++i) val[i] = lut[codes[i]];
+  } else {
+    get(val.data(), tv.vals, (size_t)nk);
+  }
+  long long bad = 0;
+  auto report = [&](const char *what, int64_t c, double got, double want) {
+    if (++bad <= 12)
+      fprintf(stderr, "[verify] chunk %lld of %lld: %s = %.17g, host %.17g\n", (long long)c, (long long)nch, what, got,
+              want);
+  };
+  if (g.packed) {
+    const int64_t nw = total / 16 + 1;
+    std::vector<uint32_t> pk((size_t)nw);
+    get(pk.data(), g.packed, (size_t)nw);
+    for (int64_t w = 0; w < nw; ++w) {
+      uint32_t want = 0;
+      for (int q = 0; q < 16; ++q) want |= enc(16 * w + q < total ? seq[16 * w + q] : (uint8_t)'N') << (30 - 2 * q);
+      if (pk[w] != want && 16 * w + 16 <= total) report("packed word", w, (double)pk[w], (double)want);
+    }
+  }
+  std::vector<int64_t> start((size_t)nch);
+  std::vector<int32_t> n((size_t)nch), run((size_t)nch), tbeg((size_t)nch), targ((size_t)nch);
+  std::vector<double> cexit((size_t)nch), tmax((size_t)nch), cx((size_t)nch);
+  std::vector<uint8_t> mode((size_t)nch);
+  get(start.data(), g.start, (size_t)nch);
+  get(n.data(), g.n, (size_t)nch);
+  get(run.data(), g.run, (size_t)nch);
+  get(tbeg.data(), p1.tbeg, (size_t)nch);
+  get(targ.data(), p1.targ, (size_t)nch);
+  get(cexit.data(), p1.cexit, (size_t)nch);
+  get(tmax.data(), p1.tmax, (size_t)nch);
+  get(cx.data(), cr.x, (size_t)nch);
+  get(mode.data(), cr.mode, (size_t)nch);
+  const uint64_t kmask = (uint64_t)nk - 1;
+  for (int64_t c = 0; c < nch; ++c) {
+    // clean trajectory from 0 over indices start .. start + n - 1 (k-mer
+    // ending at index - 1), as P1Lane::step
+    double prev = 0.0, best = 0.0;
+    int beg = -1, arg = 0;
+    for (int i = 0; i < n[c]; ++i) {
+      const int64_t p = start[c] + i;
+      uint64_t code = 0;
+      for (int64_t q = p - k; q < p; ++q) code = ((code << 2) | enc(seq[q])) & kmask;
+      const double sv = val[code];
+      const double tt = prev + sv;
+      const double S = tt > 0 ? tt : 0.0;
+      const bool open = (prev == 0) & (S > 0), close = (prev > 0) & (S == 0);
+      const bool up = open | (S > best);
+      best = up ? S : best;
+      arg = up ? i : arg;
+      beg = open ? i : (close ? -1 : beg);
+      prev = S;
+    }
+    auto ne = [](double a, double b) { return memcmp(&a, &b, 8) != 0; };
+    if (ne(cexit[c], prev)) report("clean exit", c, cexit[c], prev);
+    if (prev > 0) {
+      if (tbeg[c] != beg) report("tail begin", c, tbeg[c], beg);
+      if (targ[c] != arg) report("tail argmax", c, targ[c], arg);
+      if (ne(tmax[c], best)) report("tail max", c, tmax[c], best);
+    } else if (tbeg[c] != -1) {
+      report("tail begin (none)", c, tbeg[c], -1);
+    }
+    const bool first = c == 0 || run[c - 1] != run[c];
+    if (first && (mode[c] != kModeClean || cx[c] != 0.0)) report("run-first chunk carry mode", c, mode[c], kModeClean);
+  }
+  (void)exact;
+  if (bad) fprintf(stderr, "[verify] %lld mismatches in %lld chunks (k %d, %lld bases)\n", bad, (long long)nch, k,
+                   (long long)total);
+}
+
 ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, const RunLayout &lay, int k,
                        const TableView &tv, uint64_t mw, double min_score, uint32_t *visits,
                        uint32_t *visits_rescan, const RegionBuf &rb, ks_scan_stats *stats, const ScanMode &mode) {
@@ -3901,8 +3996,12 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // no summaries (KS_NO_EXACT: the general path, for A/B runs and tests)
   // (on the table forms of the pipelined passes -- LDS, line, expanded; an
   // unexpanded table of another size takes the code-store pass and k_summaries)
+  // (exact while every partial sum of a run is: |s| <= 2^20 over fewer than
+  // 2^32 indices stays below 2^52; KS_TEST_SEG_FALLBACK, which forces the
+  // general carry's per-run fallback, takes the general path)
+  const int force_fb = getenv("KS_TEST_SEG_FALLBACK") != nullptr ? 1 : 0;  // tests: force the fallback path
   const bool exact = tv.exact && !mode.trlr && runs.packed != nullptr && (lds_table || line || Jt >= 2) &&
-                     getenv("KS_NO_EXACT") == nullptr;
+                     lay.longest < ((int64_t)1 << 32) && !force_fb && getenv("KS_NO_EXACT") == nullptr;
   const bool p1summ = !exact && (lds_table ? lds_summ : (comp ? (Jt >= 2 || line) : f64_summ)) &&
                       runs.packed != nullptr && tv.approx != nullptr;
   // (the carry reads no replay slots unless k_marks_select wrote them)
@@ -4260,7 +4359,6 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // P2-P5 (without the candidates) of one half on stream strm, with its own
   // replay counter, error bits and fix list; ev[14] / ev[15] mark the last
   // half's phases
-  const int force_fb = getenv("KS_TEST_SEG_FALLBACK") != nullptr ? 1 : 0;  // tests: force the fallback path
   auto post = [&](int hi, const Half &h, hipStream_t strm) -> ks_status {
     const bool last = hi == nhalf - 1;
     const Chunks gv = view(h);
@@ -4431,6 +4529,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   KS_HIP(hipStreamSynchronize(st));
   std::copy(hcv.begin() + 2 * kSegs + 8, hcv.begin() + 3 * kSegs + 8, ctx->hreg);
   ctx->hreg_ok = true;
+  static const bool verify = getenv("KS_DEBUG_VERIFY") != nullptr;
+  if (verify) debug_verify(ctx, s, total, k, tv, g, p1, cr, exact, mode.trlr);
   unsigned long long cand_max = 0, res_max = 0, res_tot = 0;
   for (int q = 0; q < kSegs; ++q) {
     const unsigned long long c0 = hcv[q], c1 = hcv[3 * kSegs + 8 + q];

@@ -325,6 +325,25 @@ ks_status stage(ks_ctx *ctx, const char *const *seqs, const int64_t *lens, int32
             "synced %.2f ms\n", fmt, nchunk, n2, nr, nthr, t_q - t_enter, t_s0 - t_enter, now_ms() - t_enter);
   }
   KS_HIP(hipStreamSynchronize(ctx->stream));
+  static const bool verify = getenv("KS_DEBUG_VERIFY") != nullptr;  // (diagnostics, ks_scan_chunked.hip)
+  if (verify && total <= ((size_t)64 << 20)) {
+    std::vector<uint8_t> back(total);
+    std::vector<int64_t> ob((size_t)nseq + 1);
+    KS_HIP(hipMemcpy(back.data(), d_seq, total, hipMemcpyDeviceToHost));
+    KS_HIP(hipMemcpy(ob.data(), d_offs, ob.size() * 8, hipMemcpyDeviceToHost));
+    long long bad = 0;
+    for (int32_t q = 0; q < nseq; ++q) {
+      if (ob[q] != st->offs[q]) fprintf(stderr, "[verify] staged offset %d = %lld, host %lld\n", q, (long long)ob[q],
+                                        (long long)st->offs[q]);
+      for (int64_t i = 0; i < lens[q]; ++i) {
+        const uint8_t h = (uint8_t)seqs[q][i], d = back[st->offs[q] + i];
+        const bool same = is_n(h) ? is_n(d) : (!is_n(d) && code2(h) == code2(d));
+        if (!same && ++bad <= 8)
+          fprintf(stderr, "[verify] staged base %d:%lld = %u, host %u\n", q, (long long)i, d, h);
+      }
+    }
+    if (bad) fprintf(stderr, "[verify] %lld staged bases differ (format %d)\n", bad, fmt);
+  }
   return KS_OK;
 }
 

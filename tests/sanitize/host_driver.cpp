@@ -67,6 +67,61 @@ int main() {
   if (ks_low_comp_regions(nullptr, seqs, lens, 1, 2, 0, 0.0, 1.5, counts, wv, nn, &out) == KS_OK) return 12;
   if (std::string(ks_last_error()).find("threshold") == std::string::npos) return 13;
   if (ks_table_from_counts(nullptr, nullptr, 13, 1, 0, 0, 0, 0, nullptr, nullptr) == KS_OK) return 14;
+  // multi-device shard plan and merge (ks_multi.cpp, host only): random
+  // sequences with N gaps, every part's regions synthesised in its pieces'
+  // coordinates, merged back
+  for (int it = 0; it < 40; ++it) {
+    const int nseq = 1 + (int)(rnd() % 5), nparts = 1 + (int)(rnd() % 6);
+    std::vector<std::string> ss(nseq);
+    for (auto &s : ss) {
+      const int segs = (int)(rnd() % 6);
+      for (int g = 0; g < segs; ++g) {
+        s.append((size_t)(rnd() % 3000), 'A' + (char)(rnd() % 2) * 2);
+        s.append((size_t)(rnd() % 2) ? 1200 : 7, 'N');
+      }
+    }
+    std::vector<const char *> ptr(nseq);
+    std::vector<int64_t> len(nseq);
+    for (int q = 0; q < nseq; ++q) {
+      ptr[q] = ss[q].data();
+      len[q] = (int64_t)ss[q].size();
+    }
+    const int64_t np = ks_shard_plan(ptr.data(), len.data(), nseq, nparts, nullptr, 0);
+    if (np < 0) return 15;
+    std::vector<int64_t> plan(4 * (size_t)np + 4);
+    if (ks_shard_plan(ptr.data(), len.data(), nseq, nparts, plan.data(), np) != np) return 16;
+    std::vector<int32_t> sid, beg, end;
+    std::vector<double> sc;
+    std::vector<ks_regions> parts(nparts);
+    std::vector<std::vector<int32_t>> ps(nparts), pb(nparts), pe(nparts);
+    std::vector<std::vector<double>> pc(nparts);
+    for (int p = 0; p < nparts; ++p) {
+      int32_t local = 0;
+      for (int64_t i = 0; i < np; ++i) {
+        if (plan[4 * i] != p) continue;
+        const int64_t L = plan[4 * i + 3] - plan[4 * i + 2];
+        if (L > 10) {
+          ps[p].push_back(local);
+          pb[p].push_back(1);
+          pe[p].push_back((int32_t)(L - 2));
+          pc[p].push_back(0.5 * (double)i);
+        }
+        ++local;
+      }
+      parts[p].n = (int64_t)ps[p].size();
+      parts[p].seq_id = ps[p].data();
+      parts[p].beg = pb[p].data();
+      parts[p].end = pe[p].data();
+      parts[p].score = pc[p].data();
+    }
+    ks_regions merged;
+    if (ks_merge_parts(plan.data(), np, nparts, parts.data(), &merged) != KS_OK) return 17;
+    for (int64_t i = 1; i < merged.n; ++i)
+      if (merged.seq_id[i] < merged.seq_id[i - 1] ||
+          (merged.seq_id[i] == merged.seq_id[i - 1] && merged.beg[i] <= merged.beg[i - 1]))
+        return 18;
+    ks_regions_free(&merged);
+  }
   std::printf("host sanitizer run ok (%s)\n", ks_version());
   return 0;
 }

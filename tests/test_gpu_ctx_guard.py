@@ -62,3 +62,46 @@ def test_second_thread_is_refused():
         assert np.array_equal(sc.view(np.uint64), ref[1].view(np.uint64))
     tab.close()
     ctx.close()
+
+
+def test_refused_kmers_to_file_leaves_the_owner_alone(tmp_path):
+    """ks_kmers_to_file on the default context while another thread is inside
+    a kmer_regions call on it is refused, and the refusal does not release
+    the owner's workspace (the end-of-call guard comes after the ownership
+    check): the owner's results stay exact."""
+    import kmer_spans_amd as K
+    from kmer_spans_amd import _lib
+    s = np.frombuffer(b"ACGT", dtype=np.uint8)[np.random.default_rng(3).integers(0, 4, size=24_000_000)].tobytes().decode()
+    fa = tmp_path / "q.fa"
+    fa.write_text(">a\n" + s[:5000] + "\n>b\n" + s[5000:9000] + "\n")
+    k = 11
+    w = np.round(np.random.default_rng(1).normal(size=4 ** k) * 4) / 4 + 0.05
+    ref = K.kmer_regions(s, k, w, 40, 6.0)
+    out, errs = [], []
+    stop = threading.Event()
+
+    def owner():
+        try:
+            for _ in range(6):
+                out.append(K.kmer_regions(s, k, w, 40, 6.0))
+        except Exception as e:  # surfaced below
+            errs.append(e)
+        finally:
+            stop.set()
+
+    th = threading.Thread(target=owner)
+    th.start()
+    refused = 0
+    while not stop.is_set():
+        try:
+            K.kmers_to_file(str(fa), str(tmp_path / "o_"), [3], min_l=1)
+        except _lib.KmerSpansError as e:
+            assert "another thread" in str(e), e
+            refused += 1
+    th.join()
+    assert not errs, errs
+    assert refused > 0
+    for r in out:
+        assert np.array_equal(r["pos"], ref["pos"])
+        assert np.array_equal(r["score"].view(np.uint64), ref["score"].view(np.uint64))
+        assert np.array_equal(r["counts"], ref["counts"])

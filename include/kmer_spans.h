@@ -255,14 +255,22 @@ void ks_table_destroy(ks_table *t);
  * output blocks of >= 1 MiB (ks_regions_free) are kept for reuse and freed here too. */
 void ks_release_cache(void);
 /* Memory policy of the host-buffer entry points (ks_kmer_counts,
- * ks_kmer_regions, ks_low_comp_regions, ks_tr_lr_regions, ks_windowed_dist):
- * keep = 0 (the default; what an R session calling kmer_regions_r once
- * expects) returns the call's device memory when the call ends -- the
- * context's workspace and the pooled table buffer -- so VRAM is back at its
- * pre-call level; keep = 1 keeps them for the next call (no re-allocation:
- * faster repeated calls).  Environment KS_HOST_CACHE=1 sets keep = 1 at load.
- * The pinned host staging buffer is kept either way. */
+ * ks_kmer_regions, ks_low_comp_regions, ks_tr_lr_regions, ks_windowed_dist,
+ * ks_kmers_to_file): what happens to a call's device memory -- the context's
+ * workspace and the pooled table buffer -- when it ends.
+ *   keep = 2 (the default): kept while calls keep coming, returned once the
+ *            context has been idle for the idle time (ks_set_host_cache_idle,
+ *            20 s by default; a library thread returns it), so a session that
+ *            calls kmer_regions_r in a loop pays for fresh VRAM once (the
+ *            driver clears new VRAM: seconds for tens of GiB) and one that
+ *            called it once gets its VRAM back shortly after;
+ *   keep = 0: returned when the call ends (VRAM at its pre-call level on
+ *            return; every call allocates again);
+ *   keep = 1: kept until ks_release_cache() or ks_ctx_destroy.
+ * Environment KS_HOST_CACHE=0/1/2 and KS_HOST_CACHE_SECONDS set them at first
+ * use.  The pinned host staging buffer is kept either way. */
 ks_status ks_set_host_cache(int32_t keep);
+ks_status ks_set_host_cache_idle(double seconds);
 
 /* Fork broker (mclapply after use, test.R:351 then :554-565).  On: right
  * before this process's first HIP use the library forks a broker process (a

@@ -87,7 +87,7 @@ EXPORTS = [
     "ks_count_file_write", "ks_count_file_read", "ks_count_file_free", "ks_kmers_to_file",
     "ks_windowed_dist", "ks_windowed_dev", "ks_table_from_counts",
     "ks_release_cache", "ks_set_fork_broker", "ks_set_host_cache",
-    "ks_set_devices", "ks_get_devices", "ks_shard_plan", "ks_merge_parts",
+    "ks_set_devices", "ks_get_devices", "ks_shard_plan", "ks_merge_parts", "ks_set_host_cache_idle",
 ]
 
 SCORES = {"log2": 1, "pm1": 2, "rank": 3}  # KS_SCORE_* of ks_table_from_counts
@@ -149,6 +149,7 @@ def load():
         "ks_set_fork_broker": ([I32], I32),
         "ks_set_host_cache": ([I32], I32),
         "ks_set_devices": ([P, I32], I32),
+        "ks_set_host_cache_idle": ([D], I32),
         "ks_get_devices": ([P, I32], I32),
         "ks_shard_plan": ([P, P, I32, I32, P, I64], I64),
         "ks_merge_parts": ([P, I64, I32, P, P], I32),

@@ -5,6 +5,7 @@
 // Validation happens before any device work, with the reference's error
 // strings, because R's error() longjmps out of the caller.
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -265,6 +266,7 @@ extern "C" ks_status ks_ctx_create(int32_t device, ks_ctx **out) {
 extern "C" void ks_ctx_destroy(ks_ctx *c) {
   if (!c) return;
   if (c->pid != getpid()) return;  // inherited across fork(): its HIP handles are not ours
+  ks::janitor_forget(c);
   if (c->sub) {
     ks_ctx_destroy(c->sub);
     c->sub = nullptr;
@@ -303,7 +305,34 @@ ks_status ctx_part(ks_ctx *ctx, ks_ctx **part) {
   return KS_OK;
 }
 
-static int g_host_cache = -1;  // -1: KS_HOST_CACHE decides on first use
+// Memory policy of the host-buffer entry points (ks_set_host_cache): 0 returns
+// a call's device memory when it ends, 1 keeps it, 2 (the default) keeps it
+// while calls keep coming and returns it once the context has been idle for
+// g_idle_ms (a janitor thread).  Fresh VRAM is slow to get: the driver clears
+// it (tools/alloc_probe.py: 4-6 s for 128 GiB), so a default of "return at
+// once" made every host call pay its workspace and table buffer again.
+static std::atomic<int> g_host_cache{-1};    // -1: KS_HOST_CACHE decides on first use
+static std::atomic<double> g_idle_ms{-1.0};  // -1: KS_HOST_CACHE_SECONDS (default 20 s)
+
+static int host_cache_mode() {
+  int m = g_host_cache.load();
+  if (m < 0) {
+    const char *e = getenv("KS_HOST_CACHE");
+    m = e ? std::max(0, std::min(2, atoi(e))) : 2;
+    g_host_cache.store(m);
+  }
+  return m;
+}
+
+static double idle_ms() {
+  double v = g_idle_ms.load();
+  if (v < 0) {
+    const char *e = getenv("KS_HOST_CACHE_SECONDS");
+    v = 1000.0 * (e ? std::max(0.0, atof(e)) : 20.0);
+    g_idle_ms.store(v);
+  }
+  return v;
+}
 
 static void free_workspace(ks_ctx *c) {
   (void)hipSetDevice(c->device);
@@ -315,18 +344,146 @@ static void free_workspace(ks_ctx *c) {
   }
 }
 
+static void release_ctx_memory(ks_ctx *c) {
+  free_workspace(c);
+  if (c->sub) free_workspace(c->sub);
+  if (c->part) free_workspace(c->part);
+  pool_release_device(c->device);
+}
+
+namespace {
+// Contexts whose memory goes back at a deadline (policy 2).  The janitor
+// takes a context only when no thread is inside a call on it (the CtxUse
+// ownership word); a busy context is dropped from the list, and its call's
+// end lists it again.  Never destroyed (a process exit joins the thread).
+struct Janitor {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::pair<ks_ctx *, double>> due;  // (context, now_ms() deadline)
+  std::thread th;
+  bool started = false, exiting = false;
+};
+Janitor &janitor() {
+  static Janitor *j = new Janitor();
+  return *j;
+}
+
+bool try_own(ks_ctx *c) {
+  std::thread::id none{};
+  return c->user.compare_exchange_strong(none, std::this_thread::get_id());
+}
+
+void janitor_loop() {
+  Janitor &J = janitor();
+  std::unique_lock<std::mutex> g(J.mu);
+  while (!J.exiting) {
+    if (J.due.empty()) {
+      J.cv.wait(g);
+      continue;
+    }
+    double next = J.due.front().second;
+    for (auto &d : J.due) next = std::min(next, d.second);
+    const double now = now_ms();
+    if (std::isinf(next)) {  // (policy 1: kept until ks_release_cache)
+      J.cv.wait(g);
+      continue;
+    }
+    if (now < next) {
+      J.cv.wait_for(g, std::chrono::duration<double, std::milli>(next - now));
+      continue;
+    }
+    for (size_t i = 0; i < J.due.size();) {
+      if (J.due[i].second > now) {
+        ++i;
+        continue;
+      }
+      ks_ctx *c = J.due[i].first;
+      if (try_own(c)) {
+        release_ctx_memory(c);
+        c->user.store(std::thread::id());
+      }
+      J.due.erase(J.due.begin() + (long)i);
+    }
+  }
+}
+
+void janitor_exit() {
+  Janitor &J = janitor();
+  {
+    std::lock_guard<std::mutex> g(J.mu);
+    J.exiting = true;
+  }
+  J.cv.notify_all();
+  if (J.th.joinable() && J.th.get_id() != std::this_thread::get_id()) J.th.join();
+}
+
+void janitor_list(ks_ctx *c, double deadline) {
+  Janitor &J = janitor();
+  {
+    std::lock_guard<std::mutex> g(J.mu);
+    if (J.exiting) return;
+    bool found = false;
+    for (auto &d : J.due)
+      if (d.first == c) {
+        d.second = deadline;
+        found = true;
+      }
+    if (!found) J.due.emplace_back(c, deadline);
+    if (!J.started) {
+      J.started = true;
+      J.th = std::thread(janitor_loop);
+      atexit(janitor_exit);
+    }
+  }
+  J.cv.notify_all();
+}
+}  // namespace
+
+// (ks_ctx_destroy) a destroyed context leaves the janitor's list
+void janitor_forget(ks_ctx *c) {
+  Janitor &J = janitor();
+  std::lock_guard<std::mutex> g(J.mu);
+  for (size_t i = 0; i < J.due.size();)
+    if (J.due[i].first == c) J.due.erase(J.due.begin() + (long)i);
+    else ++i;
+}
+
+// (ks_release_cache) every listed context's memory back now, where no call holds it
+void janitor_release_all() {
+  Janitor &J = janitor();
+  std::lock_guard<std::mutex> g(J.mu);
+  for (size_t i = 0; i < J.due.size();) {
+    ks_ctx *c = J.due[i].first;
+    if (c->pid == getpid() && try_own(c)) {
+      release_ctx_memory(c);
+      c->user.store(std::thread::id());
+      J.due.erase(J.due.begin() + (long)i);
+    } else {
+      ++i;
+    }
+  }
+}
+
 void host_call_end(ks_ctx *ctx) {
-  if (g_host_cache < 0) g_host_cache = getenv("KS_HOST_CACHE") && atoi(getenv("KS_HOST_CACHE")) != 0;
-  if (g_host_cache || !ctx || ctx->pid != getpid()) return;
-  free_workspace(ctx);
-  if (ctx->sub) free_workspace(ctx->sub);
-  if (ctx->part) free_workspace(ctx->part);
-  pool_release_device(ctx->device);
+  if (!ctx || ctx->pid != getpid()) return;
+  const int mode = host_cache_mode();
+  if (mode != 0) {  // (policy 1: listed for ks_release_cache, never due)
+    janitor_list(ctx, mode == 1 ? HUGE_VAL : now_ms() + idle_ms());
+    return;
+  }
+  release_ctx_memory(ctx);
 }
 }  // namespace ks
 
 extern "C" ks_status ks_set_host_cache(int32_t keep) {
-  ks::g_host_cache = keep ? 1 : 0;
+  if (keep < 0 || keep > 2) return fail(KS_ERR_ARG, "host cache policy must be 0, 1 or 2");
+  ks::g_host_cache.store(keep);
+  return KS_OK;
+}
+
+extern "C" ks_status ks_set_host_cache_idle(double seconds) {
+  if (!(seconds >= 0) || seconds > 1e6) return fail(KS_ERR_ARG, "idle time must be between 0 and 1e6 seconds");
+  ks::g_idle_ms.store(1000.0 * seconds);
   return KS_OK;
 }
 

@@ -236,6 +236,8 @@ void pool_release_device(int dev);             // free the device's pooled expan
 // device memory (ctx's and its sub-context's workspace, the pooled table
 // buffer) goes back to the driver.
 void host_call_end(ks_ctx *ctx);
+void janitor_forget(ks_ctx *ctx);  // (ks_ctx_destroy) off the timed-release list
+void janitor_release_all();        // (ks_release_cache) the listed contexts' memory back now
 ks_status default_ctx(ks_ctx **ctx);  // *ctx or the process default context (fork-checked)
 bool hip_usable_here();  // false in a child forked after HIP was initialised
 // Region output block (ks_regions_free frees it): [seq_id | beg | end] int32,

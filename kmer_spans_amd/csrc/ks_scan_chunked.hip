@@ -3291,13 +3291,10 @@ __global__ void k_fallback_prep(unsigned int *__restrict__ err, unsigned long lo
 // lane per chunk, from the exact entry.  Uncompressed tables read the
 // expanded table (J indices per read) like P1.
 template <int J, bool kCompressed, bool kWide = false>
-__global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
-                                               int k, TableView tv, const uint16_t *__restrict__ codes,
-                                               Carry cr, unsigned int *__restrict__ err, int gated) {
+__device__ __forceinline__ void head_one(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
+                                         const TableView &tv, const uint16_t *__restrict__ codes, const Carry &cr,
+                                         unsigned int *__restrict__ err, int64_t c) {
   const uint32_t *__restrict__ packed = g.packed;
-  const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= g.nch) return;
-  if (gated && !(*(volatile unsigned int *)err & 16u)) return;  // second pass only after a fallback
   const int mode = cr.mode[c];
   if (mode == kModeL || mode == kModeU) return;  // head written by the carry (summary / replay)
   cr.hq[c] = -1;
@@ -3420,6 +3417,20 @@ __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restri
   cr.hq[c] = hq;
   cr.hmax[c] = hmax;
   cr.harg[c] = harg;
+}
+
+// gated: the second pass, after a fallback only (bit 16 of err); queued
+// unconditionally on a small grid (a grid-stride loop), so that the common
+// case costs one short launch instead of a block per 256 chunks (80 us of
+// empty blocks at the metric genome's second part)
+template <int J, bool kCompressed, bool kWide = false>
+__global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
+                                               int k, TableView tv, const uint16_t *__restrict__ codes,
+                                               Carry cr, unsigned int *__restrict__ err, int gated) {
+  if (gated && !(*(volatile unsigned int *)err & 16u)) return;  // second pass only after a fallback
+  for (int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < g.nch;
+       c += (int64_t)gridDim.x * blockDim.x)
+    head_one<J, kCompressed, kWide>(g, seq, total, k, tv, codes, cr, err, c);
 }
 
 // ------------------------------------------------------------------- P5
@@ -4443,12 +4454,14 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       KS_HIP(hipGetLastError());
     }
     auto heads = [&](int gated) {
+      // (gated: a small grid-stride grid; it exits at once unless the carry fell back)
+      const unsigned gh = gated ? std::min<unsigned>(gch_h, (unsigned)ctx->num_cus * 2) : gch_h;
 #define KS_HEADS(J, C)                                                                                           \
-  hipLaunchKernelGGL((k_heads<J, C>), dim3(gch_h), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes, cr, err_h, \
+  hipLaunchKernelGGL((k_heads<J, C>), dim3(gh), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes, cr, err_h, \
                      gated)
       if (comp) KS_HEADS(1, true);
       else if (J == 4 && tv.line)
-        hipLaunchKernelGGL((k_heads<4, false, true>), dim3(gch_h), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes,
+        hipLaunchKernelGGL((k_heads<4, false, true>), dim3(gh), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes,
                            cr, err_h, gated);
       else if (J == 4) KS_HEADS(4, false);
       else if (J == 3) KS_HEADS(3, false);

@@ -1254,6 +1254,7 @@ void pool_release_device(int dev) {
 extern "C" void ks_release_cache(void) {
   regions_cache_release();
   if (!hip_usable_here()) return;
+  janitor_release_all();
   std::lock_guard<std::mutex> g(g_pool_mu);
   for (int d = 0; d < 64; ++d) pool_free_all(d);
 }

@@ -639,11 +639,13 @@ def test_trlr_nonfinite_tables(K, oracle, ctx, nan):
     ctx.set_scan_algo(-1)
 
 
-def test_host_entry_returns_vram(K, oracle):
-    """kmer_regions_r from host memory leaves VRAM where it found it (the
-    call's workspace and its table buffer go back to the driver at the end,
-    ks_set_host_cache(0), the default); with ks_set_host_cache(1) they stay
-    for the next call.  Results are the same either way."""
+def test_host_entry_memory_policy(K, oracle):
+    """The host entries' device memory (ks_set_host_cache): policy 0 returns it
+    when the call ends (VRAM back at its pre-call level), 1 keeps it until
+    ks_release_cache, 2 (the default) keeps it while calls keep coming and
+    returns it once the context has been idle for the idle time.  Results are
+    the same under every policy."""
+    import time
     import torch
     from kmer_spans_amd import _lib
     rng = np.random.default_rng(8)
@@ -652,20 +654,30 @@ def test_host_entry_returns_vram(K, oracle):
     k = 11
     w = np.round(rng.normal(size=4 ** k) * 4) / 4 + 0.2
     L = _lib.load()
-    first = K.kmer_regions(seqs, k, w, 40, 8.0)  # warm: contexts, pinned staging
-    torch.cuda.synchronize()
-    free0 = torch.cuda.mem_get_info()[0]
-    again = K.kmer_regions(seqs, k, w, 40, 8.0)
-    free1 = torch.cuda.mem_get_info()[0]
-    assert free1 >= free0 - (16 << 20), (free0, free1)
+    free = lambda: torch.cuda.mem_get_info()[0]  # noqa: E731
+    res = []
     try:
+        assert L.ks_set_host_cache(0) == 0
+        res.append(K.kmer_regions(seqs, k, w, 40, 8.0))  # warm: contexts, pinned staging
+        torch.cuda.synchronize()
+        free0 = free()
+        res.append(K.kmer_regions(seqs, k, w, 40, 8.0))
+        assert free() >= free0 - (16 << 20), (free0, free())
         assert L.ks_set_host_cache(1) == 0
-        kept = K.kmer_regions(seqs, k, w, 40, 8.0)
-        free2 = torch.cuda.mem_get_info()[0]
-        assert free2 < free0 - (64 << 20), (free0, free2)  # the workspace stayed
+        res.append(K.kmer_regions(seqs, k, w, 40, 8.0))
+        assert free() < free0 - (64 << 20), (free0, free())  # the workspace stayed
+        L.ks_release_cache()
+        assert free() >= free0 - (16 << 20), (free0, free())
+        assert L.ks_set_host_cache(2) == 0 and L.ks_set_host_cache_idle(1.0) == 0
+        res.append(K.kmer_regions(seqs, k, w, 40, 8.0))
+        assert free() < free0 - (64 << 20), (free0, free())  # kept while idle < 1 s
+        time.sleep(3.0)
+        assert free() >= free0 - (16 << 20), (free0, free())  # returned by the library's thread
+        res.append(K.kmer_regions(seqs, k, w, 40, 8.0))
     finally:
-        L.ks_set_host_cache(0)
+        L.ks_set_host_cache(2)
+        L.ks_set_host_cache_idle(20.0)
     o = oracle.kmer_regions(seqs, k, w, 40, 8.0)
-    for r in (first, again, kept):
+    for r in res:
         _assert_same_regions(r["pos"], r["score"], o["pos"], o["score"], "host cache policy")
         assert np.array_equal(r["counts"], o["counts"])

@@ -313,8 +313,8 @@ ks_status run_layout(ks_ctx *ctx, const Runs &runs, int k, RunLayout *lay, int t
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt_c, lay->cbase, (int)(n + 1), st));
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt_t, lay->tbase, (int)(n + 1), st));
   // the first half (highest priority) ends first; its carry and stitch run
-  // under the rest of the second half (KS_SPLIT_FRAC: the first part's share)
-  const double frac = getenv("KS_SPLIT_FRAC") ? atof(getenv("KS_SPLIT_FRAC")) : -1.0;  // (-1: by size)
+  // under the rest of the second half (the first part's share by size, k_split)
+  const double frac = -1.0;
   hipLaunchKernelGGL(k_split, dim3(1), dim3(1), 0, st, lay->cbase, lay->tbase, n, frac, agg + 3);
   KS_HIP(hipGetLastError());
   unsigned long long ha[8] = {0, 0, 0, 0, 0, 0, 0, 0};

@@ -4000,9 +4000,9 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const char *f64e = getenv("KS_F64_P1SUMM");
   const bool f64_summ = !comp && !lds_table &&
                         (f64e ? atoi(f64e) != 0 && (line || (Jt >= 2 && Jt <= 4)) : (!line && Jt >= 2 && Jt <= 4));
-  // (small k, the table in LDS: KS_LDS_P1SUMM=0 leaves the summaries to
-  // k_summaries with the LDS-staged table, the former path)
-  const bool lds_summ = lds_table && !(getenv("KS_LDS_P1SUMM") && atoi(getenv("KS_LDS_P1SUMM")) == 0);
+  // (small k, the table in LDS: pass-1 summaries from the LDS-staged table;
+  // the k_summaries path after the prescan took 13.3 vs 8.8 ms at k = 7 log2)
+  const bool lds_summ = lds_table;
   // integer tables: the exact carry (k_carry_exact) needs no predictor and
   // no summaries (KS_NO_EXACT: the general path, for A/B runs and tests)
   // (on the table forms of the pipelined passes -- LDS, line, expanded; an
@@ -4019,8 +4019,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   if (!p1summ) rpb.slot = nullptr;
   // pass-1 summaries are read where pass 1 wrote them (summ_at): the selection
   // writes a byte per chunk instead of copying 56 (metric step 14.47 vs 14.61 ms
-  // median in-process, profiles/r4/ab4/ab_copy_log2.txt; KS_SUMM_COPY=1: the copy)
-  if (p1summ && getenv("KS_SUMM_COPY") == nullptr) {
+  // median in-process, profiles/r4/ab4/ab_copy_log2.txt)
+  if (p1summ) {
     sm.sel = reinterpret_cast<uint8_t *>(W + o_ssel);
     sm.pD = sp1.D;
     sm.pM = sp1.M;
@@ -4087,19 +4087,9 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       // metric step 14.48 vs 14.62 ms median with every second, predictor 0.56 vs
       // 0.64 ms; every eighth: predictor 0.21 ms but more mispredicted binades,
       // carry + stitch 1.18 vs 0.85 ms; profiles/r4/ab4/ab_pred_log2.txt).
-      // KS_PRED_PS=2 / 8 for A/B.
-      const int ps = getenv("KS_PRED_PS") ? atoi(getenv("KS_PRED_PS")) : 4;
-      const void *kf = ps == 8 ? (const void *)k_predict<8> : ps == 4 ? (const void *)k_predict<4> : (const void *)k_predict<2>;
-      KS_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      if (ps == 8)
-        hipLaunchKernelGGL(k_predict<8>, dim3(gl), dim3(1024), lds, strm, view(h), total, k, tv.approx, tv.approx_k,
-                           pp.asum, pp.cexit);
-      else if (ps == 4)
-        hipLaunchKernelGGL(k_predict<4>, dim3(gl), dim3(1024), lds, strm, view(h), total, k, tv.approx, tv.approx_k,
-                           pp.asum, pp.cexit);
-      else
-        hipLaunchKernelGGL(k_predict<2>, dim3(gl), dim3(1024), lds, strm, view(h), total, k, tv.approx, tv.approx_k,
-                           pp.asum, pp.cexit);
+      KS_HIP(hipFuncSetAttribute((const void *)k_predict<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k_predict<4>, dim3(gl), dim3(1024), lds, strm, view(h), total, k, tv.approx, tv.approx_k,
+                         pp.asum, pp.cexit);
       KS_HIP(hipGetLastError());
       return ascan(pp, d_xh, h.r0, h.r1, h.t0, h.t1, strm);
     };
@@ -4144,8 +4134,9 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   if (lds_table) {
     // small k: the whole table in LDS, persistent blocks (one per CU), no
     // code store; with pass-1 summaries the halves as for line tables
-    // integer small-k tables: the int32 pass (KS_NO_LDS_INT: the FP64 one, A/B)
-    const bool lds_int = getenv("KS_NO_LDS_INT") == nullptr;
+    // integer small-k tables: the int32 pass (4.72 vs 5.57 ms at k = 7,
+    // profiles/r4/ab3/ab_k7pm1_int.txt; KS_NO_EXACT: the FP64 pass)
+    const bool lds_int = true;
     auto p1lds = [&](const Half &h, hipStream_t strm) {
       const Chunks gv = view(h);
       const unsigned gl = (unsigned)std::max<int64_t>(1, std::min<int64_t>((h.c1 - h.c0 + 1023) / 1024, ctx->num_cus));
@@ -4518,14 +4509,13 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     return KS_OK;
   };
   if (split) {
-    // KS_RESCAN_EARLY=0 (A/B): both halves' lists after the join
-    const bool early = !(getenv("KS_RESCAN_EARLY") && atoi(getenv("KS_RESCAN_EARLY")) == 0);
+    // (the first half's rescans under the second half's post-processing: config 3
+    // 32.1 vs 32.9 ms with both after the join, profiles/r4/ab3/)
     KS_TRY(post(0, halves[0], st));         // under the second half's pass 1
-    if (early) KS_TRY(emit_rescan(0));      // under the second half's post-processing
+    KS_TRY(emit_rescan(0));                 // under the second half's post-processing
     KS_TRY(post(1, halves[1], ctx->side));
     KS_HIP(hipEventRecord(ctx->ev[13], ctx->side));
     KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
-    if (!early) KS_TRY(emit_rescan(0));
     KS_TRY(emit_rescan(1));
   } else {
     KS_TRY(post(0, halves[0], st));

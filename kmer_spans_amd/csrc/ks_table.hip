@@ -646,8 +646,8 @@ static ks_status build_approx(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev)
   // four predictor blocks per CU, and the second half's predictor no longer
   // holds whole CUs beside the first half's pass 1: metric step 14.37 vs
   // 14.89-15.18 ms with 8 bases (128 KiB, one block per CU), the summary
-  // fixes unchanged (profiles/r4/ab3/approx_k*.json); KS_APPROX_K overrides
-  const int kp_max = getenv("KS_APPROX_K") ? std::max(1, std::min(8, atoi(getenv("KS_APPROX_K")))) : 7;
+  // fixes unchanged (profiles/r4/ab3/approx_k*.json)
+  const int kp_max = 7;
   const int kp = std::min(t->k, kp_max);
   if (hipMalloc(&t->d_approx, ((size_t)2 << (2 * kp)) + 16) != hipSuccess) {
     (void)hipGetLastError();

@@ -13,13 +13,21 @@
 // free their workspace at the end of each call.
 //
 // Build: hipcc -O2 --offload-arch=gfx950 tools/alloc_race.hip -o tools/alloc_race
-// Run:   tools/alloc_race [rounds] [bufs_per_round] [big_gib]
+// Run:   tools/alloc_race [rounds] [bufs_per_round] [big_gib] [child_gib]
+// child_gib > 0: before each round a separate process (this binary, "child
+// G") allocates and writes G GiB and exits, so the round's buffers may land
+// on VRAM another process just freed (which the driver must clear first).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+
+#include <spawn.h>
+#include <sys/wait.h>
+
+extern char **environ;
 
 #define CK(x)                                                                       \
   do {                                                                              \
@@ -63,7 +71,35 @@ __global__ void k_check(const uint32_t *p, uint64_t n, uint32_t seed, unsigned l
   }
 }
 
+static int child_main(int gib) {
+  void *p = nullptr;
+  const size_t b = (size_t)gib << 30;
+  CK(hipMalloc(&p, b));
+  CK(hipMemset(p, 0x77, b));
+  CK(hipDeviceSynchronize());
+  return 0;  // (exit without freeing: the process's teardown returns it)
+}
+
+static void run_child(const char *self, int gib) {
+  char a1[] = "child";
+  char a2[16];
+  snprintf(a2, sizeof a2, "%d", gib);
+  char *argv[] = {const_cast<char *>(self), a1, a2, nullptr};
+  pid_t pid = 0;
+  if (posix_spawn(&pid, self, nullptr, nullptr, argv, environ) != 0) {
+    fprintf(stderr, "spawn failed\n");
+    exit(2);
+  }
+  int st = 0;
+  waitpid(pid, &st, 0);
+  if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+    fprintf(stderr, "child failed (%d)\n", st);
+    exit(2);
+  }
+}
+
 int main(int argc, char **argv) {
+  if (argc > 2 && strcmp(argv[1], "child") == 0) return child_main(atoi(argv[2]));
   const int rounds = argc > 1 ? atoi(argv[1]) : 400;
   const int nb = argc > 2 ? atoi(argv[2]) : 16;
   hipStream_t st, st2;
@@ -87,7 +123,9 @@ int main(int argc, char **argv) {
   std::vector<uint32_t> seeds(nb);
   std::vector<int> form(nb);
   const int big_gib = argc > 3 ? atoi(argv[3]) : 0;  // each round first dirties and frees this much VRAM
+  const int child_gib = argc > 4 ? atoi(argv[4]) : 0;
   for (int r = 0; r < rounds; ++r) {
+    if (child_gib > 0) run_child(argv[0], child_gib);
     if (big_gib > 0) {  // freshly freed, written VRAM: the small buffers below may land on it
       void *big = nullptr;
       const size_t bb = ((size_t)(1 + r % big_gib)) << 30;

@@ -858,6 +858,25 @@ ks_status ks::kmer_regions_on(ks_ctx *ctx, const char *const *seqs, const int64_
                    nullptr, mode);
   }
   const double t4 = now_ms();
+  if (rc == KS_OK && verify && st.total <= ((int64_t)64 << 20)) {  // the same scan again: same regions?
+    ks_regions again{};
+    ScanMode mode;
+    const ks_status r2 = scan_impl(ctx, &st.dev, st.total, k, t, min_width, min_score, nullptr, &again, nullptr, mode);
+    bool same = r2 == KS_OK && again.n == out->n;
+    for (int64_t i = 0; same && i < out->n; ++i)
+      same = again.seq_id[i] == out->seq_id[i] && again.beg[i] == out->beg[i] && again.end[i] == out->end[i] &&
+             memcmp(&again.score[i], &out->score[i], 8) == 0;
+    if (!same) {
+      fprintf(stderr, "[verify] replay differs: first call %lld regions, replay %lld (rc %d), k %d total %lld\n",
+              (long long)out->n, (long long)again.n, (int)r2, k, (long long)st.total);
+      for (int64_t i = 0; i < std::max(out->n, again.n) && i < 8; ++i)
+        fprintf(stderr, "[verify]   %lld: first %d %d %d %.17g | replay %d %d %d %.17g\n", (long long)i,
+                i < out->n ? out->seq_id[i] : -1, i < out->n ? out->beg[i] : -1, i < out->n ? out->end[i] : -1,
+                i < out->n ? out->score[i] : 0.0, i < again.n ? again.seq_id[i] : -1,
+                i < again.n ? again.beg[i] : -1, i < again.n ? again.end[i] : -1, i < again.n ? again.score[i] : 0.0);
+    }
+    ks_regions_free(&again);
+  }
   if (rc == KS_OK && visits) rc = copy_out(ctx, visits, d_cnt, nb);
   if (dbg)
     fprintf(stderr, "[host kmer_regions] stage %.2f table %.2f (upload %.2f compress %.2f) (both %.2f) count %.2f "

@@ -131,7 +131,11 @@ ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out) {
   DevBuf &b = ctx->slots[s];
   if (b.bytes < bytes) {
     if (b.ptr) {
-      KS_HIP(hipStreamSynchronize(ctx->stream));
+      // every stream of the context may still use the old buffer (the
+      // piecewise count of a host entry runs on the side stream, pass 1's
+      // first half on the high-priority one): all three drain before the free
+      for (hipStream_t x : {ctx->stream, ctx->side, ctx->hi})
+        if (x) KS_HIP(hipStreamSynchronize(x));
       KS_HIP(hipFree(b.ptr));
       b.ptr = nullptr;
       b.bytes = 0;

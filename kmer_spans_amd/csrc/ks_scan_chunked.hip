@@ -3749,22 +3749,25 @@ static void debug_verify(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k
       fprintf(stderr, "[verify] chunk %lld of %lld: %s = %.17g, host %.17g\n", (long long)c, (long long)nch, what, got,
               want);
   };
-  if (g.packed) {
-    const int64_t nw = total / 16 + 1;
-    std::vector<uint32_t> pk((size_t)nw);
-    get(pk.data(), g.packed, (size_t)nw);
-    for (int64_t w = 0; w < nw; ++w) {
-      uint32_t want = 0;
-      for (int q = 0; q < 16; ++q) want |= enc(16 * w + q < total ? seq[16 * w + q] : (uint8_t)'N') << (30 - 2 * q);
-      if (pk[w] != want && 16 * w + 16 <= total) report("packed word", w, (double)pk[w], (double)want);
-    }
-  }
   std::vector<int64_t> start((size_t)nch);
   std::vector<int32_t> n((size_t)nch), run((size_t)nch), tbeg((size_t)nch), targ((size_t)nch);
   std::vector<double> cexit((size_t)nch), tmax((size_t)nch), cx((size_t)nch);
   std::vector<uint8_t> mode((size_t)nch);
   get(start.data(), g.start, (size_t)nch);
   get(n.data(), g.n, (size_t)nch);
+  if (g.packed) {  // the words the chunks read (a part's run pass packs its own range only)
+    const int64_t nw = total / 16 + 1;
+    std::vector<uint32_t> pk((size_t)nw);
+    std::vector<uint8_t> used((size_t)nw, 0);
+    for (int64_t c = 0; c < nch; ++c)
+      for (int64_t w = std::max<int64_t>(0, (start[c] - k) / 16); w <= (start[c] + n[c]) / 16 && w < nw; ++w) used[w] = 1;
+    get(pk.data(), g.packed, (size_t)nw);
+    for (int64_t w = 0; w < nw; ++w) {
+      uint32_t want = 0;
+      for (int q = 0; q < 16; ++q) want |= enc(16 * w + q < total ? seq[16 * w + q] : (uint8_t)'N') << (30 - 2 * q);
+      if (used[w] && pk[w] != want && 16 * w + 16 <= total) report("packed word", w, (double)pk[w], (double)want);
+    }
+  }
   get(run.data(), g.run, (size_t)nch);
   get(tbeg.data(), p1.tbeg, (size_t)nch);
   get(targ.data(), p1.targ, (size_t)nch);

@@ -127,6 +127,33 @@ ks_status ctx_busy() {
                           "(create one context per thread)");
 }
 
+// KS_DEBUG_POISON=<byte> (tests, diagnostics): device memory the library
+// allocates or reuses is filled with that byte before the call writes it, so
+// a read of memory the call did not write shows up reproducibly: fresh
+// workspace slots (ensure), every slot at the start of a host entry call
+// (debug_poison_workspace), and the table-side allocations (ks_table.hip:
+// table values / codes / LUT, predictor table, expanded and line tables
+// including pooled buffers taken again).
+int debug_poison_byte() {
+  static const int poison = getenv("KS_DEBUG_POISON") ? (int)strtol(getenv("KS_DEBUG_POISON"), nullptr, 0) : -1;
+  return poison;
+}
+
+void debug_poison(void *p, size_t n) {
+  const int poison = debug_poison_byte();
+  if (poison < 0 || !p || !n) return;
+  (void)hipDeviceSynchronize();
+  (void)hipMemset(p, poison & 0xff, n);
+  (void)hipDeviceSynchronize();
+}
+
+void debug_poison_workspace(ks_ctx *ctx) {
+  if (debug_poison_byte() < 0 || !ctx) return;
+  for (ks_ctx *c : {ctx, ctx->sub, ctx->part})
+    if (c)
+      for (auto &b : c->slots) debug_poison(b.ptr, b.bytes);
+}
+
 ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out) {
   DevBuf &b = ctx->slots[s];
   if (b.bytes < bytes) {
@@ -148,13 +175,7 @@ ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out) {
       return fail(KS_ERR_NOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
     }
     b.bytes = want;
-    // KS_DEBUG_POISON=<byte> (tests): a fresh slot holds that byte everywhere,
-    // so a read of workspace the call did not write shows up reproducibly
-    static const int poison = getenv("KS_DEBUG_POISON") ? (int)strtol(getenv("KS_DEBUG_POISON"), nullptr, 0) : -1;
-    if (poison >= 0) {
-      KS_HIP(hipMemset(b.ptr, poison & 0xff, want));
-      KS_HIP(hipDeviceSynchronize());
-    }
+    debug_poison(b.ptr, want);  // (KS_DEBUG_POISON)
   }
   *out = b.ptr;
   return KS_OK;
@@ -704,6 +725,7 @@ ks_status ks::kmer_counts_on(ks_ctx *ctx, const char *const *seqs, const int64_t
                              int32_t *counts, double *n_words) {
   KS_ENTER(ctx);
   const HostEnd host_end{ctx};  // (ks_set_host_cache)
+  debug_poison_workspace(ctx);  // (KS_DEBUG_POISON)
   Staged st;
   KS_TRY(stage(ctx, seqs, lens, nseq, &st));
   const size_t nb = (size_t)4 << (2 * k);
@@ -791,6 +813,7 @@ ks_status ks::kmer_regions_on(ks_ctx *ctx, const char *const *seqs, const int64_
                               ks_regions *out) {
   KS_ENTER(ctx);
   const HostEnd host_end{ctx};  // (ks_set_host_cache)
+  debug_poison_workspace(ctx);  // (KS_DEBUG_POISON)
   const int64_t want = (int64_t)1 << (2 * k);
   static const bool dbg = getenv("KS_DEBUG_HOST") != nullptr;  // phase times to stderr
   const double t0 = now_ms();
@@ -908,6 +931,7 @@ extern "C" ks_status ks_low_comp_regions(ks_ctx *ctx, const char *const *seqs, c
   KS_TRY(default_ctx(&ctx));
   KS_ENTER(ctx);
   const HostEnd host_end{ctx};  // (ks_set_host_cache)
+  debug_poison_workspace(ctx);  // (KS_DEBUG_POISON)
   // the pipeline of ks_kmer_regions: the bases cross PCIe as 2-bit codes +
   // N runs and are counted in pieces meanwhile (:592-601); the weighted
   // ranks are built on the device (rank_kmers_w :602, closed-form exact

@@ -179,6 +179,11 @@ inline double now_ms() {
 }
 
 ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out);
+// KS_DEBUG_POISON (diagnostics): fill n bytes at p with the poison byte
+// (synchronous; no-op unless set), and every workspace slot of ctx and its
+// sub / part contexts
+void debug_poison(void *p, size_t n);
+void debug_poison_workspace(ks_ctx *ctx);
 ks_status ensure_pinned(ks_ctx *ctx, size_t bytes, void **out);
 // Host sequences staged on the device for a host entry point (ks_stage.cpp).
 struct Staged {

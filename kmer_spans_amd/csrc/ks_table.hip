@@ -608,15 +608,24 @@ static ks_status choose_code12(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev
 static void *ext_alloc(ks_ctx *ctx, size_t bytes, size_t *cap) {
   *cap = bytes;
   void *ext = pool_take(ctx->device, bytes, cap);
-  if (ext) return ext;
+  if (ext) {
+    debug_poison(ext, bytes);  // (KS_DEBUG_POISON: a pooled buffer taken again)
+    return ext;
+  }
   *cap = bytes;
-  if (ext_malloc(&ext, bytes) == hipSuccess) return ext;
+  if (ext_malloc(&ext, bytes) == hipSuccess) {
+    debug_poison(ext, bytes);
+    return ext;
+  }
   (void)hipGetLastError();
   {  // pooled buffers too small for this table may be what is in the way
     std::lock_guard<std::mutex> g(g_pool_mu);
     if (ctx->device >= 0 && ctx->device < 64) pool_free_all(ctx->device);
   }
-  if (ext_malloc(&ext, bytes) == hipSuccess) return ext;
+  if (ext_malloc(&ext, bytes) == hipSuccess) {
+    debug_poison(ext, bytes);
+    return ext;
+  }
   (void)hipGetLastError();
   return nullptr;
 }
@@ -654,6 +663,7 @@ static ks_status build_approx(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev)
     t->d_approx = nullptr;
     return KS_OK;
   }
+  debug_poison(t->d_approx, ((size_t)2 << (2 * kp)) + 16);
   t->approx_k = kp;
   hipLaunchKernelGGL(k_build_approx, dim3((unsigned)std::min<int64_t>(((int64_t)1 << (2 * kp)) / 256 + 1, 4096)),
                      dim3(256), 0, ctx->stream, t->d_codes, t->d_lut, t->d_vals, freq_dev, t->k, kp, t->d_approx);
@@ -930,6 +940,9 @@ ks_status ks::table_create(ks_ctx *ctx, const double *w_host, int32_t k, double 
   KS_TBL_HIP(hipMalloc(&d_w, n * sizeof(double)));
   KS_TBL_HIP(hipMalloc(&t->d_vals, n * sizeof(double)));
   if (allow_compress) KS_TBL_HIP(hipMalloc(&d_bits, n * sizeof(unsigned long long)));
+  debug_poison(d_w, n * sizeof(double));  // (KS_DEBUG_POISON)
+  debug_poison(t->d_vals, n * sizeof(double));
+  if (allow_compress) debug_poison(d_bits, n * sizeof(unsigned long long));
   if (n * sizeof(double) >= ((size_t)64 << 20)) {  // (one hipMemcpy from pageable memory: 20-55 GB/s)
     const ks_status rc = h2d_pinned(ctx, d_w, w_host, n * sizeof(double), 8);
     if (rc != KS_OK) {
@@ -975,6 +988,8 @@ ks_status ks::table_create(ks_ctx *ctx, const double *w_host, int32_t k, double 
     if (nu >= 1 && nu <= 65536) {
       KS_TBL_HIP(hipMalloc(&t->d_codes, n * sizeof(uint16_t)));
       KS_TBL_HIP(hipMalloc(&t->d_lut, nu * sizeof(double)));
+      debug_poison(t->d_codes, n * sizeof(uint16_t));
+      debug_poison(t->d_lut, nu * sizeof(double));
       KS_TBL_HIP(hipMemcpyAsync(t->d_lut, d_bits, nu * sizeof(double), hipMemcpyDeviceToDevice, st));
       hipLaunchKernelGGL(k_assign_codes, dim3(grid), dim3(256), 0, st, t->d_vals, d_bits, nu,
                          t->d_codes, n);
@@ -1034,6 +1049,7 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
     void *p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
     tmp.push_back(p);
+    debug_poison(p, bytes);  // (KS_DEBUG_POISON)
     return p;
   };
   // 1. the counts in stable (count, index) order, their distinct values and
@@ -1121,6 +1137,7 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
       KS_TFC(hipStreamSynchronize(st));
     }
     KS_TFC(hipMalloc(&t->d_vals, n * sizeof(double)));
+    debug_poison(t->d_vals, n * sizeof(double));  // (KS_DEBUG_POISON)
     hipLaunchKernelGGL(k_sub_thr, dim3(grid), dim3(256), 0, st, d_w, thr, t->d_vals, nullptr, n);
     KS_TFC(hipGetLastError());
     unsigned long long *d_am = static_cast<unsigned long long *>(dalloc(24)), h_am[3] = {0, 0, 0};
@@ -1187,6 +1204,7 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
         return fail(KS_ERR_NOMEM, "ks_table_from_counts: device allocation failed");
       }
       KS_TFC(hipMalloc(&t->d_vals, n * sizeof(double)));
+    debug_poison(t->d_vals, n * sizeof(double));  // (KS_DEBUG_POISON)
       KS_TFC(hipMemcpyAsync(d_sv, sv.data(), (size_t)nu * 8, hipMemcpyHostToDevice, st));
       hipLaunchKernelGGL(k_map_counts<double>, dim3(gm), dim3(1024), 0, st, counts_dev, n, d_uniq, (int64_t)nu, d_sv,
                          t->d_vals);

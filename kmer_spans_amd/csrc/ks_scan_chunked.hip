@@ -4347,16 +4347,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
 #undef KS_P1TC
 #undef KS_P1P
   KS_HIP(hipGetLastError());
-  // KS_POST0_HI=1 (A/B): the first half's post-processing on the
-  // high-priority stream its pass 1 ran on (ahead of the second half's
-  // pass-1 blocks when a CU frees); the main stream then marks the end of
-  // pass 1 instead of the hi stream
-  const bool post0_hi = split && getenv("KS_POST0_HI") != nullptr && atoi(getenv("KS_POST0_HI")) != 0;
-  if (post0_hi) {
-    KS_HIP(hipEventRecord(ctx->ev[18], ctx->side));
-    KS_HIP(hipStreamWaitEvent(st, ctx->ev[18], 0));
-    KS_HIP(hipEventRecord(ctx->ev[9], st));
-  } else if (split) {
+  // (the first half's post-processing on the high-priority stream, ahead of
+  // the second half's pass-1 blocks, measured the same: 14.15 vs 14.15 ms,
+  // profiles/r5/ab/ab_post0.txt)
+  if (split) {
     // end of pass 1 = the later of the halves: the hi stream (idle now) joins the side stream's
     KS_HIP(hipEventRecord(ctx->ev[18], ctx->side));
     KS_HIP(hipStreamWaitEvent(ctx->hi, ctx->ev[18], 0));
@@ -4523,11 +4517,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   if (split) {
     // (the first half's rescans under the second half's post-processing: config 3
     // 32.1 vs 32.9 ms with both after the join, profiles/r4/ab3/)
-    KS_TRY(post(0, halves[0], post0_hi ? ctx->hi : st));  // under the second half's pass 1
-    if (post0_hi) {
-      KS_HIP(hipEventRecord(ctx->ev[12], ctx->hi));
-      KS_HIP(hipStreamWaitEvent(st, ctx->ev[12], 0));
-    }
+    KS_TRY(post(0, halves[0], st));         // under the second half's pass 1
     KS_TRY(emit_rescan(0));                 // under the second half's post-processing
     KS_TRY(post(1, halves[1], ctx->side));
     KS_HIP(hipEventRecord(ctx->ev[13], ctx->side));

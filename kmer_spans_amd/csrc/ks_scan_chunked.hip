@@ -97,9 +97,35 @@ __device__ __forceinline__ SummAt summ_at(const Summ &sm, int64_t c) {
 
 struct SummP1 {  // binade summaries computed by pass 1 for the predicted binade (single trajectory)
   int32_t *e;             // [2 * nch] binade, INT32_MIN: none (no prediction, a tie, out of range)
-  long long *D, *M, *N;   // [2 * nch] total, max, lower bound of the min (units 2^(e-52))
+  long long *D, *M, *N;   // [2 * nch] total, max, min (units 2^(e-52))
   int32_t *A;             // [2 * nch] first argmax
-};                        // slot 2c: the predicted binade, 2c + 1: its neighbour near an edge
+};
+
+// A pass-1 summary of chunk c in binade e (slot t of the predicted binade and
+// its neighbour): the binade-integer map of the chunk (D, M, N, A as
+// chunk_summary_impl) from the steps r = (s + 1.5 * 2^e) - 1.5 * 2^e summed
+// in FP64.  Valid if no step was a tie (bad), every |s| < 2^(e-1) (so the
+// magic constant rounds s to the ulp 2^(e-52)) and every partial sum of the
+// r inside (-2^e, 2^e) (so the sums are exact multiples of the ulp): then D,
+// the maximum M and the minimum N are the integer trajectory's, exactly.
+// (Until round 5 every partial sum of |s| had to stay below 2^(e-1) and N was
+// a lower bound from the FP64 prefix minimum minus a 130-ulp margin; the
+// exact form measured the same: metric step 14.59 vs 14.72 ms, weighted rank
+// k = 15 61.9 vs 61.7 ms, profiles/r5/ab/ab_p1summ_exact*.txt)
+__device__ __forceinline__ void summ_put(const SummP1 &sp, int64_t c, int t, int e, bool bad, double maxabs,
+                                         double cur, double mx, double mn, int a) {
+  const double lim = ldexp(1.0, e);
+  // (a NaN step leaves cur NaN; fmin / fmax skip it in mn, mx, maxabs)
+  const bool ok = e != INT32_MIN && !bad && cur == cur && maxabs < 0.5 * lim && mn <= mx && mx < lim && mn > -lim;
+  sp.e[2 * c + t] = ok ? e : INT32_MIN;
+  if (ok) {
+    const double sc = ldexp(1.0, 52 - e);
+    sp.D[2 * c + t] = (long long)(cur * sc);
+    sp.M[2 * c + t] = (long long)(mx * sc);
+    sp.N[2 * c + t] = (long long)(mn * sc);
+    sp.A[2 * c + t] = a;
+  }
+}                        // slot 2c: the predicted binade, 2c + 1: its neighbour near an edge
 
 struct Carry {  // P3/P4
   double *x;      // exact entry value
@@ -995,8 +1021,9 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
   // FP64 prefix minimum: N is stored as a lower bound, which keeps the carry's
   // validity test conservative; both save registers in this 128-VGPR kernel.)
   int se = INT32_MIN, se2 = INT32_MIN;
-  double sC = 0.0, sH = 0.0, scur = 0.0, smx = -INFINITY;
-  double sC2 = 0.0, sH2 = 0.0, scur2 = 0.0, smx2 = -INFINITY;
+  double sC = 0.0, sH = 0.0, scur = 0.0, smx = -INFINITY, smn = INFINITY;
+  double sC2 = 0.0, sH2 = 0.0, scur2 = 0.0, smx2 = -INFINITY, smn2 = INFINITY;
+  double smaxabs = 0.0;  // max |s| (the rounding of every step, both binades)
   int sarg = 0, sarg2 = 0;
   bool sbad = false, sbad2 = false;
   {
@@ -1103,10 +1130,12 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
           if (se != INT32_MIN) {
             const double r = (s + sC) - sC;
             sbad |= fabs(r - s) == sH;
+            smaxabs = fmax(smaxabs, fabs(s));
             scur += r;
             const bool su = scur > smx;
             smx = su ? scur : smx;
             sarg = su ? i : sarg;
+            smn = fmin(smn, scur);
             if (se2 != INT32_MIN) {
               const double r2 = (s + sC2) - sC2;
               sbad2 |= fabs(r2 - s) == sH2;
@@ -1114,6 +1143,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
               const bool su2 = scur2 > smx2;
               smx2 = su2 ? scur2 : smx2;
               sarg2 = su2 ? i : sarg2;
+              smn2 = fmin(smn2, scur2);
             }
           }
           // clean trajectory, branch-free except for the rare candidate:
@@ -1158,27 +1188,8 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
       e[gi] = en[gi];
     }
   }
-  {
-    // valid if no tie, every |s| < 2^(e-1) (so (s + C) - C rounds s to the ulp
-    // 2^(e-52)) and every partial sum inside (-2^e, 2^e) (all exact).  N is a
-    // lower bound of the integer trajectory's minimum: each rounded step is
-    // within u/2 of s (<= 128 u over the chunk), the FP64 prefix sums within
-    // 256 * 2^-53 * sabs of the exact ones.
-    auto put = [&](int t, int e, bool bad, double cur, double mx, int a) {
-      const double lim = ldexp(1.0, e);
-      const bool ok = e != INT32_MIN && !bad && sabs < 0.5 * lim && mx < 0.5 * lim && pmin > -0.5 * lim;
-      sp.e[2 * c + t] = ok ? e : INT32_MIN;
-      if (ok) {
-        const double sc = ldexp(1.0, 52 - e);
-        sp.D[2 * c + t] = (long long)(cur * sc);
-        sp.M[2 * c + t] = (long long)(mx * sc);
-        sp.N[2 * c + t] = (long long)floor((pmin - sabs * 0x1p-44) * sc) - 130;
-        sp.A[2 * c + t] = a;
-      }
-    };
-    put(0, se, sbad, scur, smx, sarg);
-    put(1, se2, sbad2, scur2, smx2, sarg2);
-  }
+  summ_put(sp, c, 0, se, sbad, smaxabs, scur, smx, smn, sarg);
+  summ_put(sp, c, 1, se2, sbad2, smaxabs, scur2, smx2, smn2, sarg2);
   o.cexit[c] = prev;
   o.asum[c] = asum;
   o.pmin[c] = pmin;
@@ -1246,8 +1257,9 @@ struct P1Lane {
   int parg = 0;
   bool special = false;
   int se = INT32_MIN, se2 = INT32_MIN;
-  double sC = 0.0, sH = 0.0, scur = 0.0, smx = -INFINITY;
-  double sC2 = 0.0, sH2 = 0.0, scur2 = 0.0, smx2 = -INFINITY;
+  double sC = 0.0, sH = 0.0, scur = 0.0, smx = -INFINITY, smn = INFINITY;
+  double sC2 = 0.0, sH2 = 0.0, scur2 = 0.0, smx2 = -INFINITY, smn2 = INFINITY;
+  double smaxabs = 0.0;
   int sarg = 0, sarg2 = 0;
   bool sbad = false, sbad2 = false;
 
@@ -1280,10 +1292,12 @@ struct P1Lane {
     if (kSumm && se != INT32_MIN) {
       const double r = (s + sC) - sC;
       sbad |= fabs(r - s) == sH;
+      smaxabs = fmax(smaxabs, fabs(s));
       scur += r;
       const bool su = scur > smx;
       smx = su ? scur : smx;
       sarg = su ? i : sarg;
+      smn = fmin(smn, scur);
       if (se2 != INT32_MIN) {
         const double r2 = (s + sC2) - sC2;
         sbad2 |= fabs(r2 - s) == sH2;
@@ -1291,6 +1305,7 @@ struct P1Lane {
         const bool su2 = scur2 > smx2;
         smx2 = su2 ? scur2 : smx2;
         sarg2 = su2 ? i : sarg2;
+        smn2 = fmin(smn2, scur2);
       }
     }
     // clean trajectory (k_pass1p)
@@ -1322,20 +1337,8 @@ struct P1Lane {
 
   __device__ __forceinline__ void finish(int64_t c, const P1 &o, const SummP1 &sp) {
     if (kSumm) {  // as in k_pass1p
-      auto put = [&](int t, int e, bool bad, double cur, double mx, int aa) {
-        const double lim = ldexp(1.0, e);
-        const bool ok = e != INT32_MIN && !bad && sabs < 0.5 * lim && mx < 0.5 * lim && pmin > -0.5 * lim;
-        sp.e[2 * c + t] = ok ? e : INT32_MIN;
-        if (ok) {
-          const double sc = ldexp(1.0, 52 - e);
-          sp.D[2 * c + t] = (long long)(cur * sc);
-          sp.M[2 * c + t] = (long long)(mx * sc);
-          sp.N[2 * c + t] = (long long)floor((pmin - sabs * 0x1p-44) * sc) - 130;
-          sp.A[2 * c + t] = aa;
-        }
-      };
-      put(0, se, sbad, scur, smx, sarg);
-      put(1, se2, sbad2, scur2, smx2, sarg2);
+      summ_put(sp, c, 0, se, sbad, smaxabs, scur, smx, smn, sarg);
+      summ_put(sp, c, 1, se2, sbad2, smaxabs, scur2, smx2, smn2, sarg2);
     }
     o.cexit[c] = prev;
     o.asum[c] = asum;
@@ -1914,8 +1917,8 @@ __global__ void __launch_bounds__(1024) k_pass1_lds(Chunks g, int64_t total, int
 // (no code store: later passes re-read the table), plus (xh != nullptr) the
 // binade-integer summaries in the predicted binades (P1Lane, as k_pass1l):
 // at k = 15 a separate k_summaries pass re-read the 64 GiB table.
-template <int J, bool kTrlr>
-__global__ void __launch_bounds__(1024) k_pass1pf(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
+template <int J, bool kTrlr, int kBlock = 512>
+__global__ void __launch_bounds__(kBlock) k_pass1pf(Chunks g, const uint8_t *__restrict__ seq, int64_t total, int k,
                                                   TableView tv, EmitCfg ec, uint32_t *__restrict__ visits, P1 o,
                                                   Cand cand, const uint32_t *__restrict__ packed,
                                                   const double *__restrict__ xh, SummP1 sp) {
@@ -4242,17 +4245,20 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     hipStream_t side = ctx->side;
     const bool tail = nch > ctail;
     const double *xh = p1summ ? d_xh : nullptr;
-#define KS_P1PF(J, GV, GRID, STRM)                                                                             \
+#define KS_P1PF(J, GV, STRM, B)                                                                                \
     do {                                                                                                       \
-      if (ec.trlr) hipLaunchKernelGGL((k_pass1pf<J, true>), dim3(GRID), dim3(1024), 0, STRM, GV, s->seq, total, k, \
+      const unsigned grid_ = (unsigned)((h.c1 - h.c0 + (B) - 1) / (B));                                        \
+      if (ec.trlr) hipLaunchKernelGGL((k_pass1pf<J, true, B>), dim3(grid_), dim3(B), 0, STRM, GV, s->seq, total, k, \
                                       tv, ec, visits, p1, cand, runs.packed, xh, sp1);                         \
-      else hipLaunchKernelGGL((k_pass1pf<J, false>), dim3(GRID), dim3(1024), 0, STRM, GV, s->seq, total, k, tv, \
+      else hipLaunchKernelGGL((k_pass1pf<J, false, B>), dim3(grid_), dim3(B), 0, STRM, GV, s->seq, total, k, tv, \
                               ec, visits, p1, cand, runs.packed, xh, sp1);                                     \
     } while (0)
+    // 512-lane blocks: up to 256 VGPRs, 152 used, no spills, 3 waves per SIMD
+    // (1024-lane blocks capped it at 128 with 17-29 VGPRs spilled to scratch:
+    // weighted rank k = 15 in-process 55.3 vs 61.4 ms, profiles/r5/ab/ab_p1pf_block.txt)
     auto p1f = [&](const Half &h, hipStream_t strm) {
       const Chunks gv = view(h);
-      const unsigned grid = (unsigned)((h.c1 - h.c0 + 1023) / 1024);
-      if (J == 4) KS_P1PF(4, gv, grid, strm); else if (J == 3) KS_P1PF(3, gv, grid, strm); else KS_P1PF(2, gv, grid, strm);
+      if (J == 4) KS_P1PF(4, gv, strm, 512); else if (J == 3) KS_P1PF(3, gv, strm, 512); else KS_P1PF(2, gv, strm, 512);
     };
 #undef KS_P1PF
     auto p1tail = [&]() {

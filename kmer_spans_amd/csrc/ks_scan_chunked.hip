@@ -3229,8 +3229,12 @@ __global__ void __launch_bounds__(256) k_tile_apply(Chunks g, Summ sm, TileComp 
 // Carry by window: block w runs the segments that start in chunks
 // [64w, 64w + 64) (segment starts flagged by k_seg_marks; a segment ends at
 // the next flagged chunk, possibly windows later).
-template <bool kCompressed>
-__global__ void __launch_bounds__(256) k_carry_win(Chunks g, const uint8_t *__restrict__ flag,
+// kW: waves per SIMD the register allocation must allow (3: the FP64 form
+// fits 168 VGPRs without spills instead of taking 170 at 2 waves; weighted
+// rank in-process k = 13 30.4 vs 31.6 ms, k = 15 53.6 vs 55.1, metric
+// unchanged: profiles/r5/ab/ab_carry_occ*.txt; 4 waves spill 64-87 VGPRs)
+template <bool kCompressed, int kW = 3>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW, 8))) k_carry_win(Chunks g, const uint8_t *__restrict__ flag,
                                                   const uint8_t *__restrict__ seq, int64_t total, int k, TableView tv,
                                                   const uint16_t *__restrict__ codes, P1 o, Summ sm, Carry cr,
                                                   TileComp tc, ReplayBuf rp, unsigned long long *__restrict__ nreplay,

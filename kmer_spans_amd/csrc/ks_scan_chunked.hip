@@ -4064,7 +4064,14 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // (the exact carry's post-processing is short: one part -- two measured the
   // same at lower run-to-run spread, 6.44 vs 6.55 ms median at k = 7,
   // profiles/r4/ab3/ab_k7pm1_exact_split.txt)
-  const bool split = !ctx->no_split && (p1summ || (f64_line && !exact)) && lay.split_r > 0 && lay.split_r < nruns &&
+  // (below ~2 M chunks, ~500 Mbp, one part: at the 8-way shard, 1.5 M chunks,
+  // 2.38 vs 2.42 ms in-process; 4-way, 3 M chunks, two parts 4.24 vs 4.37;
+  // profiles/r5/ab/ab_one_part_*.txt.  KS_SPLIT_MIN_CHUNKS: the threshold --
+  // tests set 0 to run the two-part path on small genomes; KS_NO_SPLIT: one part)
+  const char *smin = getenv("KS_SPLIT_MIN_CHUNKS");
+  const int64_t split_min = smin ? atoll(smin) : ((int64_t)2 << 20);
+  const bool split = !ctx->no_split && getenv("KS_NO_SPLIT") == nullptr && (p1summ || (f64_line && !exact)) &&
+                     nch > split_min && lay.split_r > 0 && lay.split_r < nruns &&
                      lay.split_c >= 1024 && lay.split_c + 1024 <= ctail_all;
   Half halves[2];
   int nhalf = 1;

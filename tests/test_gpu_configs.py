@@ -24,7 +24,10 @@ def _same(pos, sc, o, what):
     assert np.array_equal(np.ascontiguousarray(sc).view(np.uint64), o["score"].view(np.uint64)), what
 
 
-def test_chr1_like_50mbp_k11_log2(oracle):
+@pytest.mark.parametrize("split_min", ["0", None])  # the two-part scan forced, and the default (one part here)
+def test_chr1_like_50mbp_k11_log2(oracle, monkeypatch, split_min):
+    if split_min is not None:
+        monkeypatch.setenv("KS_SPLIT_MIN_CHUNKS", split_min)
     import torch
     from kmer_spans_amd import _lib, api, device as D, genome
     ctx = _lib.context(0)
@@ -167,12 +170,13 @@ def test_rank_expanded_pass1_summaries(oracle, monkeypatch, k, jmax):
     assert not tab.compressed and tab.positions_per_read == jmax
     o = oracle.scan(host, k, w.cpu().numpy(), 0.6, 50, 5.0, visits=True)
     ctx.set_scan_algo(1)
-    for summ in ("1", "0"):
+    for summ, split_min in (("1", "0"), ("0", "0"), ("1", str(2 << 20))):  # two parts forced; the default one part
         monkeypatch.setenv("KS_F64_P1SUMM", summ)
+        monkeypatch.setenv("KS_SPLIT_MIN_CHUNKS", split_min)
         vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
         pos, sc, st = D.scan(ctx, ds, k, tab, 50, 5.0, vis)
-        _same(pos, sc, o, ("rank expanded", k, jmax, summ))
-        assert np.array_equal(vis.cpu().numpy(), o["counts"]), ("rank expanded visits", k, jmax, summ)
+        _same(pos, sc, o, ("rank expanded", k, jmax, summ, split_min))
+        assert np.array_equal(vis.cpu().numpy(), o["counts"]), ("rank expanded visits", k, jmax, summ, split_min)
     ctx.set_scan_algo(-1)
     assert o["pos"].shape[1] > 0
     tab.close()

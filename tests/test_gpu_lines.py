@@ -9,6 +9,13 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _two_parts(monkeypatch):
+    """The two-part scan (the default above ~2 M chunks, ks_scan_chunked.hip)
+    on these small genomes too, as before round 5."""
+    monkeypatch.setenv("KS_SPLIT_MIN_CHUNKS", "0")
+
 GiB = 1 << 30
 
 

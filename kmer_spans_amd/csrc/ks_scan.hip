@@ -313,9 +313,24 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                      ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed)
   if (tv.compressed) {
     if (J == 6) KS_LANE(6, true); else if (J == 5) KS_LANE(5, true); else if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
-  } else if (J == 4 && tv.line) {
-    hipLaunchKernelGGL((k_scan_lane<4, false, 8>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq,
-                       total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed);
+  } else if (J >= 2 && J <= 4) {
+    // FP64 line and expanded tables (weighted rank): wider batches, 24 / 30 /
+    // 32 indices per round trip (k = 15 rescans 5.17 -> 3.19 ms in-process,
+    // 16 reads 3.44; profiles/r5/ab/ab_lane_gw.txt).  KS_LANE_GW: the reads
+    // per batch (A/B; 0: the default batch)
+    const char *gwe = getenv("KS_LANE_GW");
+    const int gw = gwe ? atoi(gwe) : (J == 2 ? 12 : J == 3 ? 10 : 8);
+#define KS_LANE_W(J, W)                                                                                           \
+  hipLaunchKernelGGL((k_scan_lane<J, false, W>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, \
+                     total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed)
+    if (J == 2 && gw >= 16) KS_LANE_W(2, 16);
+    else if (J == 2 && gw >= 12) KS_LANE_W(2, 12);
+    else if (J == 2) KS_LANE(2, false);
+    else if (J == 3 && gw >= 10) KS_LANE_W(3, 10);
+    else if (J == 3) KS_LANE(3, false);
+    else if (gw >= 8) KS_LANE_W(4, 8);
+    else KS_LANE(4, false);
+#undef KS_LANE_W
   } else {
     if (J == 5) KS_LANE(5, false); else if (J == 4) KS_LANE(4, false); else if (J == 3) KS_LANE(3, false); else if (J == 2) KS_LANE(2, false); else KS_LANE(1, false);
   }

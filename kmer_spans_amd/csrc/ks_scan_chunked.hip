@@ -442,6 +442,41 @@ __device__ __forceinline__ void values4(const Chunks &g, const uint8_t *__restri
       if (i0 + q < n) v[q] = ev[q];
     return;
   }
+  if (!tv.compressed && !tv.line) {
+    // FP64 J = 2 / 3 expanded tables (weighted rank, k = 14, 15) and FP64
+    // base tables: the k-mers from the packed bases (prefetched by the carry),
+    // not from k + 3 bytes
+    uint64_t xp = xin;
+    if (have_x || packed_bits(g.packed, total, p - k, xp)) {
+      const uint64_t G = xp >> (64 - 2 * (k + 3));  // the (k + 3)-mer of indices i0 .. i0 + 3
+      const uint64_t mk = ((uint64_t)1 << (2 * k)) - 1;
+      double ev[4];
+      if (tv.ext && tv.ext_J == 2) {  // entries (v_j, v_j+1) of (k + 1)-mers, 16 B
+        const double2 *E = reinterpret_cast<const double2 *>(tv.ext);
+        const uint64_t m1 = ((uint64_t)1 << (2 * (k + 1))) - 1;
+        const double2 a = E[G >> 4], b = E[G & m1];
+        ev[0] = a.x;
+        ev[1] = a.y;
+        ev[2] = b.x;
+        ev[3] = b.y;
+      } else if (tv.ext && tv.ext_J == 3) {  // entries (v_j .. v_j+2, 0) of (k + 2)-mers, 32 B
+        const double2 *E = reinterpret_cast<const double2 *>(tv.ext);
+        const uint64_t e = G >> 2;
+        const double2 a = E[2 * e], b = E[2 * e + 1];
+        ev[0] = a.x;
+        ev[1] = a.y;
+        ev[2] = b.x;
+        ev[3] = tv.vals[G & mk];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ev[q] = tv.vals[(G >> (2 * (3 - q))) & mk];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (i0 + q < n) v[q] = ev[q];
+      return;
+    }
+  }
   const uint32_t mask = (1u << (2 * k)) - 1u;
   uint32_t code = prime_code(seq, p - k, k);
   v[0] = tv_get(tv, code);
@@ -2338,6 +2373,12 @@ constexpr bool kParReplay = true;
 // uncompressed base table (instantiated with kCompressed = false).  At k = 7
 // (`profiles/r3/smallk/`): +-1 (2 values) codes 3.75 ms vs values 4.18;
 // log2 (16 K values, LUT beyond LDS) values 6.4 ms vs codes 9.1.
+// (KS_NO_SUMMARIES A/B: no chunk gets a summary; every carried chunk replays)
+__global__ void __launch_bounds__(1024) k_summ_none(Chunks g, Summ sm) {
+  const int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < g.nch) sm.e[c] = INT32_MIN;
+}
+
 template <bool kCompressed, bool kLds, bool kTab = false>
 __global__ void __launch_bounds__(1024) k_summaries(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
                                                     int k, TableView tv, const uint16_t *__restrict__ codes, P1 o,
@@ -4003,13 +4044,13 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // tables on the pipelined pass with a binade predictor (a table without
   // one, a failed allocation of the predictor, is scanned unexpanded)
   const bool line = tv.line != nullptr && !lds_table && runs.packed != nullptr;  // line table: k_pass1l
-  // (FP64 expanded tables, k_pass1pf: weighted rank at k = 14, 15 -- 57.4 vs
-  // 63.2 ms at k = 15; FP64 line tables (k <= 13) measured slower with them,
-  // 32.3 vs 30.3 ms at config 3, so they keep k_summaries unless
-  // KS_F64_P1SUMM=1; KS_F64_P1SUMM=0 turns both off: profiles/r4/ab/)
+  // (FP64 tables: no summaries by default -- see no_summ below; at k = 15
+  // 50.6 vs 53.7 ms with k_pass1pf's pass-1 summaries and 59.4 with
+  // k_summaries, at k = 13 29.8 vs 30.2 with k_summaries,
+  // profiles/r5/ab/ab_nosumm_*.txt.  KS_F64_P1SUMM=1: pass-1 summaries (FP64
+  // lines, expanded J 2..4, k_pass1pf); KS_F64_P1SUMM=0: k_summaries)
   const char *f64e = getenv("KS_F64_P1SUMM");
-  const bool f64_summ = !comp && !lds_table &&
-                        (f64e ? atoi(f64e) != 0 && (line || (Jt >= 2 && Jt <= 4)) : (!line && Jt >= 2 && Jt <= 4));
+  const bool f64_summ = !comp && !lds_table && f64e && atoi(f64e) != 0 && (line || (Jt >= 2 && Jt <= 4));
   // (small k, the table in LDS: pass-1 summaries from the LDS-staged table;
   // the k_summaries path after the prescan took 13.3 vs 8.8 ms at k = 7 log2)
   const bool lds_summ = lds_table;
@@ -4023,6 +4064,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const int force_fb = getenv("KS_TEST_SEG_FALLBACK") != nullptr ? 1 : 0;  // tests: force the fallback path
   const bool exact = tv.exact && !mode.trlr && runs.packed != nullptr && (lds_table || line || Jt >= 2) &&
                      lay.longest < ((int64_t)1 << 32) && !force_fb && getenv("KS_NO_EXACT") == nullptr;
+  // FP64 tables without KS_F64_P1SUMM: no chunk summaries at all (a summary
+  // serves a chunk only while its carry-in stays >= 64 in one binade; weighted
+  // rank values in [-0.5, 0.5] keep the carry far below that: 5,598 of 11.96 M
+  // chunks at config 3 were summary-served, 1.0 M replayed)
+  const bool no_summ = getenv("KS_NO_SUMMARIES") != nullptr || (!comp && !lds_table && !f64e);
   const bool p1summ = !exact && (lds_table ? lds_summ : (comp ? (Jt >= 2 || line) : f64_summ)) &&
                       runs.packed != nullptr && tv.approx != nullptr;
   // (the carry reads no replay slots unless k_marks_select wrote them)
@@ -4070,6 +4116,9 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // tests set 0 to run the two-part path on small genomes; KS_NO_SPLIT: one part)
   const char *smin = getenv("KS_SPLIT_MIN_CHUNKS");
   const int64_t split_min = smin ? atoll(smin) : ((int64_t)2 << 20);
+  // (FP64 expanded tables without summaries stay in one part: two measured
+  // 52.1 vs 51.6 ms at k = 15, 46.0 vs 44.8 at k = 14,
+  // profiles/r5/ab/ab_nosumm_split_k15.txt, ab_nosumm_k14.txt)
   const bool split = !ctx->no_split && getenv("KS_NO_SPLIT") == nullptr && (p1summ || (f64_line && !exact)) &&
                      nch > split_min && lay.split_r > 0 && lay.split_r < nruns &&
                      lay.split_c >= 1024 && lay.split_c + 1024 <= ctail_all;
@@ -4419,6 +4468,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       const unsigned gw = (unsigned)std::max<int64_t>(1, (int64_t)ctx->num_cus * 8);
       hipLaunchKernelGGL(k_summ_fixw<false>, dim3(gw), dim3(256), 0, strm, g, s->seq, total, k, tv, xt,
                          d_fix + h.c0, d_nfix + hi, sm, rpb, hi);
+    } else if (no_summ) {
+      hipLaunchKernelGGL(k_summ_none, dim3(gsum_h), dim3(1024), 0, strm, gv, sm);
     } else if (lds_table) {
       // small k: the table staged in LDS as for k_pass1_lds (from HBM / L2: 12.8 / 18.7 vs 3.8 / 6.4 ms)
       if (comp && lds_lut) {

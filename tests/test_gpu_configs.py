@@ -152,8 +152,9 @@ def test_rank_k15(oracle):
 def test_rank_expanded_pass1_summaries(oracle, monkeypatch, k, jmax):
     """The FP64 expanded form of the k = 14 / 15 weighted-rank tables
     (k_pass1pf, forced at small k by KS_EXT_MAX_J) with its pass-1 binade
-    summaries and halves, and without them (KS_F64_P1SUMM=0): regions,
-    scores and visits equal to the oracle on a multi-contig genome."""
+    summaries and halves, with k_summaries after an unexpanded-summary pass
+    (KS_F64_P1SUMM=0), and with no summaries (the default): regions, scores
+    and visits equal to the oracle on a multi-contig genome."""
     import torch
     from kmer_spans_amd import _lib, device as D, genome
     monkeypatch.setenv("KS_EXT_MAX_J", str(jmax))
@@ -170,8 +171,12 @@ def test_rank_expanded_pass1_summaries(oracle, monkeypatch, k, jmax):
     assert not tab.compressed and tab.positions_per_read == jmax
     o = oracle.scan(host, k, w.cpu().numpy(), 0.6, 50, 5.0, visits=True)
     ctx.set_scan_algo(1)
-    for summ, split_min in (("1", "0"), ("0", "0"), ("1", str(2 << 20))):  # two parts forced; the default one part
-        monkeypatch.setenv("KS_F64_P1SUMM", summ)
+    # two parts forced; the default one part; no summaries (one part)
+    for summ, split_min in (("1", "0"), ("0", "0"), ("1", str(2 << 20)), (None, "0")):
+        if summ is None:
+            monkeypatch.delenv("KS_F64_P1SUMM", raising=False)
+        else:
+            monkeypatch.setenv("KS_F64_P1SUMM", summ)
         monkeypatch.setenv("KS_SPLIT_MIN_CHUNKS", split_min)
         vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
         pos, sc, st = D.scan(ctx, ds, k, tab, 50, 5.0, vis)

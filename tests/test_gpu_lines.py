@@ -56,13 +56,13 @@ def test_line_forms(oracle, setup, monkeypatch, k, cap, own_u16, own_f64, score)
     wh = w.cpu().numpy()
     o = oracle.scan(host, k, wh, thr, 100 if score != "pm1" else 20, 20.0 if score != "pm1" else 5.0, visits=True)
     mw, ms = (100, 20.0) if score != "pm1" else (20, 5.0)
-    for route in ("count", "atomic", "f64summ"):
+    for route in ("count", "atomic", "f64summ", "f64ksumm"):
         if route == "atomic":
             monkeypatch.setenv("KS_VISITS_ATOMIC", "1")
-        if route == "f64summ":  # FP64 lines with pass-1 summaries (off by default)
+        if route.startswith("f64"):  # FP64 lines with pass-1 summaries / k_summaries (no summaries by default)
             if score != "rank":
                 continue
-            monkeypatch.setenv("KS_F64_P1SUMM", "1")
+            monkeypatch.setenv("KS_F64_P1SUMM", "1" if route == "f64summ" else "0")
         ctx.set_scan_algo(1)
         vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
         pos, sc, st = D.scan(ctx, ds, k, tab, mw, ms, vis)

@@ -133,6 +133,7 @@ struct Carry {  // P3/P4
   int32_t *hq;    // first clamp in the chunk (relative), -1 none
   double *hmax;   // max of the carried head (valid if the head is non-empty)
   int32_t *harg;
+  int bulk;       // carry_segment: runs of clean / clamp chunks in one wave step (A/B: KS_NO_BULK_CLEAN)
 };
 
 // Composites of the global 64-chunk tiles (chunks [64t, 64t + 64)) for the
@@ -3052,6 +3053,35 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
           continue;
         }
       }
+      // Runs of clean and certain-clamp chunks at once: both leave the
+      // chunk's clean exit, so from chunk j on, a chunk entered by its
+      // predecessor's clean exit (x for chunk j) that enters at 0 or clamps
+      // for certain -- and has no summary for its entry's binade, which the
+      // serial order tries first -- takes its mode here; the first other
+      // chunk takes the serial step.  (Weighted rank at config 3: 11 M of
+      // 12 M chunks are clean or clamp; in-process k = 15 44.2 vs 44.9 ms,
+      // k = 13 30.1 vs 30.6, metric unchanged: profiles/r5/ab/ab_bulk_clean_*.txt)
+      if (cr.bulk) {
+        const double pe = __longlong_as_double(wave_prev_i64(__double_as_longlong(l_exit)));
+        const double ent = lane == j ? x : pe;
+        const bool in = live && lane >= j;
+        const bool cl = ent == 0.0;
+        const bool sm_ok = se != INT32_MIN && ent >= kLMin && ent < 1.0e18 && se == binade_of(ent);
+        const bool rc = !cl && !sm_ok && !l_spec && ent + l_pmin < -ldexp(fabs(ent) + l_sabs, -40);
+        const bool ok = lane < j || (in && (cl || rc));
+        const unsigned long long bad = __ballot(!ok);
+        const int f = bad ? __ffsll((long long)bad) - 1 : 64;
+        if (f > j) {
+          if (lane >= j && lane < f) {
+            my_x = ent;
+            my_mode = cl ? kModeClean : kModeR;
+          }
+          if (dbg) n_r += __popcll(__ballot(lane >= j && lane < f && rc));
+          x = rld(l_exit, f - 1);
+          j = f - 1;
+          continue;
+        }
+      }
       tile_done = false;
       const double cj_exit = rld(l_exit, j);
       if (lane == j) my_x = x;
@@ -3099,6 +3129,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
           v[3] = b.y;
         } else {
           const bool hx = !kCompressed && pf_c == cj && pf_ok;
+          if (dbg && hx) n_par += 1LL << 32;  // (diagnostics: replays with their bases prefetched)
           values4(g, seq, total, k, tv, kCompressed ? codes : nullptr, cj, rl64(cur.start, j), 4 * lane, n, v, hx,
                   pf_x);
         }
@@ -3935,6 +3966,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   int32_t *hqp = reinterpret_cast<int32_t *>(W + o_hq);
   Carry cr{reinterpret_cast<double *>(W + o_x), reinterpret_cast<uint8_t *>(W + o_mode), hqp,
            reinterpret_cast<double *>(W + o_hmax), hqp + nch};
+  cr.bulk = getenv("KS_NO_BULK_CLEAN") == nullptr;
   unsigned long long *cnts = reinterpret_cast<unsigned long long *>(W + o_cnt);
   uint8_t *d_flag = reinterpret_cast<uint8_t *>(W + o_flag);
   auto xtiles = [&](char *p) {
@@ -4650,9 +4682,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     long long tot[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int64_t i = 0; i < nwin; ++i)
       for (int q = 0; q < 9; ++q) tot[q] += h[9 * i + q];
-    fprintf(stderr, "[carry] windows %lld (runs %lld) chunks %lld replays %lld (wave-parallel %lld; cycles in fast tiles "
-            "%lld, in replays %lld) segments %lld L %lld R %lld\n", (long long)nwin, (long long)nruns, tot[1], tot[2],
-            tot[8], tot[6], tot[7], tot[3], tot[4], tot[5]);
+    fprintf(stderr, "[carry] windows %lld (runs %lld) chunks %lld replays %lld (wave-parallel %lld, bases prefetched "
+            "%lld; cycles %lld, in fast tiles %lld, in replays %lld) segments %lld L %lld R %lld\n", (long long)nwin,
+            (long long)nruns, tot[1], tot[2], tot[8] & 0xffffffffLL, tot[8] >> 32, tot[0], tot[6], tot[7], tot[3],
+            tot[4], tot[5]);
     for (int64_t i = 0; i < std::min<int64_t>(nwin, 8); ++i) {
       const long long *d = &h[9 * idx[i]];
       fprintf(stderr, "[carry] window %lld cycles %lld (fast tiles %lld, replays %lld) chunks %lld replays %lld "

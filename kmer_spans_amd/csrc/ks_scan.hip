@@ -35,7 +35,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                            double min_score, uint32_t *visits, const RegionBuf &out,
                            const unsigned long long *d_cnt = nullptr, int64_t segcap = 0,
                            const ScanMode &mode = ScanMode(), int init_step = 1, const int64_t *offs = nullptr,
-                           const uint32_t *packed = nullptr);
+                           const uint32_t *packed = nullptr, hipStream_t strm = nullptr);
 
 namespace {
 
@@ -291,13 +291,14 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                            const int32_t *rs, int64_t n, int k, const TableView &tv, uint64_t mw,
                            double min_score, uint32_t *visits, const RegionBuf &out,
                            const unsigned long long *d_cnt, int64_t segcap, const ScanMode &mode, int init_step,
-                           const int64_t *offs, const uint32_t *packed) {
+                           const int64_t *offs, const uint32_t *packed, hipStream_t strm) {
+  hipStream_t sq = strm ? strm : ctx->stream;
   if (n <= 0) return KS_OK;
   // line tables: own + 1 indices per read (gather_group's line form)
   const int J = tv.line ? tv.line_own + 1 : (tv.ext ? tv.ext_J : 1);
   if (mode.trlr) {
 #define KS_LANE_T(J, C)                                                                                   \
-  hipLaunchKernelGGL((k_scan_lane_trlr<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, \
+  hipLaunchKernelGGL((k_scan_lane_trlr<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, sq, seq, \
                      total, ra, rb, rs, n, k, tv, mode.ks, mode.min_len, out, d_cnt, segcap, init_step, offs)
     if (tv.compressed) {
       if (J == 6) KS_LANE_T(6, true); else if (J == 5) KS_LANE_T(5, true); else if (J == 4) KS_LANE_T(4, true); else if (J == 3) KS_LANE_T(3, true); else if (J == 2) KS_LANE_T(2, true); else KS_LANE_T(1, true);
@@ -309,7 +310,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
     return KS_OK;
   }
 #define KS_LANE(J, C)                                                                                   \
-  hipLaunchKernelGGL((k_scan_lane<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, total, \
+  hipLaunchKernelGGL((k_scan_lane<J, C>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, sq, seq, total, \
                      ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed)
   if (tv.compressed) {
     if (J == 6) KS_LANE(6, true); else if (J == 5) KS_LANE(5, true); else if (J == 4) KS_LANE(4, true); else if (J == 3) KS_LANE(3, true); else if (J == 2) KS_LANE(2, true); else KS_LANE(1, true);
@@ -321,7 +322,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
     const char *gwe = getenv("KS_LANE_GW");
     const int gw = gwe ? atoi(gwe) : (J == 2 ? 12 : J == 3 ? 10 : 8);
 #define KS_LANE_W(J, W)                                                                                           \
-  hipLaunchKernelGGL((k_scan_lane<J, false, W>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, ctx->stream, seq, \
+  hipLaunchKernelGGL((k_scan_lane<J, false, W>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, sq, seq, \
                      total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed)
     if (J == 2 && gw >= 16) KS_LANE_W(2, 16);
     else if (J == 2 && gw >= 12) KS_LANE_W(2, 12);

@@ -44,7 +44,7 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
                            double min_score, uint32_t *visits, const RegionBuf &out,
                            const unsigned long long *d_cnt = nullptr, int64_t segcap = 0,
                            const ScanMode &mode = ScanMode(), int init_step = 1, const int64_t *offs = nullptr,
-                           const uint32_t *packed = nullptr);
+                           const uint32_t *packed = nullptr, hipStream_t strm = nullptr);
 
 namespace {
 
@@ -3370,16 +3370,10 @@ __global__ void k_fallback_prep(unsigned int *__restrict__ err, unsigned long lo
 // lane per chunk, from the exact entry.  Uncompressed tables read the
 // expanded table (J indices per read) like P1.
 template <int J, bool kCompressed, bool kWide = false>
-__device__ __forceinline__ void head_one(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
-                                         const TableView &tv, const uint16_t *__restrict__ codes, const Carry &cr,
-                                         unsigned int *__restrict__ err, int64_t c) {
+__device__ __forceinline__ void head_walk(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
+                                          const TableView &tv, const uint16_t *__restrict__ codes, const Carry &cr,
+                                          unsigned int *__restrict__ err, int64_t c) {
   const uint32_t *__restrict__ packed = g.packed;
-  const int mode = cr.mode[c];
-  if (mode == kModeL || mode == kModeU) return;  // head written by the carry (summary / replay)
-  cr.hq[c] = -1;
-  cr.hmax[c] = -1.0;
-  cr.harg[c] = 0;
-  if (mode == kModeClean) return;
   const double x = cr.x[c];
   const int n = g.n[c];
   const int64_t start = g.start[c];
@@ -3498,6 +3492,19 @@ __device__ __forceinline__ void head_one(const Chunks &g, const uint8_t *__restr
   cr.harg[c] = harg;
 }
 
+template <int J, bool kCompressed, bool kWide = false>
+__device__ __forceinline__ void head_one(const Chunks &g, const uint8_t *__restrict__ seq, int64_t total, int k,
+                                         const TableView &tv, const uint16_t *__restrict__ codes, const Carry &cr,
+                                         unsigned int *__restrict__ err, int64_t c) {
+  const int mode = cr.mode[c];
+  if (mode == kModeL || mode == kModeU) return;  // head written by the carry (summary / replay)
+  cr.hq[c] = -1;
+  cr.hmax[c] = -1.0;
+  cr.harg[c] = 0;
+  if (mode == kModeClean) return;
+  head_walk<J, kCompressed, kWide>(g, seq, total, k, tv, codes, cr, err, c);
+}
+
 // gated: the second pass, after a fallback only (bit 16 of err); queued
 // unconditionally on a small grid (a grid-stride loop), so that the common
 // case costs one short launch instead of a block per 256 chunks (80 us of
@@ -3510,6 +3517,52 @@ __global__ void __launch_bounds__(256) k_heads(Chunks g, const uint8_t *__restri
   for (int64_t c = g.c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < g.nch;
        c += (int64_t)gridDim.x * blockDim.x)
     head_one<J, kCompressed, kWide>(g, seq, total, k, tv, codes, cr, err, c);
+}
+
+// k_heads with the R chunks packed densely: a wave takes 256 chunks, lists
+// its R chunks in LDS (ballot order) and walks them 64 at a time, so every
+// lane of a walking wave has a head to walk (weighted rank: ~28% of the
+// chunks are R, scattered; config 3 in-process 29.18 vs 29.90 ms, k = 15
+// 43.7 vs 43.8: profiles/r5/ab/ab_heads_dense_lane_pf_*.txt, where the next
+// rescan batch's bases loaded one batch ahead measured slower, 29.18 vs 28.51).
+constexpr int kHeadSpan = 256;
+template <int J, bool kCompressed, bool kWide = false>
+__global__ void __launch_bounds__(256) k_heads_dense(Chunks g, const uint8_t *__restrict__ seq, int64_t total,
+                                                     int k, TableView tv, const uint16_t *__restrict__ codes,
+                                                     Carry cr, unsigned int *__restrict__ err, int gated) {
+  if (gated && !(*(volatile unsigned int *)err & 16u)) return;
+  __shared__ int32_t s_list[4][kHeadSpan];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t sp = g.c0 + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * kHeadSpan; sp < g.nch;
+       sp += nw * kHeadSpan) {
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < kHeadSpan / 64; ++q) {
+      const int64_t c = sp + q * 64 + lane;
+      bool isr = false;
+      if (c < g.nch) {
+        const int mode = cr.mode[c];
+        if (mode == kModeClean || mode == kModeR) {
+          cr.hq[c] = -1;
+          cr.hmax[c] = -1.0;
+          cr.harg[c] = 0;
+        }
+        isr = mode == kModeR;
+      }
+      const unsigned long long b = __ballot(isr);
+      if (isr) s_list[w][cnt + __popcll(b & ((1ull << lane) - 1ull))] = q * 64 + lane;
+      cnt += __popcll(b);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int t = lane; t < cnt; t += 64)
+      head_walk<J, kCompressed, kWide>(g, seq, total, k, tv, codes, cr, err, sp + s_list[w][t]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
 }
 
 // ------------------------------------------------------------------- P5
@@ -4550,14 +4603,28 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       hipLaunchKernelGGL(k_tile_apply, dim3(gtc), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 0);
       KS_HIP(hipGetLastError());
     }
+    // FP64 tables: the R chunks' heads packed densely (k_heads_dense; A/B:
+    // KS_HEADS_SPARSE=1)
+    const bool dense_heads = !comp && getenv("KS_HEADS_SPARSE") == nullptr;
     auto heads = [&](int gated) {
       // (gated: a small grid-stride grid; it exits at once unless the carry fell back)
-      const unsigned gh = gated ? std::min<unsigned>(gch_h, (unsigned)ctx->num_cus * 2) : gch_h;
+      const unsigned gd = (unsigned)((nh + 4 * kHeadSpan - 1) / (4 * kHeadSpan));
+      const unsigned gh = gated ? std::min<unsigned>(dense_heads ? gd : gch_h, (unsigned)ctx->num_cus * 2)
+                                : (dense_heads ? gd : gch_h);
 #define KS_HEADS(J, C)                                                                                           \
   hipLaunchKernelGGL((k_heads<J, C>), dim3(gh), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes, cr, err_h, \
                      gated)
+#define KS_HEADS_D(J, W)                                                                                          \
+  hipLaunchKernelGGL((k_heads_dense<J, false, W>), dim3(gh), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes, \
+                     cr, err_h, gated)
       if (comp) KS_HEADS(1, true);
-      else if (J == 4 && tv.line)
+      else if (dense_heads) {
+        if (J == 4 && tv.line) KS_HEADS_D(4, true);
+        else if (J == 4) KS_HEADS_D(4, false);
+        else if (J == 3) KS_HEADS_D(3, false);
+        else if (J == 2) KS_HEADS_D(2, false);
+        else KS_HEADS_D(1, false);
+      } else if (J == 4 && tv.line)
         hipLaunchKernelGGL((k_heads<4, false, true>), dim3(gh), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes,
                            cr, err_h, gated);
       else if (J == 4) KS_HEADS(4, false);
@@ -4565,6 +4632,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       else if (J == 2) KS_HEADS(2, false);
       else KS_HEADS(1, false);
 #undef KS_HEADS
+#undef KS_HEADS_D
     };
     heads(0);
     KS_HIP(hipGetLastError());
@@ -4605,27 +4673,30 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // second half's, weighted rank: ~3.8 ms of lane walks), on st
   // (the rescan slots in list order: sorted longest first they took 5.23 vs
   // 3.56 ms at config 3, profiles/r4/ab2/ab_rank.txt)
-  auto emit_rescan = [&](int h) -> ks_status {
-    hipLaunchKernelGGL(k_candidates, dim3((unsigned)((ccap + 255) / 256)), dim3(256), 0, st, g, runs.a, d_cbase,
+  auto emit_rescan = [&](int h, hipStream_t rst) -> ks_status {
+    hipLaunchKernelGGL(k_candidates, dim3((unsigned)((ccap + 255) / 256)), dim3(256), 0, rst, g, runs.a, d_cbase,
                        nruns, runs.seq, ec, cands[h], cr, rb, rss[h]);
     KS_HIP(hipGetLastError());
-    if (h == nhalf - 1) KS_HIP(hipEventRecord(ctx->ev[10], st));
+    if (h == nhalf - 1) KS_HIP(hipEventRecord(ctx->ev[10], rst));
     KS_TRY(launch_scan_lane(ctx, s->seq, total, rss[h].a, rss[h].b, rss[h].seq, rcap, k, tv, mw, min_score,
-                            visits_rescan, rb, rss[h].count, rss[h].segcap, mode, 0, nullptr, runs.packed));
+                            visits_rescan, rb, rss[h].count, rss[h].segcap, mode, 0, nullptr, runs.packed, rst));
     return KS_OK;
   };
   if (split) {
     // (the first half's rescans under the second half's post-processing: config 3
     // 32.1 vs 32.9 ms with both after the join, profiles/r4/ab3/)
+    // (the second half's rescans on the side stream, beside the first half's
+    // instead of after the join: 28.53 vs 28.46 ms at config 3, metric 14.71
+    // vs 14.65, profiles/r5/ab/ab_rescan_side_*.txt)
     KS_TRY(post(0, halves[0], st));         // under the second half's pass 1
-    KS_TRY(emit_rescan(0));                 // under the second half's post-processing
+    KS_TRY(emit_rescan(0, st));             // under the second half's post-processing
     KS_TRY(post(1, halves[1], ctx->side));
     KS_HIP(hipEventRecord(ctx->ev[13], ctx->side));
     KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
-    KS_TRY(emit_rescan(1));
+    KS_TRY(emit_rescan(1, st));
   } else {
     KS_TRY(post(0, halves[0], st));
-    KS_TRY(emit_rescan(0));
+    KS_TRY(emit_rescan(0, st));
   }
   KS_HIP(hipEventRecord(ctx->ev[11], st));
   // the region counters too (final: the rescans above append the last

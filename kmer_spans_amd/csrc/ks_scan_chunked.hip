@@ -4186,12 +4186,12 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     int64_t c0, c1, r0, r1, t0, t1;
   };
   const int64_t ctail_all = nch > 1024 ? nch - 1024 : 0;
-  // FP64 line tables (weighted rank) are cut too: the first part's summaries,
-  // carry and heads (~10 ms in all at the metric genome) start while the
-  // second part's pass 1 drains (in-process A/B at config 3: 31.5 vs 32.7 ms
-  // one part; serialising the two pass-1 launches 31.8-32.0 by split
-  // fraction: profiles/r3/rank/split_ab.txt)
-  const bool f64_line = line && !comp;
+  // FP64 line tables (weighted rank) without pass-1 summaries: one part.
+  // Their two pass-1 launches ran side by side and ended together (15.2 ms
+  // each, profiles/r5/rank/step_timeline_rank_k13_twopart.txt), so the first part's
+  // post-processing never ran under the second's pass 1: 27.75 vs 28.56 ms
+  // in one part (profiles/r5/ab/ab_nosplit_k13.txt).  (Round 3, with
+  // k_summaries after pass 1: two parts 31.5 vs 32.7, profiles/r3/rank/.)
   // (the exact carry's post-processing is short: one part -- two measured the
   // same at lower run-to-run spread, 6.44 vs 6.55 ms median at k = 7,
   // profiles/r4/ab3/ab_k7pm1_exact_split.txt)
@@ -4204,7 +4204,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // (FP64 expanded tables without summaries stay in one part: two measured
   // 52.1 vs 51.6 ms at k = 15, 46.0 vs 44.8 at k = 14,
   // profiles/r5/ab/ab_nosumm_split_k15.txt, ab_nosumm_k14.txt)
-  const bool split = !ctx->no_split && getenv("KS_NO_SPLIT") == nullptr && (p1summ || (f64_line && !exact)) &&
+  const bool split = !ctx->no_split && getenv("KS_NO_SPLIT") == nullptr && p1summ &&
                      nch > split_min && lay.split_r > 0 && lay.split_r < nruns &&
                      lay.split_c >= 1024 && lay.split_c + 1024 <= ctail_all;
   Half halves[2];

@@ -248,3 +248,50 @@ def test_count_hot_buckets(oracle, k):
     n, oc = oracle.kmer_counts(parts, k)
     assert words == n
     assert np.array_equal(counts.cpu().numpy(), oc)
+
+
+@pytest.mark.parametrize("score,k", [("rank", 11), ("log2", 9)])
+def test_carry_and_rescan_forms(oracle, monkeypatch, score, k):
+    """The round-5 carry / heads / rescan forms and their A/B alternatives on
+    one multi-contig genome (k = 11 rank, k = 9 log2), each against the oracle (regions,
+    FP64 scores bit for bit, visits): clean / certain-clamp runs in one wave
+    step or one chunk at a time (KS_NO_BULK_CLEAN), the certain-clamp heads
+    packed densely or lane per chunk (KS_HEADS_SPARSE), wide or default
+    rescan batches (KS_LANE_GW=0), no summaries for any table
+    (KS_NO_SUMMARIES), FP64 tables with k_summaries (KS_F64_P1SUMM=0).
+    (kmer_spans.c:261-306, 298-305: the carried state, the restart.)"""
+    import torch
+    from kmer_spans_amd import _lib, device as D, genome
+    ctx = _lib.context(0)
+    D.bind_torch_stream(ctx)
+    parts = [genome.contig(L, 60 + i, device="cuda", repeats=True)
+             for i, L in enumerate((1_800_000, 900_000, 300_000, 40_000))]
+    ds = D.from_parts(parts, [p.numel() for p in parts], "cuda")
+    host = [ds.host_seq(i) for i in range(len(parts))]
+    counts = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+    words = D.count(ctx, ds, k, counts)
+    w = torch.empty(4 ** k, dtype=torch.float64, device="cuda")
+    thr = 0.6 if score == "rank" else 0.0
+    tab = D.DeviceTable.from_counts(ctx, counts, k, score, total=words, thr=thr, expand=True, w_out=w)
+    mw, ms = (50, 5.0) if score == "rank" else (20, 5.0)
+    o = oracle.scan(host, k, w.cpu().numpy(), thr, mw, ms, visits=True)
+    assert o["pos"].shape[1] > 0
+    ctx.set_scan_algo(1)
+    forms = [{}, {"KS_NO_BULK_CLEAN": "1"}, {"KS_HEADS_SPARSE": "1"}, {"KS_LANE_GW": "0"},
+             {"KS_NO_SUMMARIES": "1"}, {"KS_SPLIT_MIN_CHUNKS": "0"}]
+    if score == "rank":
+        forms.append({"KS_F64_P1SUMM": "0"})
+    try:
+        for env in forms:
+            for key, val in env.items():
+                monkeypatch.setenv(key, val)
+            vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+            pos, sc, st = D.scan(ctx, ds, k, tab, mw, ms, vis)
+            assert st["scan_algo"] == 1
+            _same(pos, sc, o, (score, env))
+            assert np.array_equal(vis.cpu().numpy(), o["counts"]), (score, env, "visits")
+            for key in env:
+                monkeypatch.delenv(key)
+    finally:
+        ctx.set_scan_algo(-1)
+        tab.close()

@@ -119,6 +119,11 @@ def parse(argv=None):
                         "for the scan modes, 32 GiB (J = 4) for --mode genomes, where it is built per genome")
     p.add_argument("--ncontigs", type=int, default=24, help="1 = the chr1-like single contig of config 2")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
+    p.add_argument("--force-dist", action="store_true",
+                   help="run the torch.distributed path (RCCL with one GPU per rank) even at --gpus 1: a world of "
+                        "one rank, so the multi-GPU code (count all-reduce, record gather + merge) runs on one GPU")
+    p.add_argument("--multi-devices", default="0,0",
+                   help="N=1: device list of the multi-device host-entry line (ks_set_devices; '' skips it)")
     return p.parse_args(argv)
 
 
@@ -322,10 +327,13 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn(args.gpus))
+    if args.force_dist and "WORLD_SIZE" not in os.environ:  # a world of one rank (no HIP call yet)
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", LOCAL_WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(_free_port()))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
+    dist = world > 1 or args.force_dist
     ndev = torch.cuda.device_count()
     gpu = local % max(ndev, 1)  # ranks > GPUs only when rehearsing N>1 on a small box
     tdist = None
@@ -337,6 +345,12 @@ def main():
             tdist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:              # rehearsal with shared GPUs: RCCL refuses duplicate GPUs
             tdist.init_process_group("gloo")
+        extra_dist = {"backend": tdist.get_backend(), "world": world}
+        if tdist.get_backend() == "nccl":
+            try:
+                extra_dist["rccl_version"] = ".".join(str(x) for x in torch.cuda.nccl.version())
+            except Exception:
+                pass
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
@@ -410,7 +424,7 @@ def main():
         return out[0], out[1], stats, max_over_ranks(time.perf_counter() - t0)
 
     setup = {}
-    extra = {}
+    extra = {"dist": extra_dist} if dist else {}
     # ------------------------------------------------------------ the input
     t0 = time.time()
     lens_all = [max(1, int(round(L * args.scale))) for L in genome.GRCH38[:args.ncontigs]]
@@ -418,15 +432,15 @@ def main():
     offsets = None  # per shard: each local sequence's start inside its contig (pieces)
     pieces_mine = None
     if args.mode == "shard":
-        from kmer_spans_amd.dist import gap_cuts, lpt_pieces, lpt_shards
+        from kmer_spans_amd.dist import lpt_shards, shard_pieces
         nsh = world if dist else max(1, args.shard_of)
         if nsh > 1 and not args.whole_contigs:
-            # LPT over pieces cut inside N gaps (exact: runs never cross an N,
-            # dist.gap_cuts); every rank generates the genome and makes the
-            # same cut, so every rank knows every shard's pieces
+            # the library's shard plan (ks_shard_plan via dist.shard_pieces: LPT
+            # over pieces cut inside N gaps when whole contigs do not balance;
+            # exact: runs never cross an N); every rank generates the genome
+            # and plans the same cut, so every rank knows every shard's pieces
             parts_all = [genome.contig(lens_all[q], args.seed + q, dev) for q in range(len(lens_all))]
-            cuts = [gap_cuts(x) for x in parts_all]
-            psh = lpt_pieces(lens_all, cuts, nsh)
+            psh = shard_pieces([x.cpu().numpy() for x in parts_all], nsh)
             shards = [[q for q, _, _ in sh] for sh in psh]
             offsets = [[lo for _, lo, _ in sh] for sh in psh]
             if dist:
@@ -666,6 +680,16 @@ def main():
         host_path["return_at_end"]["note"] = ("ks_set_host_cache(0): every call allocates its workspace and table "
                                               "buffer again (fresh VRAM, cleared by the driver) and returns them")
 
+    # ---- the drop-in host entry spread over a device list (ks_set_devices;
+    # default [0, 0]: two contexts on the one GPU), PCIe-inclusive, checked
+    # against the device-resident line; the host-side visit sum and each
+    # part's table upload reported (ks_multi_last_stats)
+    if (world == 1 and not dist and args.multi_devices and not args.no_host_path and not args.trlr
+            and thr == 0.0):
+        L = _lib.load()
+        L.ks_release_cache()
+        extra["host_multi"] = host_multi_line(args, L, host, k, w, pos, score, vis_host, n_bases)
+
     # ---- CPU baseline (N=1, one pinned core, bounded sample) and the parity
     # verdict (every contig of this rank, oracle on a host thread pool)
     cpu = None
@@ -762,6 +786,48 @@ def main():
         tdist.destroy_process_group()
 
 
+def multi_devices(args):
+    return [int(x) for x in args.multi_devices.split(",") if x.strip() != ""]
+
+
+def host_multi_line(args, L, host, k, w, pos, score, vis_host, n_bases):
+    """kmer_regions_r from host memory over a device list (csrc/ks_multi.cpp:
+    the library's shard plan, one context + host thread per entry, visit
+    histograms summed on the host, regions merged): median of 3 after a first
+    call, phases from ks_multi_last_stats, outputs vs the device-resident line."""
+    import ctypes as C
+    from kmer_spans_amd import _lib, api
+    devs = multi_devices(args)
+    arr = (C.c_int32 * len(devs))(*devs)
+    _lib.check(L.ks_set_devices(arr, len(devs)))
+    try:
+        t0 = time.perf_counter()
+        api.kmer_regions(host, k, w, args.min_width, args.min_score)
+        first = time.perf_counter() - t0
+        ts, st = [], []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            hr = api.kmer_regions(host, k, w, args.min_width, args.min_score)
+            ts.append(time.perf_counter() - t0)
+            st.append(_lib.multi_last_stats())
+    finally:
+        _lib.check(L.ks_set_devices(None, 0))
+        L.ks_release_cache()
+    i = int(np.argsort(ts)[len(ts) // 2])
+    t = ts[i]
+    return {"devices": devs, "seconds": round(t, 4), "Gbases_per_s": round(n_bases / t / 1e9, 3),
+            "all_seconds": [round(x, 4) for x in ts], "first_call_seconds": round(first, 4),
+            "phases_ms": {key: (round(v, 2) if not isinstance(v, list) else
+                                [{a: round(b, 2) for a, b in d.items()} for d in v]) for key, v in st[i].items()},
+            "regions_equal": bool(np.array_equal(hr["pos"], pos)),
+            "scores_equal": bool(np.array_equal(hr["score"].view(np.uint64), score.view(np.uint64))),
+            "visits_equal": (bool(np.array_equal(hr["counts"], vis_host)) if vis_host is not None else None),
+            "note": "ks_kmer_regions (NULL context) over the device list, PCIe-inclusive, median of 3: the library's "
+                    "shard plan, one context + host thread per entry (each uploads the score table itself), the "
+                    "visit histograms summed on the host (host_sum_ms), regions merged (merge_ms); per part: "
+                    "body, staging + count, table upload + compression, scan"}
+
+
 def rank_subline(args, ctx, ds, counts, words, make_table, timed_steps, host, D):
     """BASELINE config 3 (kmer_low_comp_regions, kmer_spans.c:548-621): the
     weighted-rank table (threshold 0.75) of the same genome's counts, scanned
@@ -824,6 +890,27 @@ def rank_subline(args, ctx, ds, counts, words, make_table, timed_steps, host, D)
     if not args.no_host_path:
         out["host_low_comp"] = hl = host_low_comp_line(args, host, hc, w, pos, score, int(ds.total), n_bases)
         hl["parity"] = bool(hl["parity"] and out["parity"] and out["table_equal_oracle"] and hl["n"][0] == words)
+        if multi_devices(args):
+            import ctypes as C
+            from kmer_spans_amd import _lib
+            L = _lib.load()
+            devs = multi_devices(args)
+            L.ks_release_cache()
+            _lib.check(L.ks_set_devices((C.c_int32 * len(devs))(*devs), len(devs)))
+            try:
+                hm = host_low_comp_line(args, host, hc, w, pos, score, int(ds.total), n_bases)
+                hm["phases_ms"] = {key: (round(v, 2) if not isinstance(v, list) else v)
+                                   for key, v in _lib.multi_last_stats().items() if key != "parts"}
+            finally:
+                _lib.check(L.ks_set_devices(None, 0))
+                L.ks_release_cache()
+            hm["devices"] = devs
+            hm["parity"] = bool(hm["parity"] and out["parity"] and out["table_equal_oracle"] and hm["n"][0] == words)
+            hm["note"] = ("ks_low_comp_regions (NULL context) over the device list: the library's shard plan; each "
+                          "part stages + counts its pieces, the count histogram summed on the host in stripes "
+                          "(host_sum_ms), each part builds the rank table from the sum and scans; median of 3 "
+                          "(phases of the last call)")
+            hl["multi"] = hm
     return out
 
 

@@ -132,15 +132,17 @@ ks_status ks_tr_lr_regions(ks_ctx *ctx, const char *const *seqs, const int64_t *
  * of two or more entries, ks_kmer_counts, ks_kmer_regions and
  * ks_low_comp_regions called with ctx == NULL (what the .Call shim does)
  * spread the call: the sequences -- a sequence longer than half a fair share
- * cut in the middle of its N gaps of >= 1000 bases when whole sequences do
- * not balance -- are dealt to the devices by LPT on length, each device
+ * cut in the middle of its N gaps of >= 1000 bases when whole sequences leave
+ * a part more than 0.5 % above the fair share -- are dealt to the devices by LPT on length, each device
  * stages, counts and scans its share on a context of its own from a host
  * thread of its own, counts and visit histograms are added exactly (uint32
  * wrap-around), kmer_low_comp_regions builds every device's weighted-rank
  * table from the summed counts, and the regions come back in the caller's
  * coordinates and (seq_id, beg) order: the results equal the one-device
  * call's.  The list may repeat a device (two contexts on one card).  A call
- * with an explicit ctx runs on that ctx's device only.  The reference runs
+ * with an explicit ctx runs on that ctx's device only.  A call owns every
+ * context of the list from its start to its end; a second thread's
+ * multi-device call meanwhile returns KS_ERR_ARG (busy).  The reference runs
  * these routines on R's main thread (kmer_spans.c:452-621); this replaces the
  * mclapply-over-sequences pattern of test.R:550-567 inside one call. */
 /* devices: n device ordinals (n = 0: device 0 alone, the default).  Read from
@@ -154,6 +156,14 @@ int32_t ks_get_devices(int32_t *devices, int32_t cap);
  * -1 on a bad argument. */
 int64_t ks_shard_plan(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t nparts,
                       int64_t *out, int64_t cap);
+/* Phases of the last multi-device call (ms, host wall clock), into out[cap]:
+ * [0] whole call, [1] the parts' first phase (kmer_counts / kmer_regions: the
+ * whole per-device body; low_comp: staging + count), [2] the host-side sum of
+ * the count / visit histograms, [3] low_comp: rank table + scan, [4] region
+ * merge, [5] parts P, then per part p: [6 + 4p] body, [7 + 4p] staging +
+ * count, [8 + 4p] score-table upload + compression, [9 + 4p] scan
+ * (kmer_regions only).  Returns the number of values available. */
+int32_t ks_multi_last_stats(double *out, int32_t cap);
 /* Merge of the parts' regions (parts[p] in the coordinates of part p's pieces
  * passed as sequences in plan order, as a call on them returns them) into the
  * caller's coordinates and (seq_id, beg) order (host only). */

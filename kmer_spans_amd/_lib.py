@@ -88,6 +88,7 @@ EXPORTS = [
     "ks_windowed_dist", "ks_windowed_dev", "ks_table_from_counts",
     "ks_release_cache", "ks_set_fork_broker", "ks_set_host_cache",
     "ks_set_devices", "ks_get_devices", "ks_shard_plan", "ks_merge_parts", "ks_set_host_cache_idle",
+    "ks_multi_last_stats",
 ]
 
 SCORES = {"log2": 1, "pm1": 2, "rank": 3}  # KS_SCORE_* of ks_table_from_counts
@@ -153,6 +154,7 @@ def load():
         "ks_get_devices": ([P, I32], I32),
         "ks_shard_plan": ([P, P, I32, I32, P, I64], I64),
         "ks_merge_parts": ([P, I64, I32, P, P], I32),
+        "ks_multi_last_stats": ([P, I32], I32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)
@@ -205,6 +207,38 @@ def regions_to_numpy(r: Regions):
     pos = np.frombuffer(ib, dtype=np.int32).reshape(3, n)
     score = np.frombuffer(sb, dtype=np.float64).reshape(2, n)
     return pos, score
+
+
+def shard_plan(seqs, nparts: int):
+    """ks_shard_plan (csrc/ks_multi.cpp): the pieces nparts devices take, as
+    (part, sequence, lo, hi) rows -- whole sequences by LPT on length, cut in
+    the middle of N gaps of >= 1000 bases when whole sequences leave a part
+    more than 0.5 % above the fair share.  seqs: uint8 numpy arrays or bytes
+    (host memory; the gap scan runs on the host, no device is touched)."""
+    arrs = [np.ascontiguousarray(np.frombuffer(s, dtype=np.uint8) if isinstance(s, (bytes, bytearray)) else s,
+                                 dtype=np.uint8) for s in seqs]
+    ptrs = (C.c_void_p * len(arrs))(*[a.ctypes.data if a.size else None for a in arrs])
+    lens = np.array([a.size for a in arrs], dtype=np.int64)
+    L = load()
+    n = L.ks_shard_plan(ptrs, lens.ctypes.data, len(arrs), int(nparts), None, 0)
+    if n < 0:
+        raise KmerSpansError("ks_shard_plan: bad argument")
+    out = np.zeros((max(n, 1), 4), dtype=np.int64)
+    L.ks_shard_plan(ptrs, lens.ctypes.data, len(arrs), int(nparts), out.ctypes.data, n)
+    return [tuple(int(x) for x in row) for row in out[:n]]
+
+
+def multi_last_stats():
+    """Phases of the last multi-device host call (ks_multi_last_stats, ms)."""
+    L = load()
+    n = L.ks_multi_last_stats(None, 0)
+    v = (C.c_double * n)()
+    L.ks_multi_last_stats(v, n)
+    v = list(v)
+    parts = int(v[5])
+    return {"total_ms": v[0], "phase1_ms": v[1], "host_sum_ms": v[2], "phase2_ms": v[3], "merge_ms": v[4],
+            "parts": [{"body_ms": v[6 + 4 * p], "stage_count_ms": v[7 + 4 * p], "table_upload_ms": v[8 + 4 * p],
+                       "scan_ms": v[9 + 4 * p]} for p in range(parts)]}
 
 
 class Context:

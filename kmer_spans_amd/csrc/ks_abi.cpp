@@ -154,6 +154,36 @@ void debug_poison_workspace(ks_ctx *ctx) {
       for (auto &b : c->slots) debug_poison(b.ptr, b.bytes);
 }
 
+// The free-ordering probe (diagnostics, tests only).
+// KS_DEBUG_SPIN_MS=<ms>: right before the library drains a context's streams
+// and frees one of its buffers (a workspace slot growing in ensure, the
+// workspace returned at the end of a host call), a kernel that spins for
+// that long is queued on the context's side and high-priority streams --
+// where the round-4 report put the unordered use.  The drain and the
+// hipFree are timed and reported to stderr: a hipFree that lasts the spin
+// although only the main stream was drained (KS_DEBUG_DRAIN_MAIN_ONLY=1, the
+// round-4 ensure) waits for the device's other streams itself.
+__global__ void k_debug_spin(long long ticks) {
+  const long long t0 = wall_clock64();  // (100 MHz constant clock)
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(64);
+}
+
+double debug_spin(ks_ctx *ctx) {
+  const char *e = getenv("KS_DEBUG_SPIN_MS");
+  const double ms = e ? std::min(2000.0, std::max(0.0, atof(e))) : 0.0;
+  if (ms <= 0) return 0.0;
+  for (hipStream_t x : {ctx->side, ctx->hi})
+    if (x) hipLaunchKernelGGL(k_debug_spin, dim3(1), dim3(64), 0, x, (long long)(ms * 1e5));
+  return ms;
+}
+
+bool debug_drain_main_only() { return getenv("KS_DEBUG_DRAIN_MAIN_ONLY") != nullptr; }
+
+void debug_spin_report(const char *where, int slot, double spin_ms, double drain_ms, double free_ms) {
+  fprintf(stderr, "[spin] %s slot %d: spin %.1f ms queued on side+hi, drain (%s) %.2f ms, hipFree %.2f ms\n", where,
+          slot, spin_ms, debug_drain_main_only() ? "main stream only" : "all streams", drain_ms, free_ms);
+}
+
 ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out) {
   DevBuf &b = ctx->slots[s];
   if (b.bytes < bytes) {
@@ -161,9 +191,18 @@ ks_status ensure(ks_ctx *ctx, Slot s, size_t bytes, void **out) {
       // every stream of the context may still use the old buffer (the
       // piecewise count of a host entry runs on the side stream, pass 1's
       // first half on the high-priority one): all three drain before the free
-      for (hipStream_t x : {ctx->stream, ctx->side, ctx->hi})
-        if (x) KS_HIP(hipStreamSynchronize(x));
+      // (KS_DEBUG_SPIN_MS / KS_DEBUG_DRAIN_MAIN_ONLY: the ordering probe, below)
+      const double spin = debug_spin(ctx);
+      const double t0 = spin > 0 ? now_ms() : 0.0;
+      if (debug_drain_main_only()) {
+        KS_HIP(hipStreamSynchronize(ctx->stream));
+      } else {
+        for (hipStream_t x : {ctx->stream, ctx->side, ctx->hi})
+          if (x) KS_HIP(hipStreamSynchronize(x));
+      }
+      const double t1 = spin > 0 ? now_ms() : 0.0;
       KS_HIP(hipFree(b.ptr));
+      if (spin > 0) debug_spin_report("ensure", (int)s, spin, t1 - t0, now_ms() - t1);
       b.ptr = nullptr;
       b.bytes = 0;
     }
@@ -301,17 +340,16 @@ extern "C" void ks_ctx_destroy(ks_ctx *c) {
     c->part = nullptr;
   }
   (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
+  // every stream drains before anything it may still use is freed
+  for (hipStream_t x : {c->stream, c->side, c->hi})
+    if (x) (void)hipStreamSynchronize(x);
   for (auto &b : c->slots)
     if (b.ptr) (void)hipFree(b.ptr);
   if (c->pinned) (void)hipHostFree(c->pinned);
   for (auto &e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (hipStream_t x : {c->side, c->hi})
-    if (x) {
-      (void)hipStreamSynchronize(x);
-      (void)hipStreamDestroy(x);
-    }
+    if (x) (void)hipStreamDestroy(x);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   ks::pool_release_device(c->device);  // a destroyed table's pooled expanded-table buffer (ks_table.hip)
   delete c;
@@ -361,12 +399,22 @@ static double idle_ms() {
 
 static void free_workspace(ks_ctx *c) {
   (void)hipSetDevice(c->device);
-  for (hipStream_t x : {c->stream, c->side, c->hi})
-    if (x) (void)hipStreamSynchronize(x);
+  bool any = false;
+  for (auto &b : c->slots) any = any || b.ptr;
+  const double spin = any ? debug_spin(c) : 0.0;  // (KS_DEBUG_SPIN_MS: the ordering probe, ensure)
+  const double t0 = spin > 0 ? now_ms() : 0.0;
+  if (debug_drain_main_only()) {
+    (void)hipStreamSynchronize(c->stream);
+  } else {
+    for (hipStream_t x : {c->stream, c->side, c->hi})
+      if (x) (void)hipStreamSynchronize(x);
+  }
+  const double t1 = spin > 0 ? now_ms() : 0.0;
   for (auto &b : c->slots) {
     if (b.ptr) (void)hipFree(b.ptr);
     b = DevBuf();
   }
+  if (spin > 0) debug_spin_report("host_call_end", -1, spin, t1 - t0, now_ms() - t1);
 }
 
 static void release_ctx_memory(ks_ctx *c) {
@@ -393,9 +441,25 @@ Janitor &janitor() {
   return *j;
 }
 
-bool try_own(ks_ctx *c) {
+// The library takes a context to return its memory: `reclaim` is raised
+// before the ownership word is taken and lowered after it is given back, so an
+// entry point that finds the word taken meanwhile waits (CtxUse) instead of
+// failing as busy.
+bool reclaim_begin(ks_ctx *c) {
+  c->reclaim.store(1);
   std::thread::id none{};
-  return c->user.compare_exchange_strong(none, std::this_thread::get_id());
+  if (c->user.compare_exchange_strong(none, std::this_thread::get_id())) return true;
+  c->reclaim.store(0);
+  return false;
+}
+
+void reclaim_end(ks_ctx *c) {
+  // KS_DEBUG_JANITOR_HOLD_MS (tests): hold the context that long after its
+  // memory went back, so a test can call into it during a release
+  if (const char *e = getenv("KS_DEBUG_JANITOR_HOLD_MS"))
+    std::this_thread::sleep_for(std::chrono::milliseconds(std::min(10000, std::max(0, atoi(e)))));
+  c->user.store(std::thread::id());
+  c->reclaim.store(0);
 }
 
 void janitor_loop() {
@@ -423,9 +487,9 @@ void janitor_loop() {
         continue;
       }
       ks_ctx *c = J.due[i].first;
-      if (try_own(c)) {
+      if (reclaim_begin(c)) {
         release_ctx_memory(c);
-        c->user.store(std::thread::id());
+        reclaim_end(c);
       }
       J.due.erase(J.due.begin() + (long)i);
     }
@@ -479,9 +543,9 @@ void janitor_release_all() {
   std::lock_guard<std::mutex> g(J.mu);
   for (size_t i = 0; i < J.due.size();) {
     ks_ctx *c = J.due[i].first;
-    if (c->pid == getpid() && try_own(c)) {
+    if (c->pid == getpid() && reclaim_begin(c)) {
       release_ctx_memory(c);
-      c->user.store(std::thread::id());
+      reclaim_end(c);
       J.due.erase(J.due.begin() + (long)i);
     } else {
       ++i;
@@ -905,6 +969,10 @@ ks_status ks::kmer_regions_on(ks_ctx *ctx, const char *const *seqs, const int64_
     ks_regions_free(&again);
   }
   if (rc == KS_OK && visits) rc = copy_out(ctx, visits, d_cnt, nb);
+  ctx->host_ms[0] = t_stage - t0;
+  ctx->host_ms[1] = t_table - t0;
+  ctx->host_ms[2] = t4 - t3;
+  ctx->host_ms[3] = now_ms() - t0;
   if (dbg)
     fprintf(stderr, "[host kmer_regions] stage %.2f table %.2f (upload %.2f compress %.2f) (both %.2f) count %.2f "
             "expand %.2f (J %d) scan %.2f visits D2H %.2f ms\n", t_stage - t0, t_table - t0, t->ms_upload,

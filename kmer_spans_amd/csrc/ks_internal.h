@@ -90,6 +90,14 @@ struct DevBuf {
 
 struct ks_ctx {
   std::atomic<std::thread::id> user{};  // the thread inside an entry point (CtxUse)
+  // 1 while the library itself holds `user` to return this context's memory
+  // (the policy-2 janitor, ks_release_cache): an entry point that finds the
+  // context taken then waits for the release instead of failing as busy
+  std::atomic<int> reclaim{0};
+  uint32_t scan_epoch = 0;  // chunked scans on this context (the pass-1 epoch stamp, ks_scan_chunked.hip)
+  // phases of the last host-buffer kmer_regions call on this context (ms):
+  // staging + count, score-table upload + compression, scan, whole body
+  double host_ms[4] = {};
   int device = 0;
   int pid = 0;  // creating process (fork check)
   hipStream_t stream = nullptr;
@@ -218,10 +226,24 @@ struct CtxUse {
   bool owner = false, busy = false;
   explicit CtxUse(ks_ctx *ctx) : c(ctx) {
     if (!c) return;
-    std::thread::id none{};
     const std::thread::id me = std::this_thread::get_id();
-    if (c->user.compare_exchange_strong(none, me)) owner = true;
-    else busy = none != me;
+    for (int tries = 0;; ++tries) {
+      std::thread::id none{};
+      if (c->user.compare_exchange_strong(none, me)) {
+        owner = true;
+        return;
+      }
+      if (none == me) return;  // nested entry point of the same thread
+      // the library is returning the context's memory (janitor): wait for it;
+      // one more try after that, as a release may have ended just now
+      if (c->reclaim.load() != 0) {
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+        continue;
+      }
+      if (tries == 0) continue;
+      busy = true;
+      return;
+    }
   }
   ~CtxUse() {
     if (owner) c->user.store(std::thread::id());

@@ -23,8 +23,11 @@
 // tests use [0, 0]).  Only NULL-context calls spread; a call with an explicit
 // context runs on that context's device, as before.
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -43,7 +46,6 @@ constexpr int64_t kMinGap = 1000;  // N gaps a long sequence may be cut in (dist
 std::mutex g_mu;
 bool g_init = false;
 std::vector<int32_t> g_devs;       // the list (empty: device 0 alone)
-std::vector<ks_ctx *> g_ctx;       // one context per list entry, created on first use
 
 void init_locked() {
   if (g_init) return;
@@ -120,8 +122,9 @@ std::vector<std::vector<Piece>> lpt(const std::vector<Piece> &pieces, int nparts
 }
 
 // The shard plan: whole sequences by LPT, unless that leaves a part more than
-// 5 % above the fair share; then the sequences longer than half a share are
-// cut in their N gaps first.
+// 0.5 % above the fair share; then the sequences longer than half a share are
+// cut in their N gaps first (the gap scans on up to 16 host threads).  The
+// one planner of the library and of bench.py / dist.py (ks_shard_plan).
 std::vector<std::vector<Piece>> shard_plan(const char *const *seqs, const int64_t *lens, int32_t nseq, int nparts) {
   int64_t total = 0;
   for (int32_t q = 0; q < nseq; ++q) total += std::max<int64_t>(lens[q], 0);
@@ -132,13 +135,27 @@ std::vector<std::vector<Piece>> shard_plan(const char *const *seqs, const int64_
     if (lens[q] > 0) whole.push_back(Piece{q, 0, lens[q]});  // (an empty sequence counts and scans nothing)
   int64_t worst = 0;
   auto parts = lpt(whole, nparts, &worst);
-  if (nparts == 1 || worst <= fair + fair / 20) return parts;
+  if (nparts == 1 || worst <= fair + fair / 200) return parts;
+  std::vector<std::vector<int64_t>> cuts(whole.size());
+  std::vector<size_t> todo;
+  for (size_t i = 0; i < whole.size(); ++i)
+    if (whole[i].hi > fair / 2 && whole[i].hi >= 2 * kMinGap) todo.push_back(i);
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> th;
+  const size_t nt = std::min<size_t>(16, todo.size());
+  for (size_t t = 0; t < nt; ++t)
+    th.emplace_back([&] {
+      for (size_t j = next++; j < todo.size(); j = next++) {
+        const Piece &w = whole[todo[j]];
+        cuts[todo[j]] = gap_cuts(seqs[w.seq], w.hi);
+      }
+    });
+  for (auto &x : th) x.join();
   std::vector<Piece> pieces;
-  for (const Piece &w : whole) {
-    std::vector<int64_t> cuts;
-    if (w.hi > fair / 2 && w.hi >= 2 * kMinGap) cuts = gap_cuts(seqs[w.seq], w.hi);
+  for (size_t i = 0; i < whole.size(); ++i) {
+    const Piece &w = whole[i];
     int64_t a = 0;
-    for (int64_t c : cuts) {
+    for (int64_t c : cuts[i]) {
       pieces.push_back(Piece{w.seq, a, c});
       a = c;
     }
@@ -194,33 +211,91 @@ ks_status merge_parts(const std::vector<std::vector<Piece>> &parts, const std::v
   return KS_OK;
 }
 
-// The contexts of the list (created on first use, kept for the process).
-ks_status list_contexts(std::vector<ks_ctx *> *out) {
+// The contexts of the list: one immutable set per list, shared by the calls
+// that use it.  ks_set_devices (or a change of the list's length) replaces the
+// set; the old one is destroyed when its last call drops it, never under a
+// running call.
+struct CtxSet {
+  std::vector<ks_ctx *> c;
+  ~CtxSet() {
+    for (ks_ctx *x : c) ks_ctx_destroy(x);  // (a no-op for contexts inherited across fork())
+  }
+};
+std::shared_ptr<CtxSet> g_set;
+// One multi-device call at a time: its threads own every context of the set
+// from its first phase to its end; a second thread's call meanwhile is
+// refused (as a second thread on one context is, include/kmer_spans.h).
+std::mutex g_call_mu;
+
+ks_status list_contexts(std::shared_ptr<CtxSet> *out) {
   std::lock_guard<std::mutex> g(g_mu);
   init_locked();
-  if (g_ctx.size() != g_devs.size()) {
-    for (ks_ctx *c : g_ctx) ks_ctx_destroy(c);
-    g_ctx.assign(g_devs.size(), nullptr);
+  bool fresh = !g_set || g_set->c.size() != g_devs.size();
+  for (size_t i = 0; !fresh && i < g_set->c.size(); ++i)
+    fresh = g_set->c[i]->pid != (int)getpid();  // inherited across fork(): a new set
+  if (fresh) {
+    auto set = std::make_shared<CtxSet>();
+    for (size_t i = 0; i < g_devs.size(); ++i) {
+      ks_ctx *c = nullptr;
+      KS_TRY(ks_ctx_create(g_devs[i], &c));  // (on failure the partial set destroys what it made)
+      set->c.push_back(c);
+    }
+    g_set = std::move(set);
   }
-  for (size_t i = 0; i < g_devs.size(); ++i) {
-    if (g_ctx[i] && g_ctx[i]->pid != (int)getpid()) g_ctx[i] = nullptr;  // inherited across fork()
-    if (!g_ctx[i]) KS_TRY(ks_ctx_create(g_devs[i], &g_ctx[i]));
-  }
-  *out = g_ctx;
+  *out = g_set;
   return KS_OK;
 }
 
-// Runs fn(part index) on one host thread per non-empty part; the first
-// failure's status and message are returned.
+// Phase times of the last multi-device call (ks_multi_last_stats).
+struct MultiStats {
+  double total = 0, phase1 = 0, host_sum = 0, phase2 = 0, merge = 0;
+  std::vector<double> part;  // per part: body, staging + count, table upload, scan (ms)
+};
+std::mutex g_stats_mu;
+MultiStats g_stats;
+
+// A barrier of the call's part threads; a part that fails breaks it for all.
+class PartBarrier {
+ public:
+  explicit PartBarrier(int n) : n_(n) {}
+  // false: a part failed (the caller returns at once)
+  bool arrive(bool ok) {
+    std::unique_lock<std::mutex> g(mu_);
+    if (!ok) broken_ = true;
+    const int gen = gen_;
+    if (++here_ == n_) {
+      here_ = 0;
+      ++gen_;
+      cv_.notify_all();
+    } else {
+      cv_.wait(g, [&] { return gen_ != gen; });
+    }
+    return !broken_;
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int n_, here_ = 0, gen_ = 0;
+  bool broken_ = false;
+};
+
+// Runs fn(part index) on one host thread per non-empty part, each holding
+// its part's context (KS_ENTER) for the whole of fn; the first failure's
+// status and message are returned.
 template <typename F>
-ks_status run_parts(size_t nparts, const std::vector<std::vector<Piece>> &parts, F fn) {
+ks_status run_parts(const std::vector<ks_ctx *> &ctx, const std::vector<std::vector<Piece>> &parts, F fn) {
+  const size_t nparts = parts.size();
   std::vector<ks_status> rc(nparts, KS_OK);
   std::vector<std::string> err(nparts);
   std::vector<std::thread> th;
   for (size_t p = 0; p < nparts; ++p) {
     if (parts[p].empty()) continue;
     th.emplace_back([&, p] {
-      rc[p] = fn(p);
+      rc[p] = [&]() -> ks_status {
+        KS_ENTER(ctx[p]);
+        return fn(p);
+      }();
       if (rc[p] != KS_OK) err[p] = ks_last_error();  // (thread-local)
     });
   }
@@ -233,6 +308,34 @@ ks_status run_parts(size_t nparts, const std::vector<std::vector<Piece>> &parts,
   return KS_OK;
 }
 
+// dst += every src (uint32 wrap-around, the reference's int counters), on up
+// to 16 threads over stripes of the histogram
+void add_hists(int32_t *dst, const std::vector<const int32_t *> &src, size_t n) {
+  const size_t nt = std::max<size_t>(1, std::min<size_t>(16, n >> 20));
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      const size_t a = n * t / nt, b = n * (t + 1) / nt;
+      uint32_t *d = reinterpret_cast<uint32_t *>(dst);
+      for (const int32_t *s : src) {
+        const uint32_t *u = reinterpret_cast<const uint32_t *>(s);
+        for (size_t i = a; i < b; ++i) d[i] += u[i];
+      }
+    });
+  for (auto &x : th) x.join();
+}
+
+size_t live_parts(const std::vector<std::vector<Piece>> &parts) {
+  size_t n = 0;
+  for (const auto &v : parts) n += !v.empty();
+  return n;
+}
+
+void record_stats(const MultiStats &m) {
+  std::lock_guard<std::mutex> g(g_stats_mu);
+  g_stats = m;
+}
+
 }  // namespace
 
 int multi_devices() {
@@ -243,131 +346,193 @@ int multi_devices() {
 
 ks_status multi_kmer_counts(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k, int32_t *counts,
                             double *n_words) {
-  std::vector<ks_ctx *> ctx;
-  KS_TRY(list_contexts(&ctx));
+  std::unique_lock<std::mutex> call(g_call_mu, std::try_to_lock);
+  if (!call.owns_lock()) return ctx_busy();
+  std::shared_ptr<CtxSet> set;
+  KS_TRY(list_contexts(&set));
+  const std::vector<ks_ctx *> &ctx = set->c;
+  const double t0 = now_ms();
   const auto parts = shard_plan(seqs, lens, nseq, (int)ctx.size());
   const size_t nk = (size_t)1 << (2 * k);
   std::vector<std::vector<int32_t>> c(parts.size());
   std::vector<double> w(parts.size(), 0.0);
-  KS_TRY(run_parts(parts.size(), parts, [&](size_t p) -> ks_status {
+  KS_TRY(run_parts(ctx, parts, [&](size_t p) -> ks_status {
     const PartIn in = part_input(seqs, parts[p]);
     c[p].assign(nk, 0);
     return kmer_counts_on(ctx[p], in.ptr.data(), in.len.data(), (int32_t)in.len.size(), k, c[p].data(), &w[p]);
   }));
+  const double t1 = now_ms();
   memset(counts, 0, nk * 4);
   double words = 0;
-  for (size_t p = 0; p < parts.size(); ++p) {
-    if (parts[p].empty()) continue;
-    words += w[p];
-    uint32_t *dst = reinterpret_cast<uint32_t *>(counts);
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(c[p].data());
-    for (size_t i = 0; i < nk; ++i) dst[i] += src[i];
-  }
+  std::vector<const int32_t *> src;
+  for (size_t p = 0; p < parts.size(); ++p)
+    if (!parts[p].empty()) {
+      words += w[p];
+      src.push_back(c[p].data());
+    }
+  add_hists(counts, src, nk);
   *n_words = words;
+  MultiStats m;
+  m.phase1 = t1 - t0;
+  m.host_sum = now_ms() - t1;
+  m.total = now_ms() - t0;
+  record_stats(m);
   return KS_OK;
 }
 
 ks_status multi_kmer_regions(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k, const double *w,
                              int32_t min_width, double min_score, int32_t *visits, ks_regions *out) {
-  std::vector<ks_ctx *> ctx;
-  KS_TRY(list_contexts(&ctx));
+  std::unique_lock<std::mutex> call(g_call_mu, std::try_to_lock);
+  if (!call.owns_lock()) return ctx_busy();
+  std::shared_ptr<CtxSet> set;
+  KS_TRY(list_contexts(&set));
+  const std::vector<ks_ctx *> &ctx = set->c;
+  const double t0 = now_ms();
   const auto parts = shard_plan(seqs, lens, nseq, (int)ctx.size());
   const size_t nk = (size_t)1 << (2 * k);
   std::vector<std::vector<int32_t>> v(parts.size());
   std::vector<ks_regions> rs(parts.size());
   for (ks_regions &r : rs) memset(&r, 0, sizeof(r));
-  ks_status rc = run_parts(parts.size(), parts, [&](size_t p) -> ks_status {
+  MultiStats m;
+  m.part.assign(4 * parts.size(), 0.0);
+  ks_status rc = run_parts(ctx, parts, [&](size_t p) -> ks_status {
     const PartIn in = part_input(seqs, parts[p]);
     if (visits) v[p].assign(nk, 0);
-    return kmer_regions_on(ctx[p], in.ptr.data(), in.len.data(), (int32_t)in.len.size(), k, w, min_width, min_score,
-                           visits ? v[p].data() : nullptr, &rs[p]);
+    const ks_status r = kmer_regions_on(ctx[p], in.ptr.data(), in.len.data(), (int32_t)in.len.size(), k, w, min_width,
+                                        min_score, visits ? v[p].data() : nullptr, &rs[p]);
+    m.part[4 * p] = ctx[p]->host_ms[3];
+    m.part[4 * p + 1] = ctx[p]->host_ms[0];
+    m.part[4 * p + 2] = ctx[p]->host_ms[1];
+    m.part[4 * p + 3] = ctx[p]->host_ms[2];
+    return r;
   });
+  const double t1 = now_ms();
   if (rc == KS_OK) rc = merge_parts(parts, rs, out);
+  const double t2 = now_ms();
   for (ks_regions &r : rs) ks_regions_free(&r);
   if (rc != KS_OK) return rc;
   if (visits) {
     memset(visits, 0, nk * 4);
-    uint32_t *dst = reinterpret_cast<uint32_t *>(visits);
-    for (size_t p = 0; p < parts.size(); ++p) {
-      if (v[p].empty()) continue;
-      const uint32_t *src = reinterpret_cast<const uint32_t *>(v[p].data());
-      for (size_t i = 0; i < nk; ++i) dst[i] += src[i];
-    }
+    std::vector<const int32_t *> src;
+    for (size_t p = 0; p < parts.size(); ++p)
+      if (!v[p].empty()) src.push_back(v[p].data());
+    add_hists(visits, src, nk);
   }
+  m.phase1 = t1 - t0;
+  m.merge = t2 - t1;
+  m.host_sum = now_ms() - t2;
+  m.total = now_ms() - t0;
+  record_stats(m);
   return KS_OK;
 }
 
 ks_status multi_low_comp_regions(const char *const *seqs, const int64_t *lens, int32_t nseq, int32_t k,
                                  int32_t min_width, double min_score, double thr, int32_t *counts, double *ranks,
                                  double *n, ks_regions *out) {
-  std::vector<ks_ctx *> ctx;
-  KS_TRY(list_contexts(&ctx));
+  std::unique_lock<std::mutex> call(g_call_mu, std::try_to_lock);
+  if (!call.owns_lock()) return ctx_busy();
+  std::shared_ptr<CtxSet> set;
+  KS_TRY(list_contexts(&set));
+  const std::vector<ks_ctx *> &ctx = set->c;
+  const double t0 = now_ms();
   const auto parts = shard_plan(seqs, lens, nseq, (int)ctx.size());
   const size_t np = parts.size();
   const size_t nk = (size_t)1 << (2 * k), nb = nk * 4, rb = nk * 8;
-  // The contexts stay this call's until the end: phase 1 stages and counts
-  // each shard, the host adds the counts, phase 2 builds every shard's rank
-  // table from the sum and scans; the staged bases stay on the devices
-  // between the phases.
+  // One thread per part holds its context from the first phase to the end
+  // (run_parts): phase 1 stages and counts the part's bases; after a barrier
+  // each part adds one stripe of the histogram over every part's device
+  // counts into the caller's buffer (D2H stripe by stripe: no full host copy
+  // per part); after a second barrier every part builds the rank table from
+  // the sum and scans the bases it still holds.
   struct Shard {
     Staged st;
-    std::vector<int32_t> cnt;
     double words = 0;
+    int32_t *d_counts = nullptr;
   };
   std::vector<Shard> sh(np);
-  for (size_t p = 0; p < np; ++p)
-    if (!parts[p].empty() && ctx[p]->user.load() != std::thread::id()) return ctx_busy();
-  struct End {  // the host-entry memory policy of every context, at the end of the call
-    std::vector<ks_ctx *> &c;
-    ~End() {
-      for (ks_ctx *x : c) host_call_end(x);
-    }
-  } const end{ctx};
-  KS_TRY(run_parts(np, parts, [&](size_t p) -> ks_status {
-    KS_ENTER(ctx[p]);
-    const PartIn in = part_input(seqs, parts[p]);
-    void *d_counts = nullptr;
-    KS_TRY(ensure(ctx[p], SLOT_COUNTS, nb, &d_counts));
-    KS_TRY(stage_counted(ctx[p], in.ptr.data(), in.len.data(), (int32_t)in.len.size(), k,
-                         static_cast<int32_t *>(d_counts), &sh[p].st, &sh[p].words));
-    sh[p].cnt.resize(nk);
-    return copy_out(ctx[p], sh[p].cnt.data(), d_counts, nb);
-  }));
-  memset(counts, 0, nb);
-  double words = 0;
-  for (size_t p = 0; p < np; ++p) {
-    if (parts[p].empty()) continue;
-    words += sh[p].words;
-    uint32_t *dst = reinterpret_cast<uint32_t *>(counts);
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(sh[p].cnt.data());
-    for (size_t i = 0; i < nk; ++i) dst[i] += src[i];
-  }
-  n[0] = words;
-  n[1] = 0;  // Q8 (:613)
   size_t first = np;
   for (size_t p = 0; p < np && first == np; ++p)
     if (!parts[p].empty()) first = p;
+  const size_t nlive = live_parts(parts);
+  PartBarrier bar((int)nlive);
+  std::vector<size_t> live;
+  for (size_t p = 0; p < np; ++p)
+    if (!parts[p].empty()) live.push_back(p);
   std::vector<ks_regions> rs(np);
   for (ks_regions &r : rs) memset(&r, 0, sizeof(r));
-  ks_status rc = run_parts(np, parts, [&](size_t p) -> ks_status {
-    KS_ENTER(ctx[p]);
-    void *d_counts = nullptr, *d_rk = nullptr;
-    KS_TRY(ensure(ctx[p], SLOT_COUNTS, nb, &d_counts));
+  double t_p1 = 0, t_sum = 0;
+  ks_status rc = run_parts(ctx, parts, [&](size_t p) -> ks_status {
+    struct End {  // the host-entry memory policy, at the end of the part's call
+      ks_ctx *c;
+      ~End() { host_call_end(c); }
+    } const end{ctx[p]};
+    debug_poison_workspace(ctx[p]);  // (KS_DEBUG_POISON)
+    // ---- phase 1: stage + count
+    ks_status r = [&]() -> ks_status {
+      const PartIn in = part_input(seqs, parts[p]);
+      void *d = nullptr;
+      KS_TRY(ensure(ctx[p], SLOT_COUNTS, nb, &d));
+      sh[p].d_counts = static_cast<int32_t *>(d);
+      KS_TRY(stage_counted(ctx[p], in.ptr.data(), in.len.data(), (int32_t)in.len.size(), k, sh[p].d_counts, &sh[p].st,
+                           &sh[p].words));
+      KS_HIP(hipStreamSynchronize(ctx[p]->stream));
+      return KS_OK;
+    }();
+    if (!bar.arrive(r == KS_OK)) return r != KS_OK ? r : fail(KS_ERR_DEVICE, "another device list entry failed");
+    // KS_DEBUG_MULTI_PHASE_SLEEP_MS (tests): a long gap between the phases,
+    // during which the contexts must stay this call's (janitor, other threads)
+    if (const char *e = getenv("KS_DEBUG_MULTI_PHASE_SLEEP_MS"))
+      std::this_thread::sleep_for(std::chrono::milliseconds(std::min(10000, std::max(0, atoi(e)))));
+    // ---- the count sum: this part's stripe over every part's counts
+    const size_t ip = (size_t)(std::find(live.begin(), live.end(), p) - live.begin());
+    if (ip == 0) t_p1 = now_ms() - t0;
+    r = [&]() -> ks_status {
+      const size_t a = nk * ip / nlive, b = nk * (ip + 1) / nlive;
+      if (b <= a) return KS_OK;
+      uint32_t *dst = reinterpret_cast<uint32_t *>(counts) + a;
+      memset(dst, 0, (b - a) * 4);
+      std::vector<uint32_t> tmp(b - a);
+      for (size_t q : live) {
+        KS_HIP(hipMemcpy(tmp.data(), sh[q].d_counts + a, (b - a) * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < b - a; ++i) dst[i] += tmp[i];
+      }
+      return KS_OK;
+    }();
+    if (!bar.arrive(r == KS_OK)) return r != KS_OK ? r : fail(KS_ERR_DEVICE, "another device list entry failed");
+    if (ip == 0) t_sum = now_ms() - t0 - t_p1;
+    // ---- phase 2: the rank table from the sum, the scan
+    KS_TRY(activate(ctx[p]));
+    double words = 0;
+    for (size_t q : live) words += sh[q].words;
+    void *d_rk = nullptr;
     KS_TRY(ensure(ctx[p], SLOT_RANKS, rb, &d_rk));
-    KS_HIP(hipMemcpy(d_counts, counts, nb, hipMemcpyHostToDevice));
+    KS_HIP(hipMemcpy(sh[p].d_counts, counts, nb, hipMemcpyHostToDevice));
     ks_table *t = nullptr;
-    KS_TRY(ks_table_from_counts(ctx[p], static_cast<const int32_t *>(d_counts), k, KS_SCORE_RANK, words, thr,
-                                KS_TABLE_EXPAND, host_ext_cap(sh[p].st.total), static_cast<double *>(d_rk), &t));
-    ks_status r = KS_OK;
-    if (p == first) r = copy_out(ctx[p], ranks, d_rk, rb);  // (every shard's ranks are the same)
+    KS_TRY(ks_table_from_counts(ctx[p], sh[p].d_counts, k, KS_SCORE_RANK, words, thr, KS_TABLE_EXPAND,
+                                host_ext_cap(sh[p].st.total), static_cast<double *>(d_rk), &t));
+    r = KS_OK;
+    if (p == first) r = copy_out(ctx[p], ranks, d_rk, rb);  // (every part's ranks are the same)
     if (r == KS_OK) r = scan_impl(ctx[p], &sh[p].st.dev, sh[p].st.total, k, t, min_width, min_score, nullptr, &rs[p],
                                   nullptr);
     ks_table_destroy(t);
     return r;
   });
+  const double t1 = now_ms();
+  double words = 0;
+  for (size_t q : live) words += sh[q].words;
+  if (nlive == 0) memset(counts, 0, nb);
+  n[0] = words;
+  n[1] = 0;  // Q8 (:613)
   if (first == np) memset(ranks, 0, rb);  // (no sequence: no ranks were built)
   if (rc == KS_OK) rc = merge_parts(parts, rs, out);
   for (ks_regions &r : rs) ks_regions_free(&r);
+  MultiStats m;
+  m.phase1 = t_p1;
+  m.host_sum = t_sum;
+  m.phase2 = t1 - t0 - t_p1 - t_sum;
+  m.merge = now_ms() - t1;
+  m.total = now_ms() - t0;
+  record_stats(m);
   return rc;
 }
 
@@ -380,12 +545,24 @@ extern "C" ks_status ks_set_devices(const int32_t *devices, int32_t n) {
     return fail(KS_ERR_ARG, "a device list holds 0 to %d devices", kMaxDevices);
   for (int32_t i = 0; i < n; ++i)
     if (devices[i] < 0) return fail(KS_ERR_ARG, "device %d out of range", devices[i]);
-  std::lock_guard<std::mutex> g(g_mu);
-  init_locked();
-  for (ks_ctx *c : g_ctx) ks_ctx_destroy(c);
-  g_ctx.clear();
-  g_devs.assign(devices, devices + n);
+  std::shared_ptr<CtxSet> old;  // destroyed outside the lock, after any call still using it
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    init_locked();
+    old = std::move(g_set);
+    g_set.reset();
+    g_devs.assign(devices, devices + n);
+  }
   return KS_OK;
+}
+
+extern "C" int32_t ks_multi_last_stats(double *out, int32_t cap) {
+  std::lock_guard<std::mutex> g(g_stats_mu);
+  std::vector<double> v = {g_stats.total, g_stats.phase1, g_stats.host_sum, g_stats.phase2, g_stats.merge,
+                           (double)(g_stats.part.size() / 4)};
+  v.insert(v.end(), g_stats.part.begin(), g_stats.part.end());
+  for (int32_t i = 0; out && i < cap && (size_t)i < v.size(); ++i) out[i] = v[(size_t)i];
+  return (int32_t)v.size();
 }
 
 extern "C" int32_t ks_get_devices(int32_t *devices, int32_t cap) {

@@ -66,6 +66,11 @@ struct P1 {  // per-chunk results of the gather pass
   int32_t *tbeg, *targ;  // trailing open excursion (relative), tbeg = -1: none
   uint8_t *special;      // a non-finite value occurred
   int32_t *parg;         // first index of the prefix maximum pmax
+  // epoch guard: pass 1 stamps every chunk it wrote with this call's epoch
+  // (ks_ctx::scan_epoch); the stitch checks the stamp of every chunk whose
+  // pass-1 results it reads (error bit 32: results of another call)
+  uint32_t *ep = nullptr;
+  uint32_t epoch = 0;
 };
 
 struct Summ {  // binade-integer summaries for the predicted binade (P2)
@@ -915,6 +920,7 @@ __global__ void __launch_bounds__(J == 1 ? 256 : 1024) k_pass1(Chunks g, const u
   o.parg[c] = parg;
   o.sabs[c] = sabs;
   o.special[c] = special ? 1 : 0;
+  o.ep[c] = o.epoch;
   if (prev > 0) {
     o.tbeg[c] = beg; o.tmax[c] = best; o.targ[c] = arg;
   } else {
@@ -1233,6 +1239,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
   o.parg[c] = parg;
   o.sabs[c] = sabs;
   o.special[c] = special ? 1 : 0;
+  o.ep[c] = o.epoch;
   if (prev > 0) {
     o.tbeg[c] = beg; o.tmax[c] = best; o.targ[c] = arg;
   } else {
@@ -1383,6 +1390,7 @@ struct P1Lane {
     o.parg[c] = parg;
     o.sabs[c] = sabs;
     o.special[c] = special ? 1 : 0;
+    o.ep[c] = o.epoch;
     if (prev > 0) {
       o.tbeg[c] = beg; o.tmax[c] = best; o.targ[c] = arg;
     } else {
@@ -1815,6 +1823,7 @@ __global__ void __launch_bounds__(1024) k_pass1_lds_int(Chunks g, int64_t total,
     o.parg[c] = parg;
     o.sabs[c] = 0.0;
     o.special[c] = 0;
+    o.ep[c] = o.epoch;
     if (prev > 0) {
       o.tbeg[c] = beg; o.tmax[c] = (double)best; o.targ[c] = arg;
     } else {
@@ -1937,6 +1946,7 @@ __global__ void __launch_bounds__(1024) k_pass1_lds(Chunks g, int64_t total, int
     o.parg[c] = parg;
     o.sabs[c] = sabs;
     o.special[c] = special ? 1 : 0;
+    o.ep[c] = o.epoch;
     if (prev > 0) {
       o.tbeg[c] = beg; o.tmax[c] = best; o.targ[c] = arg;
     } else {
@@ -3793,7 +3803,10 @@ __global__ void __launch_bounds__(256) k_stitch_emit(Chunks g, const int64_t *__
   ChunkOp op;
   op.f = XState{0, 0, 0, 0, -INFINITY};
   op.closes = false;
-  if (live) op = chunk_op(g, o, cr, c);
+  if (live) {
+    op = chunk_op(g, o, cr, c);
+    if (o.ep[c] != o.epoch) atomicOr(err, 32u);  // pass-1 results of another call
+  }
   const XState inc = wave_inclusive(op.f, lane);
   const XState exc = dpp_x<kDppWaveShr1, 0xf>(inc);  // (lane 0: the identity)
   const XState in = x_compose(xt_load(tin, t), exc);  // state entering chunk c
@@ -3967,6 +3980,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   const size_t o_p1d = off; off += al(nch * 8 * 6);
   const size_t o_p1i = off; off += al(nch * 4 * 3);
   const size_t o_spec = off; off += al(nch);
+  const size_t o_ep = off; off += al(nch * 4);
   const size_t o_xt = off; off += al(nch * 8);
   const size_t o_se = off; off += al(nch * 4);
   const size_t o_sD = off; off += al(nch * 8 * 6);
@@ -4012,6 +4026,8 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   int32_t *p1i = reinterpret_cast<int32_t *>(W + o_p1i);
   P1 p1{p1d, p1d + nch, p1d + 2 * nch, p1d + 3 * nch, p1d + 4 * nch, p1d + 5 * nch, p1i, p1i + nch,
         reinterpret_cast<uint8_t *>(W + o_spec), p1i + 2 * nch};
+  p1.ep = reinterpret_cast<uint32_t *>(W + o_ep);
+  p1.epoch = ++ctx->scan_epoch;
   double *xt = reinterpret_cast<double *>(W + o_xt);
   long long *sD = reinterpret_cast<long long *>(W + o_sD);
   Summ sm{reinterpret_cast<int32_t *>(W + o_se), sD, sD + 2 * nch, sD + 4 * nch,
@@ -4509,6 +4525,10 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   } else {
     KS_HIP(hipEventRecord(ctx->ev[9], split ? ctx->side : st));  // end of pass 1 (the last half's stream)
   }
+  // KS_TEST_EPOCH_STALE (tests): the post-processing expects another epoch
+  // than pass 1 stamped -- what it would see reading an earlier call's
+  // pass-1 results -- so the epoch guard must fail the call
+  if (getenv("KS_TEST_EPOCH_STALE")) ++p1.epoch;
   if (ctx->on_pass1) {  // a staggered scan's later part starts now (scan_impl)
     auto go = std::move(ctx->on_pass1);
     ctx->on_pass1 = nullptr;
@@ -4763,6 +4783,9 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
               "segments %lld L %lld R %lld\n", (long long)idx[i], d[0], d[6], d[7], d[1], d[2], d[3], d[4], d[5]);
     }
   }
+  if (errbits & 32u)
+    return fail(KS_ERR_DEVICE, "chunked scan epoch check failed: the stitch read pass-1 results not written by this "
+                                 "call (epoch %u)", p1.epoch);
   if (errbits & ~16u) return fail(KS_ERR_INTERNAL, "chunked scan consistency check failed (bits %u)", errbits);
   if ((int64_t)cand_max > csegcap) {  // grow the candidate buffers and rerun the pass
     void *grown = nullptr;

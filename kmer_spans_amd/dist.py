@@ -8,8 +8,8 @@ The only collectives are after the scan:
     RCCL over xGMI with the "nccl" backend, gloo in the CPU tests;
   * an int32 sum of per-rank histograms when one genome's counts or visits
     are split across ranks (exact, order-independent).
-Contigs, or their pieces cut inside N gaps (gap_cuts), are assigned by LPT
-(longest processing time first) on length.
+Contigs, or their pieces cut inside N gaps, are assigned by LPT (longest
+processing time first) on length: shard_pieces, the library's own planner.
 """
 from __future__ import annotations
 
@@ -32,34 +32,22 @@ def lpt_shards(lengths, n: int):
     return [sorted(x) for x in shards]
 
 
-def gap_cuts(seq: torch.Tensor, min_gap: int = 1000) -> list:
-    """Cut points of one sequence (uint8 tensor, any device) at the middle of
-    every N gap of at least min_gap bases: the pieces between them have
-    exactly the sequence's N-free runs, each piece starting and ending inside
-    an N gap.  Runs never interact across N bases -- the scan restarts after
-    every N (kmer_spans.c:261-265, 281, 303), and the count's end-of-string
-    quirk (:143) cannot apply at a cut that has N on both sides -- so scanning
-    and counting the pieces is exactly scanning and counting the sequence."""
-    if seq.numel() < 2 * min_gap:
-        return []
-    isn = ((seq | 0x20) == ord("n")).to(torch.int8)
-    d = torch.diff(isn, prepend=isn.new_zeros(1), append=isn.new_zeros(1))
-    starts = torch.nonzero(d == 1).flatten()
-    ends = torch.nonzero(d == -1).flatten()
-    keep = (ends - starts) >= min_gap
-    mids = ((starts[keep] + ends[keep]) // 2).cpu().tolist()
-    return [int(m) for m in mids if 0 < m < seq.numel()]
-
-
-def lpt_pieces(lengths, cuts, n: int):
-    """LPT over the pieces of every sequence (cuts[q]: its cut points).
-    Returns per shard a list of (sequence id, lo, hi), ordered by (id, lo)."""
-    pieces = []
-    for q, L in enumerate(lengths):
-        b = [0] + list(cuts[q]) + [int(L)]
-        pieces += [(q, b[i], b[i + 1]) for i in range(len(b) - 1) if b[i + 1] > b[i]]
-    shards = lpt_shards([hi - lo for _, lo, hi in pieces], n)
-    return [sorted(pieces[i] for i in sh) for sh in shards]
+def shard_pieces(seqs, n: int):
+    """The library's shard plan (ks_shard_plan, csrc/ks_multi.cpp -- the one
+    planner of the drop-in multi-device entry points and of bench.py): per
+    shard a list of (sequence id, lo, hi) ordered by (id, lo).  Whole
+    sequences by LPT on length, unless that leaves a shard more than 0.5 %
+    above the fair share; then the sequences longer than half a share are cut
+    in the middle of their N gaps of >= 1000 bases.  Runs never interact
+    across N bases -- the scan restarts after every N (kmer_spans.c:261-265,
+    281, 303), and the count's end-of-string quirk (:143) cannot apply at a
+    cut with N on both sides -- so scanning and counting the pieces is exactly
+    scanning and counting the sequences.  seqs: host uint8 arrays / bytes."""
+    from . import _lib
+    out = [[] for _ in range(n)]
+    for p, q, lo, hi in _lib.shard_plan(seqs, n):
+        out[p].append((q, lo, hi))
+    return out
 
 
 def _pack(pos: np.ndarray, score: np.ndarray) -> np.ndarray:
@@ -109,7 +97,7 @@ def merge_shards(shard_ids, pos_list, score_list, one_based: bool = False, offse
     """Map shard-local seq ids back to global contig ids and order the union
     by (seq_id, beg) -- the reference's emission order.  one_based: the
     records carry 1-based seq ids (tr_lr_regions_r, kmer_spans.c:699).
-    offsets (pieces, lpt_pieces): per shard the start of each local sequence
+    offsets (pieces, shard_pieces): per shard the start of each local sequence
     inside its contig, added to beg / end."""
     if not pos_list:
         return np.zeros((3, 0), np.int32), np.zeros((2, 0), np.float64)

@@ -142,21 +142,59 @@ def test_sharded_equals_unsharded_gloo_world2(oracle):
     assert np.array_equal(tscore.view(np.uint64), tfull["score"].view(np.uint64))
 
 
+def _gapped_genome(seed=11):
+    """A genome with one dominant contig carrying N gaps of >= 1000 bases
+    (where the library's shard plan may cut), plus short contigs."""
+    rng = np.random.default_rng(seed)
+    lens = [120000, 9000, 26000, 3000, 17000, 5, 31000]
+    seqs = []
+    for L in lens:
+        b = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=L, p=[0.3, 0.2, 0.2, 0.3])
+        for _ in range(L // 8000):  # short N runs everywhere
+            a = int(rng.integers(0, max(L - 300, 1)))
+            b[a:a + int(rng.integers(1, 300))] = ord("N")
+        if L > 2000:  # a low-complexity stretch so that regions exist
+            a = int(rng.integers(0, L - 1500))
+            b[a:a + 1200] = np.frombuffer((b"CA" * 600), np.uint8)
+        if L >= 100000:  # assembly gaps of 1000-1500 Ns
+            for a in range(9000, L - 3000, 15000):
+                b[a:a + int(rng.integers(1000, 1500))] = ord("N")
+        seqs.append(b.tobytes())
+    return seqs, lens
+
+
 def test_pieces_cut_in_n_gaps_equal_whole(oracle):
-    """Contigs cut in the middle of their N gaps (dist.gap_cuts), the pieces
-    LPT-sharded over three shards, scanned and counted per shard, merged with
-    the pieces' offsets == the whole genome's scan and counts, bit for bit
+    """The library's shard plan (ks_shard_plan via dist.shard_pieces: contigs
+    cut in the middle of N gaps of >= 1000 bases when whole contigs do not
+    balance), the pieces scanned and counted per shard and merged with the
+    pieces' offsets == the whole genome's scan and counts, bit for bit
     (kmer_regions and 1-based tr_lr)."""
-    import torch
     from kmer_spans_amd import dist
     O = oracle
     k = 6
-    seqs, lens = _genome(11)
-    cuts = [dist.gap_cuts(torch.from_numpy(np.frombuffer(s, np.uint8).copy()), min_gap=40) for s in seqs]
-    assert sum(len(c) for c in cuts) >= 3
-    psh = dist.lpt_pieces(lens, cuts, 3)
-    assert sorted((q, lo, hi) for sh in psh for q, lo, hi in sh) == sorted(
-        (q, b[i], b[i + 1]) for q in range(len(lens)) for b in [[0] + cuts[q] + [lens[q]]] for i in range(len(b) - 1))
+    seqs, lens = _gapped_genome(11)
+    psh = dist.shard_pieces(seqs, 3)
+    rows = sorted((q, lo, hi) for sh in psh for q, lo, hi in sh)
+    # every non-empty sequence covered once, in order, by its pieces
+    for q, L in enumerate(lens):
+        mine = [(lo, hi) for qq, lo, hi in rows if qq == q]
+        assert mine[0][0] == 0 and mine[-1][1] == L
+        assert all(a[1] == b[0] for a, b in zip(mine, mine[1:]))
+        for lo, _ in mine[1:]:  # a cut lies inside an N gap of >= 1000 bases
+            s = seqs[q]
+            assert s[lo - 1:lo + 1] == b"NN"
+            a = lo
+            while a > 0 and s[a - 1:a] == b"N":
+                a -= 1
+            e = lo
+            while e < L and s[e:e + 1] == b"N":
+                e += 1
+            assert e - a >= 1000
+    assert sum(1 for r in rows if r[0] == 0) >= 3  # the dominant contig was cut
+    loads = [sum(hi - lo for _, lo, hi in sh) for sh in psh]
+    assert max(loads) / (sum(lens) / 3) < 1.15
+    for sh in psh:
+        assert sh == sorted(sh)
     ids = [[q for q, _, _ in sh] for sh in psh]
     offs = [[lo for _, lo, _ in sh] for sh in psh]
     piece_seqs = [[seqs[q][lo:hi] for q, lo, hi in sh] for sh in psh]
@@ -176,3 +214,22 @@ def test_pieces_cut_in_n_gaps_equal_whole(oracle):
                                      offsets=offs)
     assert np.array_equal(tpos, tfull["pos"])
     assert np.array_equal(tscore.view(np.uint64), tfull["score"].view(np.uint64))
+
+
+def test_shard_plan_grch38_balance():
+    """The planner on GRCh38-shaped contig lengths with 10 kb N gaps every
+    ~5 Mbp (lengths scaled 1/100): whole contigs at 2 shards, gap cuts that
+    bring the 8-shard maximum to within 1 % of the mean."""
+    from kmer_spans_amd import dist, genome
+    lens = [L // 100 for L in genome.GRCH38]
+    seqs = []
+    for L in lens:
+        b = np.full(L, ord("A"), np.uint8)
+        for a in range(20000, L - 20000, 50000):
+            b[a:a + 1000] = ord("N")
+        seqs.append(b)
+    for n, tol in ((2, 1.005), (4, 1.01), (8, 1.01)):
+        psh = dist.shard_pieces(seqs, n)
+        loads = [sum(hi - lo for _, lo, hi in sh) for sh in psh]
+        assert sum(loads) == sum(lens)
+        assert max(loads) / (sum(lens) / n) < tol, (n, max(loads) / (sum(lens) / n))

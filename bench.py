@@ -560,7 +560,7 @@ def main():
         roofline["traffic_note"] = why
     # the bound that applies to a gather pass: random requests (every table
     # read is one 64-B request whatever its width; the chip's measured ceiling
-    # for such requests from 32-128 GiB tables is ~48-50 G/s, tools/line_bench.hip)
+    # for such requests from 32-128 GiB tables is ~48-50 G/s, tools/probes/line_bench.hip)
     # (not for the LDS-staged small-k passes: they make no random HBM reads)
     if stats[-1]["scan_algo"] == 1 and not kernel.startswith("k_pass1_lds"):
         J = max(1, int(table.positions_per_read))

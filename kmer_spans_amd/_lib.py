@@ -14,7 +14,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # KS_LIB_PATH: an alternative build of the same library (kernel-variant
-# experiments, tools/p1_variants.sh); the in-tree build is the default.
+# experiments); the in-tree build is the default.
 LIB_PATH = os.environ.get("KS_LIB_PATH") or os.path.join(_HERE, "libkmerspans.so")
 
 KS_OK = 0

@@ -149,7 +149,7 @@ void debug_poison(void *p, size_t n) {
 
 void debug_poison_workspace(ks_ctx *ctx) {
   if (debug_poison_byte() < 0 || !ctx) return;
-  for (ks_ctx *c : {ctx, ctx->sub, ctx->part})
+  for (ks_ctx *c : {ctx, ctx->sub})
     if (c)
       for (auto &b : c->slots) debug_poison(b.ptr, b.bytes);
 }
@@ -335,10 +335,6 @@ extern "C" void ks_ctx_destroy(ks_ctx *c) {
     ks_ctx_destroy(c->sub);
     c->sub = nullptr;
   }
-  if (c->part) {
-    ks_ctx_destroy(c->part);
-    c->part = nullptr;
-  }
   (void)hipSetDevice(c->device);
   // every stream drains before anything it may still use is freed
   for (hipStream_t x : {c->stream, c->side, c->hi})
@@ -362,17 +358,12 @@ ks_status ctx_sub(ks_ctx *ctx, ks_ctx **sub) {
   return KS_OK;
 }
 
-ks_status ctx_part(ks_ctx *ctx, ks_ctx **part) {
-  if (!ctx->part) KS_TRY(ks_ctx_create(ctx->device, &ctx->part));
-  *part = ctx->part;
-  return KS_OK;
-}
 
 // Memory policy of the host-buffer entry points (ks_set_host_cache): 0 returns
 // a call's device memory when it ends, 1 keeps it, 2 (the default) keeps it
 // while calls keep coming and returns it once the context has been idle for
 // g_idle_ms (a janitor thread).  Fresh VRAM is slow to get: the driver clears
-// it (tools/alloc_probe.py: 4-6 s for 128 GiB), so a default of "return at
+// it (tools/probes/alloc_probe.py: 4-6 s for 128 GiB), so a default of "return at
 // once" made every host call pay its workspace and table buffer again.
 static std::atomic<int> g_host_cache{-1};    // -1: KS_HOST_CACHE decides on first use
 static std::atomic<double> g_idle_ms{-1.0};  // -1: KS_HOST_CACHE_SECONDS (default 20 s)
@@ -420,7 +411,6 @@ static void free_workspace(ks_ctx *c) {
 static void release_ctx_memory(ks_ctx *c) {
   free_workspace(c);
   if (c->sub) free_workspace(c->sub);
-  if (c->part) free_workspace(c->part);
   pool_release_device(c->device);
 }
 

@@ -112,11 +112,6 @@ struct ks_ctx {
   hipStream_t side = nullptr;  // forked work that overlaps the main stream (joined by events; lowest priority)
   hipStream_t hi = nullptr;    // highest-priority stream: the first half's pass 1 (ks_scan_chunked.hip)
   ks_ctx *sub = nullptr;       // second context of the same device (host entries' table / count / output copies)
-  ks_ctx *part = nullptr;      // third context: the later part of a staggered two-part scan (scan_impl)
-  // called once by scan_chunked right after it has queued pass 1 (ev[8] marks
-  // the end of the pre-pass-1 work): the staggered scan starts its later part
-  std::function<void()> on_pass1;
-  bool no_split = false;  // scan_chunked runs its runs as one part (the staggered scan's parts, one stream each)
   unsigned long long hreg[64] = {};  // region counters per segment read back with the chunked scan's counters
   bool hreg_ok = false;              // (kSegs entries, valid until the next scan attempt)
   int64_t rescan_segcap = 0;  // grow-only rescan capacity per segment (tr_lr rescans outnumber regions)
@@ -257,7 +252,6 @@ ks_status ctx_busy();  // the KS_ERR_ARG of a context used by another thread
   if (ks_use_.busy) return ks::ctx_busy();   \
   KS_TRY(activate(ctx))
 ks_status ctx_sub(ks_ctx *ctx, ks_ctx **sub);  // ctx->sub, created on first use
-ks_status ctx_part(ks_ctx *ctx, ks_ctx **part);  // ctx->part, created on first use
 void pool_release_device(int dev);             // free the device's pooled expanded-table buffer
 // End of a host-buffer entry point: unless ks_set_host_cache(1), the call's
 // device memory (ctx's and its sub-context's workspace, the pooled table

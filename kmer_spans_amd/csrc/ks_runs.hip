@@ -39,14 +39,7 @@ __device__ __forceinline__ uint32_t enc_pack4(uint32_t w) {
 __device__ __forceinline__ uint32_t enc_pack4m(uint32_t w) {
   return (((w >> 1) & 0x03030303u) * 0x40100401u) >> 24;
 }
-// n_mask4 with one multiply: the zero-byte flags at bits 0, 8, 16, 24 (after
-// >> 7) land at bits 28..31; the cross terms are distinct bits below 24.
-__device__ __forceinline__ uint32_t n_mask4m(uint32_t w) {
-  const uint32_t x = (w | 0x20202020u) ^ 0x6e6e6e6eu;
-  const uint32_t z = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
-  return ((z >> 7) * 0x10204080u) >> 28;
-}
-// 0x80 in each N / n byte of w (n_mask4m before the bit gather)
+// 0x80 in each N / n byte of w
 __device__ __forceinline__ uint32_t n_flags4(uint32_t w) {
   const uint32_t x = (w | 0x20202020u) ^ 0x6e6e6e6eu;
   return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;

@@ -317,20 +317,13 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
   } else if (J >= 2 && J <= 4) {
     // FP64 line and expanded tables (weighted rank): wider batches, 24 / 30 /
     // 32 indices per round trip (k = 15 rescans 5.17 -> 3.19 ms in-process,
-    // 16 reads 3.44; profiles/r5/ab/ab_lane_gw.txt).  KS_LANE_GW: the reads
-    // per batch (A/B; 0: the default batch)
-    const char *gwe = getenv("KS_LANE_GW");
-    const int gw = gwe ? atoi(gwe) : (J == 2 ? 12 : J == 3 ? 10 : 8);
+    // 16 reads 3.44; profiles/r5/ab/ab_lane_gw.txt)
 #define KS_LANE_W(J, W)                                                                                           \
   hipLaunchKernelGGL((k_scan_lane<J, false, W>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, sq, seq, \
                      total, ra, rb, rs, n, k, tv, mw, min_score, visits, out, d_cnt, segcap, packed)
-    if (J == 2 && gw >= 16) KS_LANE_W(2, 16);
-    else if (J == 2 && gw >= 12) KS_LANE_W(2, 12);
-    else if (J == 2) KS_LANE(2, false);
-    else if (J == 3 && gw >= 10) KS_LANE_W(3, 10);
-    else if (J == 3) KS_LANE(3, false);
-    else if (gw >= 8) KS_LANE_W(4, 8);
-    else KS_LANE(4, false);
+    if (J == 2) KS_LANE_W(2, 12);
+    else if (J == 3) KS_LANE_W(3, 10);
+    else KS_LANE_W(4, 8);
 #undef KS_LANE_W
   } else {
     if (J == 5) KS_LANE(5, false); else if (J == 4) KS_LANE(4, false); else if (J == 3) KS_LANE(3, false); else if (J == 2) KS_LANE(2, false); else KS_LANE(1, false);
@@ -340,19 +333,9 @@ ks_status launch_scan_lane(ks_ctx *ctx, const uint8_t *seq, int64_t total, const
   return KS_OK;
 }
 
-// One part of a staggered two-part scan (scan_impl): positions [p_lo, p_hi),
-// sequences [q_lo, q_hi).  A part never takes the lane kernel (it returns
-// KS_INTERNAL_PART_ABORT and scan_impl redoes the call in one part) and
-// counts no visits.
-struct ScanPart {
-  int64_t p_lo = 0, p_hi = 0;
-  int32_t q_lo = 0, q_hi = 0;
-};
-constexpr ks_status KS_INTERNAL_PART_ABORT = static_cast<ks_status>(101);
-
 static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, const ks_table *t,
                            int32_t min_width, double min_score, int32_t *visits_dev, ks_regions *out,
-                           ks_scan_stats *stats, const ScanMode &mode, const ScanPart *part = nullptr) {
+                           ks_scan_stats *stats, const ScanMode &mode) {
   hipStream_t st = ctx->stream;
   ks_scan_stats local{};
   ks_scan_stats *S = stats ? stats : &local;
@@ -360,15 +343,14 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
   KS_HIP(hipEventRecord(ctx->ev[2], st));
   Runs runs;
   // (no timing sync here: the run phase's events are read after the call's last sync)
-  KS_TRY(find_runs(ctx, s, total, &runs, nullptr, /*want_packed=*/true, part ? part->p_lo : 0,
-                   part ? part->p_hi : -1));
+  KS_TRY(find_runs(ctx, s, total, &runs, nullptr, /*want_packed=*/true));
   // chunk layout, statistics and algorithm choice (device-side, one sync)
   RunLayout lay;
   if (runs.n) KS_TRY(run_layout(ctx, runs, k, &lay, mode.trlr, s->offsets_dev));
   const int64_t longest = lay.longest, scored = lay.scored;
   S->n_scored = scored;
   S->n_runs = lay.nscan;
-  for (int32_t q = part ? part->q_lo : 0; q < (part ? part->q_hi : s->nseq); ++q) {
+  for (int32_t q = 0; q < s->nseq; ++q) {
     const int64_t L = s->offsets_host[q + 1] - s->offsets_host[q];
     if (L >= k) S->n_bases += L;
   }
@@ -384,7 +366,6 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
   int algo = ctx->scan_algo;
   if (algo < 0) algo = (longest > (1 << 15)) ? 1 : 0;
   if (mode.trlr && !(mode.finite && mode.maxabs * (double)(longest + 2) < 1e300)) algo = 0;  // literal NaN rules
-  if (part && algo != 1) return KS_INTERNAL_PART_ABORT;
   S->scan_algo = algo;
 
   // region capacity: what the (grow-only) slot already holds, so that the
@@ -475,8 +456,6 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
                              vis, vscr, n);
           KS_HIP(hipGetLastError());
         }
-      } else if (rc == KS_ERR_INTERNAL && part) {
-        return KS_INTERNAL_PART_ABORT;  // scan_impl redoes the whole call in one part
       } else if (rc == KS_ERR_INTERNAL) {
         fprintf(stderr, "kmer_spans_amd: chunked scan fell back to the lane kernel: %s\n", ks_last_error());
         ctx->hreg_ok = false;  // the lane kernel recounts the regions
@@ -587,168 +566,21 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
 }
 
 
-// Staggered two-part scan.  The input is cut at the sequence boundary nearest
-// a fraction f of its bases (KS_PARTS_FRAC; default 0 = one part).  The
-// first part [0, m) runs here; the second [m, nseq) on the part context from
-// a second host thread, which starts only once the first part has queued its
-// pass 1 and whose stream waits for the first part's pre-pass-1 work (ev[8]):
-// the first part's run segmentation, layout and predictor (the critical path
-// before any gather) cover only its own bases, and the second part's run
-// through its host round trips under the first part's request-bound pass 1.
-// The first part's post-processing then runs under the second part's pass 1.
-// Runs never cross a sequence, so the parts are independent and their region
-// lists (each in (seq, beg) order) concatenate.  Returns KS_INTERNAL_PART_ABORT
-// when the call should take the one-part path (a part that needs the lane
-// kernel, or an input that does not cut well).
-static ks_status scan_parts(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, const ks_table *t,
-                            int32_t min_width, double min_score, ks_regions *out, ks_scan_stats *stats,
-                            const ScanMode &mode) {
-  // (read per call: in-process A/B runs switch them)
-  const double frac = getenv("KS_PARTS_FRAC") ? atof(getenv("KS_PARTS_FRAC")) : 0.0;  // (opt-in: DESIGN.md §6)
-  const int64_t min_total = getenv("KS_PARTS_MIN") ? atoll(getenv("KS_PARTS_MIN")) : ((int64_t)1 << 28);
-  if (!(frac > 0.0 && frac < 1.0) || mode.trlr || ctx->scan_algo == 0 || total < min_total || s->nseq < 2)
-    return KS_INTERNAL_PART_ABORT;
-  int32_t m = -1;
-  int64_t best = INT64_MAX;
-  for (int32_t q = 1; q < s->nseq; ++q) {
-    const int64_t d = std::llabs(s->offsets_host[q] - (int64_t)(frac * (double)total));
-    if (d < best) {
-      best = d;
-      m = q;
-    }
-  }
-  const double got = m > 0 ? (double)s->offsets_host[m] / (double)total : 0.0;
-  if (m <= 0 || got < 0.15 || got > 0.85) return KS_INTERNAL_PART_ABORT;
-  ks_ctx *pc = nullptr;
-  KS_TRY(ctx_part(ctx, &pc));
-  pc->scan_algo = ctx->scan_algo;
-  const double t0 = now_ms();
-  ScanPart pa, pb;
-  pa.p_lo = 0;
-  pa.p_hi = s->offsets_host[m];
-  pa.q_lo = 0;
-  pa.q_hi = m;
-  pb.p_lo = s->offsets_host[m];
-  pb.p_hi = total;
-  pb.q_lo = m;
-  pb.q_hi = s->nseq;
-  // the go signal: the first part has queued its pass 1 (with_event: wait for
-  // its ev[8]), or ended without one
-  std::mutex mu;
-  std::condition_variable cv;
-  bool fired = false, with_event = false;
-  auto fire = [&](bool ev) {
-    {
-      std::lock_guard<std::mutex> g(mu);
-      if (fired) return;
-      fired = true;
-      with_event = ev;
-    }
-    cv.notify_all();
-  };
-  ctx->on_pass1 = [&] { fire(true); };
-  // each part on one stream (its halves not split) unless KS_PARTS_HALVES=1:
-  // the device has 4 hardware queues per process, and streams sharing one
-  // serialise against each other
-  const bool halves = getenv("KS_PARTS_HALVES") && atoi(getenv("KS_PARTS_HALVES")) != 0;
-  struct NoSplit {
-    ks_ctx *a, *b;
-    bool on;
-    NoSplit(ks_ctx *x, ks_ctx *y, bool o) : a(x), b(y), on(o) { a->no_split = b->no_split = on; }
-    ~NoSplit() { a->no_split = b->no_split = false; }
-  } no_split(ctx, pc, !halves);
-  // the part context's stream starts after the caller's work on ctx->stream
-  KS_HIP(hipEventRecord(ctx->ev[19], ctx->stream));
-  KS_HIP(hipStreamWaitEvent(pc->stream, ctx->ev[19], 0));
-  ks_regions ra{}, rb{};
-  ks_scan_stats sa{}, sb{};
-  ks_status rc_b = KS_OK;
-  std::string err_b;
-  std::thread th([&] {
-    {
-      std::unique_lock<std::mutex> g(mu);
-      cv.wait(g, [&] { return fired; });
-    }
-    rc_b = activate(pc);
-    if (rc_b == KS_OK && with_event && hipStreamWaitEvent(pc->stream, ctx->ev[8], 0) != hipSuccess)
-      rc_b = fail(KS_ERR_DEVICE, "part ordering failed");
-    if (rc_b == KS_OK) rc_b = scan_core(pc, s, total, k, t, min_width, min_score, nullptr, &rb, &sb, mode, &pb);
-    if (rc_b != KS_OK) err_b = ks_last_error();  // (thread-local)
-  });
-  const ks_status rc_a = scan_core(ctx, s, total, k, t, min_width, min_score, nullptr, &ra, &sa, mode, &pa);
-  ctx->on_pass1 = nullptr;
-  fire(false);  // (the first part queued no pass 1)
-  th.join();
-  if (rc_a != KS_OK || rc_b != KS_OK) {
-    if (rc_a == KS_OK) ks_regions_free(&ra);
-    if (rc_b == KS_OK) ks_regions_free(&rb);
-    const bool abort = (rc_a == KS_OK || rc_a == KS_INTERNAL_PART_ABORT) &&
-                       (rc_b == KS_OK || rc_b == KS_INTERNAL_PART_ABORT);
-    if (abort) {
-      KS_HIP(hipStreamSynchronize(pc->stream));
-      return KS_INTERNAL_PART_ABORT;
-    }
-    if (rc_a == KS_OK || rc_a == KS_INTERNAL_PART_ABORT) {
-      set_error("%s", err_b.c_str());
-      return rc_b;
-    }
-    return rc_a;
-  }
-  // one output block (regions_alloc): the parts' regions in order
-  const int64_t n = ra.n + rb.n;
-  ks_status rc = regions_alloc(out, n);
-  if (rc == KS_OK) {
-    int64_t o = 0;
-    for (const ks_regions *r : {&ra, &rb}) {
-      if (r->n > 0) {
-        memcpy(out->seq_id + o, r->seq_id, (size_t)r->n * 4);
-        memcpy(out->beg + o, r->beg, (size_t)r->n * 4);
-        memcpy(out->end + o, r->end, (size_t)r->n * 4);
-        memcpy(out->score + o, r->score, (size_t)r->n * 8);
-      }
-      o += r->n;
-    }
-    if (n > 0) memset(out->score + n, 0, (size_t)n * 8);  // second row of `score`
-  }
-  ks_regions_free(&ra);
-  ks_regions_free(&rb);
-  if (rc != KS_OK) return rc;
-  if (stats) {
-    *stats = sa;  // phase timings: the first part's (its own streams)
-    stats->n_bases += sb.n_bases;
-    stats->n_scored += sb.n_scored;
-    stats->n_runs += sb.n_runs;
-    stats->n_regions = n;
-    stats->n_rescan += sb.n_rescan;
-    stats->n_replay += sb.n_replay;
-    // the gather pass of the call: from the first part's start of pass 1 to
-    // the later end of the two (hipEvents on both contexts' streams)
-    float a9 = 0, b9 = 0;
-    KS_HIP(hipEventElapsedTime(&a9, ctx->ev[8], ctx->ev[9]));
-    KS_HIP(hipEventElapsedTime(&b9, ctx->ev[8], pc->ev[9]));
-    stats->ms_scan = std::max(a9, b9);
-    stats->ms_total = now_ms() - t0;
-  }
-  return KS_OK;
-}
-
 // Scan of one call.  With the visit histogram on the chunked path, the
-// top-level count runs concurrently on the sub-context (below); without it,
-// a large multi-sequence input takes the staggered two-part scan.
+// top-level count runs concurrently on the sub-context (below).  (The
+// staggered two-part scan of round 4 -- the input cut at a sequence boundary,
+// the later part on a context of its own -- measured no gain and is gone:
+// DESIGN.md section 6.)
 ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, const ks_table *t,
                     int32_t min_width, double min_score, int32_t *visits_dev, ks_regions *out,
                     ks_scan_stats *stats, const ScanMode &mode) {
-  if (!visits_dev) {
-    const ks_status rc = scan_parts(ctx, s, total, k, t, min_width, min_score, out, stats, mode);
-    if (rc != KS_INTERNAL_PART_ABORT) return rc;
-  }
   {
     // Visits of the one-part chunked scan: the top-level count (the k-mer
     // histogram, ~24 ms at k = 13, streaming + LDS work) runs on the
     // sub-context's stream from a second host thread while the scan's gather
     // pass (random requests) runs here; the count lands in the sub-context's
-    // histogram and is added once both are done.  KS_VISITS_SERIAL: the
-    // count after the scan on this stream (A/B).
+    // histogram and is added once both are done (the count after the scan on
+    // this stream: 42.2 vs 37.3 ms in round 2, retired).
     // Only when the chunked path is certain or likely: forced, or some
     // sequence longer than the lane kernel's limit (a run longer than 2^15
     // needs one); otherwise the lane kernel counts its own visits and a
@@ -758,7 +590,7 @@ ks_status scan_impl(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int k, con
       longest_seq = std::max<int64_t>(longest_seq, s->offsets_host[q + 1] - s->offsets_host[q]);
     const bool chunked_likely = ctx->scan_algo == 1 || (ctx->scan_algo < 0 && longest_seq > (1 << 15));
     const bool vis_conc = visits_dev && !mode.trlr && !mode.visits_counted && chunked_likely && total > 0 &&
-                          getenv("KS_VISITS_ATOMIC") == nullptr && getenv("KS_VISITS_SERIAL") == nullptr;
+                          getenv("KS_VISITS_ATOMIC") == nullptr;
     if (!vis_conc) return scan_core(ctx, s, total, k, t, min_width, min_score, visits_dev, out, stats, mode);
     ks_ctx *vsub = nullptr;
     KS_TRY(ctx_sub(ctx, &vsub));

@@ -138,7 +138,6 @@ struct Carry {  // P3/P4
   int32_t *hq;    // first clamp in the chunk (relative), -1 none
   double *hmax;   // max of the carried head (valid if the head is non-empty)
   int32_t *harg;
-  int bulk;       // carry_segment: runs of clean / clamp chunks in one wave step (A/B: KS_NO_BULK_CLEAN)
 };
 
 // Composites of the global 64-chunk tiles (chunks [64t, 64t + 64)) for the
@@ -1260,7 +1259,7 @@ __global__ void __launch_bounds__(kP1Block) k_pass1p(Chunks g, const uint8_t *__
 // Lines are fetched cooperatively: four lanes load the four 16-B pieces of
 // one lane's line (global_load_lds_dwordx4: a wave instruction touches 16
 // whole lines; random 64-B lines come at ~50 G/s from a 64-128 GiB table,
-// against 25-38 G/s when each lane loads its own entry, tools/line_bench*.hip,
+// against 25-38 G/s when each lane loads its own entry, tools/probes/line_bench*.hip,
 // profiles/r3/line_bench*.txt), straight into a two-slot LDS ring per wave:
 // the lines land in lane order (lane L's line at L x 64 B), and the next
 // step's lines are in flight while a step is processed.  The loads are inline
@@ -3071,7 +3070,7 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
       // chunk takes the serial step.  (Weighted rank at config 3: 11 M of
       // 12 M chunks are clean or clamp; in-process k = 15 44.2 vs 44.9 ms,
       // k = 13 30.1 vs 30.6, metric unchanged: profiles/r5/ab/ab_bulk_clean_*.txt)
-      if (cr.bulk) {
+      {
         const double pe = __longlong_as_double(wave_prev_i64(__double_as_longlong(l_exit)));
         const double ent = lane == j ? x : pe;
         const bool in = live && lane >= j;
@@ -4035,7 +4034,6 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   int32_t *hqp = reinterpret_cast<int32_t *>(W + o_hq);
   Carry cr{reinterpret_cast<double *>(W + o_x), reinterpret_cast<uint8_t *>(W + o_mode), hqp,
            reinterpret_cast<double *>(W + o_hmax), hqp + nch};
-  cr.bulk = getenv("KS_NO_BULK_CLEAN") == nullptr;
   unsigned long long *cnts = reinterpret_cast<unsigned long long *>(W + o_cnt);
   uint8_t *d_flag = reinterpret_cast<uint8_t *>(W + o_flag);
   auto xtiles = [&](char *p) {
@@ -4197,7 +4195,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // Two halves of the runs (pass-1-summary path): the second half's pass 1
   // (side stream) runs while the first half's latency-bound later passes
   // (carry, stitch) run on the main stream; halves split at a run boundary,
-  // so no carry or stitch crosses it.  KS_NO_SPLIT: one half.
+  // so no carry or stitch crosses it.
   struct Half {
     int64_t c0, c1, r0, r1, t0, t1;
   };
@@ -4214,13 +4212,13 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // (below ~2 M chunks, ~500 Mbp, one part: at the 8-way shard, 1.5 M chunks,
   // 2.38 vs 2.42 ms in-process; 4-way, 3 M chunks, two parts 4.24 vs 4.37;
   // profiles/r5/ab/ab_one_part_*.txt.  KS_SPLIT_MIN_CHUNKS: the threshold --
-  // tests set 0 to run the two-part path on small genomes; KS_NO_SPLIT: one part)
+  // tests set 0 to run the two-part path on small genomes)
   const char *smin = getenv("KS_SPLIT_MIN_CHUNKS");
   const int64_t split_min = smin ? atoll(smin) : ((int64_t)2 << 20);
   // (FP64 expanded tables without summaries stay in one part: two measured
   // 52.1 vs 51.6 ms at k = 15, 46.0 vs 44.8 at k = 14,
   // profiles/r5/ab/ab_nosumm_split_k15.txt, ab_nosumm_k14.txt)
-  const bool split = !ctx->no_split && getenv("KS_NO_SPLIT") == nullptr && p1summ &&
+  const bool split = p1summ &&
                      nch > split_min && lay.split_r > 0 && lay.split_r < nruns &&
                      lay.split_c >= 1024 && lay.split_c + 1024 <= ctail_all;
   Half halves[2];
@@ -4529,11 +4527,6 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
   // than pass 1 stamped -- what it would see reading an earlier call's
   // pass-1 results -- so the epoch guard must fail the call
   if (getenv("KS_TEST_EPOCH_STALE")) ++p1.epoch;
-  if (ctx->on_pass1) {  // a staggered scan's later part starts now (scan_impl)
-    auto go = std::move(ctx->on_pass1);
-    ctx->on_pass1 = nullptr;
-    go();
-  }
 
   // P2-P5 (without the candidates) of one half on stream strm, with its own
   // replay counter, error bits and fix list; ev[14] / ev[15] mark the last
@@ -4623,35 +4616,26 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       hipLaunchKernelGGL(k_tile_apply, dim3(gtc), dim3(256), 0, strm, gv, sm, tch, cr, err_h, 0);
       KS_HIP(hipGetLastError());
     }
-    // FP64 tables: the R chunks' heads packed densely (k_heads_dense; A/B:
-    // KS_HEADS_SPARSE=1)
-    const bool dense_heads = !comp && getenv("KS_HEADS_SPARSE") == nullptr;
+    // FP64 tables: the R chunks' heads packed densely (k_heads_dense; lane per
+    // chunk, k_heads, measured slower at config 3: 29.9 vs 29.2 ms,
+    // profiles/r5/ab/ab_heads_dense_lane_pf_*.txt); compressed tables: k_heads
+    const bool dense_heads = !comp;
     auto heads = [&](int gated) {
       // (gated: a small grid-stride grid; it exits at once unless the carry fell back)
       const unsigned gd = (unsigned)((nh + 4 * kHeadSpan - 1) / (4 * kHeadSpan));
       const unsigned gh = gated ? std::min<unsigned>(dense_heads ? gd : gch_h, (unsigned)ctx->num_cus * 2)
                                 : (dense_heads ? gd : gch_h);
-#define KS_HEADS(J, C)                                                                                           \
-  hipLaunchKernelGGL((k_heads<J, C>), dim3(gh), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes, cr, err_h, \
-                     gated)
 #define KS_HEADS_D(J, W)                                                                                          \
   hipLaunchKernelGGL((k_heads_dense<J, false, W>), dim3(gh), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes, \
                      cr, err_h, gated)
-      if (comp) KS_HEADS(1, true);
-      else if (dense_heads) {
-        if (J == 4 && tv.line) KS_HEADS_D(4, true);
-        else if (J == 4) KS_HEADS_D(4, false);
-        else if (J == 3) KS_HEADS_D(3, false);
-        else if (J == 2) KS_HEADS_D(2, false);
-        else KS_HEADS_D(1, false);
-      } else if (J == 4 && tv.line)
-        hipLaunchKernelGGL((k_heads<4, false, true>), dim3(gh), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes,
-                           cr, err_h, gated);
-      else if (J == 4) KS_HEADS(4, false);
-      else if (J == 3) KS_HEADS(3, false);
-      else if (J == 2) KS_HEADS(2, false);
-      else KS_HEADS(1, false);
-#undef KS_HEADS
+      if (comp) {
+        hipLaunchKernelGGL((k_heads<1, true>), dim3(gh), dim3(256), 0, strm, gv, s->seq, total, k, tv, codes, cr,
+                           err_h, gated);
+      } else if (J == 4 && tv.line) KS_HEADS_D(4, true);
+      else if (J == 4) KS_HEADS_D(4, false);
+      else if (J == 3) KS_HEADS_D(3, false);
+      else if (J == 2) KS_HEADS_D(2, false);
+      else KS_HEADS_D(1, false);
 #undef KS_HEADS_D
     };
     heads(0);

@@ -444,7 +444,7 @@ __global__ void k_build_approx(const uint16_t *__restrict__ codes, const double 
 // sum stays within kPoolPairMax (two tables alive at once, e.g. genome g + 1's
 // table built while genome g is scanned).  A fresh hipMalloc of 32-128 GiB
 // takes 0.3 ms to 6 s on the box (the driver clears new VRAM;
-// tools/alloc_probe.py), while a buffer freed by this process is handed back
+// tools/probes/alloc_probe.py), while a buffer freed by this process is handed back
 // at once; tables built per call (one table per genome) would pay that on
 // every table.  A destroyed table's buffer is kept here and reused by the
 // next expansion that fits in it; ks_release_cache() returns them to the
@@ -515,7 +515,7 @@ void pool_give(int dev, void *p, size_t bytes) {
 // Expanded-table allocation: physically contiguous VRAM when the driver has
 // it (hipDeviceMallocContiguous), else a plain hipMalloc.  Random 16-byte
 // gathers over 128 GiB run at 49.3-50.6 G/s from a contiguous buffer and
-// 47.5-48.7 G/s from a plain one on the same box (tools/frag_probe.hip,
+// 47.5-48.7 G/s from a plain one on the same box (tools/probes/frag_probe.hip,
 // profiles/r2/frag_probe.txt): fewer, larger translation fragments.
 static hipError_t ext_malloc(void **p, size_t bytes) {
   static const bool dbg = getenv("KS_DEBUG_ALLOC") != nullptr;

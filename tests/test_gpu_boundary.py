@@ -192,7 +192,7 @@ def test_free_waits_for_the_other_streams(oracle, capfd, main_only):
     the all-stream drain (the fix) the drain lasts the spin; with the round-4
     drain of the main stream only (KS_DEBUG_DRAIN_MAIN_ONLY) the call's
     results are exact too, and the report says whether hipFree itself waited
-    (tools/free_order_probe.py records both for DESIGN.md)."""
+    (tools/probes/free_order_probe.py records both for DESIGN.md)."""
     import kmer_spans_amd as K
     from kmer_spans_amd import _lib
     L = _lib.load()

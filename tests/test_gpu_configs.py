@@ -254,11 +254,11 @@ def test_count_hot_buckets(oracle, k):
 def test_carry_and_rescan_forms(oracle, monkeypatch, score, k):
     """The round-5 carry / heads / rescan forms and their A/B alternatives on
     one multi-contig genome (k = 11 rank, k = 9 log2), each against the oracle (regions,
-    FP64 scores bit for bit, visits): clean / certain-clamp runs in one wave
-    step or one chunk at a time (KS_NO_BULK_CLEAN), the certain-clamp heads
-    packed densely or lane per chunk (KS_HEADS_SPARSE), wide or default
-    rescan batches (KS_LANE_GW=0), no summaries for any table
-    (KS_NO_SUMMARIES), FP64 tables with k_summaries (KS_F64_P1SUMM=0).
+    FP64 scores bit for bit, visits): the default forms (clean / certain-clamp
+    runs in one wave step, certain-clamp heads packed densely, wide rescan
+    batches), no summaries for any table (KS_NO_SUMMARIES), the two-part path
+    on a small genome (KS_SPLIT_MIN_CHUNKS=0), FP64 tables with k_summaries
+    (KS_F64_P1SUMM=0).
     (kmer_spans.c:261-306, 298-305: the carried state, the restart.)"""
     import torch
     from kmer_spans_amd import _lib, device as D, genome
@@ -277,8 +277,7 @@ def test_carry_and_rescan_forms(oracle, monkeypatch, score, k):
     o = oracle.scan(host, k, w.cpu().numpy(), thr, mw, ms, visits=True)
     assert o["pos"].shape[1] > 0
     ctx.set_scan_algo(1)
-    forms = [{}, {"KS_NO_BULK_CLEAN": "1"}, {"KS_HEADS_SPARSE": "1"}, {"KS_LANE_GW": "0"},
-             {"KS_NO_SUMMARIES": "1"}, {"KS_SPLIT_MIN_CHUNKS": "0"}]
+    forms = [{}, {"KS_NO_SUMMARIES": "1"}, {"KS_SPLIT_MIN_CHUNKS": "0"}]
     if score == "rank":
         forms.append({"KS_F64_P1SUMM": "0"})
     try:

@@ -270,11 +270,11 @@ def test_human_like_device_path(K, oracle, ctx, k, score):
     D.bind_torch_stream(ctx)
 
 
-@pytest.mark.parametrize("mode", ["concurrent", "KS_VISITS_SERIAL", "KS_VISITS_ATOMIC"])
+@pytest.mark.parametrize("mode", ["concurrent", "KS_VISITS_ATOMIC"])
 def test_visit_histogram_modes(K, oracle, ctx, monkeypatch, mode):
     """The visit histogram of kmer_regions_r (kmer_spans.c:266-267) by each
     route: the top-level count on the sub-context concurrently with the scan
-    (default), the count after the scan, one atomic per scanned index -- all
+    (default), one atomic per scanned index -- both
     equal to the oracle's, with the same regions; twice in a row (the
     sub-context's workspace is reused)."""
     import torch

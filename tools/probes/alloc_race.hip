@@ -12,8 +12,8 @@
 // The buffers are freed at the end of the round, as the host entry points
 // free their workspace at the end of each call.
 //
-// Build: hipcc -O2 --offload-arch=gfx950 tools/alloc_race.hip -o tools/alloc_race
-// Run:   tools/alloc_race [rounds] [bufs_per_round] [big_gib] [child_gib]
+// Build: hipcc -O2 --offload-arch=gfx950 tools/probes/alloc_race.hip -o tools/probes/alloc_race
+// Run:   tools/probes/alloc_race [rounds] [bufs_per_round] [big_gib] [child_gib]
 // child_gib > 0: before each round a separate process (this binary, "child
 // G") allocates and writes G GiB and exits, so the round's buffers may land
 // on VRAM another process just freed (which the driver must clear first).

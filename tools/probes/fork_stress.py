@@ -7,7 +7,7 @@ random host-entry corpus of tests/test_gpu_parity.py (scan algorithm 1)
 against the oracle: before any fork, while a forked child of this process is
 alive (it sleeps), and after it exited.  Mismatches are printed per phase.
 
-  python tools/fork_stress.py [linger_seconds]
+  python tools/probes/fork_stress.py [linger_seconds]
 """
 import os
 import random

@@ -10,7 +10,7 @@ spin in the second case, hipFree orders the free after every stream's work
 by itself and the round-4 "recycling edge" could not have let a kernel read
 a freed-and-recycled buffer.  Results to JSON (one object per variant).
 
-    python tools/free_order_probe.py --out gpurun_out/free_order.json
+    python tools/probes/free_order_probe.py --out gpurun_out/free_order.json
 """
 import argparse
 import json

@@ -3,7 +3,7 @@
 // every lane owns a sequence of random lines; a wave fetches its 64 lanes'
 // lines cooperatively (L/16 lanes per line, one 16-B piece each: a wave
 // instruction touches 64/(L/16) lines, the shape that reaches ~50 G lines/s,
-// tools/line_bench.hip), and each owner then reads 3 x 8 B of its own line.
+// tools/probes/line_bench.hip), and each owner then reads 3 x 8 B of its own line.
 //   glds : global_load_lds_dwordx4 straight into an LDS ring of NB batches
 //          (lines land in owner order: no transpose), owner reads from LDS
 //   reg  : global_load_dwordx4 into VGPRs, ds_write_b128 into LDS, owner reads

@@ -1,7 +1,7 @@
 // Host <-> device transfer rates on the GPU box (what bounds the host entry
 // points' staging): pinned and pageable H2D / D2H, multi-threaded host
 // memcpy into pinned memory, and the same with the 4-bit base packing.
-// Build: hipcc -O3 -std=c++17 -mssse3 tools/pcie_bench.cpp -o tools/pcie_bench
+// Build: hipcc -O3 -std=c++17 -mssse3 tools/probes/pcie_bench.cpp -o tools/probes/pcie_bench
 #include <hip/hip_runtime.h>
 #include <tmmintrin.h>
 

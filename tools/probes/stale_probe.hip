@@ -17,8 +17,8 @@
 //           round's tag (stale), zero, or other,
 // then hipFree.  A persistent counter buffer collects the counts.
 //
-// Build: hipcc -O2 --offload-arch=gfx950 tools/stale_probe.hip -o tools/stale_probe
-// Run:   tools/stale_probe [rounds] [big_mib] [span_kib] [pre 0/1] [sizes 0/1]
+// Build: hipcc -O2 --offload-arch=gfx950 tools/probes/stale_probe.hip -o tools/probes/stale_probe
+// Run:   tools/probes/stale_probe [rounds] [big_mib] [span_kib] [pre 0/1] [sizes 0/1]
 // sizes 1: alternate two allocation sizes (a slot that grows and shrinks);
 // sizes 2: a host call's pattern -- 16 buffers a round, sizes drawn from
 // 4 KiB .. big in a random order (addresses and pages shuffle between

@@ -64,6 +64,13 @@ def algo_bytes_per_base(kernel: str) -> float:
     kernel: 1 B when the table lives in LDS (k <= 7, k_pass1_lds), else 9 B."""
     return ALGO_BYTES_PER_BASE_LDS if kernel.startswith("k_pass1_lds") else ALGO_BYTES_PER_BASE
 RANDOM_WALL_GPS = 50.0         # measured random-request ceiling, contiguous 128 GiB table (profiles/r2/frag_probe.txt)
+# Random 128-B line reads from a 128 GiB table (the wide-line table's size):
+# 48.2 G lines/s = 6.17 TB/s of line bytes, the chip's measured ceiling for
+# this access; rocprofv3 FETCH_SIZE counts 64 B per such read (one 128-B
+# request tallied at 64 B, as the guide's gfx950 note says of wide streaming
+# reads), 64 B per 32- or 64-B line read (profiles/r6/linecal/line_rates.txt)
+LINE128_CEILING_GBS = 6170.0
+FETCH_B_PER_READ = {"k_pass1w": 128.0}   # physical bytes per FETCH_SIZE-tallied 64 B request: line bytes
 METRIC = "Gbases/sec scanned (k=13, log-ratio score) at 1/2/4/8 MI355X; spans bit-exact"
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 
@@ -199,9 +206,20 @@ def pmc_traffic(kernel_prefix, build_id, workload):
             write += cs["WRITE_SIZE"] * 1e3 * n
             names.append(name)
     if names:
-        corr = pmc.get("streaming_read_bytes_per_step", {}).get(kernel_prefix, 0.0) / 2.0
-        return {"bytes": int(round(fetch + write + corr)), "fetch": int(fetch), "write": int(write),
-                "streaming_correction": int(corr), "read_requests": int(fetch / 64.0), "kernels": names,
+        # gfx950 corrections (MI355X_MICROARCH.md HBM section; calibrated on this
+        # access pattern in profiles/r6/linecal/line_rates.txt): the packed-base
+        # stream (16-B loads) is tallied at half its bytes; each table line read
+        # is one request tallied at 64 B, which moves 128 B for a 128-B wide line
+        stream = pmc.get("streaming_read_bytes_per_step", {}).get(kernel_prefix, 0.0)
+        line_fetch = max(0.0, fetch - stream / 2.0)  # the tallied bytes of the table reads
+        per_req = FETCH_B_PER_READ.get(kernel_prefix, 64.0)
+        corrected = line_fetch / 64.0 * per_req + stream + write
+        return {"bytes": int(round(corrected)), "fetch": int(fetch), "write": int(write),
+                "streaming_read": int(stream), "table_read_requests": int(line_fetch / 64.0),
+                "bytes_per_table_request": per_req, "kernels": names,
+                "correction": "FETCH_SIZE counts 64 B per request: the packed-base stream's half is added back and "
+                              "each table read counts its line's bytes (128 B for wide lines: calibrated, "
+                              "profiles/r6/linecal/line_rates.txt)",
                 "per": "step (all launches of the kernel)"}, "ok"
     return None, "kernel not in the PMC summary"
 
@@ -575,9 +593,25 @@ def main():
               "wall_source": "profiles/r3/line_bench.txt (random 16-128-B lines from a physically contiguous "
                              "128 GiB buffer, fetched by 1-8 lanes each: 49.9-50.3 G lines/s)"}
         if traffic:
-            ra["memory_read_requests_per_launch"] = traffic["read_requests"]
-            ra["memory_requests_G_per_s"] = round(traffic["read_requests"] / (ms_kernel * 1e-3) / 1e9, 2)
+            ra["memory_read_requests_per_launch"] = traffic["table_read_requests"]
+            ra["memory_requests_G_per_s"] = round(traffic["table_read_requests"] / (ms_kernel * 1e-3) / 1e9, 2)
         roofline["random_access"] = ra
+        if kernel == "k_pass1w":
+            # the bytes the wide-line form moves: a whole 128-B line per read
+            # (6 positions of 13/11-bit codes plus the 81 continuation codes a
+            # read does not use) and the packed bases, against the chip's peak
+            # and against the measured ceiling of random 128-B line reads
+            pb = reads * 128.0 + n_bases / 4.0
+            roofline["physical"] = {
+                "bytes_per_launch": int(pb), "bytes_per_position": round(pb / n_scored, 2),
+                "achieved": round(pb / (ms_kernel * 1e-3) / 1e9, 1), "unit": "GB/s",
+                "frac_of_peak": round(pb / (ms_kernel * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "frac_of_line_ceiling": round(pb / (ms_kernel * 1e-3) / 1e9 / LINE128_CEILING_GBS, 4),
+                "line_ceiling_GB_per_s": LINE128_CEILING_GBS,
+                "note": "random 128-B line reads cannot move fewer bytes than their lines: at 6 positions per line "
+                        "the form's floor is 21.3 B per position against the 9 algorithmic bytes; the ceiling is "
+                        "tools/probes/line_bench.hip's 128-B group reads from a 128 GiB table "
+                        "(profiles/r6/linecal/line_rates.txt)"}
 
     # ---- the same step with the visit histogram kmer_regions_r returns
     # (kmer_spans.c:266-267,523-537): device-resident, count-derived top-level

@@ -88,16 +88,20 @@ void run(const char *mode, int grid) {
     else
       hipLaunchKernelGGL((k_lane<kPer, U>), dim3(grid), dim3(256), 0, 0, g_tab, lines - 1, n, g_out);
   }, 3);
-  printf("{\"mode\":\"%s\",\"line_B\":%d,\"in_flight\":%d,\"grid\":%d,\"table_GiB\":%.0f,\"G_lines_per_s\":%.2f,"
+  printf("{\"mode\":\"%s\",\"line_B\":%d,\"in_flight\":%d,\"grid\":%d,\"table_GiB\":%.3f,\"G_lines_per_s\":%.2f,"
          "\"GB_per_s\":%.0f,\"G_64B_per_s\":%.2f}\n",
          mode, 16 * kPer, U, grid, g_bytes / 1073741824.0, n / (ms * 1e6), n * 16.0 * kPer / (ms * 1e6),
          n * 16.0 * kPer / 64.0 / (ms * 1e6));
   fflush(stdout);
 }
 
+// usage: line_bench [table MiB (131072)] [group]  -- "group": the coalesced
+// group forms only (the PMC calibration of round 6 runs them under
+// rocprofv3 --pmc FETCH_SIZE: HBM bytes counted per line read)
 int main(int argc, char **argv) {
-  const size_t gib = (size_t)1 << 30;
-  g_bytes = (argc > 1 ? (size_t)atoi(argv[1]) : 128) * gib;
+  const size_t mib = (size_t)1 << 20;
+  g_bytes = (argc > 1 ? (size_t)atoll(argv[1]) : 131072) * mib;
+  const bool only_group = argc > 2 && strcmp(argv[2], "group") == 0;
   void *tab = nullptr;
   if (hipExtMallocWithFlags(&tab, g_bytes, hipDeviceMallocContiguous) != hipSuccess) {
     (void)hipGetLastError();
@@ -109,12 +113,14 @@ int main(int argc, char **argv) {
   CK(hipDeviceSynchronize());
   g_tab = (const uint4 *)tab;
   const int grid = 256 * 32;
-  run<1, 4, false>("lane", grid);
-  run<1, 8, false>("lane", grid);
-  run<2, 4, false>("lane", grid);
-  run<4, 2, false>("lane", grid);
-  run<4, 4, false>("lane", grid);
-  run<8, 2, false>("lane", grid);
+  if (!only_group) {
+    run<1, 4, false>("lane", grid);
+    run<1, 8, false>("lane", grid);
+    run<2, 4, false>("lane", grid);
+    run<4, 2, false>("lane", grid);
+    run<4, 4, false>("lane", grid);
+    run<8, 2, false>("lane", grid);
+  }
   run<2, 8, true>("group", grid);
   run<4, 4, true>("group", grid);
   run<4, 8, true>("group", grid);

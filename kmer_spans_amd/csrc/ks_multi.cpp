@@ -211,6 +211,27 @@ ks_status merge_parts(const std::vector<std::vector<Piece>> &parts, const std::v
   return KS_OK;
 }
 
+// dst[i] += src[i] (uint32 wrap-around: the reference's int counters)
+__global__ void k_add_u32(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] += src[i];
+}
+
+// Peer access between the list's distinct devices (xGMI copies of the count
+// stripes, multi_low_comp_regions); a device pair without it still copies
+// (the runtime stages through the host).
+void enable_peers(const std::vector<int32_t> &devs) {
+  for (int32_t a : devs)
+    for (int32_t b : devs) {
+      if (a == b) continue;
+      int ok = 0;
+      if (hipDeviceCanAccessPeer(&ok, a, b) != hipSuccess || !ok) continue;
+      if (hipSetDevice(a) != hipSuccess) continue;
+      (void)hipDeviceEnablePeerAccess(b, 0);  // (already enabled: an error we ignore)
+      (void)hipGetLastError();
+    }
+}
+
 // The contexts of the list: one immutable set per list, shared by the calls
 // that use it.  ks_set_devices (or a change of the list's length) replaces the
 // set; the old one is destroyed when its last call drops it, never under a
@@ -241,6 +262,7 @@ ks_status list_contexts(std::shared_ptr<CtxSet> *out) {
       set->c.push_back(c);
     }
     g_set = std::move(set);
+    enable_peers(g_devs);
   }
   *out = g_set;
   return KS_OK;
@@ -439,11 +461,12 @@ ks_status multi_low_comp_regions(const char *const *seqs, const int64_t *lens, i
   const size_t np = parts.size();
   const size_t nk = (size_t)1 << (2 * k), nb = nk * 4, rb = nk * 8;
   // One thread per part holds its context from the first phase to the end
-  // (run_parts): phase 1 stages and counts the part's bases; after a barrier
-  // each part adds one stripe of the histogram over every part's device
-  // counts into the caller's buffer (D2H stripe by stripe: no full host copy
-  // per part); after a second barrier every part builds the rank table from
-  // the sum and scans the bases it still holds.
+  // (run_parts): phase 1 stages and counts the part's bases; then the parts
+  // sum their histograms on the devices (a reduce-scatter and an all-gather
+  // of stripes, device-to-device, with barriers between); every part builds
+  // the rank table from the sum and scans the bases it still holds.  (Round
+  // 5 summed on the host from a full host copy per part; round 6's first form
+  // summed stripes on the host: 114 ms for two parts at the metric genome.)
   struct Shard {
     Staged st;
     double words = 0;
@@ -483,21 +506,49 @@ ks_status multi_low_comp_regions(const char *const *seqs, const int64_t *lens, i
     // during which the contexts must stay this call's (janitor, other threads)
     if (const char *e = getenv("KS_DEBUG_MULTI_PHASE_SLEEP_MS"))
       std::this_thread::sleep_for(std::chrono::milliseconds(std::min(10000, std::max(0, atoi(e)))));
-    // ---- the count sum: this part's stripe over every part's counts
+    // ---- the count sum on the devices: each part adds its stripe of every
+    // other part's counts into its own (device-to-device copies, xGMI between
+    // GPUs), then, after a barrier, copies every other part's summed stripe
+    // into its own histogram -- every part then holds the whole input's
+    // counts, and the caller's copy comes from one part
     const size_t ip = (size_t)(std::find(live.begin(), live.end(), p) - live.begin());
     if (ip == 0) t_p1 = now_ms() - t0;
+    auto stripe = [&](size_t i, size_t *a, size_t *b) {
+      *a = nk * i / nlive;
+      *b = nk * (i + 1) / nlive;
+    };
+    hipStream_t sp = ctx[p]->stream;
     r = [&]() -> ks_status {
-      const size_t a = nk * ip / nlive, b = nk * (ip + 1) / nlive;
-      if (b <= a) return KS_OK;
-      uint32_t *dst = reinterpret_cast<uint32_t *>(counts) + a;
-      memset(dst, 0, (b - a) * 4);
-      std::vector<uint32_t> tmp(b - a);
+      size_t a = 0, b = 0;
+      stripe(ip, &a, &b);
+      if (b <= a || nlive < 2) return KS_OK;
+      void *tmp = nullptr;
+      KS_TRY(ensure(ctx[p], SLOT_TABLE_TMP, (b - a) * 4, &tmp));
       for (size_t q : live) {
-        KS_HIP(hipMemcpy(tmp.data(), sh[q].d_counts + a, (b - a) * 4, hipMemcpyDeviceToHost));
-        for (size_t i = 0; i < b - a; ++i) dst[i] += tmp[i];
+        if (q == p) continue;
+        KS_HIP(hipMemcpyAsync(tmp, sh[q].d_counts + a, (b - a) * 4, hipMemcpyDeviceToDevice, sp));
+        hipLaunchKernelGGL(k_add_u32, dim3((unsigned)std::min<size_t>((b - a + 255) / 256, 8192)), dim3(256), 0, sp,
+                           reinterpret_cast<uint32_t *>(sh[p].d_counts + a), static_cast<const uint32_t *>(tmp),
+                           (int64_t)(b - a));
+        KS_HIP(hipGetLastError());
       }
+      KS_HIP(hipStreamSynchronize(sp));
       return KS_OK;
     }();
+    if (!bar.arrive(r == KS_OK)) return r != KS_OK ? r : fail(KS_ERR_DEVICE, "another device list entry failed");
+    r = [&]() -> ks_status {
+      for (size_t j = 0; j < nlive && nlive > 1; ++j) {
+        if (j == ip) continue;
+        size_t a = 0, b = 0;
+        stripe(j, &a, &b);
+        if (b > a)
+          KS_HIP(hipMemcpyAsync(sh[p].d_counts + a, sh[live[j]].d_counts + a, (b - a) * 4, hipMemcpyDeviceToDevice,
+                                sp));
+      }
+      KS_HIP(hipStreamSynchronize(sp));
+      return KS_OK;
+    }();
+    // (every part has read its stripes before any part's phase 2 touches its histogram)
     if (!bar.arrive(r == KS_OK)) return r != KS_OK ? r : fail(KS_ERR_DEVICE, "another device list entry failed");
     if (ip == 0) t_sum = now_ms() - t0 - t_p1;
     // ---- phase 2: the rank table from the sum, the scan
@@ -506,7 +557,7 @@ ks_status multi_low_comp_regions(const char *const *seqs, const int64_t *lens, i
     for (size_t q : live) words += sh[q].words;
     void *d_rk = nullptr;
     KS_TRY(ensure(ctx[p], SLOT_RANKS, rb, &d_rk));
-    KS_HIP(hipMemcpy(sh[p].d_counts, counts, nb, hipMemcpyHostToDevice));
+    if (p == first) KS_TRY(copy_out(ctx[p], counts, sh[p].d_counts, nb));  // (the summed counts: the caller's)
     ks_table *t = nullptr;
     KS_TRY(ks_table_from_counts(ctx[p], sh[p].d_counts, k, KS_SCORE_RANK, words, thr, KS_TABLE_EXPAND,
                                 host_ext_cap(sh[p].st.total), static_cast<double *>(d_rk), &t));

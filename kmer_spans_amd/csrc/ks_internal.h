@@ -172,6 +172,20 @@ struct ks_table {
   // predicts which binade the exact carry will be in (k_predict); never a result.
   uint16_t *d_approx = nullptr;
   int approx_k = 0;
+  // Weighted-rank code lines for pass 1 (k_pass1r; k = 13 rank tables from
+  // counts, ks_table_from_counts): each k-mer's rank as a 32-bit code
+  // (piece << 18 | offset) of the closed-form prefix (RankPiece), decoded as
+  // bits(R) = base[piece] + offset * inc[piece]; 128-B lines of the codes of
+  // own 3 + L1 4 + L2 16 (J = 5 per read, against 4 for the FP64 64-B lines
+  // that the later passes keep reading).  Pieces in weight order: the first
+  // ones are the hottest (k_pass1r stages them in LDS).
+  uint32_t *d_rcodes = nullptr;             // [4^k] (freed once the lines are built)
+  unsigned long long *d_rpieces = nullptr;  // [2 * n_rpieces]: base bits, increment
+  int32_t n_rpieces = 0;
+  double rpieces_cover = 0.0;               // share of the positions whose piece is LDS-staged
+  void *d_rlines = nullptr;
+  size_t rlines_bytes = 0, rlines_cap = 0;
+  double ms_rlines = 0;                     // code build + verification + line build (ms)
 };
 
 namespace ks {
@@ -475,6 +489,11 @@ __host__ __device__ __forceinline__ double rank_piece_value(const RankPiece &p, 
   u.i = ((int64_t)(p.e + 1023) << 52) | (mt - (1LL << 52));
   return u.d;
 }
+// Weighted-rank codes (ks_table::d_rcodes): a code is piece << kRankOffBits |
+// offset; at most 2^(32 - kRankOffBits) pieces; the first kRankPieceLds
+// (the hottest) are staged in LDS by k_pass1r.
+constexpr int kRankOffBits = 18;
+constexpr int kRankPieceLds = 7040;  // 110 KiB beside k_pass1r's 48 KiB ring
 // Pieces of the whole prefix from the distinct counts (ascending) and their
 // multiplicities.  Empty if a count is negative (wrapped int32 counts: the
 // caller then runs the sequential prefix).

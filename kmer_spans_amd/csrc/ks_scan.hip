@@ -362,6 +362,12 @@ static ks_status scan_core(ks_ctx *ctx, const ks_dev_seqs *s, int64_t total, int
                line ? 1 : t->ext_J, (int)t->distinct, t->ext_bits, t->d_lut12, t->d_map12, t->d_approx, t->approx_k,
                line ? static_cast<const uint8_t *>(t->d_ext) : nullptr, t->line_kind, t->line_own,
                t->int_exact ? 1 : 0};
+  if (t->d_rlines) {  // (weighted-rank code lines: pass 1 only, k_pass1r)
+    tv.rline = static_cast<const uint8_t *>(t->d_rlines);
+    tv.rpc = t->d_rpieces;
+    tv.nrpc = t->n_rpieces;
+    tv.rthr = t->thr;
+  }
   const uint64_t mw = (uint64_t)(int64_t)min_width;
   int algo = ctx->scan_algo;
   if (algo < 0) algo = (longest > (1 << 15)) ? 1 : 0;

@@ -1743,6 +1743,127 @@ __global__ void __launch_bounds__(kWideBlock) k_pass1w(Chunks g, int64_t total, 
   if (live) L.finish(c, o, sp);
 }
 
+// Pass 1 over weighted-rank code lines (ks_table::d_rlines, line kind 4):
+// one 128-B line per 15-mer x holding the 32-bit rank codes of its OWN
+// k-mers and of every one- and two-base continuation (L1: 4, L2: 16), so a
+// line read serves J = OWN + 2 consecutive indices (5 at k = 13, against 4
+// for the FP64 64-B lines of k_pass1l).  The 8 lanes that share a line fetch
+// the 5 dwords a step needs with LDS-DMA (k_pass1w's ring and counted waits).
+// A code is piece << kRankOffBits | offset, and the k-mer's weighted rank --
+// R_j of the sorted position j, the closed-form prefix of rank_kmers_w
+// (kmer_spans.c:196-200; RankPiece) -- is bits(R) = base + offset * inc of its
+// piece; s = R - thr in FP64, as the FP64 table holds it (k_sub_thr).  The
+// kRankPieceLds hottest pieces (weight order) are staged in LDS, the rest
+// read from the L2-resident piece table.  Same outputs as k_pass1l<OWN, true>.
+constexpr int kRankBlock = 768;
+
+template <int OWN>
+__global__ void __launch_bounds__(kRankBlock) k_pass1r(Chunks g, int64_t total, int k, TableView tv, EmitCfg ec,
+                                                       uint32_t *__restrict__ visits, P1 o, Cand cand) {
+  constexpr int BS = kRankBlock;
+  constexpr int J = OWN + 2;
+  constexpr int NS = (CH + J - 1) / J;
+  static_assert(OWN + 2 <= 8, "own, L1, L2 dwords in 8 lanes");
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[(BS / 64) * 2 * 2048];
+  __shared__ unsigned long long s_pc[2 * kRankPieceLds];
+  const int nl = min(tv.nrpc, kRankPieceLds);
+  for (int i = threadIdx.x; i < 2 * nl; i += BS) s_pc[i] = tv.rpc[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t c = g.c0 + (int64_t)blockIdx.x * BS + threadIdx.x;
+  if (c - lane >= g.nch) return;
+  const bool live = c < g.nch;
+  const int64_t start = live ? g.start[c] : (int64_t)k;
+  const int n = live ? g.n[c] : 0;
+  const bool first = live && (c == 0 || g.run[c - 1] != g.run[c]);
+  const uint32_t kmask = (1u << (2 * k)) - 1u;
+  P1Lane<false, false> L;  // (FP64 tables take no chunk summaries)
+  L.init(start, n, first, live, 0.0);
+  LaneBases B;
+  B.load(g.packed, total, start - k);
+  const int kx = k + J - 1;  // key length: the 15-mer of the line and the two continuation bases
+  const uint64_t xmask = (1ull << (2 * kx)) - 1ull;
+  uint64_t x = B.first_key(kx);
+  uint8_t *const ring = s_ring + wv * 4096;
+  const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+  const uint8_t *__restrict__ lines = tv.rline;
+  const unsigned long long *__restrict__ gpc = tv.rpc;
+  const double thr = tv.rthr;
+  // the dwords a step reads (key xk): own 0 .. OWN - 1, L1 OWN + c1, L2 OWN + 4 + 4 c1 + c2
+  auto issue = [&](uint64_t xk, int slot) {
+    const uint32_t idx = (uint32_t)(xk >> 4);
+    const uint32_t c1 = (uint32_t)(xk >> 2) & 3u, c2 = (uint32_t)xk & 3u;
+    const uint32_t dd = (OWN + c1) | ((OWN + 4 + 4 * c1 + c2) << 8);
+    const int j = lane & 7;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int ow = 8 * q + (lane >> 3);
+      const uint32_t li = (uint32_t)__shfl((int)idx, ow);
+      const uint32_t od = (uint32_t)__shfl((int)dd, ow);
+      const uint32_t dw = j < OWN ? (uint32_t)j : (j == OWN ? (od & 0xffu) : (j == OWN + 1 ? (od >> 8) : 0u));
+      glds4(lines + (size_t)li * 128 + dw * 4, ring_lds + (uint32_t)(slot * 2048 + q * 256));
+    }
+  };
+  auto decode = [&](uint32_t code) -> double {
+    const uint32_t p = code >> kRankOffBits;
+    const unsigned long long off = code & ((1u << kRankOffBits) - 1u);
+    unsigned long long base, inc;
+    if ((int)p < nl) {
+      base = s_pc[2 * p];
+      inc = s_pc[2 * p + 1];
+    } else {  // a cold piece: the L2-resident table
+      base = gpc[2 * p];
+      inc = gpc[2 * p + 1];
+    }
+    return __longlong_as_double((long long)(base + off * inc)) - thr;
+  };
+  double vp[J];
+  uint64_t xp = 0;
+  auto process = [&](int sp_, const double *vv, uint64_t xk) {
+#pragma unroll
+    for (int t = 0; t < J; ++t) {
+      const int i = sp_ * J + t;
+      if (i < n) {
+        if (visits) atomicAdd(&visits[(uint32_t)(xk >> (2 * (J - 1 - t))) & kmask], 1u);
+        L.step(vv[t], i, ec, cand);
+      }
+    }
+  };
+  uint64_t x1 = 0, x2 = 0;
+  issue(x, 0);
+  x1 = B.next_key(x, J, xmask);
+  issue(x1, 1);
+  for (int st = 0; st < NS; ++st) {
+    const uint64_t xs = x;
+    // this step's lines complete (the next step's eight loads may stay in flight)
+    if (st + 1 < NS) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint8_t *ln = ring + (st & 1) * 2048 + lane * 32;
+    uint32_t cs[J];
+    {
+      const uint4 q0 = *reinterpret_cast<const uint4 *>(ln);
+      const uint4 q1 = *reinterpret_cast<const uint4 *>(ln + 16);
+      const uint32_t D[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+      for (int t = 0; t < J; ++t) cs[t] = D[t];
+    }
+    x = x1;
+    if (st + 2 < NS) {
+      x2 = B.next_key(x1, J, xmask);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done before it is refilled
+      issue(x2, st & 1);
+      x1 = x2;
+    }
+    if (st > 0) process(st - 1, vp, xp);
+#pragma unroll
+    for (int t = 0; t < J; ++t) vp[t] = decode(cs[t]);
+    xp = xs;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  process(NS - 1, vp, xp);
+  if (live) L.finish(c, o, SummP1{});
+}
+
 // Pass 1 for small k (north_star: "the frequency table LDS-staged for small
 // k"): the 4^k FP64 values s[code] (k <= 7: <= 128 KiB) are staged in LDS
 // once per persistent block, so every scanned index costs one LDS read and no
@@ -4349,6 +4470,11 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
     auto p1l = [&](const Half &h, hipStream_t strm) {
       const Chunks gv = view(h);
       const int own = tv.line_own;
+      if (tv.rline && !ec.trlr && !p1summ && own == 3) {  // weighted-rank code lines (k = 13)
+        hipLaunchKernelGGL(k_pass1r<3>, dim3((unsigned)((h.c1 - h.c0 + kRankBlock - 1) / kRankBlock)),
+                           dim3(kRankBlock), 0, strm, gv, total, k, tv, ec, visits, p1, cand);
+        return;
+      }
       if (tv.line_kind == 3) {  // wide lines
         const unsigned grid = (unsigned)((h.c1 - h.c0 + kWideBlock - 1) / kWideBlock);
 #define KS_P1W(O)                                                                                             \
@@ -4419,6 +4545,18 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       const Chunks gv = view(h);
       if (J == 4) KS_P1PF(4, gv, strm, 512); else if (J == 3) KS_P1PF(3, gv, strm, 512); else KS_P1PF(2, gv, strm, 512);
     };
+    if (tv.rline && !ec.trlr && !p1summ && !split && (k == 14 || k == 15)) {
+      // weighted-rank code lines (k = 14 / 15: J = 4 / 3 per 128-B line read
+      // against 3 / 2 per FP64 expanded entry); every chunk (guarded base loads)
+      const unsigned grid = (unsigned)((nch + kRankBlock - 1) / kRankBlock);
+      if (k == 15)
+        hipLaunchKernelGGL(k_pass1r<1>, dim3(grid), dim3(kRankBlock), 0, st, view(halves[0]), total, k, tv, ec, visits,
+                           p1, cand);
+      else
+        hipLaunchKernelGGL(k_pass1r<2>, dim3(grid), dim3(kRankBlock), 0, st, view(halves[0]), total, k, tv, ec, visits,
+                           p1, cand);
+      KS_HIP(hipGetLastError());
+    } else {
 #undef KS_P1PF
     auto p1tail = [&]() {
       if (J == 4) KS_P1TC(4, false, false); else if (J == 3) KS_P1TC(3, false, false); else KS_P1TC(2, false, false);
@@ -4448,6 +4586,7 @@ ks_status scan_chunked(ks_ctx *ctx, const ks_dev_seqs *s, const Runs &runs, cons
       p1f(halves[0], st);
       KS_HIP(hipGetLastError());
       if (tail) KS_HIP(hipStreamWaitEvent(st, ctx->ev[13], 0));
+    }
     }
     KS_HIP(hipGetLastError());
   } else if (p1summ || exact) {

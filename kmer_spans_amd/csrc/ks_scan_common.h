@@ -24,6 +24,11 @@ struct TableView {
   int line_kind;           // 1: uint16 codes, 2: FP64 values
   int line_own;
   int exact;               // ks_table::int_exact
+  // weighted-rank code lines of pass 1 (ks_table::d_rlines, k_pass1r), nullptr if absent
+  const uint8_t *rline = nullptr;
+  const unsigned long long *rpc = nullptr;  // pieces: (base bits, increment) pairs, hottest first
+  int nrpc = 0;
+  double rthr = 0.0;                         // s = R - thr
 };
 
 // LUT entries that fit the LDS copy used by the streaming passes (64 KiB).

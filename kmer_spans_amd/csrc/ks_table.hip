@@ -274,13 +274,16 @@ typedef uint32_t ks_u32x4 __attribute__((ext_vector_type(4)));
 // LDS each 16-B store instruction writes 1 KiB of whole lines.  Mode 0: uint16 64-B lines, 1: FP64 64-B
 // lines, 2: wide 128-B lines (13-bit own / L1 / L2 codes at bits 13 j, the
 // 64 L3 codes as 11-bit codes from bit 13 (own + 20), >= 2047 -> 2047).
+// Mode 3: weighted-rank code lines, 128 B: the 32-bit rank codes (ks_table::
+// d_rcodes) of own, L1 and L2 at dwords 0 .. own + 19 (k_pass1r).
 template <int OWN, int kMode>
 __global__ void __launch_bounds__(256) k_build_lines(const uint16_t *__restrict__ codes,
-                                                     const double *__restrict__ vals, int k, int m,
+                                                     const double *__restrict__ vals,
+                                                     const uint32_t *__restrict__ codes32, int k, int m,
                                                      ks_u32x4 *__restrict__ out) {
-  constexpr int LB = kMode == 2 ? 128 : 64;  // line bytes
+  constexpr int LB = kMode >= 2 ? 128 : 64;  // line bytes
   constexpr int NP = LB / 16;               // 16-B pieces per line
-  constexpr int LEV = kMode == 0 ? 2 : (kMode == 1 ? 1 : 3);
+  constexpr int LEV = kMode == 0 || kMode == 3 ? 2 : (kMode == 1 ? 1 : 3);
   __shared__ ks_u32x4 s_t[4][64 * NP];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t kmask = (uint32_t)(((uint64_t)1 << (2 * k)) - 1);
@@ -292,7 +295,18 @@ __global__ void __launch_bounds__(256) k_build_lines(const uint16_t *__restrict_
     uint32_t w[LB / 4];
 #pragma unroll
     for (int q = 0; q < LB / 4; ++q) w[q] = 0;
-    if (kMode == 1) {  // FP64: [own][L1]
+    if (kMode == 3) {  // 32-bit rank codes: [own][L1][L2]
+#pragma unroll
+      for (int t = 0; t < OWN; ++t) w[t] = codes32[(uint32_t)(x >> (2 * (OWN - 1 - t))) & kmask];
+      const uint4 l1 = *reinterpret_cast<const uint4 *>(codes32 + (((uint32_t)(x << 2)) & kmask));
+      w[OWN] = l1.x; w[OWN + 1] = l1.y; w[OWN + 2] = l1.z; w[OWN + 3] = l1.w;
+      const uint4 *l2 = reinterpret_cast<const uint4 *>(codes32 + (((uint32_t)(x << 4)) & kmask));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = l2[q];
+        w[OWN + 4 + 4 * q] = v.x; w[OWN + 5 + 4 * q] = v.y; w[OWN + 6 + 4 * q] = v.z; w[OWN + 7 + 4 * q] = v.w;
+      }
+    } else if (kMode == 1) {  // FP64: [own][L1]
       double d[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) d[t] = 0.0;
@@ -409,6 +423,45 @@ __global__ void k_rank_fill(const uint32_t *__restrict__ idx, int64_t n, const R
   }
 }
 
+// Rank codes (ks_table::d_rcodes): sorted position j takes the code of its
+// uniform piece (pieces sorted by start uj0; uh = the piece's index in
+// weight order, the code's piece field).
+__global__ void k_rank_codes(const uint32_t *__restrict__ idx, int64_t n, const int64_t *__restrict__ uj0,
+                             const int32_t *__restrict__ uh, int64_t np, uint32_t *__restrict__ codes) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g * 16 < n; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j0 = g * 16;
+    int64_t lo = 0, hi = np - 1;  // last piece starting at or before j0
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (uj0[mid] <= j0) lo = mid; else hi = mid - 1;
+    }
+    const int64_t j1 = min(n, j0 + 16);
+    for (int64_t j = j0; j < j1; ++j) {
+      while (lo + 1 < np && uj0[lo + 1] <= j) ++lo;
+      codes[idx[j]] = ((uint32_t)uh[lo] << kRankOffBits) | (uint32_t)(j - uj0[lo]);
+    }
+  }
+}
+
+// Every code decodes to the rank the closed form filled, bit for bit
+// (mismatches counted; the code lines are built only with none).
+__global__ void k_rank_codes_check(const uint32_t *__restrict__ codes, const unsigned long long *__restrict__ pc,
+                                   const double *__restrict__ ranks, int64_t n, int64_t np,
+                                   unsigned long long *__restrict__ bad) {
+  unsigned long long nb = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = codes[i];
+    const uint32_t p = c >> kRankOffBits;
+    if ((int64_t)p >= np) {
+      ++nb;
+      continue;
+    }
+    const unsigned long long bits = pc[2 * p] + (unsigned long long)(c & ((1u << kRankOffBits) - 1)) * pc[2 * p + 1];
+    if (bits != (unsigned long long)__double_as_longlong(ranks[i])) ++nb;
+  }
+  if (nb) atomicAdd(bad, nb);
+}
+
 __global__ void k_iota(uint32_t *__restrict__ x, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     x[i] = (uint32_t)i;
@@ -456,7 +509,9 @@ struct PoolBuf {
   void *p = nullptr;
   size_t bytes = 0;
 };
-constexpr size_t kPoolPairMax = (size_t)130 << 30;  // (two 64 GiB tables; one 128 GiB table alone)
+// (two 64 GiB tables; a weighted-rank table's 128 GiB code lines and 64 GiB
+// FP64 form, round 6 -- the pool then holds both between tables)
+constexpr size_t kPoolPairMax = (size_t)200 << 30;
 PoolBuf g_pool[64][2];
 bool pool_on() {
   static const bool on = !(getenv("KS_EXT_POOL") && atoi(getenv("KS_EXT_POOL")) == 0);
@@ -638,13 +693,13 @@ constexpr int64_t kWideLut = 7168;
 // split over grid rows until ~2^20 lanes run.
 template <int OWN, int kMode>
 static void launch_build_lines(hipStream_t st, const ks_table *t, int m, void *out) {
-  const int lev = kMode == 0 ? 2 : (kMode == 1 ? 1 : 3);
+  const int lev = kMode == 0 || kMode == 3 ? 2 : (kMode == 1 ? 1 : 3);
   const int lb = 2 * t->k - 2 * lev;
   const int hb = 2 * m - lb;  // >= 4 (m >= k + 1, levmax >= 1)
   int ys = 0;
   while (lb + ys < 22 && ys + 2 < hb) ++ys;
   hipLaunchKernelGGL((k_build_lines<OWN, kMode>), dim3((unsigned)(((uint64_t)1 << lb) / 64), 1u << ys), dim3(256), 0,
-                     st, t->d_codes, t->d_vals, t->k, m, (ks_u32x4 *)out);
+                     st, t->d_codes, t->d_vals, t->d_rcodes, t->k, m, (ks_u32x4 *)out);
 }
 
 // Binade predictor of the pass-1 summaries (k_predict), built with the
@@ -675,7 +730,7 @@ static ks_status build_approx(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev)
 // 128-B lines where they apply (below), else the largest own count of 64-B
 // lines (m = k + own - 1 <= 15, own <= 5 / 4, k <= 13) whose 4^m x 64 B fit
 // the budget, own >= 2.  Sets *built.
-static ks_status table_lines(ks_ctx *ctx, ks_table *t, size_t budget, const int32_t *freq_dev, bool *built) {
+static ks_status table_lines(ks_ctx *ctx, ks_table *t, size_t &budget, const int32_t *freq_dev, bool *built) {
   *built = false;
   const bool u16 = t->compressed;
   if (t->k < 8 || t->k > 15 || getenv("KS_NO_LINES")) return KS_OK;
@@ -733,6 +788,32 @@ static ks_status table_lines(ks_ctx *ctx, ks_table *t, size_t budget, const int3
         return KS_OK;
       }
     }
+  }
+  // weighted-rank code lines for pass 1 (k = 13..15: one 128-B line per
+  // 15-mer, own = 16 - k, J = own + 2 = 5 / 4 / 3 against 4 / 3 / 2 for the
+  // FP64 forms; 128 GiB) when the FP64 form the later passes read (64-B lines
+  // at k = 13, the expanded table above it: 64 GiB) fits beside them
+  if (!u16 && t->d_rcodes && t->k >= 13 && t->k <= 15 && ((size_t)192 << 30) <= budget) {
+    const double t0 = now_ms();
+    const size_t bytes = ((size_t)1 << 30) * 128;
+    size_t cap = 0;
+    void *rl = ext_alloc(ctx, bytes, &cap);
+    if (rl) {
+      if (t->k == 13) launch_build_lines<3, 3>(ctx->stream, t, 15, rl);
+      else if (t->k == 14) launch_build_lines<2, 3>(ctx->stream, t, 15, rl);
+      else launch_build_lines<1, 3>(ctx->stream, t, 15, rl);
+      KS_HIP(hipGetLastError());
+      KS_HIP(hipStreamSynchronize(ctx->stream));
+      t->d_rlines = rl;
+      t->rlines_bytes = bytes;
+      t->rlines_cap = cap;
+      budget -= bytes;
+    }
+    t->ms_rlines += now_ms() - t0;
+  }
+  if (t->d_rcodes) {  // (only the lines read the codes)
+    (void)hipFree(t->d_rcodes);
+    t->d_rcodes = nullptr;
   }
   if (t->k > 13) return KS_OK;  // (64-B lines need own >= 2: m <= 15)
   int own = std::min(u16 ? 5 : 4, 16 - t->k);
@@ -792,8 +873,9 @@ ks_status table_expand(ks_ctx *ctx, ks_table *t, size_t max_bytes, const int32_t
     if (ctx->device >= 0 && ctx->device < 64) free_b += pool_bytes(ctx->device);
   }
   // leave room for the sequences and the scan workspace
-  const size_t reserve = std::max<size_t>((size_t)32 << 30, total_b / 4);
-  const size_t budget = std::min(max_bytes, free_b > reserve ? free_b - reserve : (size_t)0);
+  // (total / 8: ~34 GiB on MI355X; the metric scan's workspace is ~4 GB)
+  const size_t reserve = std::max<size_t>((size_t)32 << 30, total_b / 8);
+  size_t budget = std::min(max_bytes, free_b > reserve ? free_b - reserve : (size_t)0);
   const char *jmax_env = getenv("KS_EXT_MAX_J");  // tests: cap J to exercise every table form
   if (!jmax_env) {  // line tables first (k_pass1l); KS_NO_LINES: the (k+J-1)-mer forms below
     bool built = false;
@@ -1005,7 +1087,7 @@ ks_status ks::table_create(ks_ctx *ctx, const double *w_host, int32_t k, double 
   cleanup();
   t->ms_compress = now_ms() - t_start - t->ms_upload;
   if (flags & KS_TABLE_EXPAND) {
-    const ks_status rc = table_expand(ctx, t, max_ext_bytes > 0 ? (size_t)max_ext_bytes : (size_t)160 << 30, freq_dev);
+    const ks_status rc = table_expand(ctx, t, max_ext_bytes > 0 ? (size_t)max_ext_bytes : (size_t)200 << 30, freq_dev);
     if (rc != KS_OK) { ks_table_destroy(t); return rc; }
   }
   t->ms_total = now_ms() - t_start;
@@ -1122,6 +1204,97 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
       const unsigned g = (unsigned)std::min<int64_t>(((n + 15) / 16 + 255) / 256, 8192);
       hipLaunchKernelGGL(k_rank_fill, dim3(g), dim3(256), 0, st, d_idx, n, d_p, (int64_t)P.size(), d_w);
       KS_TFC(hipGetLastError());
+      // 2r'. the 32-bit rank codes of the code lines (k = 13, expanded tables)
+      if (k >= 13 && k <= 15 && (flags & KS_TABLE_EXPAND) && !getenv("KS_NO_RANK_CODES")) {
+        const double tr0 = now_ms();
+        // uniform pieces: bits(R_j) = base + (j - j0) * inc over [j0, j0 + len),
+        // len <= 2^kRankOffBits; a kind-1 piece's first position is a piece of
+        // its own (rank_piece_value); weight = positions covered (count x len)
+        std::vector<int64_t> cls(nu + 1, 0);
+        for (int i = 0; i < nu; ++i) cls[i + 1] = cls[i] + dm[i];
+        struct UP {
+          int64_t j0;
+          unsigned long long base, inc;
+          double wt;
+        };
+        std::vector<UP> up;
+        bool ok = true;
+        const int64_t lim = (int64_t)1 << kRankOffBits;
+        for (size_t i = 0; i < P.size() && ok; ++i) {
+          const int64_t a = P[i].j0, b = i + 1 < P.size() ? P[i + 1].j0 : n;
+          const int ci = (int)(std::upper_bound(cls.begin(), cls.end(), a) - cls.begin()) - 1;
+          const double c = (double)std::max(0, dv[std::max(0, std::min(ci, nu - 1))]);
+          unsigned long long r0b;
+          memcpy(&r0b, &P[i].r0, 8);
+          auto add = [&](int64_t j0, int64_t j1, unsigned long long base, unsigned long long inc) {
+            for (int64_t s0 = j0; s0 < j1; s0 += lim)
+              up.push_back(UP{s0, base + (unsigned long long)(s0 - j0) * inc, inc, c * (double)(std::min(j1, s0 + lim) - s0)});
+          };
+          if (P[i].kind == 0) {
+            add(a, b, r0b, 0ull);
+          } else {
+            add(a, a + 1, r0b, 0ull);
+            if (b > a + 1) {
+              const unsigned long long m = (r0b & ((1ull << 52) - 1)) | (1ull << 52);
+              const unsigned long long base = ((unsigned long long)(P[i].e + 1023) << 52) + (m + (unsigned long long)P[i].inc1 - (1ull << 52));
+              add(a + 1, b, base, (unsigned long long)P[i].inc);
+            }
+          }
+          ok = up.size() <= ((size_t)1 << (32 - kRankOffBits));
+        }
+        if (ok && !up.empty()) {
+          const int64_t np = (int64_t)up.size();
+          std::vector<int32_t> ord(np);
+          for (int64_t i = 0; i < np; ++i) ord[i] = (int32_t)i;
+          std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) { return up[x].wt > up[y].wt; });
+          std::vector<int32_t> uh(np);
+          std::vector<unsigned long long> pc(2 * np);
+          double wall = 0, whot = 0;
+          for (int64_t h = 0; h < np; ++h) {
+            const UP &u = up[ord[h]];
+            uh[ord[h]] = (int32_t)h;
+            pc[2 * h] = u.base;
+            pc[2 * h + 1] = u.inc;
+            wall += u.wt;
+            if (h < kRankPieceLds) whot += u.wt;
+          }
+          std::vector<int64_t> uj0(np);
+          for (int64_t i = 0; i < np; ++i) uj0[i] = up[i].j0;
+          int64_t *d_uj0 = static_cast<int64_t *>(dalloc((size_t)np * 8));
+          int32_t *d_uh = static_cast<int32_t *>(dalloc((size_t)np * 4));
+          unsigned long long *d_bad = static_cast<unsigned long long *>(dalloc(8));
+          uint32_t *d_rc = nullptr;
+          unsigned long long *d_pc = nullptr;
+          if (d_uj0 && d_uh && d_bad && hipMalloc(&d_rc, (size_t)n * 4) == hipSuccess &&
+              hipMalloc(&d_pc, (size_t)np * 16) == hipSuccess) {
+            KS_TFC(hipMemcpyAsync(d_uj0, uj0.data(), (size_t)np * 8, hipMemcpyHostToDevice, st));
+            KS_TFC(hipMemcpyAsync(d_uh, uh.data(), (size_t)np * 4, hipMemcpyHostToDevice, st));
+            KS_TFC(hipMemcpyAsync(d_pc, pc.data(), (size_t)np * 16, hipMemcpyHostToDevice, st));
+            KS_TFC(hipMemsetAsync(d_bad, 0, 8, st));
+            hipLaunchKernelGGL(k_rank_codes, dim3(g), dim3(256), 0, st, d_idx, n, d_uj0, d_uh, np, d_rc);
+            hipLaunchKernelGGL(k_rank_codes_check, dim3(grid), dim3(256), 0, st, d_rc, d_pc, d_w, n, np, d_bad);
+            KS_TFC(hipGetLastError());
+            unsigned long long bad = 0;
+            KS_TFC(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, st));
+            KS_TFC(hipStreamSynchronize(st));
+            if (bad == 0) {
+              t->d_rcodes = d_rc;
+              t->d_rpieces = d_pc;
+              t->n_rpieces = (int32_t)np;
+              t->rpieces_cover = wall > 0 ? whot / wall : 1.0;
+              d_rc = nullptr;
+              d_pc = nullptr;
+            } else {
+              fprintf(stderr, "kmer_spans_amd: %llu rank codes do not decode to their ranks; no code lines\n", bad);
+            }
+          } else {
+            (void)hipGetLastError();
+          }
+          if (d_rc) (void)hipFree(d_rc);
+          if (d_pc) (void)hipFree(d_pc);
+        }
+        t->ms_rlines = now_ms() - tr0;
+      }
     } else {  // wrapped (negative) counts: the host's sequential prefix
       std::vector<int32_t> hc(n);
       std::vector<double> hr(n);
@@ -1232,7 +1405,7 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
   }
   t->ms_compress = now_ms() - t_start - t->ms_upload;
   if (flags & KS_TABLE_EXPAND) {
-    const size_t cap = max_ext_bytes > 0 ? (size_t)max_ext_bytes : (size_t)160 << 30;
+    const size_t cap = max_ext_bytes > 0 ? (size_t)max_ext_bytes : (size_t)200 << 30;
     const ks_status rc = table_expand(ctx, t, cap, counts_dev);
     if (rc != KS_OK) {
       ks_table_destroy(t);
@@ -1257,6 +1430,9 @@ extern "C" void ks_table_destroy(ks_table *t) {
   if (t->d_map12) (void)hipFree(t->d_map12);
   if (t->d_lut12) (void)hipFree(t->d_lut12);
   if (t->d_approx) (void)hipFree(t->d_approx);
+  if (t->d_rcodes) (void)hipFree(t->d_rcodes);
+  if (t->d_rpieces) (void)hipFree(t->d_rpieces);
+  if (t->d_rlines) pool_give(t->device, t->d_rlines, t->rlines_cap);
   delete t;
 }
 
@@ -1279,7 +1455,9 @@ extern "C" void ks_release_cache(void) {
 
 extern "C" int32_t ks_table_is_compressed(const ks_table *t) { return t && t->compressed ? 1 : 0; }
 extern "C" int64_t ks_table_distinct(const ks_table *t) { return t ? t->distinct : -1; }
-extern "C" int32_t ks_table_positions_per_read(const ks_table *t) { return t ? t->ext_J : 0; }
+extern "C" int32_t ks_table_positions_per_read(const ks_table *t) {
+  return t ? (t->d_rlines ? 18 - t->k : t->ext_J) : 0;  // (rank code lines: own 16 - k + L1 + L2)
+}
 extern "C" int32_t ks_table_code_bits(const ks_table *t) {
   if (!t) return 0;
   if (t->ext_J > 1 && t->compressed) return t->ext_bits;
@@ -1290,18 +1468,18 @@ extern "C" ks_status ks_table_get_info(const ks_table *t, ks_table_info *out) {
   memset(out, 0, sizeof(*out));
   out->k = t->k;
   out->compressed = t->compressed ? 1 : 0;
-  out->positions_per_read = t->ext_J;
-  out->code_bits = ks_table_code_bits(t);
+  out->positions_per_read = ks_table_positions_per_read(t);  // (pass 1's: the rank code lines, k_pass1r)
+  out->code_bits = t->d_rlines ? 32 : ks_table_code_bits(t);
   out->distinct = t->distinct;
-  out->ext_bytes = (int64_t)t->ext_bytes;
+  out->ext_bytes = (int64_t)(t->ext_bytes + t->rlines_bytes);
   out->escape_fraction = ks_table_escape_fraction(t);
   out->ms_upload = t->ms_upload;
   out->ms_compress = t->ms_compress;
   out->ms_codes12 = t->ms_codes12;
   out->ms_ext_alloc = t->ms_ext_alloc;
-  out->ms_ext_build = t->ms_ext;
+  out->ms_ext_build = t->ms_ext + t->ms_rlines;
   out->ms_total = t->ms_total;
-  out->line_kind = t->line_kind;
+  out->line_kind = t->d_rlines ? 4 : t->line_kind;  // (4: rank code lines for pass 1, FP64 lines after it)
   out->line_own = t->line_own;
   return KS_OK;
 }

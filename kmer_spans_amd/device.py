@@ -149,7 +149,8 @@ class DeviceTable:
     @property
     def line_kind(self) -> int:
         """0: no line table; 1: uint16 64-B lines (k_pass1l); 2: FP64 64-B lines
-        (k_pass1l); 3: 128-B lines (k_pass1w)."""
+        (k_pass1l); 3: 128-B lines (k_pass1w); 4: weighted-rank 128-B code lines
+        for pass 1 (k_pass1r) beside FP64 64-B lines for the later passes."""
         return int(self.info()["line_kind"])
 
     @property
@@ -160,6 +161,8 @@ class DeviceTable:
             return "k_pass1_lds"
         if lk == 3:
             return "k_pass1w"
+        if lk == 4:
+            return "k_pass1r"
         if lk:
             return "k_pass1l"
         if self.positions_per_read > 1:

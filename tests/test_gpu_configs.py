@@ -148,6 +148,49 @@ def test_rank_k15(oracle):
     tab.close()
 
 
+@pytest.mark.parametrize("k,sizes", [(13, (9_000_000, 4_000_000, 700_000, 30_000)), (15, (3_000_000, 900_000, 20_000))])
+def test_rank_code_lines(oracle, monkeypatch, k, sizes):
+    """Configs 3 and 4's table form (weighted rank at k = 13 / 15,
+    kmer_spans.c:189-202): the 32-bit rank codes (piece, offset) of the
+    closed-form prefix -- verified on the device against the FP64 ranks when
+    built -- in 128-B code lines of 15-mers that pass 1 reads 5 / 3 positions
+    at a time (k_pass1r), beside the FP64 form of the later passes (64-B lines
+    at k = 13, the expanded table at k = 15); regions, FP64 scores and visits
+    against the oracle, and equal to the FP64 scan (KS_NO_RANK_CODES=1) on a
+    multi-contig genome with repeats."""
+    import torch
+    from kmer_spans_amd import _lib, device as D, genome
+    ctx = _lib.context(0)
+    D.bind_torch_stream(ctx)
+    torch.cuda.empty_cache()
+    parts = [genome.contig(L, 80 + i, device="cuda", repeats=True) for i, L in enumerate(sizes)]
+    ds = D.from_parts(parts, [p.numel() for p in parts], "cuda")
+    host = [ds.host_seq(i) for i in range(len(parts))]
+    counts = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+    words = D.count(ctx, ds, k, counts)
+    w = torch.empty(4 ** k, dtype=torch.float64, device="cuda")
+    tab = D.DeviceTable.from_counts(ctx, counts, k, "rank", total=words, thr=0.75, expand=True, w_out=w)
+    assert tab.line_kind == 4 and tab.pass1_kernel == "k_pass1r" and tab.positions_per_read == 18 - k
+    wh = w.cpu().numpy()
+    o = oracle.scan(host, k, wh, 0.75, 100, 20.0, visits=True)
+    assert o["pos"].shape[1] > 10
+    ctx.set_scan_algo(1)
+    try:
+        vis = torch.zeros(4 ** k, dtype=torch.int32, device="cuda")
+        pos, sc, st = D.scan(ctx, ds, k, tab, 100, 20.0, vis)
+        _same(pos, sc, o, "rank code lines")
+        assert np.array_equal(vis.cpu().numpy(), o["counts"]), "rank code lines: visits"
+        tab.close()
+        monkeypatch.setenv("KS_NO_RANK_CODES", "1")
+        tab = D.DeviceTable.from_counts(ctx, counts, k, "rank", total=words, thr=0.75, expand=True)
+        assert tab.line_kind == (2 if k == 13 else 0)
+        pos2, sc2, _ = D.scan(ctx, ds, k, tab, 100, 20.0)
+        _same(pos2, sc2, o, "rank FP64 lines")
+    finally:
+        ctx.set_scan_algo(-1)
+        tab.close()
+
+
 @pytest.mark.parametrize("k,jmax", [(10, 2), (11, 3), (9, 4)])
 def test_rank_expanded_pass1_summaries(oracle, monkeypatch, k, jmax):
     """The FP64 expanded form of the k = 14 / 15 weighted-rank tables

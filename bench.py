@@ -868,7 +868,7 @@ def rank_subline(args, ctx, ds, counts, words, make_table, timed_steps, host, D)
     like the metric line; parity over every contig; the CPU phases of the
     reference operation (count, rank, scan) on one pinned core."""
     k = args.k
-    w_dev, thr, table, init, tt = make_table(counts, words, "rank", warm=False)
+    w_dev, thr, table, init, tt = make_table(counts, words, "rank", warm=True)
     pos, score, stats, elapsed = timed_steps(ds, table, init, args.rank_steps, 1)
     n_bases = int(stats[-1]["n_bases"])
     ms = elapsed / args.rank_steps * 1e3

@@ -17,6 +17,7 @@
 #include <cstring>
 
 #include "ks_internal.h"
+#include "ks_kmer_swar.h"
 
 namespace ks {
 namespace {
@@ -325,35 +326,28 @@ __device__ __forceinline__ void lane_bytes(const uint8_t *__restrict__ seq, int6
 // p0 + i.  kStarts: some sequence starts inside the tile, marked in bmask
 // (bit r = position base + r): a start resets the run, and the k-mer test
 // drops a run of exactly k bases ending right before a start (Q1).  Without
-// starts the tile needs neither.
-template <bool kStarts, typename F>
-__device__ __forceinline__ void lane_kmers(const uint32_t (&x)[8], int64_t p0, int64_t total, int64_t base,
-                                           const uint32_t *bmask, int k, uint32_t mask, F emit) {
+// starts the tile needs neither.  Word-parallel (ks_kmer_swar.h).
+static_assert(kLook == 16 && kPer == 16, "ks_kmer_swar.h: 16 look-back bytes, 16 positions per lane");
+template <bool kStarts>
+__device__ __forceinline__ SwarWin lane_window(const uint32_t (&x)[8], int64_t p0, int64_t total, int64_t base,
+                                               const uint32_t *bmask, int k) {
   // byte j is position p0 - kLook + j: in the sequence while j < jend, bit r0 + j of bmask
   const int jend = p0 + kPer <= total ? kLook + kPer : (int)(total - (p0 - kLook));
-  const int r0 = (int)(p0 - kLook - base);
-  uint32_t code = 0;
-  int len = 0;
-#pragma unroll
-  for (int j = 1; j < kLook + kPer; ++j) {
-    const int r = r0 + j;
-    if (kStarts && ((bmask[r >> 5] >> (r & 31)) & 1u)) len = 0;
-    const uint8_t c = (uint8_t)(x[j >> 2] >> (8 * (j & 3)));
-    if (!is_n(c)) {
-      code = ((code << 2) | enc(c)) & mask;
-      ++len;
-    } else {
-      len = 0;
-    }
-    if (j >= kLook && j < jend && len >= k) {
-      bool q1 = false;
-      if (kStarts) {
-        const int r1 = r + 1;
-        q1 = (len == k) && ((bmask[r1 >> 5] >> (r1 & 31)) & 1u);
-      }
-      if (!q1) emit(j - kLook, code);
-    }
+  uint64_t sm = 0;
+  if (kStarts) {
+    const int r0 = (int)(p0 - kLook - base);  // (a multiple of 16: bits r0 .. r0 + 32 lie in two words)
+    sm = ((((uint64_t)bmask[(r0 >> 5) + 1]) << 32) | bmask[r0 >> 5]) >> (r0 & 31);
   }
+  return swar_window(x, sm, jend, k);
+}
+
+// Bucket of the lane's position i for the LDS bucket counters: positions that
+// count nothing take a lane-private spare counter (index kT1 buckets + lane),
+// so the counter updates need no per-position branch and never collide.
+constexpr int kSpare = 64;
+__device__ __forceinline__ uint32_t lane_bucket(const SwarWin &w, int i, uint32_t mask, int shift) {
+  const bool on = (w.emit >> (kLook + i)) & 1u;
+  return on ? swar_code(w, i, mask) >> shift : (uint32_t)((1 << kT1) + (threadIdx.x & 63));
 }
 
 // Per block, the sequence starts (offs[0..nseq], ascending) ahead of its
@@ -404,12 +398,13 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
                                               unsigned long long *__restrict__ mat, int pad,
                                               unsigned long long *__restrict__ words, int64_t tile0, int64_t ntiles) {
   constexpr int kWords = (kPTile + kLook + 32) / 32 + 1;
-  __shared__ uint32_t lds_b[1 << kT1];
+  __shared__ uint32_t lds_b[(1 << kT1) + kSpare];
   __shared__ uint32_t bmask[kWords];
   __shared__ unsigned long long wsum[kPT / 64];
   const int nb = 1 << (2 * k - shift);
   const int G = gridDim.x;
   for (int i = threadIdx.x; i < nb; i += kPT) lds_b[i] = 0;
+  if (threadIdx.x < kSpare) lds_b[(1 << kT1) + threadIdx.x] = 0;
   const uint32_t mask = (1u << (2 * k)) - 1u;
   int32_t ci = 0;
   int64_t nx = 0;
@@ -430,9 +425,10 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
     if (p0 < total) {
       uint32_t x[8];
       lane_bytes(seq, total, p0, cur, x);
-      auto add = [&](int, uint32_t code) { atomicAdd(&lds_b[code >> shift], 1u); };
-      if (st) lane_kmers<true>(x, p0, total, base, bmask, k, mask, add);
-      else lane_kmers<false>(x, p0, total, base, bmask, k, mask, add);
+      const SwarWin w = st ? lane_window<true>(x, p0, total, base, bmask, k)
+                           : lane_window<false>(x, p0, total, base, bmask, k);
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) atomicAdd(&lds_b[lane_bucket(w, i, mask, shift)], 1u);
     }
     if (st) __syncthreads();  // (bmask is rewritten by the next tile holding starts)
     cur = nxt;
@@ -457,19 +453,26 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
 // Single-level scatter through a per-bucket LDS stage of kS items: every
 // (bucket, block) region is a multiple of kS items (k_part with pad = kS)
 // starting 2*kS-byte aligned, and is written only in whole aligned pieces of
-// kS items, so each HBM write request carries 2*kS bytes (the counting-sort
-// scatter below writes ~4 items per bucket and sub-tile: 27.5 GB of partial
-// writes for 6.1 GB of items at the metric genome).  Per sub-tile: a k-mer
-// takes slot = fill[bucket]++ (LDS atomic); slots < kS go to the stage, the
-// rest stay in registers; buckets that reach kS flush the stage's piece
-// (16-B stores), the registers' slots below the last whole piece go straight
-// out (lanes of one wave hold consecutive slots of a hot bucket, so those
-// stores coalesce) and the remainder moves into the stage.  The bucket state
-// (fill, cursor) is double-buffered: the flush writes the next sub-tile's
-// state while the register phase still reads this one, two barriers per
-// sub-tile.  The block's last remainders go out padded with kSentinel, which
-// k_bins skips.
+// kS items, so each HBM write request carries 2*kS bytes.  The scatter is
+// bound by its write requests, ~28 G/s for these scattered pieces (round 6:
+// 16-B pieces 14.0 ms, 32-B pieces 6.9 ms, at the metric genome's 6.2 GB of
+// items; the counting-sort scatter below writes ~4 items per bucket and
+// sub-tile: 27.5 GB of partial writes), so the pieces are 64 B: 2,048 x 32
+// items of stage fill 128 KiB of the 160 KiB LDS, and the per-bucket fill
+// counters are 16-bit halves of words (a sub-tile adds at most 16 K items).
+// Per sub-tile: a k-mer takes slot = fill[bucket]++ (LDS atomic); slots < kS
+// go to the stage, the rest stay in registers; buckets that reach kS flush
+// the stage's piece (16-B stores), the registers' slots below the last whole
+// piece go straight out (lanes of one wave hold consecutive slots of a hot
+// bucket, so those stores coalesce) and the remainder moves into the stage.
+// The bucket state (fill, cursor) is double-buffered: the flush writes the
+// next sub-tile's state while the register phase still reads this one, two
+// barriers per sub-tile.  The block's last remainders go out padded with
+// kSentinel, which k_bins skips.
 constexpr uint16_t kSentinel = 0xffffu;  // payloads are < 2^15 on the single level
+__device__ __forceinline__ uint32_t fill_get(const uint32_t *f, uint32_t b) {
+  return (f[b >> 1] >> ((b & 1u) << 4)) & 0xffffu;
+}
 template <int kS, int kT>
 __global__ void __launch_bounds__(kT) k_part_scatter_st(const uint8_t *__restrict__ seq, int64_t total,
                                                          const int64_t *__restrict__ offs, int32_t nseq, int k,
@@ -479,17 +482,16 @@ __global__ void __launch_bounds__(kT) k_part_scatter_st(const uint8_t *__restric
   constexpr int kSub = kPTile / kTile;
   constexpr int kV = kS / 8;        // 16-B vectors per piece
   constexpr int kWords = (kTile + kLook + 32) / 32 + 1;
-  static_assert(kPTile % kTile == 0 && kS % 8 == 0, "sub-tiles, pieces");
+  constexpr int kFW = ((1 << kT1) + kSpare) / 2;  // fill words (two 16-bit counters each)
+  static_assert(kPTile % kTile == 0 && kS % 8 == 0 && kTile + kS < 65536, "sub-tiles, pieces, 16-bit fills");
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
   uint16_t *stage = reinterpret_cast<uint16_t *>(dyn);  // [nb][kS]
-  __shared__ uint32_t fill[2][1 << kT1], cur[2][1 << kT1];
+  __shared__ uint32_t fill[2][kFW], cur[2][1 << kT1];
   __shared__ uint32_t bmask[kWords];
-  const int nb = 1 << (2 * k - shift);
+  const int nb = 1 << (2 * k - shift);  // (even: k >= kPartMinK)
   const int G = gridDim.x;
-  for (int i = threadIdx.x; i < nb; i += kT) {
-    fill[0][i] = 0;
-    cur[0][i] = (uint32_t)ex[(size_t)i * G + blockIdx.x];
-  }
+  for (int i = threadIdx.x; i < kFW; i += kT) fill[0][i] = fill[1][i] = 0;
+  for (int i = threadIdx.x; i < nb; i += kT) cur[0][i] = (uint32_t)ex[(size_t)i * G + blockIdx.x];
   const uint32_t mask = (1u << (2 * k)) - 1u;
   const uint32_t pmask = (1u << shift) - 1u;
   // the positions k_part's block counted: its kPTile-position tiles, each as
@@ -522,45 +524,61 @@ __global__ void __launch_bounds__(kT) k_part_scatter_st(const uint8_t *__restric
     if (p0 < total) {
       uint32_t x[8];
       lane_bytes(seq, total, p0, win, x);
-      auto take = [&](int i, uint32_t code) {
-        const uint32_t bk = code >> shift;
-        const uint32_t slot = atomicAdd(&fl[bk], 1u);
-        const uint32_t v = code & pmask;
-        if (slot < (uint32_t)kS) {
-          stage[bk * kS + slot] = (uint16_t)v;
+      const SwarWin w = st ? lane_window<true>(x, p0, total, base, bmask, k)
+                           : lane_window<false>(x, p0, total, base, bmask, k);
+      // the lane's 16 slot atomics back to back (one wait for all of them,
+      // not one LDS round trip per position), then the stage stores
+      uint32_t slot[kPer];
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const uint32_t b = lane_bucket(w, i, mask, shift), sh = (b & 1u) << 4;
+        slot[i] = ((atomicAdd(&fl[b >> 1], 1u << sh)) >> sh) & 0xffffu;
+      }
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        if (!((w.emit >> (kLook + i)) & 1u)) continue;
+        const uint32_t code = swar_code(w, i, mask);
+        const uint32_t bk = code >> shift, v = code & pmask;
+        if (slot[i] < (uint32_t)kS) {
+          stage[bk * kS + slot[i]] = (uint16_t)v;
         } else {
-          br[i] = (bk << 16) | slot;
+          br[i] = (bk << 16) | slot[i];
           pay[i >> 1] = (i & 1) ? ((pay[i >> 1] & 0xffffu) | (v << 16)) : ((pay[i >> 1] & 0xffff0000u) | v);
         }
-      };
-      if (st) lane_kmers<true>(x, p0, total, base, bmask, k, mask, take);
-      else lane_kmers<false>(x, p0, total, base, bmask, k, mask, take);
-    }
-    __syncthreads();
-    // whole stage pieces out; the next sub-tile's state
-    uint32_t *fl2 = fill[ph ^ 1], *cu2 = cur[ph ^ 1];
-    for (int i = threadIdx.x; i < nb; i += kT) {
-      const uint32_t f = fl[i], c = cu[i];
-      if (f >= (uint32_t)kS) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(stage + i * kS);
-        uint4 *dst = reinterpret_cast<uint4 *>(part + c);
-#pragma unroll
-        for (int v = 0; v < kV; ++v) dst[v] = src[v];
-        const uint32_t F = f / kS * kS;
-        fl2[i] = f - F;
-        cu2[i] = c + F;
-      } else {
-        fl2[i] = f;
-        cu2[i] = c;
       }
     }
+    __syncthreads();
+    // whole stage pieces out; the next sub-tile's state (a thread per fill
+    // word: its two buckets)
+    uint32_t *fl2 = fill[ph ^ 1], *cu2 = cur[ph ^ 1];
+    for (int wd = threadIdx.x; wd < nb / 2; wd += kT) {
+      const uint32_t fw = fl[wd];
+      uint32_t nf = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int i = 2 * wd + h;
+        const uint32_t f = (fw >> (16 * h)) & 0xffffu, c = cu[i];
+        uint32_t F = 0;
+        if (f >= (uint32_t)kS) {
+          const uint4 *src = reinterpret_cast<const uint4 *>(stage + i * kS);
+          uint4 *dst = reinterpret_cast<uint4 *>(part + c);
+#pragma unroll
+          for (int v = 0; v < kV; ++v) dst[v] = src[v];
+          F = f / kS * kS;
+        }
+        nf |= (f - F) << (16 * h);
+        cu2[i] = c + F;
+      }
+      fl2[wd] = nf;
+    }
+    if (threadIdx.x < kSpare / 2) fl2[(1 << kT1) / 2 + threadIdx.x] = 0;
     __syncthreads();
     // register slots: below the last whole piece straight out, the rest staged
 #pragma unroll
     for (int j = 0; j < kPer; ++j)
       if (br[j] != ~0u) {
         const uint32_t bk = br[j] >> 16, slot = br[j] & 0xffffu;
-        const uint32_t F = fl[bk] / kS * kS;
+        const uint32_t F = fill_get(fl, bk) / kS * kS;
         const uint16_t v = (uint16_t)(pay[j >> 1] >> (16 * (j & 1)));
         if (slot < F) part[cu[bk] + slot] = v;
         else stage[bk * kS + slot - F] = v;
@@ -570,7 +588,7 @@ __global__ void __launch_bounds__(kT) k_part_scatter_st(const uint8_t *__restric
   __syncthreads();
   // the block's remainders, padded to a whole piece
   for (int i = threadIdx.x; i < nb; i += kT) {
-    const uint32_t f = fill[ph][i];
+    const uint32_t f = fill_get(fill[ph], i);
     if (f == 0) continue;
     uint4 *dst = reinterpret_cast<uint4 *>(part + cur[ph][i]);
     for (int v = 0; v < kV; ++v) {
@@ -1006,10 +1024,10 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   unsigned long long *s1 = ex2 + m2;            // [nb1 + 1]
   unsigned long long *sf = s1 + nb1 + 1;        // [nbf + 1]
   unsigned long long *last = sf + nbf + 1;      // [2]: level ends; [2]: the k-mer total
-  // single level: the staged scatter, 16-item pieces x 1024 lanes (A/Bs in
-  // the counting-sort scatter below, 512-lane staging; 32-item
-  // pieces do not fit the LDS next to the double-buffered bucket state)
-  const int stS = 16, stT = kPT;
+  // single level: the staged scatter, 32-item (64-B) pieces x 1024 lanes
+  // (A/Bs in DESIGN.md: the counting-sort scatter below, 512-lane staging,
+  // 8- and 16-item pieces; KS_SCATTER_S=16 selects the round-5 16-item pieces)
+  const int stS = (getenv("KS_SCATTER_S") && atoi(getenv("KS_SCATTER_S")) == 16) ? 16 : 32;
   const int64_t n_items = total - p_lo;
   const bool staged = !g.T2 && stS > 0 && n_items + (int64_t)m1 * stS < ((int64_t)1 << 32);
   const int pad = staged ? stS : 1;
@@ -1044,8 +1062,8 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
     hipLaunchKernelGGL((k_part_scatter_st<S, T>), dim3(G), dim3(T), lds, st, s->seq, total, s->offsets_dev, s->nseq, \
                        k, shift, ex1, static_cast<uint16_t *>(p1), tile0, ntiles);                           \
   } while (0)
-    static_assert(stT == kPT, "the staged scatter runs on 1024-lane blocks");
-    KS_ST(16, kPT);
+    if (stS == 16) KS_ST(16, kPT);
+    else KS_ST(32, kPT);
 #undef KS_ST
   } else {
     // single level (k <= 13) past the staged scatter's index range: 512-lane

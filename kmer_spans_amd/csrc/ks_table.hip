@@ -470,23 +470,46 @@ __global__ void k_iota(uint32_t *__restrict__ x, int64_t n) {
 // Approximate prefix table (the binade predictor of the chunked scan): for
 // each kp-base prefix p, the mean of s over the 4^(k-kp) k-mers extending it,
 // weighted by their position frequency (the counts hint; 1 without one).
-// Non-finite values and zero weights are left out.
-__global__ void k_build_approx(const uint16_t *__restrict__ codes, const double *__restrict__ lut,
-                               const double *__restrict__ vals, const int32_t *__restrict__ freq, int k, int kp,
-                               uint16_t *__restrict__ out) {
+// Non-finite values and zero weights are left out.  A wave per prefix when
+// it has >= 64 k-mers (coalesced reads, one wave reduction; round 6:
+// the lane-per-prefix walk took 1.6 ms at k = 13 -- 16 K lanes each reading
+// 4,096 entries 8 KiB apart -- and sat in every table build), else a lane.
+__device__ __forceinline__ void approx_acc(const uint16_t *__restrict__ codes, const double *__restrict__ lut,
+                                           const double *__restrict__ vals, const int32_t *__restrict__ freq,
+                                           int64_t i, double &num, double &den) {
+  const double v = codes ? lut[codes[i]] : vals[i];
+  const double wt = freq ? (double)(uint32_t)freq[i] : 1.0;
+  if (wt > 0 && isfinite(v)) {
+    num += wt * v;
+    den += wt;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_build_approx(const uint16_t *__restrict__ codes, const double *__restrict__ lut,
+                                                      const double *__restrict__ vals, const int32_t *__restrict__ freq,
+                                                      int k, int kp, uint16_t *__restrict__ out) {
   const int64_t np = (int64_t)1 << (2 * kp);
   const int sub = 2 * (k - kp);
+  if (sub >= 6) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t p = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); p < np; p += nw) {
+      double num = 0.0, den = 0.0;
+      const int64_t b = p << sub, e = (p + 1) << sub;
+      for (int64_t i = b + lane; i < e; i += 64) approx_acc(codes, lut, vals, freq, i, num, den);
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        num += __shfl_xor(num, d, 64);
+        den += __shfl_xor(den, d, 64);
+      }
+      if (lane == 0) out[p] = __half_as_ushort(__float2half(den > 0 ? (float)(num / den) : 0.0f));
+    }
+    return;
+  }
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np; p += (int64_t)gridDim.x * blockDim.x) {
     double num = 0.0, den = 0.0;
     const int64_t b = p << sub, e = (p + 1) << sub;
-    for (int64_t i = b; i < e; ++i) {
-      const double v = codes ? lut[codes[i]] : vals[i];
-      const double wt = freq ? (double)(uint32_t)freq[i] : 1.0;
-      if (wt > 0 && isfinite(v)) {
-        num += wt * v;
-        den += wt;
-      }
-    }
+    for (int64_t i = b; i < e; ++i) approx_acc(codes, lut, vals, freq, i, num, den);
     out[p] = __half_as_ushort(__float2half(den > 0 ? (float)(num / den) : 0.0f));
   }
 }
@@ -720,7 +743,9 @@ static ks_status build_approx(ks_ctx *ctx, ks_table *t, const int32_t *freq_dev)
   }
   debug_poison(t->d_approx, ((size_t)2 << (2 * kp)) + 16);
   t->approx_k = kp;
-  hipLaunchKernelGGL(k_build_approx, dim3((unsigned)std::min<int64_t>(((int64_t)1 << (2 * kp)) / 256 + 1, 4096)),
+  const int64_t np = (int64_t)1 << (2 * kp);
+  const int64_t per_block = 2 * (t->k - kp) >= 6 ? 4 : 256;  // (a wave per prefix, else a lane)
+  hipLaunchKernelGGL(k_build_approx, dim3((unsigned)std::min<int64_t>((np + per_block - 1) / per_block, 4096)),
                      dim3(256), 0, ctx->stream, t->d_codes, t->d_lut, t->d_vals, freq_dev, t->k, kp, t->d_approx);
   KS_HIP(hipGetLastError());
   return KS_OK;

@@ -1044,8 +1044,14 @@ def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over
     def one(ds):
         counts.zero_()
         words = D.count(ctx, ds, k, counts)
-        _, _, table, init, _ = make_table(counts, words, args.score,
-                                          ext_gib=args.ext_max_gib if args.ext_max_gib else 32.0, warm=False)
+        if args.trlr:  # (tr_lr needs the weights for its init table)
+            _, _, table, init, _ = make_table(counts, words, args.score,
+                                              ext_gib=args.ext_max_gib if args.ext_max_gib else 32.0, warm=False)
+        else:  # the table alone: the weights of the parity leg are rebuilt after timing
+            init = None
+            table = D.DeviceTable.from_counts(ctx, counts, k, args.score, total=words,
+                                              thr=0.75 if args.score == "rank" else 0.0, expand=not args.no_expand,
+                                              max_ext_bytes=int((args.ext_max_gib or 32.0) * (1 << 30)))
         if args.trlr:
             out = D.tr_lr(ctx, ds, k, table, init, args.min_width)
         else:

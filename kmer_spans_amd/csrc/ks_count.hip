@@ -453,13 +453,12 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
 // Single-level scatter through a per-bucket LDS stage of kS items: every
 // (bucket, block) region is a multiple of kS items (k_part with pad = kS)
 // starting 2*kS-byte aligned, and is written only in whole aligned pieces of
-// kS items, so each HBM write request carries 2*kS bytes.  The scatter is
-// bound by its write requests, ~28 G/s for these scattered pieces (round 6:
-// 16-B pieces 14.0 ms, 32-B pieces 6.9 ms, at the metric genome's 6.2 GB of
-// items; the counting-sort scatter below writes ~4 items per bucket and
-// sub-tile: 27.5 GB of partial writes), so the pieces are 64 B: 2,048 x 32
-// items of stage fill 128 KiB of the 160 KiB LDS, and the per-bucket fill
-// counters are 16-bit halves of words (a sub-tile adds at most 16 K items).
+// kS items, so each HBM write request carries 2*kS bytes (round 6 at the
+// metric genome's 6.2 GB of items: 16-B pieces 14.0 ms, 32-B 6.9 ms, 64-B
+// no faster -- 2,048 x 32 items of stage fill 128 KiB of the 160 KiB LDS;
+// the counting-sort scatter below writes ~4 items per bucket and sub-tile:
+// 27.5 GB of partial writes).  The per-bucket fill counters are 16-bit halves
+// of words (a sub-tile adds at most 16 K items).
 // Per sub-tile: a k-mer takes slot = fill[bucket]++ (LDS atomic); slots < kS
 // go to the stage, the rest stay in registers; buckets that reach kS flush
 // the stage's piece (16-B stores), the registers' slots below the last whole
@@ -1024,10 +1023,11 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   unsigned long long *s1 = ex2 + m2;            // [nb1 + 1]
   unsigned long long *sf = s1 + nb1 + 1;        // [nbf + 1]
   unsigned long long *last = sf + nbf + 1;      // [2]: level ends; [2]: the k-mer total
-  // single level: the staged scatter, 32-item (64-B) pieces x 1024 lanes
-  // (A/Bs in DESIGN.md: the counting-sort scatter below, 512-lane staging,
-  // 8- and 16-item pieces; KS_SCATTER_S=16 selects the round-5 16-item pieces)
-  const int stS = (getenv("KS_SCATTER_S") && atoi(getenv("KS_SCATTER_S")) == 16) ? 16 : 32;
+  // single level: the staged scatter, 16-item (32-B) pieces x 1024 lanes
+  // (A/Bs in DESIGN.md: the counting-sort scatter below, 512-lane staging;
+  // 8-item pieces 14.0 vs 9.9 ms, 32-item pieces 10.67 vs 10.51 ms per count,
+  // profiles/r6/count/)
+  const int stS = 16;
   const int64_t n_items = total - p_lo;
   const bool staged = !g.T2 && stS > 0 && n_items + (int64_t)m1 * stS < ((int64_t)1 << 32);
   const int pad = staged ? stS : 1;
@@ -1062,8 +1062,7 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
     hipLaunchKernelGGL((k_part_scatter_st<S, T>), dim3(G), dim3(T), lds, st, s->seq, total, s->offsets_dev, s->nseq, \
                        k, shift, ex1, static_cast<uint16_t *>(p1), tile0, ntiles);                           \
   } while (0)
-    if (stS == 16) KS_ST(16, kPT);
-    else KS_ST(32, kPT);
+    KS_ST(16, kPT);
 #undef KS_ST
   } else {
     // single level (k <= 13) past the staged scatter's index range: 512-lane

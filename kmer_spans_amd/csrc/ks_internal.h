@@ -127,6 +127,7 @@ struct ks_table {
   int k = 0;
   double thr = 0;
   bool compressed = false;
+  bool codes_pooled = false;  // d_codes came from / goes back to the per-device code-array pool
   int64_t distinct = 0;
   double *d_vals = nullptr;     // full table s = w - thr (uncompressed), 4^k doubles
   uint16_t *d_codes = nullptr;  // compressed: 4^k u16 codes

@@ -55,6 +55,22 @@ __global__ void k_absmax(const double *__restrict__ s, int64_t n, unsigned long 
   }
 }
 
+// OR of all counts (as uint32): its highest set bit bounds the key bits the
+// count sort must order (a wrapped, negative count sets bit 31: all 32 bits)
+__global__ void k_count_or(const int32_t *__restrict__ c, int64_t n, unsigned int *__restrict__ out) {
+  unsigned int m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m |= (unsigned int)c[i];
+  for (int d = 32; d >= 1; d >>= 1) m |= __shfl_down(m, d, 64);
+  __shared__ unsigned int wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // (one atomic per block: a wave each serialised 16 K of them on one address, 0.2 ms)
+    const unsigned int b = wm[0] | wm[1] | wm[2] | wm[3];
+    if (b) atomicOr(out, b);
+  }
+}
+
 __global__ void k_assign_codes(const double *__restrict__ s, const unsigned long long *__restrict__ uniq,
                                int64_t nu, uint16_t *__restrict__ codes, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -541,11 +557,14 @@ bool pool_on() {
   return on;
 }
 size_t pool_bytes(int dev) { return g_pool[dev][0].bytes + g_pool[dev][1].bytes; }  // (under g_pool_mu)
+PoolBuf g_cpool[64];  // (cpool_take / cpool_give below)
 void pool_free_all(int dev) {  // (under g_pool_mu)
   for (PoolBuf &b : g_pool[dev]) {
     if (b.p) (void)hipFree(b.p);
     b = PoolBuf();
   }
+  if (g_cpool[dev].p) (void)hipFree(g_cpool[dev].p);
+  g_cpool[dev] = PoolBuf();
 }
 void *pool_take(int dev, size_t bytes, size_t *cap) {
   if (!pool_on() || dev < 0 || dev >= 64) return nullptr;
@@ -585,6 +604,33 @@ void pool_give(int dev, void *p, size_t bytes) {
         std::swap(small->bytes, bytes);
       }
     }
+  }
+  if (p) (void)hipFree(p);
+}
+// One kept uint16 code array per device (4^k x 2 B: 128 MiB at k = 13): a
+// table built per genome (config 5) otherwise pays a fresh hipMalloc of it
+// (~0.4 ms) on every build.  Given back by ks_table_destroy after the device
+// synchronisation pool_give already does for the expanded table.
+void *cpool_take(int dev, size_t bytes) {
+  if (!pool_on() || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  PoolBuf &b = g_cpool[dev];
+  if (!b.p || b.bytes != bytes) return nullptr;
+  void *p = b.p;
+  b = PoolBuf();
+  return p;
+}
+void cpool_give(int dev, void *p, size_t bytes) {
+  if (!p) return;
+  if (pool_on() && dev >= 0 && dev < 64) {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(dev);
+    (void)hipDeviceSynchronize();
+    if (cur >= 0) (void)hipSetDevice(cur);
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    std::swap(g_cpool[dev].p, p);
+    std::swap(g_cpool[dev].bytes, bytes);
   }
   if (p) (void)hipFree(p);
 }
@@ -1194,10 +1240,24 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
     hipLaunchKernelGGL(k_iota, dim3(grid), dim3(256), 0, st, d_idx_in, n);
     KS_TFC(hipGetLastError());
   }
+  // the sort orders only the bits some count uses (metric genome: < 2^24, three
+  // 8-bit passes instead of four); a negative (wrapped) count keeps all 32
+  int end_bit = 32;
+  {
+    unsigned int *d_or = reinterpret_cast<unsigned int *>(d_nu) + 4, h_or = 0;
+    KS_TFC(hipMemsetAsync(d_or, 0, 4, st));
+    hipLaunchKernelGGL(k_count_or, dim3((unsigned)std::min<int64_t>((n + 4095) / 4096, 1024)), dim3(256), 0, st,
+                       counts_dev, n, d_or);
+    KS_TFC(hipGetLastError());
+    KS_TFC(hipMemcpyAsync(&h_or, d_or, 4, hipMemcpyDeviceToHost, st));
+    KS_TFC(hipStreamSynchronize(st));
+    end_bit = 1;
+    while (end_bit < 32 && (h_or >> end_bit) != 0) ++end_bit;
+  }
   if (rank)
-    KS_TFC(hipcub::DeviceRadixSort::SortPairs(d_tmp, b1, counts_dev, d_keys, d_idx_in, d_idx, (int)n, 0, 32, st));
+    KS_TFC(hipcub::DeviceRadixSort::SortPairs(d_tmp, b1, counts_dev, d_keys, d_idx_in, d_idx, (int)n, 0, end_bit, st));
   else
-    KS_TFC(hipcub::DeviceRadixSort::SortKeys(d_tmp, b1, counts_dev, d_keys, (int)n, 0, 32, st));
+    KS_TFC(hipcub::DeviceRadixSort::SortKeys(d_tmp, b1, counts_dev, d_keys, (int)n, 0, end_bit, st));
   KS_TFC(hipcub::DeviceRunLengthEncode::Encode(d_tmp, b2, d_keys, d_uniq, d_mult, d_nu, (int)n, st));
   int nu = 0;
   KS_TFC(hipMemcpyAsync(&nu, d_nu, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1386,7 +1446,9 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
         ks_table_destroy(t);
         return fail(KS_ERR_NOMEM, "ks_table_from_counts: device allocation failed");
       }
-      KS_TFC(hipMalloc(&t->d_codes, n * sizeof(uint16_t)));
+      t->d_codes = static_cast<uint16_t *>(cpool_take(ctx->device, n * sizeof(uint16_t)));
+      t->codes_pooled = true;
+      if (!t->d_codes) KS_TFC(hipMalloc(&t->d_codes, n * sizeof(uint16_t)));
       KS_TFC(hipMalloc(&t->d_lut, nv * sizeof(double)));
       KS_TFC(hipMemcpyAsync(t->d_lut, ub.data(), nv * 8, hipMemcpyHostToDevice, st));
       KS_TFC(hipMemcpyAsync(d_cmap, cmap.data(), (size_t)nu * 2, hipMemcpyHostToDevice, st));
@@ -1449,7 +1511,8 @@ extern "C" void ks_table_destroy(ks_table *t) {
     return;
   }
   if (t->d_vals) (void)hipFree(t->d_vals);
-  if (t->d_codes) (void)hipFree(t->d_codes);
+  if (t->d_codes && t->codes_pooled) cpool_give(t->device, t->d_codes, ((size_t)2) << (2 * t->k));
+  else if (t->d_codes) (void)hipFree(t->d_codes);
   if (t->d_lut) (void)hipFree(t->d_lut);
   if (t->d_ext) pool_give(t->device, t->d_ext, t->ext_cap);
   if (t->d_map12) (void)hipFree(t->d_map12);

@@ -61,11 +61,13 @@ bool hip_usable_here() { return g_hip_pid == 0 || g_hip_pid == getpid(); }
 bool use_broker() { return broker_wanted(g_hip_pid); }
 
 
-// Region output blocks carry their capacity in a 64-B header.  The last two
-// freed blocks of >= 1 MiB are kept and handed to the next allocation they
-// fit (up to 4x its size): a fresh block of tens of MB pays its page faults
-// in the host copy-out (config 3: 1.09 M regions, 30 MB, ~1.5 ms per call);
-// ks_release_cache frees them.
+// Region output blocks carry their capacity (and whether they are pinned) in
+// a 64-B header.  The last two freed blocks of >= 1 MiB are kept and handed
+// to the next allocation they fit (up to 4x its size): a fresh block of tens
+// of MB pays its page faults in the host copy-out (config 3: 1.09 M regions,
+// 30 MB, ~1.5 ms per call); ks_release_cache frees them.  A kept block the
+// scan pinned (regions_pin) stays pinned, so the regions land in it by DMA
+// with no staging copy (round 6: the 30 MB host copy of config 3).
 namespace {
 constexpr size_t kBlkHdr = 64;
 std::mutex g_blk_mu;
@@ -74,14 +76,34 @@ struct FreeBlk {
   size_t cap = 0;
 };
 FreeBlk g_blk[2];
+size_t &blk_cap(char *base) { return *reinterpret_cast<size_t *>(base); }
+size_t &blk_pinned(char *base) { return *reinterpret_cast<size_t *>(base + 8); }
+void blk_free(char *base) {
+  if (!base) return;
+  if (blk_pinned(base) && hip_usable_here()) (void)hipHostUnregister(base);
+  free(base);
+}
 }  // namespace
 
 void regions_cache_release() {
   std::lock_guard<std::mutex> g(g_blk_mu);
   for (FreeBlk &b : g_blk) {
-    free(b.base);
+    blk_free(b.base);
     b = FreeBlk();
   }
+}
+
+bool regions_pin(ks_regions *out) {
+  if (!out || !out->seq_id) return false;
+  char *base = reinterpret_cast<char *>(out->seq_id) - kBlkHdr;
+  if (blk_pinned(base)) return true;
+  if (blk_cap(base) < ((size_t)1 << 20)) return false;
+  if (hipHostRegister(base, kBlkHdr + blk_cap(base), hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  blk_pinned(base) = 1;
+  return true;
 }
 
 ks_status regions_alloc(ks_regions *out, int64_t n) {
@@ -104,7 +126,8 @@ ks_status regions_alloc(ks_regions *out, int64_t n) {
       memset(out, 0, sizeof(*out));
       return fail(KS_ERR_NOMEM, "out of host memory for %lld regions", (long long)n);
     }
-    *reinterpret_cast<size_t *>(base) = need;
+    blk_cap(base) = need;
+    blk_pinned(base) = 0;
   }
   char *blk = base + kBlkHdr;
   out->n = n;
@@ -285,15 +308,15 @@ extern "C" void ks_regions_free(ks_regions *r) {
   if (!r) return;
   if (r->seq_id) {  // one block holds all four arrays (regions_alloc)
     char *base = reinterpret_cast<char *>(r->seq_id) - kBlkHdr;
-    const size_t cap = *reinterpret_cast<size_t *>(base);
+    const size_t cap = blk_cap(base);
     if (cap >= ((size_t)1 << 20)) {  // keep it for the next call (the smaller of the two kept goes)
       std::lock_guard<std::mutex> g(g_blk_mu);
       FreeBlk &v = !g_blk[0].base ? g_blk[0] : !g_blk[1].base ? g_blk[1] : (g_blk[0].cap <= g_blk[1].cap ? g_blk[0] : g_blk[1]);
-      free(v.base);
+      blk_free(v.base);
       v.base = base;
       v.cap = cap;
     } else {
-      free(base);
+      blk_free(base);
     }
   }
   memset(r, 0, sizeof(*r));

@@ -279,6 +279,9 @@ bool hip_usable_here();  // false in a child forked after HIP was initialised
 // Region output block (ks_regions_free frees it): [seq_id | beg | end] int32,
 // then [score | 0.0] doubles.
 ks_status regions_alloc(ks_regions *out, int64_t n);
+// Pins out's block for direct D2H copies (hipHostRegister, once per kept
+// block); false when it cannot (small block, registration refused).
+bool regions_pin(ks_regions *out);
 void regions_cache_release();  // the kept output blocks (ks_release_cache)
 struct Staged;
 // Host entry bodies on one context, arguments validated (ks_abi.cpp); the

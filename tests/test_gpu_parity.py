@@ -681,3 +681,34 @@ def test_host_entry_memory_policy(K, oracle):
     for r in res:
         _assert_same_regions(r["pos"], r["score"], o["pos"], o["score"], "host cache policy")
         assert np.array_equal(r["counts"], o["counts"])
+
+
+def test_many_regions_pinned_output_block(oracle, ctx):
+    """A scan with > 100 K regions: the output block (>= 1 MiB) is kept and
+    pinned by the library, and the regions are copied into it by DMA with no
+    staging copy (ks_abi.cpp regions_pin, ks_scan.hip).  Three calls: the
+    first pins a fresh block, the second reuses the kept pinned block, the
+    third follows ks_release_cache (a fresh block again); every result equal
+    to the oracle bit for bit, and equal to each other."""
+    import torch
+    from kmer_spans_amd import _lib, device as D, genome
+    D.bind_torch_stream(ctx)
+    k = 9
+    s = genome.contig(12_000_000, 77, device="cuda", repeats=True)
+    ds = D.from_parts([s], [s.numel()], "cuda")
+    host = [ds.host_seq(0)]
+    rng = np.random.default_rng(5)
+    w = rng.normal(0.0, 1.0, 4 ** k)  # low thresholds below: many short regions
+    o = oracle.scan(host, k, w, 0.0, 3, 1.0)
+    assert o["pos"].shape[1] > 100_000, o["pos"].shape
+    tab = D.DeviceTable(ctx, w, k, 0.0, compress=False, expand=True)
+    try:
+        for call in range(3):
+            if call == 2:
+                _lib.load().ks_release_cache()
+            pos, sc, _ = D.scan(ctx, ds, k, tab, 3, 1.0)
+            _assert_same_regions(pos, sc, o["pos"], o["score"], f"many regions, call {call}")
+            assert np.all(sc[1] == 0.0)
+            del pos, sc  # (the block goes back to the library's keep list)
+    finally:
+        tab.close()

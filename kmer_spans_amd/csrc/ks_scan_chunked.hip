@@ -407,6 +407,49 @@ __device__ __forceinline__ void values16_f64(const Chunks &g, const uint8_t *__r
   }
 }
 
+// The values4 of a replay from an FP64 64-B line table with own = 3 (weighted
+// rank, k = 13: one line per lane, its three own entries and the L1 entry of
+// the next base), fetched by the whole wave together: lanes 4m .. 4m + 3 load
+// the four 16-B pieces of line 16 r + m (r = 0 .. 3), so each line costs one
+// coalesced 64-B request instead of three divergent loads of one lane
+// (round 6: half of the weighted-rank rescans' time was those loads,
+// DESIGN.md section 10), by LDS-DMA into 4 KiB of LDS per wave.  Every lane of the
+// wave calls it (uniform), each with its packed bases x of index i0's k-mer.
+__device__ __forceinline__ void values4_coop_f64(const TableView &tv, uint64_t x, int k, int i0, int n,
+                                                 double v[4], uint4 *__restrict__ s_piece,
+                                                 unsigned long long *__restrict__ s_key) {
+  const int lane = threadIdx.x & 63;
+  const int kx = k + 3;
+  const uint64_t key = (x >> (64 - 2 * kx)) & ((1ull << (2 * kx)) - 1ull);
+  const bool valid = i0 < n;
+  s_key[lane] = valid ? (unsigned long long)(key >> 2) : ~0ull;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  // LDS-DMA (global_load_lds_dwordx4): lane l's piece lands at s_piece[64 r + l] = piece l & 3 of
+  // line 16 r + (l >> 2), no VGPRs on the way (the FP64 carry holds 168); a lane without a line
+  // reads line 0 into a slot nobody reads
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const unsigned long long ln = s_key[16 * r + (lane >> 2)];
+    const uint8_t *src = tv.line + (ln != ~0ull ? (size_t)ln * 64 : (size_t)0) + 16 * (lane & 3);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                     (__attribute__((address_space(3))) void *)(s_piece + 64 * r), 16, 0, 0);
+  }
+  // the DMA writes must have landed before any lane reads them: an explicit
+  // vmcnt(0) lgkmcnt(0) (hipcc placed its own wait only before the
+  // conditional reads below, not before the hoisted L1 one)
+  __builtin_amdgcn_s_waitcnt(0x0070);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const double *L = reinterpret_cast<const double *>(s_piece + 4 * lane);
+  const double l1 = L[3 + (int)(key & 3u)];
+  v[0] = valid ? L[0] : 0.0;
+  v[1] = i0 + 1 < n ? L[1] : 0.0;
+  v[2] = i0 + 2 < n ? L[2] : 0.0;
+  v[3] = i0 + 3 < n ? l1 : 0.0;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // (the next call's writes after these reads)
+}
+
 // Values of scan indices i0 .. i0+3 of chunk c (0 past n): one 8-byte code
 // load (compressed) or one k-mer prime plus three rolls.  start: the chunk's
 // first scan index (g.start[c]), loaded by the caller ahead of time; xin
@@ -3021,6 +3064,9 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
                                               unsigned int *__restrict__ err, long long *__restrict__ dbg,
                                               int64_t r) {
   const int lane = threadIdx.x & 63;
+  // (the cooperative FP64 line fetch of the replays, values4_coop_f64: a wave's slice)
+  __shared__ uint4 s_coop[4][256];
+  __shared__ unsigned long long s_ckey[4][64];
   double x = (c0 > 0 && g.run[c0] == g.run[c0 - 1]) ? o.cexit[c0 - 1] : 0.0;
   unsigned long long replays = 0;
   const long long t_start = dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
@@ -3260,8 +3306,17 @@ __device__ __forceinline__ void carry_segment(const Chunks &g, int64_t c0, int64
         } else {
           const bool hx = !kCompressed && pf_c == cj && pf_ok;
           if (dbg && hx) n_par += 1LL << 32;  // (diagnostics: replays with their bases prefetched)
-          values4(g, seq, total, k, tv, kCompressed ? codes : nullptr, cj, rl64(cur.start, j), 4 * lane, n, v, hx,
-                  pf_x);
+          uint64_t xq = pf_x;
+          // (in-process at config 3: 24.63 vs 25.00 ms min, carry 4.83 vs 5.18 ms,
+          // profiles/r6/rank/ab_carry_coop.txt)
+          const bool coop = !kCompressed && tv.line && tv.line_kind == 2 && tv.line_own == 3 &&
+                            __ballot(!(hx || packed_bits(g.packed, total, rl64(cur.start, j) + 4 * lane - k, xq))) == 0;
+          if (coop) {
+            values4_coop_f64(tv, xq, k, 4 * lane, n, v, s_coop[threadIdx.x >> 6], s_ckey[threadIdx.x >> 6]);
+          } else {
+            values4(g, seq, total, k, tv, kCompressed ? codes : nullptr, cj, rl64(cur.start, j), 4 * lane, n, v, hx,
+                    pf_x);
+          }
         }
         if (!kCompressed && cj + 1 < c1) {  // the next chunk's packed bases, under this replay's reads
           const int64_t stn = (j + 1 < nb) ? rl64(cur.start, j + 1) : rl64(nxt.start, 0);

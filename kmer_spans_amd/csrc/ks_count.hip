@@ -304,6 +304,17 @@ __device__ __forceinline__ void lane_load(const uint8_t *__restrict__ seq, int64
   }
 }
 
+// The same, always two loads (from the sequence's first bytes when the
+// window is not in bounds): a loop that issues it has a fixed number of
+// memory instructions per iteration.
+__device__ __forceinline__ void lane_load_all(const uint8_t *__restrict__ seq, int64_t total, int64_t p0,
+                                              LaneWin &w) {
+  w.fast = p0 >= kLook && p0 + kPer <= total;
+  const uint8_t *p = w.fast ? seq + p0 - kLook : seq;
+  w.a = *reinterpret_cast<const uint4 *>(p);
+  w.b = *reinterpret_cast<const uint4 *>(p + kLook);
+}
+
 // The lane's 32 bytes as 8 little-endian words (byte j = bits 8(j%4) of word j/4).
 __device__ __forceinline__ void lane_bytes(const uint8_t *__restrict__ seq, int64_t total, int64_t p0,
                                            const LaneWin &w, uint32_t (&x)[8]) {
@@ -388,14 +399,23 @@ __device__ __forceinline__ void starts_mark(const int64_t *__restrict__ offs, in
   __syncthreads();
 }
 
+// Grouped region layout of the staged scatter: blocks in groups of gs, each
+// group's regions bucket-major ([bucket][block of the group]).  A group spans
+// under 2 GiB (a buffer-store window from its first region); a bucket is one
+// contiguous segment per group.
+__host__ __device__ __forceinline__ size_t grp_index(int blk, int b, int nb, int G, int gs) {
+  const int g0 = blk / gs * gs, gsz = min(gs, G - g0);
+  return (size_t)g0 * nb + (size_t)b * gsz + (blk - g0);
+}
+
 // Level 1 over the sequence: per block, the LDS histogram of the buckets
 // (code >> shift, shift = 2k - T1) of the k-mers in its tiles, each count
 // rounded up to a multiple of pad (the staged scatter writes whole pieces of
-// pad items), into mat[bucket][block]; the unrounded total is added to
-// *words.
+// pad items), into mat[bucket][block] (gs > 0: the grouped layout of
+// grp_index); the unrounded total is added to *words.
 __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, int64_t total,
                                               const int64_t *__restrict__ offs, int32_t nseq, int k, int shift,
-                                              unsigned long long *__restrict__ mat, int pad,
+                                              unsigned long long *__restrict__ mat, int pad, int gs,
                                               unsigned long long *__restrict__ words, int64_t tile0, int64_t ntiles) {
   constexpr int kWords = (kPTile + kLook + 32) / 32 + 1;
   __shared__ uint32_t lds_b[(1 << kT1) + kSpare];
@@ -438,7 +458,8 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
   for (int i = threadIdx.x; i < nb; i += kPT) {
     const uint32_t c = lds_b[i];
     t += c;
-    mat[(size_t)i * G + blockIdx.x] = (c + (uint32_t)pad - 1u) / (uint32_t)pad * (uint32_t)pad;
+    mat[gs ? grp_index(blockIdx.x, i, nb, G, gs) : (size_t)i * G + blockIdx.x] =
+        (c + (uint32_t)pad - 1u) / (uint32_t)pad * (uint32_t)pad;
   }
   for (int d = 32; d >= 1; d >>= 1) t += __shfl_down(t, d, 64);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
@@ -451,7 +472,8 @@ __global__ void __launch_bounds__(kPT) k_part(const uint8_t *__restrict__ seq, i
 }
 
 // Single-level scatter through a per-bucket LDS stage of kS items: every
-// (bucket, block) region is a multiple of kS items (k_part with pad = kS)
+// (block, bucket) region is a multiple of kS items (k_part with pad = kS,
+// grouped: grp_index)
 // starting 2*kS-byte aligned, and is written only in whole aligned pieces of
 // kS items, so each HBM write request carries 2*kS bytes (round 6 at the
 // metric genome's 6.2 GB of items: 16-B pieces 14.0 ms, 32-B 6.9 ms, 64-B
@@ -476,21 +498,29 @@ template <int kS, int kT>
 __global__ void __launch_bounds__(kT) k_part_scatter_st(const uint8_t *__restrict__ seq, int64_t total,
                                                          const int64_t *__restrict__ offs, int32_t nseq, int k,
                                                          int shift, const unsigned long long *__restrict__ ex,
-                                                         uint16_t *__restrict__ part, int64_t tile0, int64_t ntiles) {
+                                                         int gs, uint16_t *__restrict__ part, int64_t tile0,
+                                                         int64_t ntiles) {
   constexpr int kTile = kT * kPer;  // positions per sub-tile
   constexpr int kSub = kPTile / kTile;
   constexpr int kV = kS / 8;        // 16-B vectors per piece
   constexpr int kWords = (kTile + kLook + 32) / 32 + 1;
   constexpr int kFW = ((1 << kT1) + kSpare) / 2;  // fill words (two 16-bit counters each)
+  constexpr uint32_t kDrop = 0x80000000u;         // a store offset past the window: the store is dropped
   static_assert(kPTile % kTile == 0 && kS % 8 == 0 && kTile + kS < 65536, "sub-tiles, pieces, 16-bit fills");
+  static_assert(kT >= (1 << kT1) / 2, "one thread per fill word");
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
   uint16_t *stage = reinterpret_cast<uint16_t *>(dyn);  // [nb][kS]
   __shared__ uint32_t fill[2][kFW], cur[2][1 << kT1];
   __shared__ uint32_t bmask[kWords];
   const int nb = 1 << (2 * k - shift);  // (even: k >= kPartMinK)
   const int G = gridDim.x;
+  // the block's group's regions lie in one window of under 2 GiB from the
+  // group's first region on; cursors are item offsets in the window
+  const unsigned long long wbase = ex[(size_t)(blockIdx.x / gs * gs) * nb];
+  const __amdgpu_buffer_rsrc_t win_rs = __builtin_amdgcn_make_buffer_rsrc(part + wbase, (short)0, 0x7fffffff, 0x00020000);
   for (int i = threadIdx.x; i < kFW; i += kT) fill[0][i] = fill[1][i] = 0;
-  for (int i = threadIdx.x; i < nb; i += kT) cur[0][i] = (uint32_t)ex[(size_t)i * G + blockIdx.x];
+  for (int i = threadIdx.x; i < nb; i += kT) cur[0][i] = (uint32_t)(ex[grp_index(blockIdx.x, i, nb, G, gs)] - wbase);
   const uint32_t mask = (1u << (2 * k)) - 1u;
   const uint32_t pmask = (1u << shift) - 1u;
   // the positions k_part's block counted: its kPTile-position tiles, each as
@@ -502,22 +532,31 @@ __global__ void __launch_bounds__(kT) k_part_scatter_st(const uint8_t *__restric
   LaneWin win;
   if (nit) {
     starts_init(offs, nseq, sub_t0(0) - kLook, &ci, &nx);
-    lane_load(seq, total, sub_t0(0) + (int64_t)threadIdx.x * kPer, win);
+    lane_load_all(seq, total, sub_t0(0) + (int64_t)threadIdx.x * kPer, win);
+    // (the first window waited for here: the loop's waits then need not
+    // cover loads from before the loop, which would drain its stores)
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
   }
+  // Every iteration issues the same memory instructions -- two window loads,
+  // kV stores per fill-word half, kPer register-slot stores -- with the
+  // stores that have nothing to write dropped by offset, not skipped by a
+  // branch: the wait for the next window then counts past this iteration's
+  // stores instead of draining them (gfx9 counts loads and stores on one
+  // in-order counter).
   int ph = 0;
   for (int64_t it = 0; it < nit; ++it, ph ^= 1) {
     const int64_t t0 = sub_t0(it);
     const int64_t base = t0 - kLook, lim = t0 + kTile;
     const int64_t p0 = t0 + (int64_t)threadIdx.x * kPer;
     LaneWin nxt;
-    if (it + 1 < nit) lane_load(seq, total, sub_t0(it + 1) + (int64_t)threadIdx.x * kPer, nxt);
+    lane_load_all(seq, total, sub_t0(it + 1 < nit ? it + 1 : it) + (int64_t)threadIdx.x * kPer, nxt);
     starts_seek(offs, nseq, base, &ci, &nx);
     const bool st = nx <= lim;  // (uniform over the block)
     __syncthreads();            // this phase's state is complete (init, or the last flush)
     if (st) starts_mark<kWords>(offs, nseq, ci, base, lim, bmask);
     uint32_t *fl = fill[ph], *cu = cur[ph];
     uint32_t br[kPer];    // bucket << 16 | slot of the items left in registers, or ~0u
-    uint32_t pay[kPer / 2];  // their payloads, two per word
+    uint32_t pay[kPer / 2] = {};  // their payloads, two per word
 #pragma unroll
     for (int j = 0; j < kPer; ++j) br[j] = ~0u;
     if (p0 < total) {
@@ -550,46 +589,53 @@ __global__ void __launch_bounds__(kT) k_part_scatter_st(const uint8_t *__restric
     // whole stage pieces out; the next sub-tile's state (a thread per fill
     // word: its two buckets)
     uint32_t *fl2 = fill[ph ^ 1], *cu2 = cur[ph ^ 1];
-    for (int wd = threadIdx.x; wd < nb / 2; wd += kT) {
-      const uint32_t fw = fl[wd];
+    {
+      const int wd = threadIdx.x;
+      const bool own = wd < nb / 2;
+      const uint32_t fw = own ? fl[wd] : 0u;
       uint32_t nf = 0;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int i = 2 * wd + h;
+        const int i = own ? 2 * wd + h : 0;
         const uint32_t f = (fw >> (16 * h)) & 0xffffu, c = cu[i];
-        uint32_t F = 0;
-        if (f >= (uint32_t)kS) {
-          const uint4 *src = reinterpret_cast<const uint4 *>(stage + i * kS);
-          uint4 *dst = reinterpret_cast<uint4 *>(part + c);
+        const uint32_t F = f / kS * kS;
+        const uint4 *src = reinterpret_cast<const uint4 *>(stage + i * kS);
+        const uint32_t off = f >= (uint32_t)kS ? c * 2u : kDrop;
 #pragma unroll
-          for (int v = 0; v < kV; ++v) dst[v] = src[v];
-          F = f / kS * kS;
+        for (int v = 0; v < kV; ++v) {
+          const uint4 y = src[v];
+          const u32x4 yv = {y.x, y.y, y.z, y.w};
+          __builtin_amdgcn_raw_buffer_store_b128(yv, win_rs, off + 16 * v, 0, 0);
         }
         nf |= (f - F) << (16 * h);
-        cu2[i] = c + F;
+        if (own) cu2[i] = c + F;
       }
-      fl2[wd] = nf;
+      if (own) fl2[wd] = nf;
     }
     if (threadIdx.x < kSpare / 2) fl2[(1 << kT1) / 2 + threadIdx.x] = 0;
     __syncthreads();
     // register slots: below the last whole piece straight out, the rest staged
 #pragma unroll
-    for (int j = 0; j < kPer; ++j)
+    for (int j = 0; j < kPer; ++j) {
+      uint32_t off = kDrop;
+      const uint16_t v = (uint16_t)(pay[j >> 1] >> (16 * (j & 1)));
       if (br[j] != ~0u) {
         const uint32_t bk = br[j] >> 16, slot = br[j] & 0xffffu;
         const uint32_t F = fill_get(fl, bk) / kS * kS;
-        const uint16_t v = (uint16_t)(pay[j >> 1] >> (16 * (j & 1)));
-        if (slot < F) part[cu[bk] + slot] = v;
+        if (slot < F) off = (cu[bk] + slot) * 2u;
         else stage[bk * kS + slot - F] = v;
       }
+      __builtin_amdgcn_raw_buffer_store_b16(v, win_rs, off, 0, 0);
+    }
     win = nxt;
   }
   __syncthreads();
   // the block's remainders, padded to a whole piece
+  uint16_t *wpart = part + wbase;
   for (int i = threadIdx.x; i < nb; i += kT) {
     const uint32_t f = fill_get(fill[ph], i);
     if (f == 0) continue;
-    uint4 *dst = reinterpret_cast<uint4 *>(part + cur[ph][i]);
+    uint4 *dst = reinterpret_cast<uint4 *>(wpart + cur[ph][i]);
     for (int v = 0; v < kV; ++v) {
       uint32_t w[4];
 #pragma unroll
@@ -857,6 +903,20 @@ __global__ void k_part_starts(const unsigned long long *__restrict__ ex, int str
   if (i == nb) bstart[nb] = *last;
 }
 
+// Bucket sizes of the grouped layout (grp_index): the sum over groups of
+// the bucket's segment, a thread per bucket.
+__global__ void k_bucket_tot(const unsigned long long *__restrict__ mat, const unsigned long long *__restrict__ ex,
+                             int G, int gs, int nb, unsigned long long *__restrict__ bsize) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  unsigned long long t = 0;
+  for (int g0 = 0; g0 < G; g0 += gs) {
+    const size_t i0 = grp_index(g0, b, nb, G, gs), i1 = i0 + min(gs, G - g0) - 1;
+    t += ex[i1] + mat[i1] - ex[i0];
+  }
+  bsize[b] = t;
+}
+
 // Work list of k_bins (one block, nb <= 4096): the non-empty buckets in
 // descending size (bitonic sort of (size, index) keys in LDS), each cut into
 // shares = ceil(size / target) blocks of about target items, target = the
@@ -865,15 +925,20 @@ __global__ void k_part_starts(const unsigned long long *__restrict__ ex, int str
 // k-mer -- no longer end the kernel as one block each.  work[i] = bucket |
 // share << 12 | shares << 22 for block i < *nwork.
 constexpr int kWorkMax = 4096 + 2048;
-__global__ void __launch_bounds__(1024) k_bins_work(const unsigned long long *__restrict__ bstart, int nb,
+// Bucket sizes from bstart (contiguous buckets) or, when bsize is given,
+// from bsize with *btotal their sum (segmented buckets).
+__global__ void __launch_bounds__(1024) k_bins_work(const unsigned long long *__restrict__ bstart,
+                                                    const unsigned long long *__restrict__ bsize,
+                                                    const unsigned long long *__restrict__ btotal, int nb,
                                                     uint32_t *__restrict__ work, uint32_t *__restrict__ nwork) {
   __shared__ unsigned long long key[4096];
   __shared__ uint32_t shs[4096];
   __shared__ uint32_t wsum[16];
-  const unsigned long long tot = bstart[nb] - bstart[0];
+  auto size_of = [&](int b) -> unsigned long long { return bsize ? bsize[b] : bstart[b + 1] - bstart[b]; };
+  const unsigned long long tot = bsize ? *btotal : bstart[nb] - bstart[0];
   const unsigned long long target = tot / 2048 + 1;
   for (int i = threadIdx.x; i < 4096; i += 1024) {
-    const unsigned long long sz = i < nb ? bstart[i + 1] - bstart[i] : 0;
+    const unsigned long long sz = i < nb ? size_of(i) : 0;
     key[i] = ((0xffffffffull - (sz > 0xffffffffull ? 0xffffffffull : sz)) << 12) | (unsigned)(i & 4095);
   }
   __syncthreads();
@@ -895,7 +960,7 @@ __global__ void __launch_bounds__(1024) k_bins_work(const unsigned long long *__
   // shares of the r-th largest bucket, then an exclusive scan over r
   for (int r = threadIdx.x; r < 4096; r += 1024) {
     const int b = (int)(key[r] & 4095);
-    const unsigned long long sz = b < nb ? bstart[b + 1] - bstart[b] : 0;
+    const unsigned long long sz = b < nb ? size_of(b) : 0;
     shs[r] = sz ? (uint32_t)min<unsigned long long>((sz + target - 1) / target, 1023) : 0;
   }
   __syncthreads();
@@ -932,10 +997,17 @@ __global__ void __launch_bounds__(1024) k_bins_work(const unsigned long long *__
 // owns those counters; shares of a cut bucket add with atomics).  Runs of
 // equal items (the hot buckets' single-k-mer runs) are added once per run of
 // a lane's 8 items.  kSentinel (the staged scatter's padding) is skipped.
+// Grouped buckets (sex given: the staged scatter's grp_index layout; bstart
+// is then the bucket sizes): bucket b is one contiguous segment per group of
+// gs blocks, [sex[i0], sex[i1] + smat[i1]) for its first and last region of
+// the group; share s of split takes [size s / split, size (s + 1) / split)
+// of the segments' concatenation.
 __global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
                                               const unsigned long long *__restrict__ bstart, int L,
                                               uint32_t *__restrict__ counts, const uint32_t *__restrict__ work,
-                                              const uint32_t *__restrict__ nwork) {
+                                              const uint32_t *__restrict__ nwork,
+                                              const unsigned long long *__restrict__ sex,
+                                              const unsigned long long *__restrict__ smat, int G, int gs, int snb) {
   extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [2^L]
   // (no work list: block = bucket, one share; the two-level counts' 2^13-2^15 buckets)
   if (work && blockIdx.x >= *nwork) return;
@@ -945,19 +1017,6 @@ __global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
   const int nbin = 1 << L;
   for (int i = threadIdx.x; i < nbin; i += kPT) h[i] = 0;
   __syncthreads();
-  const unsigned long long a0 = bstart[bucket], a1 = bstart[bucket + 1];
-  const unsigned long long n = a1 - a0;
-  const unsigned long long a = a0 + n * s / split, e = a0 + n * (s + 1) / split;
-  // aligned body: 8 bins per 16-byte load
-  unsigned long long ah = (a + 7) & ~7ull;
-  if (ah > e) ah = e;
-  const unsigned long long eb = ah + ((e - ah) & ~7ull);
-  for (unsigned long long i = a + threadIdx.x; i < ah; i += kPT)
-    if (part[i] != kSentinel) atomicAdd(&h[part[i]], 1u);
-  for (unsigned long long i = eb + threadIdx.x; i < e; i += kPT)
-    if (part[i] != kSentinel) atomicAdd(&h[part[i]], 1u);
-  const uint4 *v = reinterpret_cast<const uint4 *>(part + ah);
-  const unsigned long long nv = (eb - ah) / 8;
   auto add8 = [&](const uint4 &x) {
     const uint32_t w[4] = {x.x, x.y, x.z, x.w};
     uint32_t cur = w[0] & 0xffffu, run = 0;
@@ -973,15 +1032,43 @@ __global__ void __launch_bounds__(kPT) k_bins(const uint16_t *__restrict__ part,
     }
     if (cur != kSentinel) atomicAdd(&h[cur], run);
   };
-  unsigned long long i = threadIdx.x;
-  for (; i + 3 * kPT < nv; i += 4 * kPT) {  // four loads in flight per lane
-    const uint4 x0 = v[i], x1 = v[i + kPT], x2 = v[i + 2 * kPT], x3 = v[i + 3 * kPT];
-    add8(x0);
-    add8(x1);
-    add8(x2);
-    add8(x3);
+  // the items [a, e) of part (head and tail one by one, the aligned body
+  // 8 per 16-byte load)
+  auto range = [&](unsigned long long a, unsigned long long e) {
+    unsigned long long ah = (a + 7) & ~7ull;
+    if (ah > e) ah = e;
+    const unsigned long long eb = ah + ((e - ah) & ~7ull);
+    for (unsigned long long i = a + threadIdx.x; i < ah; i += kPT)
+      if (part[i] != kSentinel) atomicAdd(&h[part[i]], 1u);
+    for (unsigned long long i = eb + threadIdx.x; i < e; i += kPT)
+      if (part[i] != kSentinel) atomicAdd(&h[part[i]], 1u);
+    const uint4 *v = reinterpret_cast<const uint4 *>(part + ah);
+    const unsigned long long nv = (eb - ah) / 8;
+    unsigned long long i = threadIdx.x;
+    for (; i + 3 * kPT < nv; i += 4 * kPT) {  // four loads in flight per lane
+      const uint4 x0 = v[i], x1 = v[i + kPT], x2 = v[i + 2 * kPT], x3 = v[i + 3 * kPT];
+      add8(x0);
+      add8(x1);
+      add8(x2);
+      add8(x3);
+    }
+    for (; i < nv; i += kPT) add8(v[i]);
+  };
+  if (sex) {
+    const unsigned long long tot = bstart[bucket];
+    const unsigned long long vs = tot * s / split, ve = tot * (s + 1) / split;
+    unsigned long long vo = 0;
+    for (int g0 = 0; g0 < G && vo < ve; g0 += gs) {
+      const size_t i0 = grp_index(g0, bucket, snb, G, gs), i1 = i0 + min(gs, G - g0) - 1;
+      const unsigned long long st = sex[i0], len = sex[i1] + smat[i1] - st;
+      const unsigned long long lo = vs > vo ? vs : vo, hi = ve < vo + len ? ve : vo + len;
+      if (lo < hi) range(st + lo - vo, st + hi - vo);
+      vo += len;
+    }
+  } else {
+    const unsigned long long a0 = bstart[bucket], n = bstart[bucket + 1] - a0;
+    range(a0 + n * s / split, a0 + n * (s + 1) / split);
   }
-  for (; i < nv; i += kPT) add8(v[i]);
   __syncthreads();
   uint32_t *out = counts + ((size_t)bucket << L);
   if (split == 1) {
@@ -1029,7 +1116,12 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   // profiles/r6/count/)
   const int stS = 16;
   const int64_t n_items = total - p_lo;
-  const bool staged = !g.T2 && stS > 0 && n_items + (int64_t)m1 * stS < ((int64_t)1 << 32);
+  // (groups of gs blocks, 8 groups at full size: group windows under 2 GiB,
+  // the staged scatter's buffer-store offsets)
+  const int gs = (G + 7) / 8;
+  const int64_t grp_items = (((ntiles + G - 1) / G) * kPTile + (int64_t)nb1 * stS) * gs;
+  const bool staged = !g.T2 && stS > 0 && n_items + (int64_t)m1 * stS < ((int64_t)1 << 32) &&
+                      grp_items * 2 < ((int64_t)1 << 31) - 64 && total >= kLook + kPer;
   const int pad = staged ? stS : 1;
   const size_t item1 = g.T2 ? 4 : 2;
   KS_TRY(ensure(ctx, SLOT_CHUNK_B, (size_t)(n_items + (int64_t)m1 * (pad - 1)) * item1 + 64, &p1));
@@ -1042,11 +1134,12 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   // level 1
   KS_HIP(hipMemsetAsync(last + 2, 0, 8, st));
   hipLaunchKernelGGL(k_part, dim3(G), dim3(kPT), 0, st, s->seq, total, s->offsets_dev, s->nseq, k, shift, mat1, pad,
-                     last + 2, tile0, ntiles);
+                     staged ? gs : 0, last + 2, tile0, ntiles);
   KS_HIP(hipGetLastError());
   KS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, mat1, ex1, (int64_t)m1, st));
   hipLaunchKernelGGL(k_part_sum_last, dim3(1), dim3(1), 0, st, mat1, ex1, m1, last);
-  hipLaunchKernelGGL(k_part_starts, dim3((nb1 + 1 + 255) / 256), dim3(256), 0, st, ex1, G, nb1, s1, last);
+  if (staged) hipLaunchKernelGGL(k_bucket_tot, dim3((nb1 + 255) / 256), dim3(256), 0, st, mat1, ex1, G, gs, nb1, s1);
+  else hipLaunchKernelGGL(k_part_starts, dim3((nb1 + 1 + 255) / 256), dim3(256), 0, st, ex1, G, nb1, s1, last);
   if (g.T2) {
     const size_t lds = (size_t)kPTile * (4 + 2);  // items + u16 bucket tags
     KS_HIP(hipFuncSetAttribute((const void *)k_part_scatter<uint32_t, kPT>,
@@ -1060,7 +1153,7 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
     KS_HIP(hipFuncSetAttribute((const void *)k_part_scatter_st<S, T>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                (int)lds));                                                                   \
     hipLaunchKernelGGL((k_part_scatter_st<S, T>), dim3(G), dim3(T), lds, st, s->seq, total, s->offsets_dev, s->nseq, \
-                       k, shift, ex1, static_cast<uint16_t *>(p1), tile0, ntiles);                           \
+                       k, shift, ex1, gs, static_cast<uint16_t *>(p1), tile0, ntiles);                       \
   } while (0)
     KS_ST(16, kPT);
 #undef KS_ST
@@ -1095,15 +1188,18 @@ static ks_status count_partitioned(ks_ctx *ctx, const ks_dev_seqs *s, int64_t to
   KS_HIP(hipFuncSetAttribute((const void *)k_bins, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_h));
   if (nbf > 4096) {  // two-level counts (k >= 14): a block per final bucket
     hipLaunchKernelGGL(k_bins, dim3((unsigned)nbf), dim3(kPT), lds_h, st, bins, bstart, g.L, (uint32_t *)counts_dev,
-                       nullptr, nullptr);
+                       nullptr, nullptr, nullptr, nullptr, 0, 1, 0);
   } else {
     void *ob = nullptr;
     KS_TRY(ensure(ctx, SLOT_CHUNK_D, (size_t)(kWorkMax + 16) * 4, &ob));
     uint32_t *work = static_cast<uint32_t *>(ob), *nwork = work + kWorkMax;
-    hipLaunchKernelGGL(k_bins_work, dim3(1), dim3(1024), 0, st, bstart, nbf, work, nwork);
+    // (staged: s1 holds the bucket sizes, last[0] their sum, and each
+    // bucket is a segment per group of the grouped regions)
+    hipLaunchKernelGGL(k_bins_work, dim3(1), dim3(1024), 0, st, bstart, staged ? s1 : nullptr, last, nbf, work,
+                       nwork);
     KS_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_bins, dim3((unsigned)(nbf + 2048)), dim3(kPT), lds_h, st, bins, bstart, g.L,
-                       (uint32_t *)counts_dev, work, nwork);
+                       (uint32_t *)counts_dev, work, nwork, staged ? ex1 : nullptr, mat1, G, gs, nb1);
   }
   KS_HIP(hipGetLastError());
   if (!n_words) return KS_OK;

@@ -71,6 +71,62 @@ __global__ void k_count_or(const int32_t *__restrict__ c, int64_t n, unsigned in
   }
 }
 
+// The distinct count values and their multiplicities without a sort (log2 /
+// pm1 tables need only those, ascending): a dense histogram hist[R] of the
+// values, R = max(2^end_bit, kValLds).  Per block an LDS histogram of the
+// values below kValLds, written as the block's row of rows[G][kValLds] and
+// summed over the rows by k_val_cols; values above it (repeat k-mers, rare)
+// add to hist with global atomics.  Then the nonzero bins compacted in order
+// (flags, exclusive sum, k_val_compact), and dense[v] = v's index among them
+// for k_map_dense.
+constexpr int kValLds = 8192;
+constexpr int kValBlocks = 256;
+__global__ void __launch_bounds__(1024) k_val_hist(const int32_t *__restrict__ c, int64_t n,
+                                                   uint32_t *__restrict__ rows, uint32_t *__restrict__ hist) {
+  __shared__ uint32_t h[kValLds];
+  for (int i = threadIdx.x; i < kValLds; i += 1024) h[i] = 0;
+  __syncthreads();
+  const int4 *c4 = reinterpret_cast<const int4 *>(c);  // (n = 4^k: a multiple of 4)
+  for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n / 4; i += (int64_t)gridDim.x * 1024) {
+    const int4 q = c4[i];
+    const uint32_t v[4] = {(uint32_t)q.x, (uint32_t)q.y, (uint32_t)q.z, (uint32_t)q.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (v[j] < (uint32_t)kValLds) atomicAdd(&h[v[j]], 1u);
+      else atomicAdd(&hist[v[j]], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kValLds; i += 1024) rows[(size_t)blockIdx.x * kValLds + i] = h[i];
+}
+
+__global__ void k_val_cols(const uint32_t *__restrict__ rows, int G, uint32_t *__restrict__ hist) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= kValLds) return;
+  uint32_t t = 0;
+  for (int g = 0; g < G; ++g) t += rows[(size_t)g * kValLds + v];
+  hist[v] = t;
+}
+
+__global__ void k_val_flags(const uint32_t *__restrict__ hist, int64_t R, uint32_t *__restrict__ flags) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < R; v += (int64_t)gridDim.x * blockDim.x)
+    flags[v] = hist[v] != 0;
+}
+
+__global__ void k_val_compact(const uint32_t *__restrict__ hist, const uint32_t *__restrict__ pos, int64_t R,
+                              int32_t *__restrict__ uniq, int *__restrict__ mult, int *__restrict__ nu,
+                              uint32_t *__restrict__ dense) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < R; v += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t m = hist[v], p = pos[v];
+    if (m) {
+      uniq[p] = (int32_t)v;
+      mult[p] = (int)m;
+      dense[v] = p;
+    }
+    if (v == R - 1) *nu = (int)(p + (m != 0));
+  }
+}
+
 __global__ void k_assign_codes(const double *__restrict__ s, const unsigned long long *__restrict__ uniq,
                                int64_t nu, uint16_t *__restrict__ codes, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -416,6 +472,15 @@ __global__ void __launch_bounds__(1024) k_map_counts(const int32_t *__restrict__
     }
     out[i] = lds ? s_lut[lo] : lut[lo];
   }
+}
+
+// out[i] = lut[dense[counts[i]]] (dense from k_val_compact: every count's
+// index among the distinct values).
+template <typename V>
+__global__ void k_map_dense(const int32_t *__restrict__ counts, int64_t n, const uint32_t *__restrict__ dense,
+                            const V *__restrict__ lut, V *__restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = lut[dense[counts[i]]];
 }
 
 // Weighted ranks from the closed-form prefix (RankPiece, ks_internal.h):
@@ -1215,9 +1280,10 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
   KS_TFC(hipcub::DeviceRunLengthEncode::Encode(nullptr, b2, (int32_t *)nullptr, (int32_t *)nullptr, (int *)nullptr,
                                                (int *)nullptr, (int)n, st));
   {
-    size_t bk = 0;
+    size_t bk = 0, bs = 0;
     KS_TFC(hipcub::DeviceRadixSort::SortKeys(nullptr, bk, counts_dev, (int32_t *)nullptr, (int)n, 0, 32, st));
-    b1 = std::max(b1, bk);
+    KS_TFC(hipcub::DeviceScan::ExclusiveSum(nullptr, bs, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, st));
+    b1 = std::max(b1, std::max(bk, bs));
   }
   const size_t sn = ((size_t)n * 4 + 255) & ~(size_t)255, tmpb = (std::max(b1, b2) + 255) & ~(size_t)255;
   void *ws = nullptr;
@@ -1254,11 +1320,29 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
     end_bit = 1;
     while (end_bit < 32 && (h_or >> end_bit) != 0) ++end_bit;
   }
-  if (rank)
-    KS_TFC(hipcub::DeviceRadixSort::SortPairs(d_tmp, b1, counts_dev, d_keys, d_idx_in, d_idx, (int)n, 0, end_bit, st));
-  else
-    KS_TFC(hipcub::DeviceRadixSort::SortKeys(d_tmp, b1, counts_dev, d_keys, (int)n, 0, end_bit, st));
-  KS_TFC(hipcub::DeviceRunLengthEncode::Encode(d_tmp, b2, d_keys, d_uniq, d_mult, d_nu, (int)n, st));
+  // log2 / pm1 with a value histogram that fits the scratch: no sort (the
+  // metric genome: 1.3 ms of radix sort and run-length encoding per table)
+  const int64_t R = std::max<int64_t>((int64_t)1 << end_bit, kValLds);
+  const uint32_t *d_dense = nullptr;
+  if (!rank && end_bit < 32 && (size_t)R * 4 <= sn && (size_t)kValBlocks * kValLds * 4 <= sn) {
+    uint32_t *hist = reinterpret_cast<uint32_t *>(d_keys), *rows = d_idx_in, *flags = d_idx, *pos = d_idx_in;
+    const int gv = (int)std::min<int64_t>((R + 255) / 256, 4096);
+    KS_TFC(hipMemsetAsync(hist, 0, (size_t)R * 4, st));
+    hipLaunchKernelGGL(k_val_hist, dim3(kValBlocks), dim3(1024), 0, st, counts_dev, n, rows, hist);
+    hipLaunchKernelGGL(k_val_cols, dim3(kValLds / 256), dim3(256), 0, st, rows, kValBlocks, hist);
+    hipLaunchKernelGGL(k_val_flags, dim3(gv), dim3(256), 0, st, hist, R, flags);
+    KS_TFC(hipGetLastError());
+    KS_TFC(hipcub::DeviceScan::ExclusiveSum(d_tmp, b1, flags, pos, (int)R, st));  // (rows are summed by now)
+    hipLaunchKernelGGL(k_val_compact, dim3(gv), dim3(256), 0, st, hist, pos, R, d_uniq, d_mult, d_nu, flags);
+    KS_TFC(hipGetLastError());
+    d_dense = flags;
+  } else {
+    if (rank)
+      KS_TFC(hipcub::DeviceRadixSort::SortPairs(d_tmp, b1, counts_dev, d_keys, d_idx_in, d_idx, (int)n, 0, end_bit, st));
+    else
+      KS_TFC(hipcub::DeviceRadixSort::SortKeys(d_tmp, b1, counts_dev, d_keys, (int)n, 0, end_bit, st));
+    KS_TFC(hipcub::DeviceRunLengthEncode::Encode(d_tmp, b2, d_keys, d_uniq, d_mult, d_nu, (int)n, st));
+  }
   int nu = 0;
   KS_TFC(hipMemcpyAsync(&nu, d_nu, sizeof(int), hipMemcpyDeviceToHost, st));
   KS_TFC(hipStreamSynchronize(st));
@@ -1452,8 +1536,11 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
       KS_TFC(hipMalloc(&t->d_lut, nv * sizeof(double)));
       KS_TFC(hipMemcpyAsync(t->d_lut, ub.data(), nv * 8, hipMemcpyHostToDevice, st));
       KS_TFC(hipMemcpyAsync(d_cmap, cmap.data(), (size_t)nu * 2, hipMemcpyHostToDevice, st));
-      hipLaunchKernelGGL(k_map_counts<uint16_t>, dim3(gm), dim3(1024), 0, st, counts_dev, n, d_uniq, (int64_t)nu, d_cmap,
-                         t->d_codes);
+      if (d_dense)
+        hipLaunchKernelGGL(k_map_dense<uint16_t>, dim3(gm), dim3(1024), 0, st, counts_dev, n, d_dense, d_cmap, t->d_codes);
+      else
+        hipLaunchKernelGGL(k_map_counts<uint16_t>, dim3(gm), dim3(1024), 0, st, counts_dev, n, d_uniq, (int64_t)nu,
+                           d_cmap, t->d_codes);
       KS_TFC(hipGetLastError());
       t->compressed = true;
     } else {
@@ -1466,8 +1553,11 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
       KS_TFC(hipMalloc(&t->d_vals, n * sizeof(double)));
     debug_poison(t->d_vals, n * sizeof(double));  // (KS_DEBUG_POISON)
       KS_TFC(hipMemcpyAsync(d_sv, sv.data(), (size_t)nu * 8, hipMemcpyHostToDevice, st));
-      hipLaunchKernelGGL(k_map_counts<double>, dim3(gm), dim3(1024), 0, st, counts_dev, n, d_uniq, (int64_t)nu, d_sv,
-                         t->d_vals);
+      if (d_dense)
+        hipLaunchKernelGGL(k_map_dense<double>, dim3(gm), dim3(1024), 0, st, counts_dev, n, d_dense, d_sv, t->d_vals);
+      else
+        hipLaunchKernelGGL(k_map_counts<double>, dim3(gm), dim3(1024), 0, st, counts_dev, n, d_uniq, (int64_t)nu, d_sv,
+                           t->d_vals);
       KS_TFC(hipGetLastError());
     }
     if (w_dev) {
@@ -1478,8 +1568,11 @@ extern "C" ks_status ks_table_from_counts(ks_ctx *ctx, const int32_t *counts_dev
         return fail(KS_ERR_NOMEM, "ks_table_from_counts: device allocation failed");
       }
       KS_TFC(hipMemcpyAsync(d_wv, wv.data(), (size_t)nu * 8, hipMemcpyHostToDevice, st));
-      hipLaunchKernelGGL(k_map_counts<double>, dim3(gm), dim3(1024), 0, st, counts_dev, n, d_uniq, (int64_t)nu, d_wv,
-                         w_dev);
+      if (d_dense)
+        hipLaunchKernelGGL(k_map_dense<double>, dim3(gm), dim3(1024), 0, st, counts_dev, n, d_dense, d_wv, w_dev);
+      else
+        hipLaunchKernelGGL(k_map_counts<double>, dim3(gm), dim3(1024), 0, st, counts_dev, n, d_uniq, (int64_t)nu, d_wv,
+                           w_dev);
       KS_TFC(hipGetLastError());
     }
   }

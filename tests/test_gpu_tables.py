@@ -26,8 +26,10 @@ def _counts(k, seed, kind):
 
 
 @pytest.mark.parametrize("k,kind", [(3, "skewed"), (7, "skewed"), (9, "wide"), (11, "skewed"), (12, "huge"),
-                                    (6, "zeros")])
+                                    (6, "zeros"), (11, "wide"), (12, "skewed"), (11, "zeros")])
 def test_from_counts_equals_host_builders(k, kind):
+    """(k >= 11 log2 / pm1: the distinct values from a value histogram, not a
+    sort; the huge counts keep the sort)"""
     import torch
     import kmer_spans_amd as K
     from kmer_spans_amd import _lib, device as D

@@ -92,6 +92,8 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--mode", choices=["shard", "genome", "genomes"], default="shard")
     p.add_argument("--genomes-per-rank", type=int, default=2, help="--mode genomes: genomes per rank")
+    p.add_argument("--count-priority", type=int, default=None,
+                   help="genomes mode, pipelined: the next genome's count/table stream priority (torch's scale)")
     p.add_argument("--genomes-serial", action="store_true",
                    help="--mode genomes: no overlap of genome g+1's count and table with genome g's scan")
     p.add_argument("--scale", type=float, default=1.0, help="genome scale (1.0 = 3.09 Gbp)")
@@ -1072,7 +1074,7 @@ def run_genomes(args, ctx, ds0, dev, rank, world, dist, tdist, barrier, max_over
         # its own context (workspace, streams): _lib.context(dev) is the cached
         # per-device context that ctx already is
         ctx2 = L_.Context(torch.cuda.current_device())
-        s_b = torch.cuda.Stream()
+        s_b = torch.cuda.Stream(priority=args.count_priority) if args.count_priority is not None else torch.cuda.Stream()
         ctx2.set_stream(s_b.cuda_stream)
         counts2 = [torch.zeros(4 ** k, dtype=torch.int32, device=dev) for _ in range(2)]
         cap = int((args.ext_max_gib if args.ext_max_gib else 32.0) * (1 << 30))
